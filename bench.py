@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MNIST images/sec, 784-100-10 MLP, batch=800, on N MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
+is launched under ``torch.distributed.run`` (one rank per GPU, RCCL).  W untimed
+warm-up steps, then EXACTLY K timed optimizer steps bracketed by barrier +
+synchronize on both sides; the max time over ranks is reported; rank 0 prints
+one JSON line.
+
+What a step is (the reference's ``parallel_train`` inner loop,
+fpcode/neural_network.cpp:449-555): one synchronous SGD update on a global
+batch of 800 synthetic MNIST-shaped images (random-init 784-100-10 weights,
+seeded as the reference does), split across the N ranks
+(``n = 800 / N`` columns each, strong scaling like the reference), forward +
+backward on every rank, gradient all-reduce over RCCL, SGD update.  Nothing
+is skipped inside the timed region.  Steps cycle over the 67 full batches of
+the 54,000-image training split; steps are replayed from a captured HIP graph.
+
+``--scaling weak`` keeps 800 images per GPU instead (global batch 800*N).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+METRIC = "MNIST images/sec, 784-100-10 MLP batch=800 at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # BASELINE.json "published": {} -- no reference number exists
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=4000)
+    ap.add_argument("--warmup", type=int, default=400)
+    ap.add_argument("--hidden", type=int, default=100)
+    ap.add_argument("--batch", type=int, default=800, help="global batch (strong) or per-GPU batch (weak)")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--train-size", type=int, default=54000)
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    import numpy as np
+    import torch
+
+    from cme213_sp18_amd.models.mlp import NeuralNetwork
+    from cme213_sp18_amd.parallel.launcher import init_distributed, shutdown
+    from cme213_sp18_amd.parallel.trainer import DataParallelTrainer, EpochPlan
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != a.gpus:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE", file=sys.stderr)
+    comm, device = init_distributed()
+    R, rank = comm.world_size, comm.rank
+    global_batch = a.batch * R if a.scaling == "weak" else a.batch
+
+    x, y = synthetic_mnist(a.train_size, seed=0)  # identical on every rank, no broadcast
+    nn = NeuralNetwork([784, a.hidden, 10])
+    tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=global_batch,
+                             backend=a.backend, use_graphs=not a.no_graphs)
+    tr.load(x, y)
+    full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == global_batch]
+    if not full:
+        raise SystemExit("training split smaller than one global batch")
+    lr, reg = 1e-3, 1e-4  # reference defaults (fpcode/main.cpp:58-60)
+
+    def plans_for(k: int):
+        out, i = [], 0
+        while i < k:
+            m = min(len(full), k - i)
+            out.append(EpochPlan(full[:m]))
+            i += m
+        return out
+
+    warm_plans, timed_plans = plans_for(a.warmup), plans_for(a.steps)
+    if tr.use_graphs:  # capture outside the timed region (graphs are cached by plan)
+        for p in {tuple(p.steps): p for p in warm_plans + timed_plans}.values():
+            tr.capture(p, lr, reg)
+    for p in warm_plans:
+        tr.run_plan(p, lr, reg)
+    torch.cuda.synchronize(device)
+    comm.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for p in timed_plans:
+        tr.run_plan(p, lr, reg)
+    torch.cuda.synchronize(device)
+    comm.barrier()
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    dt = comm.allreduce_scalar(dt, op="max")
+
+    # sanity: parameters finite after training
+    ok = bool(torch.isfinite(tr.engine.params).all().item())
+    images = a.steps * global_batch
+    value = images / dt
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "images/s",
+            "n_gpus": R,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * dt / a.steps, 6),
+            "higher_is_better": True,
+            "scaling": a.scaling,
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": {"f32": "fp32", "f64": "fp64", "bf16": "bf16"}[a.dtype],
+            "data": "synthetic (MNIST-shaped 784-dim uint8 images, random-init weights)",
+            "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": global_batch, "seq_len": None,
+                       "parallelism": f"dp{R}", "per_gpu_batch": global_batch // R, "backend": a.backend,
+                       "hip_graphs": tr.use_graphs, "params_finite": ok},
+        }
+        print(json.dumps(rec), flush=True)
+    shutdown()
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

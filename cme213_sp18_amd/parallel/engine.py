@@ -1,0 +1,266 @@
+"""Device-resident MLP training engine (one per rank).
+
+Replaces the reference's per-batch host<->device shuffle
+(fpcode/neural_network.cpp:484-499: X, y and ALL weights uploaded every batch,
+all gradients downloaded) and its ``device_cache`` of 18 separate cudaMallocs
+(fpcode/inc/gpu_func.h:49-101) with:
+
+* the WHOLE training set uploaded once per GPU in the GEMM dtype (54,000 x 784
+  fp32 = 169 MB, a rounding error of 288 GB of HBM), so a batch is a pointer
+  offset -- no scatter, no H2D copies;
+* one flat parameter arena ``[W1|b1|W2|b2]`` and a gradient bucket with the same
+  layout, so a single all-reduce and a single fused SGD kernel cover every
+  parameter;
+* activations ``a1, dZ1 [H][ld]``, ``D [C][ld]`` sized once for the per-rank
+  batch.
+
+Two interchangeable compute backends execute a step:
+* ``"hip"``   -- the hand-written gfx950 kernels (csrc/mlp): 3 launches per step.
+* ``"torch"`` -- the same math in plain PyTorch ops; the numerics reference for
+  the kernels and the backend for CPU-only (gloo) data-parallel tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .._native import DTYPE_CODES, hip
+
+_ALIGN = 64  # elements; keeps every arena segment 256-byte aligned for f32
+
+
+def _round_up(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+def param_dtype(dtype: str) -> torch.dtype:
+    return torch.float64 if dtype == "f64" else torch.float32
+
+
+def gemm_dtype(dtype: str) -> torch.dtype:
+    return {"f32": torch.float32, "f64": torch.float64, "bf16": torch.bfloat16}[dtype]
+
+
+class FlatLayout:
+    """Offsets of W1, b1, W2, b2 inside the flat arena (each 64-element aligned)."""
+
+    def __init__(self, P: int, H: int, C: int):
+        self.P, self.H, self.C = P, H, C
+        sizes = [H * P, H, C * H, C]
+        self.offsets = []
+        o = 0
+        for s in sizes:
+            self.offsets.append(o)
+            o += _round_up(s, _ALIGN)
+        self.sizes = sizes
+        self.total = o
+
+    def views(self, flat: torch.Tensor):
+        P, H, C = self.P, self.H, self.C
+        o = self.offsets
+        return (flat[o[0]:o[0] + H * P].view(H, P), flat[o[1]:o[1] + H], flat[o[2]:o[2] + C * H].view(C, H),
+                flat[o[3]:o[3] + C])
+
+
+class MlpEngine:
+    def __init__(self, H=(784, 100, 10), dtype: str = "f32", max_cols: int = 800, device=None,
+                 backend: str = "hip", shift: bool = True, feature_major_copy: bool = True):
+        if dtype not in DTYPE_CODES:
+            raise ValueError(f"dtype must be one of {list(DTYPE_CODES)}")
+        self.P, self.H, self.C = (int(h) for h in H)
+        self.dtype = dtype
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        if backend == "hip" and self.device.type != "cuda":
+            raise RuntimeError("the 'hip' backend needs a GPU; use backend='torch' on CPU")
+        self.backend = backend
+        self.shift = bool(shift)
+        self.pdt = param_dtype(dtype)
+        self.gdt = gemm_dtype(dtype)
+        self.layout = FlatLayout(self.P, self.H, self.C)
+        dev = self.device
+        self.params = torch.zeros(self.layout.total, dtype=self.pdt, device=dev)
+        self.grads = torch.zeros(self.layout.total, dtype=self.pdt, device=dev)
+        self.W1, self.b1, self.W2, self.b2 = self.layout.views(self.params)
+        self.gW1, self.gb1, self.gW2, self.gb2 = self.layout.views(self.grads)
+        self.W1g = (torch.zeros(self.H, self.P, dtype=torch.bfloat16, device=dev) if dtype == "bf16" else self.W1)
+        self.X = None
+        self.XT = None
+        self.labels = None
+        self._normalize = False
+        # keep a second, feature-major copy of the dataset ([P][N]) so the dW1 GEMM
+        # reads its B operand K-contiguous (16-byte loads); +1x dataset bytes, which
+        # is nothing next to 288 GB of HBM.
+        self.feature_major_copy = bool(feature_major_copy)
+        self._alloc_acts(max_cols)
+        self._step = None
+
+    # ------------------------------------------------------------------ setup
+    def _alloc_acts(self, max_cols: int):
+        self.ld = _round_up(max(int(max_cols), 1), 16)
+        dev, H, C, ld = self.device, self.H, self.C, self.ld
+        self.a1 = torch.zeros(H, ld, dtype=self.pdt, device=dev)
+        self.dZ1 = torch.zeros(H, ld, dtype=self.pdt, device=dev)
+        self.D = torch.zeros(C, ld, dtype=self.pdt, device=dev)
+        self.dZ1g = torch.zeros(H, ld, dtype=torch.bfloat16, device=dev) if self.dtype == "bf16" else self.dZ1
+        nblk = (ld + 15) // 16
+        self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
+        self._step = None
+
+    def load_dataset(self, x, labels, normalize: bool = False):
+        """Upload the training set once (uint8 or float [N][P]) in the GEMM dtype."""
+        x = torch.as_tensor(np.ascontiguousarray(x) if isinstance(x, np.ndarray) else x)
+        if x.ndim != 2 or x.shape[1] != self.P:
+            raise ValueError(f"expected [N][{self.P}] samples, got {tuple(x.shape)}")
+        xd = x.to(self.device)
+        xd = xd.to(torch.float64 if self.dtype == "f64" else torch.float32)
+        self._normalize = bool(normalize)
+        if normalize:
+            xd = xd / 255.0
+        self.X = xd.to(self.gdt).contiguous()
+        self.XT = self.X.t().contiguous() if self.feature_major_copy else None
+        self.labels = torch.as_tensor(np.asarray(labels, dtype=np.int32)).to(self.device).contiguous()
+        self.num_samples = int(self.X.shape[0])
+        self._step = None
+
+    def set_params(self, W1, b1, W2, b2):
+        with torch.no_grad():
+            for dst, src in ((self.W1, W1), (self.b1, b1), (self.W2, W2), (self.b2, b2)):
+                dst.copy_(torch.as_tensor(np.asarray(src)).to(dst.dtype))
+            self.refresh_shadow()
+
+    def refresh_shadow(self):
+        if self.dtype == "bf16":
+            self.W1g.copy_(self.W1.to(torch.bfloat16))
+
+    def get_params(self):
+        """Host float64 copies (W1, b1, W2, b2)."""
+        return tuple(t.detach().to("cpu", torch.float64).numpy().copy()
+                     for t in (self.W1, self.b1, self.W2, self.b2))
+
+    # -------------------------------------------------------------- one step
+    def _hip_step(self):
+        if self._step is None:
+            m = hip()
+            s = m.MlpStep()
+            s.dt = DTYPE_CODES[self.dtype]
+            s.P, s.H, s.C, s.ld = self.P, self.H, self.C, self.ld
+            s.X, s.labels = self.X.data_ptr(), self.labels.data_ptr()
+            s.XT = self.XT.data_ptr() if self.XT is not None else 0
+            s.N = self.num_samples
+            s.W1, s.b1, s.W2, s.b2 = (t.data_ptr() for t in (self.W1, self.b1, self.W2, self.b2))
+            s.W1g = self.W1g.data_ptr()
+            s.gW1, s.gb1, s.gW2, s.gb2 = (t.data_ptr() for t in (self.gW1, self.gb1, self.gW2, self.gb2))
+            s.a1, s.D, s.dZ1, s.dZ1g = (t.data_ptr() for t in (self.a1, self.D, self.dZ1, self.dZ1g))
+            s.loss = self.loss_buf.data_ptr()
+            s.shift = int(self.shift)
+            s.act = 1
+            self._step = s
+        return self._step
+
+    def run(self, off: int, n: int, scale: float, reg: float, lr: float, sgd: bool, with_loss: bool = False):
+        """Forward + backward on samples [off, off+n).  sgd=True: update params in
+        place; else write pre-scaled gradients into ``self.grads``."""
+        if self.X is None:
+            raise RuntimeError("load_dataset() first")
+        if n > self.ld:
+            raise ValueError(f"batch slice {n} exceeds activation capacity {self.ld}")
+        if off < 0 or off + n > self.num_samples:
+            raise IndexError("batch slice outside the resident dataset")
+        if self.backend == "hip":
+            self._hip_step().run(int(off), int(n), float(scale), float(reg), float(lr), int(bool(sgd)),
+                                 int(bool(with_loss)), torch.cuda.current_stream(self.device).cuda_stream)
+        else:
+            self._torch_step(off, n, scale, reg, lr, sgd, with_loss)
+
+    def _torch_step(self, off, n, scale, reg, lr, sgd, with_loss):
+        """Same math as the HIP step in PyTorch ops (param dtype accumulation)."""
+        with torch.no_grad():
+            Xb = self.X[off:off + n].to(self.pdt)
+            W1g = self.W1g.to(self.pdt)
+            z1 = Xb @ W1g.t() + self.b1
+            a1 = torch.sigmoid(z1)
+            z2 = a1 @ self.W2.t() + self.b2
+            if self.shift:
+                z2 = z2 - z2.max(dim=1, keepdim=True).values
+            e = torch.exp(z2)
+            p = e / e.sum(dim=1, keepdim=True)
+            lab = self.labels[off:off + n].long()
+            if with_loss:
+                self.loss_buf.zero_()
+                self.loss_buf[0] = -torch.log(p[torch.arange(n, device=p.device), lab]).sum().float()
+            onehot = torch.zeros_like(p)
+            onehot[torch.arange(n, device=p.device), lab] = 1.0
+            D = (p - onehot) * scale
+            dZ1 = (D @ self.W2) * a1 * (1 - a1)
+            self.a1[:, :n] = a1.t()
+            self.D[:, :n] = D.t()
+            self.dZ1[:, :n] = dZ1.t()
+            gW1 = dZ1.t() @ Xb + reg * self.W1
+            gW2 = D.t() @ a1 + reg * self.W2
+            gb1 = dZ1.sum(0)
+            gb2 = D.sum(0)
+            if sgd:
+                self.W1.sub_(lr * gW1)
+                self.W2.sub_(lr * gW2)
+                self.b1.sub_(lr * gb1)
+                self.b2.sub_(lr * gb2)
+                self.refresh_shadow()
+            else:
+                self.gW1.copy_(gW1)
+                self.gW2.copy_(gW2)
+                self.gb1.copy_(gb1)
+                self.gb2.copy_(gb2)
+
+    def sgd(self, lr: float):
+        """params -= lr * grads over the whole flat arena (one fused kernel)."""
+        if self.backend == "hip":
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            shadow = self.W1g.data_ptr() if self.dtype == "bf16" else 0
+            hip().sgd_flat(DTYPE_CODES[self.dtype], self.params.data_ptr(), self.grads.data_ptr(),
+                           self.layout.total, float(lr), shadow, self.H * self.P if shadow else 0, stream)
+        else:
+            with torch.no_grad():
+                self.params.sub_(lr * self.grads)
+                self.refresh_shadow()
+
+    def reg_only_grads(self, reg: float):
+        """Gradient of an EMPTY shard: reg*W for weights, 0 for biases (the
+        reference's in_proc == 0 case, neural_network.cpp:458)."""
+        with torch.no_grad():
+            self.grads.zero_()
+            self.gW1.copy_(reg * self.W1)
+            self.gW2.copy_(reg * self.W2)
+
+    def loss_sum(self) -> float:
+        """Sum of -log(yhat[label]) over the last step's local samples (if requested)."""
+        return float(self.loss_buf.double().sum().item())
+
+    # --------------------------------------------------------------- predict
+    def predict(self, x, chunk: int | None = None) -> np.ndarray:
+        """argmax labels for samples ``x`` ([N][P], host or device); GPU forward."""
+        xt = torch.as_tensor(np.ascontiguousarray(x) if isinstance(x, np.ndarray) else x)
+        n = int(xt.shape[0])
+        out = torch.empty(n, dtype=torch.int32, device=self.device)
+        chunk = chunk or max(self.ld, 4096)
+        a1 = torch.empty(self.H, _round_up(chunk, 16), dtype=self.pdt, device=self.device)
+        for s in range(0, n, chunk):
+            e = min(n, s + chunk)
+            xb = xt[s:e].to(self.device).to(torch.float64 if self.dtype == "f64" else torch.float32)
+            if getattr(self, "_normalize", False):
+                xb = xb / 255.0
+            xb = xb.to(self.gdt).contiguous()
+            if self.backend == "hip":
+                m = hip()
+                st = torch.cuda.current_stream(self.device).cuda_stream
+                dt = DTYPE_CODES[self.dtype]
+                m.mlp_forward1(dt, self.W1g.data_ptr(), self.b1.data_ptr(), xb.data_ptr(), self.P, self.H, e - s,
+                               a1.data_ptr(), a1.shape[1], 1, st)
+                m.mlp_head(dt if self.dtype != "bf16" else 0, 1, a1.data_ptr(), a1.shape[1], self.W2.data_ptr(),
+                           self.b2.data_ptr(), H=self.H, C=self.C, n=e - s, pred=out[s:e].data_ptr(), stream=st)
+            else:
+                with torch.no_grad():
+                    z1 = xb.to(self.pdt) @ self.W1g.to(self.pdt).t() + self.b1
+                    z2 = torch.sigmoid(z1) @ self.W2.t() + self.b2
+                    out[s:e] = z2.argmax(dim=1).to(torch.int32)
+        return out.cpu().numpy()

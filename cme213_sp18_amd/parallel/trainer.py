@@ -1,0 +1,228 @@
+"""Synchronous data-parallel SGD trainer -- the reference's ``parallel_train``.
+
+Semantics kept from fpcode/neural_network.cpp:401-575 (so a run on R ranks
+reproduces the single-process result for the same global batch):
+  * every global batch of B columns is split into R contiguous shards of
+    ``n = floor(min(B, N - start) / R)`` columns; the remainder columns are
+    dropped, exactly like the reference (:458);
+  * local gradients are pre-scaled so that their SUM over ranks is the
+    global-batch gradient: D scaled by ``1/(n*R)`` and ``reg/R`` (:330-334);
+  * one SUM all-reduce, then every rank applies the same SGD update (:538-541);
+  * identical seeded init on every rank -> no parameter broadcast.
+
+What changes (MI355X-first):
+  * no scatter and no host staging: each rank indexes its shard of the
+    device-resident dataset; gradients stay in one flat device bucket;
+  * one all-reduce over RCCL (instead of 4 blocking MPI_Allreduce on host
+    buffers) followed by one fused SGD kernel; world_size == 1 applies SGD
+    inside the weight-gradient kernel and communicates nothing;
+  * the whole epoch (3-5 launches + 1 collective per step) is captured once
+    into a HIP graph and replayed, so the CPU never sits on the critical path.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .comm import Communicator, NullComm
+from .engine import MlpEngine
+
+
+@dataclass
+class EpochPlan:
+    steps: list  # [(start, length)]
+
+
+@dataclass
+class TrainStats:
+    seconds: float = 0.0
+    steps: int = 0
+    images: int = 0
+    losses: list = field(default_factory=list)
+
+    @property
+    def images_per_sec(self) -> float:
+        return self.images / self.seconds if self.seconds > 0 else float("nan")
+
+
+class DataParallelTrainer:
+    def __init__(self, nn, comm: Communicator | None = None, device=None, dtype: str = "f32",
+                 batch_size: int = 800, backend: str = "hip", shift: bool = True, use_graphs: bool = True,
+                 normalize: bool = False):
+        self.nn = nn
+        self.comm = comm or NullComm()
+        self.R = self.comm.world_size
+        self.rank = self.comm.rank
+        self.B = int(batch_size)
+        self.dtype = dtype
+        self.normalize = normalize
+        self.use_graphs = bool(use_graphs) and backend == "hip" and (self.R == 1 or self.comm.graph_capturable)
+        max_cols = max(1, self.B // self.R)
+        self.engine = MlpEngine(nn.H, dtype=dtype, max_cols=max_cols, device=device, backend=backend, shift=shift)
+        self.engine.set_params(*nn.params)
+        self._graphs: dict = {}
+        self.iter = 0
+
+    # ---------------------------------------------------------------- data
+    def load(self, x_train, y_train):
+        self.engine.load_dataset(x_train, y_train, normalize=self.normalize)
+        self.N = self.engine.num_samples
+        self._graphs.clear()
+
+    def epoch_plan(self, N: int | None = None) -> EpochPlan:
+        N = self.N if N is None else N
+        nb = (N + self.B - 1) // self.B
+        return EpochPlan([(b * self.B, min(self.B, N - b * self.B)) for b in range(nb)])
+
+    # ---------------------------------------------------------------- step
+    def shard(self, start: int, length: int) -> tuple[int, int]:
+        n = length // self.R
+        return start + self.rank * n, n
+
+    def step(self, start: int, length: int, lr: float, reg: float, with_loss: bool = False) -> None:
+        """Enqueue one global SGD step on the current stream (no host sync)."""
+        e = self.engine
+        off, n = self.shard(start, length)
+        if n == 0:  # fewer columns than ranks: only the regulariser contributes
+            e.reg_only_grads(reg / self.R)
+            self.comm.allreduce_(e.grads)
+            e.sgd(lr)
+            return
+        scale = 1.0 / (n * self.R)
+        if self.R == 1:
+            e.run(off, n, scale, reg, lr, sgd=True, with_loss=with_loss)
+        else:
+            e.run(off, n, scale, reg / self.R, lr, sgd=False, with_loss=with_loss)
+            self.comm.allreduce_(e.grads)
+            e.sgd(lr)
+
+    def step_loss(self, start: int, length: int, lr: float, reg: float) -> float:
+        """One step that also returns the (pre-update) global loss -- reference
+        ``loss()`` definition (neural_network.cpp:144-154)."""
+        e = self.engine
+        with torch.no_grad():
+            nrm = float((e.W1.double() ** 2).sum() + (e.W2.double() ** 2).sum())
+        self.step(start, length, lr, reg, with_loss=True)
+        _, n = self.shard(start, length)
+        ce = self.comm.allreduce_scalar(e.loss_sum()) if n > 0 else 0.0
+        return ce / max(1, n * self.R) + 0.5 * reg * nrm
+
+    # -------------------------------------------------------------- graphs
+    def _snapshot(self):
+        e = self.engine
+        return e.params.clone(), (e.W1g.clone() if e.dtype == "bf16" else None)
+
+    def _restore(self, snap):
+        e = self.engine
+        e.params.copy_(snap[0])
+        if snap[1] is not None:
+            e.W1g.copy_(snap[1])
+
+    def capture(self, plan: EpochPlan, lr: float, reg: float) -> torch.cuda.CUDAGraph:
+        """Capture every step of ``plan`` into one HIP graph (state-neutral warm-up first)."""
+        key = (tuple(plan.steps), float(lr), float(reg))
+        g = self._graphs.get(key)
+        if g is not None:
+            return g
+        snap = self._snapshot()
+        side = torch.cuda.Stream(self.engine.device)
+        side.wait_stream(torch.cuda.current_stream(self.engine.device))
+        with torch.cuda.stream(side):  # warm-up: lazy kernel loads, communicator init
+            self.step(*plan.steps[0], lr, reg)
+        torch.cuda.current_stream(self.engine.device).wait_stream(side)
+        torch.cuda.synchronize(self.engine.device)
+        self._restore(snap)
+        torch.cuda.synchronize(self.engine.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for s, ln in plan.steps:
+                self.step(s, ln, lr, reg)
+        torch.cuda.synchronize(self.engine.device)
+        self._graphs[key] = g
+        return g
+
+    def run_plan(self, plan: EpochPlan, lr: float, reg: float) -> None:
+        if self.use_graphs:
+            self.capture(plan, lr, reg).replay()
+        else:
+            for s, ln in plan.steps:
+                self.step(s, ln, lr, reg)
+
+    # ---------------------------------------------------------------- train
+    def train(self, epochs: int, lr: float, reg: float, print_every: int = 0, debug: bool = False,
+              outdir: str = "Outputs", log=print) -> TrainStats:
+        """Full training loop (neural_network.cpp:446-555).  Eager steps where the
+        host must look at a step (loss printing / debug diffs), graphs elsewhere."""
+        from ..utils.checkpoint import write_diff_gpu_cpu
+
+        stats = TrainStats()
+        plan = self.epoch_plan()
+        err_file = None
+        if debug and self.rank == 0:  # only rank 0 owns the diff file (reference truncates it on every rank)
+            import os
+
+            os.makedirs(outdir, exist_ok=True)
+            err_file = open(os.path.join(outdir, "CpuGpuDiff.txt"), "w")
+        host_needed = print_every > 0 or debug
+        dev = self.engine.device
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        self.comm.barrier()
+        t0 = time.perf_counter()
+        try:
+            for epoch in range(epochs):
+                if not host_needed:
+                    self.run_plan(plan, lr, reg)
+                    self.iter += len(plan.steps)
+                    stats.steps += len(plan.steps)
+                    stats.images += sum((ln // self.R) * self.R for _, ln in plan.steps)
+                    continue
+                for bi, (s, ln) in enumerate(plan.steps):
+                    it = self.iter
+                    if print_every > 0 and it % print_every == 0:
+                        l = self.step_loss(s, ln, lr, reg)
+                        stats.losses.append(l)
+                        if self.rank == 0:
+                            log(f"Loss at iteration {it} of epoch {epoch}/{epochs} = {l:.10g}")
+                    else:
+                        self.step(s, ln, lr, reg)
+                    print_flag = (bi == 0) if print_every <= 0 else (it % print_every == 0)
+                    if debug and print_flag and self.rank == 0:
+                        self.sync_to(self.nn)
+                        write_diff_gpu_cpu(self.nn, it, err_file, outdir)
+                    self.iter += 1
+                    stats.steps += 1
+                    stats.images += (ln // self.R) * self.R
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            self.comm.barrier()
+        finally:
+            if err_file is not None:
+                err_file.close()
+        stats.seconds = time.perf_counter() - t0
+        self.sync_to(self.nn)
+        return stats
+
+    def sync_to(self, nn) -> None:
+        W1, b1, W2, b2 = self.engine.get_params()
+        nn.W[0][...] = W1
+        nn.b[0][...] = b1
+        nn.W[1][...] = W2
+        nn.b[1][...] = b2
+
+    def predict(self, x) -> np.ndarray:
+        return self.engine.predict(x)
+
+
+def parallel_train(nn, X, y, learning_rate: float, reg: float = 0.0, epochs: int = 15, batch_size: int = 800,
+                   grad_check: bool = False, print_every: int = -1, debug: bool = False, comm=None, device=None,
+                   dtype: str = "f32", backend: str = "hip", use_graphs: bool = True, shift: bool = True,
+                   outdir: str = "Outputs", normalize: bool = False) -> TrainStats:
+    """Reference-compatible entry point (inc/neural_network.h:45-48): trains ``nn`` in place."""
+    tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=dtype, batch_size=batch_size, backend=backend,
+                             shift=shift, use_graphs=use_graphs, normalize=normalize)
+    tr.load(X, y)
+    return tr.train(epochs, learning_rate, reg, print_every=max(0, print_every), debug=debug, outdir=outdir)

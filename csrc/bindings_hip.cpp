@@ -1,0 +1,200 @@
+// pybind11 bindings for the gfx950 kernels (module cme213_sp18_amd._hip).
+//
+// Tensors cross the boundary as raw device pointers (int) and the HIP stream
+// as an int handle (torch.cuda.current_stream().cuda_stream), so any launch
+// issued while torch is capturing a HIP graph is recorded into that graph.
+// No torch headers: the extension only depends on the HIP runtime, which it
+// shares with torch (same SONAME, torch is always imported first).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "common/hip_common.h"
+#include "mlp/mlp_kernels.h"
+#include "suite/suite_kernels.h"
+
+namespace py = pybind11;
+using cme::DType;
+
+namespace {
+
+template <typename T>
+inline T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+inline DType to_dt(int d) {
+  if (d < 0 || d > 2) throw std::invalid_argument("dtype code must be 0 (f32), 1 (f64) or 2 (bf16)");
+  return static_cast<DType>(d);
+}
+
+// Hot-path step object: everything a training step needs, bound once.  One
+// Python call launches the whole fused step (3 kernels), keeping host overhead
+// out of eager-mode steps; graph capture records the same launches.
+struct MlpStep {
+  int dt = 0;
+  int P = 784, H = 100, C = 10, ld = 0;
+  uintptr_t X = 0, labels = 0;            // device-resident dataset (gemm dtype) + int32 labels
+  uintptr_t XT = 0;                       // optional feature-major copy [P][N]
+  int64_t N = 0;                          // samples in the resident dataset (ld of XT)
+  uintptr_t W1 = 0, b1 = 0, W2 = 0, b2 = 0, W1g = 0;  // params (+ bf16 shadow of W1)
+  uintptr_t gW1 = 0, gb1 = 0, gW2 = 0, gb2 = 0;       // gradient bucket views
+  uintptr_t a1 = 0, D = 0, dZ1 = 0, dZ1g = 0;         // activations [rows][ld]
+  uintptr_t loss = 0;                                 // float partials, >= head blocks
+  int shift = 1, act = 1;
+
+  // Forward + backward for samples [off, off+n) of the resident dataset.
+  // sgd=1 applies the update in place (single process); sgd=0 writes the
+  // pre-scaled gradients into the bucket for the all-reduce.
+  void run(int64_t off, int n, double scale, double reg, double lr, int sgd, int with_loss, uintptr_t stream) {
+    CME_REQUIRE(n > 0 && n <= ld, "MlpStep.run: 0 < n <= ld required");
+    const DType d = to_dt(dt);
+    const size_t xe = d == DType::F64 ? 8 : (d == DType::BF16 ? 2 : 4);
+    const void* Xb = reinterpret_cast<const char*>(X) + (size_t)off * P * xe;
+    const int* lab = P_<int>(labels) + off;
+    cme::mlp_forward1(d, reinterpret_cast<void*>(W1g), reinterpret_cast<void*>(b1), Xb, P, H, n,
+                      reinterpret_cast<void*>(a1), ld, act, S(stream));
+    cme::HeadArgs h{};
+    h.a1 = reinterpret_cast<void*>(a1); h.lda = ld;
+    h.W2 = reinterpret_cast<void*>(W2); h.b2 = reinterpret_cast<void*>(b2);
+    h.labels = lab; h.H = H; h.C = C; h.n = n; h.scale = scale;
+    h.D = reinterpret_cast<void*>(D); h.ldd = ld;
+    h.dZ1 = reinterpret_cast<void*>(dZ1); h.ldz = ld;
+    h.dZ1_bf16 = d == DType::BF16 ? reinterpret_cast<void*>(dZ1g) : nullptr;
+    h.loss_partial = with_loss ? P_<float>(loss) : nullptr;
+    h.shift = shift; h.mode = cme::HEAD_TRAIN;
+    cme::mlp_head(d, h, S(stream));
+    cme::WgradArgs w{};
+    w.roles = 7;
+    w.dZ1g = reinterpret_cast<void*>(d == DType::BF16 ? dZ1g : dZ1); w.ldz = ld;
+    w.X = Xb; w.P = P;
+    w.XT = XT ? reinterpret_cast<const char*>(XT) + (size_t)off * xe : nullptr;
+    w.ldxt = (int)N;
+    w.dZ1 = reinterpret_cast<void*>(dZ1);
+    w.D = reinterpret_cast<void*>(D); w.ldd = ld;
+    w.a1 = reinterpret_cast<void*>(a1); w.lda = ld;
+    w.H = H; w.C = C; w.n = n; w.reg = reg; w.lr = lr; w.sgd = sgd;
+    w.W1 = reinterpret_cast<void*>(W1); w.b1 = reinterpret_cast<void*>(b1);
+    w.W2 = reinterpret_cast<void*>(W2); w.b2 = reinterpret_cast<void*>(b2);
+    w.gW1 = reinterpret_cast<void*>(gW1); w.gb1 = reinterpret_cast<void*>(gb1);
+    w.gW2 = reinterpret_cast<void*>(gW2); w.gb2 = reinterpret_cast<void*>(gb2);
+    w.W1_bf16 = d == DType::BF16 ? reinterpret_cast<void*>(W1g) : nullptr;
+    cme::mlp_wgrad(d, w, S(stream));
+  }
+
+  template <typename T>
+  static T* P_(uintptr_t p) { return reinterpret_cast<T*>(p); }
+};
+
+}  // namespace
+
+void bind_suite(py::module_& m);  // suite_bindings.cpp
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "cme213_sp18_amd gfx950 HIP kernels (MFMA MLP engine + homework kernel suite)";
+
+  m.def(
+      "mlp_forward1",
+      [](int dt, uintptr_t W1g, uintptr_t b1, uintptr_t X, int Pd, int H, int n, uintptr_t a1, int lda, int act,
+         uintptr_t s) {
+        cme::mlp_forward1(to_dt(dt), P<void>(W1g), P<void>(b1), P<void>(X), Pd, H, n, P<void>(a1), lda, act, S(s));
+      },
+      py::arg("dt"), py::arg("W1g"), py::arg("b1"), py::arg("X"), py::arg("P"), py::arg("H"), py::arg("n"),
+      py::arg("a1"), py::arg("lda"), py::arg("act"), py::arg("stream"));
+
+  m.def(
+      "mlp_head",
+      [](int dt, int mode, uintptr_t a1, int lda, uintptr_t W2, uintptr_t b2, uintptr_t labels, int H, int C,
+         int n, double scale, uintptr_t Dp, int ldd, uintptr_t dZ1, int ldz, uintptr_t dZ1_bf16, uintptr_t loss,
+         uintptr_t pred, uintptr_t probs, int ldp, int shift, uintptr_t s) {
+        cme::HeadArgs h{};
+        h.a1 = P<void>(a1); h.lda = lda; h.W2 = P<void>(W2); h.b2 = P<void>(b2);
+        h.labels = P<int>(labels); h.H = H; h.C = C; h.n = n; h.scale = scale;
+        h.D = P<void>(Dp); h.ldd = ldd; h.dZ1 = P<void>(dZ1); h.ldz = ldz; h.dZ1_bf16 = P<void>(dZ1_bf16);
+        h.loss_partial = P<float>(loss); h.pred = P<int>(pred); h.probs = P<void>(probs); h.ldp = ldp;
+        h.shift = shift; h.mode = mode;
+        cme::mlp_head(to_dt(dt), h, S(s));
+      },
+      py::arg("dt"), py::arg("mode"), py::arg("a1"), py::arg("lda"), py::arg("W2"), py::arg("b2"),
+      py::arg("labels") = 0, py::arg("H"), py::arg("C"), py::arg("n"), py::arg("scale") = 1.0,
+      py::arg("D") = 0, py::arg("ldd") = 0, py::arg("dZ1") = 0, py::arg("ldz") = 0, py::arg("dZ1_bf16") = 0,
+      py::arg("loss") = 0, py::arg("pred") = 0, py::arg("probs") = 0, py::arg("ldp") = 0,
+      py::arg("shift") = 1, py::arg("stream") = 0);
+  m.def("mlp_head_num_blocks", &cme::mlp_head_num_blocks);
+
+  m.def(
+      "mlp_wgrad",
+      [](int dt, uintptr_t dZ1g, int ldz, uintptr_t X, int Pd, uintptr_t dZ1, uintptr_t Dp, int ldd, uintptr_t a1,
+         int lda, int H, int C, int n, double reg, double lr, int sgd, uintptr_t W1, uintptr_t b1, uintptr_t W2,
+         uintptr_t b2, uintptr_t gW1, uintptr_t gb1, uintptr_t gW2, uintptr_t gb2, uintptr_t W1_bf16,
+         uintptr_t XT, int ldxt, int roles, uintptr_t s) {
+        cme::WgradArgs w{};
+        w.XT = P<void>(XT); w.ldxt = ldxt; w.roles = roles;
+        w.dZ1g = P<void>(dZ1g); w.ldz = ldz; w.X = P<void>(X); w.P = Pd; w.dZ1 = P<void>(dZ1);
+        w.D = P<void>(Dp); w.ldd = ldd; w.a1 = P<void>(a1); w.lda = lda; w.H = H; w.C = C; w.n = n;
+        w.reg = reg; w.lr = lr; w.sgd = sgd; w.W1 = P<void>(W1); w.b1 = P<void>(b1); w.W2 = P<void>(W2);
+        w.b2 = P<void>(b2); w.gW1 = P<void>(gW1); w.gb1 = P<void>(gb1); w.gW2 = P<void>(gW2);
+        w.gb2 = P<void>(gb2); w.W1_bf16 = P<void>(W1_bf16);
+        cme::mlp_wgrad(to_dt(dt), w, S(s));
+      },
+      py::arg("dt"), py::arg("dZ1g"), py::arg("ldz"), py::arg("X"), py::arg("P"), py::arg("dZ1"), py::arg("D"),
+      py::arg("ldd"), py::arg("a1"), py::arg("lda"), py::arg("H"), py::arg("C"), py::arg("n"), py::arg("reg"),
+      py::arg("lr"), py::arg("sgd"), py::arg("W1"), py::arg("b1"), py::arg("W2"), py::arg("b2"),
+      py::arg("gW1") = 0, py::arg("gb1") = 0, py::arg("gW2") = 0, py::arg("gb2") = 0, py::arg("W1_bf16") = 0,
+      py::arg("XT") = 0, py::arg("ldxt") = 0, py::arg("roles") = 7, py::arg("stream") = 0);
+
+  m.def(
+      "sgd_flat",
+      [](int dt, uintptr_t params, uintptr_t grads, int64_t count, double lr, uintptr_t shadow,
+         int64_t shadow_count, uintptr_t s) {
+        cme::sgd_flat(to_dt(dt), P<void>(params), P<void>(grads), count, lr, P<void>(shadow), shadow_count, S(s));
+      },
+      py::arg("dt"), py::arg("params"), py::arg("grads"), py::arg("count"), py::arg("lr"), py::arg("shadow") = 0,
+      py::arg("shadow_count") = 0, py::arg("stream") = 0);
+
+  m.def(
+      "gemm",
+      [](int dt, bool tA, bool tB, int M, int N, int K, double alpha, uintptr_t A, int lda, uintptr_t B, int ldb,
+         double beta, uintptr_t Cp, int ldc, uintptr_t s) {
+        cme::gemm(to_dt(dt), tA, tB, M, N, K, alpha, P<void>(A), lda, P<void>(B), ldb, beta, P<void>(Cp), ldc, S(s));
+      },
+      py::arg("dt"), py::arg("transA"), py::arg("transB"), py::arg("M"), py::arg("N"), py::arg("K"),
+      py::arg("alpha"), py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("beta"), py::arg("C"),
+      py::arg("ldc"), py::arg("stream") = 0);
+
+  m.def(
+      "convert_f32_to_bf16",
+      [](uintptr_t src, uintptr_t dst, int64_t n, uintptr_t s) {
+        cme::convert_f32_to_bf16(P<const float>(src), P<void>(dst), n, S(s));
+      },
+      py::arg("src"), py::arg("dst"), py::arg("n"), py::arg("stream") = 0);
+
+  py::class_<MlpStep>(m, "MlpStep")
+      .def(py::init<>())
+      .def_readwrite("dt", &MlpStep::dt)
+      .def_readwrite("P", &MlpStep::P)
+      .def_readwrite("H", &MlpStep::H)
+      .def_readwrite("C", &MlpStep::C)
+      .def_readwrite("ld", &MlpStep::ld)
+      .def_readwrite("X", &MlpStep::X)
+      .def_readwrite("labels", &MlpStep::labels)
+      .def_readwrite("XT", &MlpStep::XT)
+      .def_readwrite("N", &MlpStep::N)
+      .def_readwrite("W1", &MlpStep::W1)
+      .def_readwrite("b1", &MlpStep::b1)
+      .def_readwrite("W2", &MlpStep::W2)
+      .def_readwrite("b2", &MlpStep::b2)
+      .def_readwrite("W1g", &MlpStep::W1g)
+      .def_readwrite("gW1", &MlpStep::gW1)
+      .def_readwrite("gb1", &MlpStep::gb1)
+      .def_readwrite("gW2", &MlpStep::gW2)
+      .def_readwrite("gb2", &MlpStep::gb2)
+      .def_readwrite("a1", &MlpStep::a1)
+      .def_readwrite("D", &MlpStep::D)
+      .def_readwrite("dZ1", &MlpStep::dZ1)
+      .def_readwrite("dZ1g", &MlpStep::dZ1g)
+      .def_readwrite("loss", &MlpStep::loss)
+      .def_readwrite("shift", &MlpStep::shift)
+      .def_readwrite("act", &MlpStep::act)
+      .def("run", &MlpStep::run, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"), py::arg("lr"),
+           py::arg("sgd"), py::arg("with_loss"), py::arg("stream"));
+
+  bind_suite(m);
+}

@@ -1,0 +1,562 @@
+// Fused MLP step kernels for MI355X (gfx950).  See mlp_kernels.h for the
+// step decomposition and mma_tile.h for the MFMA tile engine.
+#include "mlp_kernels.h"
+
+#include "mma_tile.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace cme {
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ T dev_exp(T x);
+template <>
+__device__ __forceinline__ float dev_exp<float>(float x) { return __expf(x); }
+template <>
+__device__ __forceinline__ double dev_exp<double>(double x) { return exp(x); }
+
+template <typename T>
+__device__ __forceinline__ T dev_log(T x);
+template <>
+__device__ __forceinline__ float dev_log<float>(float x) { return __logf(x); }
+template <>
+__device__ __forceinline__ double dev_log<double>(double x) { return log(x); }
+
+template <typename T>
+__device__ __forceinline__ T sigmoid_(T x) { return T(1) / (T(1) + dev_exp<T>(-x)); }
+
+// ---------------------------------------------------------------- K1: forward
+template <typename P>  // param / activation type
+struct EpiBiasAct {
+  const P* __restrict__ bias;
+  P* __restrict__ out;
+  int ldo;
+  int act;  // 0 none, 1 sigmoid, 2 relu
+  template <typename A>
+  __device__ __forceinline__ void operator()(int row, int col, A v) {
+    P z = P(v) + bias[row];
+    if (act == 1) z = sigmoid_<P>(z);
+    else if (act == 2) z = z > P(0) ? z : P(0);
+    out[(size_t)row * ldo + col] = z;
+  }
+};
+
+constexpr int kFwdMB = 1, kFwdNB = 2, kKS = 8;
+constexpr int kThreads = 64 * kKS;
+
+// chunks-per-iteration: enough to issue a wave's whole K-slice in one burst
+template <typename T>
+constexpr int unroll_for() { return sizeof(T) == 4 ? 8 : 4; }
+
+template <typename T, typename P, bool VEC>
+__global__ __launch_bounds__(kThreads) void fwd1_kernel(const T* __restrict__ W1, const P* __restrict__ b1,
+                                                   const T* __restrict__ X, int Pdim, int H, int n,
+                                                   P* __restrict__ a1, int lda, int act, int tiles_n) {
+  using acc_t = typename MmaTraits<T>::acc_t;
+  __shared__ acc_t red[kKS * kFwdMB * kFwdNB * 4 * 64];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  TileGeom g{H, n, Pdim, (bid / tiles_n) * 16 * kFwdMB, (bid % tiles_n) * 16 * kFwdNB};
+  EpiBiasAct<P> epi{b1, a1, lda, act};
+  constexpr int U = unroll_for<T>();
+  wsk_tile<T, kFwdMB, kFwdNB, kKS, true, true, VEC, U>(W1, Pdim, X, Pdim, g, epi, red);
+}
+
+// ------------------------------------------------------------------ K2: head
+// One workgroup = COLS columns (samples) x (256/COLS) parts of the hidden dim.
+// NC = number of classes padded to a compile-time constant (10 or 16): class
+// loops are fully unrolled with no data-dependent branches around loads.
+// W2^T is staged once per workgroup in LDS ([h][NC]) when it fits, so every
+// weight read in both passes is an LDS broadcast instead of a global load.
+constexpr int kHeadCols = 16;
+constexpr int kCMax = 16;
+constexpr int kHeadLdsMax = 64 * 1024;
+
+template <typename P, int NC, bool LDSW>
+__global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
+  constexpr int COLS = kHeadCols;
+  constexpr int NPART = 256 / COLS;
+  extern __shared__ __attribute__((aligned(16))) char head_dyn[];
+  __shared__ P zred[4][NC][COLS];
+  __shared__ float lred[4];
+
+  const P* __restrict__ a1 = static_cast<const P*>(a.a1);
+  const P* __restrict__ W2 = static_cast<const P*>(a.W2);
+  const P* __restrict__ b2 = static_cast<const P*>(a.b2);
+  P* ws = reinterpret_cast<P*>(head_dyn);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int col = t % COLS, part = t / COLS;
+  const int H = a.H, C = a.C;
+  const int bcol = blockIdx.x * COLS + col;
+  const bool valid = bcol < a.n;
+  const int b = valid ? bcol : a.n - 1;  // clamped: loads stay in bounds, results discarded
+
+  if constexpr (LDSW) {
+    for (int i = t; i < H * NC; i += 256) {
+      const int h = i / NC, c = i - h * NC;
+      ws[i] = c < C ? W2[c * H + h] : P(0);
+    }
+    __syncthreads();
+  }
+  auto w2 = [&](int c, int h) -> P {
+    if constexpr (LDSW) return ws[h * NC + c];
+    else return c < C ? W2[(c < C ? c : C - 1) * H + h] : P(0);
+  };
+
+  // ---- pass 1: z2 partial sums over this thread's hidden units
+  P z[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) z[c] = P(0);
+  {
+    int h = part;
+    for (; h + 3 * NPART < H; h += 4 * NPART) {
+      P x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = a1[(size_t)(h + u * NPART) * a.lda + b];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) z[c] += w2(c, h + u * NPART) * x[u];
+    }
+    for (; h < H; h += NPART) {
+      const P x = a1[(size_t)h * a.lda + b];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) z[c] += w2(c, h) * x;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+#pragma unroll
+    for (int o = COLS; o < 64; o <<= 1) z[c] += __shfl_xor(z[c], o, 64);
+  }
+  if (lane < COLS) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) zred[wave][c][col] = z[c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    z[c] = zred[0][c][col] + zred[1][c][col] + zred[2][c][col] + zred[3][c][col] + (c < C ? b2[c < C ? c : 0] : P(0));
+
+  if (a.mode == HEAD_PREDICT) {
+    if (part == 0 && valid) {
+      int best = 0;
+      P bv = z[0];
+#pragma unroll
+      for (int c = 1; c < NC; ++c)
+        if (c < C && z[c] > bv) { bv = z[c]; best = c; }
+      a.pred[bcol] = best;
+    }
+    return;
+  }
+
+  // ---- softmax over the C classes of this column (registers only)
+  P m = P(0);
+  if (a.shift) {
+    m = z[0];
+#pragma unroll
+    for (int c = 1; c < NC; ++c) m = (c < C && z[c] > m) ? z[c] : m;
+  }
+  P s = P(0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    z[c] = c < C ? dev_exp<P>(z[c] - m) : P(0);
+    s += z[c];
+  }
+  const P inv = P(1) / s;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) z[c] *= inv;  // yhat
+
+  if (a.mode == HEAD_PROBS) {
+    if (part == 0 && valid) {
+      P* probs = static_cast<P*>(a.probs);
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c < C) probs[(size_t)c * a.ldp + bcol] = z[c];
+    }
+    return;
+  }
+
+  // ---- train: D = (yhat - onehot) * scale  (fused softmax + cross-entropy gradient)
+  const int lab = a.labels[b];
+  float lpart = 0.f;
+  if (a.loss_partial && part == 0 && valid) {
+    P pl = P(0);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) pl = c == lab ? z[c] : pl;
+    lpart = -(float)dev_log<P>(pl);
+  }
+  const P sc = P(a.scale);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) z[c] = (z[c] - (c == lab ? P(1) : P(0))) * sc;  // D
+  if (part == 0 && valid) {
+    P* D = static_cast<P*>(a.D);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (c < C) D[(size_t)c * a.ldd + bcol] = z[c];
+  }
+  if (a.loss_partial) {
+    const float v = wave_sum(lpart);
+    if (lane == 0) lred[wave] = v;
+    __syncthreads();
+    if (t == 0) a.loss_partial[blockIdx.x] = lred[0] + lred[1] + lred[2] + lred[3];
+  }
+  // ---- pass 2: dZ1 = (W2^T D) .* a1 .* (1 - a1)
+  if (valid) {
+    P* dZ1 = static_cast<P*>(a.dZ1);
+    __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
+    int h = part;
+    for (; h + 3 * NPART < H; h += 4 * NPART) {
+      P x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = a1[(size_t)(h + u * NPART) * a.lda + bcol];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        P da = P(0);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) da += w2(c, h + u * NPART) * z[c];
+        const P dz = da * x[u] * (P(1) - x[u]);
+        const size_t zi = (size_t)(h + u * NPART) * a.ldz + bcol;
+        dZ1[zi] = dz;
+        if (dZlo) dZlo[zi] = __float2bfloat16((float)dz);
+      }
+    }
+    for (; h < H; h += NPART) {
+      P da = P(0);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) da += w2(c, h) * z[c];
+      const P x = a1[(size_t)h * a.lda + bcol];
+      const P dz = da * x * (P(1) - x);
+      const size_t zi = (size_t)h * a.ldz + bcol;
+      dZ1[zi] = dz;
+      if (dZlo) dZlo[zi] = __float2bfloat16((float)dz);
+    }
+  }
+}
+
+template <typename P, int NC>
+void launch_head(const HeadArgs& a, hipStream_t s) {
+  const dim3 grid((a.n + kHeadCols - 1) / kHeadCols);
+  const size_t lds = (size_t)a.H * NC * sizeof(P);
+  if (lds <= (size_t)kHeadLdsMax)
+    head_kernel<P, NC, true><<<grid, 256, lds, s>>>(a);
+  else
+    head_kernel<P, NC, false><<<grid, 256, 0, s>>>(a);
+}
+
+// ----------------------------------------------------------------- K3: wgrad
+template <typename P>
+struct EpiWgrad {
+  P* __restrict__ W;       // params [rows][ldw]
+  P* __restrict__ G;       // gradient out (sgd == 0)
+  __hip_bfloat16* __restrict__ Wlo;  // optional bf16 shadow of W
+  int ldw;
+  P reg, lr;
+  int sgd;
+  template <typename A>
+  __device__ __forceinline__ void operator()(int row, int col, A v) {
+    const size_t i = (size_t)row * ldw + col;
+    const P w = W[i];
+    const P gr = P(v) + reg * w;
+    if (sgd) {
+      const P nw = w - lr * gr;
+      W[i] = nw;
+      if (Wlo) Wlo[i] = __float2bfloat16((float)nw);
+    } else {
+      G[i] = gr;
+    }
+  }
+};
+
+constexpr int kW1MB = 1, kW1NB = 2, kW2MB = 1, kW2NB = 2;
+
+template <typename T, typename P>
+__global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradArgs a, int t1, int t1n, int t2, int t2n,
+                                                    int vec1) {
+  using acc1_t = typename MmaTraits<T>::acc_t;
+  using acc2_t = typename MmaTraits<P>::acc_t;
+  constexpr int R1 = kKS * kW1MB * kW1NB * 4 * 64 * sizeof(acc1_t);
+  constexpr int R2 = kKS * kW2MB * kW2NB * 4 * 64 * sizeof(acc2_t);
+  __shared__ __attribute__((aligned(16))) char smem[R1 > R2 ? R1 : R2];
+  const int bid = blockIdx.x;
+  const P reg = P(a.reg), lr = P(a.lr);
+
+  if (bid < t1) {  // ---- dW1 = dZ1 * X^T  (K = batch)
+    if (!(a.roles & 1)) return;
+    const int tb = xcd_remap(bid, t1);
+    TileGeom g{a.H, a.P, a.n, (tb / t1n) * 16 * kW1MB, (tb % t1n) * 16 * kW1NB};
+    EpiWgrad<P> epi{static_cast<P*>(a.W1), static_cast<P*>(a.gW1),
+                    static_cast<__hip_bfloat16*>(a.W1_bf16), a.P, reg, lr, a.sgd};
+    const T* A = static_cast<const T*>(a.dZ1g);
+    constexpr int U = unroll_for<T>();
+    if (a.XT) {  // B(k=b, n=p) = XT[p*ldxt + b]: K-contiguous, 16-byte loads
+      const T* B = static_cast<const T*>(a.XT);
+      if (vec1)
+        wsk_tile<T, kW1MB, kW1NB, kKS, true, true, true, U>(A, a.ldz, B, a.ldxt, g, epi, (acc1_t*)smem);
+      else
+        wsk_tile<T, kW1MB, kW1NB, kKS, true, true, false, U>(A, a.ldz, B, a.ldxt, g, epi, (acc1_t*)smem);
+    } else {     // B(k=b, n=p) = X[b*P + p]: n-contiguous, coalesced scalar loads
+      const T* B = static_cast<const T*>(a.X);
+      wsk_tile<T, kW1MB, kW1NB, kKS, true, false, false, U>(A, a.ldz, B, a.P, g, epi, (acc1_t*)smem);
+    }
+    return;
+  }
+  if (bid < t1 + t2) {  // ---- dW2 = D * a1^T
+    if (!(a.roles & 2)) return;
+    const int tb = bid - t1;
+    TileGeom g{a.C, a.H, a.n, (tb / t2n) * 16 * kW2MB, (tb % t2n) * 16 * kW2NB};
+    EpiWgrad<P> epi{static_cast<P*>(a.W2), static_cast<P*>(a.gW2), nullptr, a.H, reg, lr, a.sgd};
+    constexpr int U = unroll_for<P>();
+    wsk_tile<P, kW2MB, kW2NB, kKS, true, true, false, U>(static_cast<const P*>(a.D), a.ldd,
+                                                          static_cast<const P*>(a.a1), a.lda, g, epi,
+                                                          (acc2_t*)smem);
+    return;
+  }
+  // ---- bias gradients: one wave per row; rows [0,H) -> db1 from dZ1, [H,H+C) -> db2 from D
+  const int row = (bid - t1 - t2) * kKS + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.H + a.C || !(a.roles & 4)) return;
+  const bool first = row < a.H;
+  const P* src = first ? static_cast<const P*>(a.dZ1) + (size_t)row * a.ldz
+                       : static_cast<const P*>(a.D) + (size_t)(row - a.H) * a.ldd;
+  P s = P(0);
+  for (int j = lane; j < a.n; j += 64) s += src[j];
+  s = wave_sum(s);
+  if (lane == 0) {
+    P* bp = static_cast<P*>(first ? a.b1 : a.b2);
+    const int r = first ? row : row - a.H;
+    if (a.sgd) bp[r] -= lr * s;
+    else static_cast<P*>(first ? a.gb1 : a.gb2)[r] = s;
+  }
+}
+
+// -------------------------------------------------------------- SGD (flat)
+template <typename P>
+__global__ __launch_bounds__(256) void sgd_flat_kernel(P* __restrict__ p, const P* __restrict__ g, int64_t n,
+                                                       P lr, __hip_bfloat16* __restrict__ shadow,
+                                                       int64_t shadow_n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const P v = p[i] - lr * g[i];
+    p[i] = v;
+    if (shadow && i < shadow_n) shadow[i] = __float2bfloat16((float)v);
+  }
+}
+
+template <>
+__global__ __launch_bounds__(256) void sgd_flat_kernel<float>(float* __restrict__ p, const float* __restrict__ g,
+                                                              int64_t n, float lr,
+                                                              __hip_bfloat16* __restrict__ shadow,
+                                                              int64_t shadow_n) {
+  // 16-byte vectorised body (flat arena segments are 64-element aligned)
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = p4[i];
+    const float4 d = g4[i];
+    v.x -= lr * d.x; v.y -= lr * d.y; v.z -= lr * d.z; v.w -= lr * d.w;
+    p4[i] = v;
+    if (shadow && 4 * i < shadow_n) {
+      const int64_t b = 4 * i;
+      shadow[b] = __float2bfloat16(v.x);
+      if (b + 1 < shadow_n) shadow[b + 1] = __float2bfloat16(v.y);
+      if (b + 2 < shadow_n) shadow[b + 2] = __float2bfloat16(v.z);
+      if (b + 3 < shadow_n) shadow[b + 3] = __float2bfloat16(v.w);
+    }
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    p[i] -= lr * g[i];
+    if (shadow && i < shadow_n) shadow[i] = __float2bfloat16(p[i]);
+  }
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ s, __hip_bfloat16* __restrict__ d, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    d[i] = __float2bfloat16(s[i]);
+}
+
+// ----------------------------------------------------------- generic GEMM
+template <typename T>
+struct EpiColMajor {
+  T* __restrict__ C;
+  int ldc;
+  T alpha, beta;
+  template <typename A>
+  __device__ __forceinline__ void operator()(int row, int col, A v) {
+    const size_t i = (size_t)row + (size_t)col * ldc;
+    T r = alpha * T(v);
+    if (beta != T(0)) r += beta * C[i];
+    C[i] = r;
+  }
+};
+template <>
+struct EpiColMajor<__hip_bfloat16> {
+  __hip_bfloat16* __restrict__ C;
+  int ldc;
+  float alpha, beta;
+  __device__ __forceinline__ void operator()(int row, int col, float v) {
+    const size_t i = (size_t)row + (size_t)col * ldc;
+    float r = alpha * v;
+    if (beta != 0.f) r += beta * __bfloat162float(C[i]);
+    C[i] = __float2bfloat16(r);
+  }
+};
+
+constexpr int kGMB = 2, kGNB = 2;
+
+template <typename T, bool AK, bool BK, bool VEC>
+__global__ __launch_bounds__(kThreads) void gemm_kernel(const T* __restrict__ A, int lda, const T* __restrict__ B,
+                                                   int ldb, int M, int N, int K, EpiColMajor<T> epi,
+                                                   int tiles_n) {
+  using acc_t = typename MmaTraits<T>::acc_t;
+  __shared__ acc_t red[kKS * kGMB * kGNB * 4 * 64];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  TileGeom g{M, N, K, (bid / tiles_n) * 16 * kGMB, (bid % tiles_n) * 16 * kGNB};
+  constexpr int U = sizeof(T) == 4 ? 4 : 2;
+  wsk_tile<T, kGMB, kGNB, kKS, AK, BK, VEC, U>(A, lda, B, ldb, g, epi, red);
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <typename T>
+void launch_fwd1(const void* W1, const void* b1, const void* X, int P, int H, int n, void* a1, int lda, int act,
+                 hipStream_t s) {
+  using Par = std::conditional_t<std::is_same_v<T, __hip_bfloat16>, float, T>;
+  const int tn = cdiv(n, 16 * kFwdNB), tm = cdiv(H, 16 * kFwdMB);
+  constexpr int V = MmaTraits<T>::V;
+  const bool vec = aligned16(W1) && aligned16(X) && (P % V == 0);
+  if (vec)
+    fwd1_kernel<T, Par, true><<<tm * tn, kThreads, 0, s>>>((const T*)W1, (const Par*)b1, (const T*)X, P, H, n,
+                                                       (Par*)a1, lda, act, tn);
+  else
+    fwd1_kernel<T, Par, false><<<tm * tn, kThreads, 0, s>>>((const T*)W1, (const Par*)b1, (const T*)X, P, H, n,
+                                                        (Par*)a1, lda, act, tn);
+  CME_LAUNCH_CHECK(s);
+}
+
+template <typename T, typename Par>
+void launch_wgrad(const WgradArgs& a, hipStream_t s) {
+  const int t1n = cdiv(a.P, 16 * kW1NB), t1 = cdiv(a.H, 16 * kW1MB) * t1n;
+  const int t2n = cdiv(a.H, 16 * kW2NB), t2 = cdiv(a.C, 16 * kW2MB) * t2n;
+  const int tb = cdiv(a.H + a.C, kKS);
+  constexpr int V = MmaTraits<T>::V;
+  const int vec1 = aligned16(a.dZ1g) && (a.ldz % V == 0) && (a.n % V == 0) &&
+                   (!a.XT || (aligned16(a.XT) && a.ldxt % V == 0));
+  wgrad_kernel<T, Par><<<t1 + t2 + tb, kThreads, 0, s>>>(a, t1, t1n, t2, t2n, vec1);
+  CME_LAUNCH_CHECK(s);
+}
+
+template <typename T>
+void launch_gemm(bool tA, bool tB, int M, int N, int K, double alpha, const void* A, int lda, const void* B,
+                 int ldb, double beta, void* C, int ldc, hipStream_t s) {
+  if (M <= 0 || N <= 0) return;
+  using E = EpiColMajor<T>;
+  E epi;
+  epi.C = (T*)C;
+  epi.ldc = ldc;
+  if constexpr (std::is_same_v<T, __hip_bfloat16>) {
+    epi.alpha = (float)alpha;
+    epi.beta = (float)beta;
+  } else {
+    epi.alpha = (T)alpha;
+    epi.beta = (T)beta;
+  }
+  const int tn = cdiv(N, 16 * kGNB), tm = cdiv(M, 16 * kGMB);
+  const dim3 grid(tm * tn);
+  constexpr int V = MmaTraits<T>::V;
+  // column-major: A(m,k) = A[m + k*lda] (k strided) unless transposed.
+  const bool AK = tA, BK = !tB;
+  const bool vec = aligned16(A) && aligned16(B) && (!AK || lda % V == 0) && (!BK || ldb % V == 0) && (K % V == 0);
+  const T* a = (const T*)A;
+  const T* b = (const T*)B;
+#define CME_GEMM_CASE(ak, bk)                                                                      \
+  if (AK == ak && BK == bk) {                                                                      \
+    if (vec) gemm_kernel<T, ak, bk, true><<<grid, kThreads, 0, s>>>(a, lda, b, ldb, M, N, K, epi, tn); \
+    else gemm_kernel<T, ak, bk, false><<<grid, kThreads, 0, s>>>(a, lda, b, ldb, M, N, K, epi, tn);    \
+  }
+  CME_GEMM_CASE(true, true)
+  CME_GEMM_CASE(true, false)
+  CME_GEMM_CASE(false, true)
+  CME_GEMM_CASE(false, false)
+#undef CME_GEMM_CASE
+  CME_LAUNCH_CHECK(s);
+}
+
+}  // namespace
+
+// ================================================================ public API
+void mlp_forward1(DType dt, const void* W1g, const void* b1, const void* X, int P, int H, int n, void* a1,
+                  int lda, int act, hipStream_t s) {
+  if (n <= 0) return;
+  CME_REQUIRE(lda >= n, "mlp_forward1: lda < n");
+  switch (dt) {
+    case DType::F32: launch_fwd1<float>(W1g, b1, X, P, H, n, a1, lda, act, s); break;
+    case DType::F64: launch_fwd1<double>(W1g, b1, X, P, H, n, a1, lda, act, s); break;
+    case DType::BF16: launch_fwd1<__hip_bfloat16>(W1g, b1, X, P, H, n, a1, lda, act, s); break;
+  }
+}
+
+int mlp_head_num_blocks(int n) { return cdiv(n, kHeadCols); }
+
+void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  CME_REQUIRE(a.C >= 1 && a.C <= kCMax, "mlp_head: 1 <= C <= 16 required");
+  if (dt == DType::F64) {
+    if (a.C == 10) launch_head<double, 10>(a, s);
+    else launch_head<double, 16>(a, s);
+  } else {
+    if (a.C == 10) launch_head<float, 10>(a, s);
+    else launch_head<float, 16>(a, s);
+  }
+  CME_LAUNCH_CHECK(s);
+}
+
+void mlp_wgrad(DType dt, const WgradArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  switch (dt) {
+    case DType::F32: launch_wgrad<float, float>(a, s); break;
+    case DType::F64: launch_wgrad<double, double>(a, s); break;
+    case DType::BF16: launch_wgrad<__hip_bfloat16, float>(a, s); break;
+  }
+}
+
+void sgd_flat(DType dt, void* params, const void* grads, int64_t count, double lr, void* shadow,
+              int64_t shadow_count, hipStream_t s) {
+  if (count <= 0) return;
+  const int grid = (int)std::min<int64_t>(2048, (count / 4 + 255) / 256 + 1);
+  if (dt == DType::F64)
+    sgd_flat_kernel<double><<<grid, 256, 0, s>>>((double*)params, (const double*)grads, count, lr,
+                                                 (__hip_bfloat16*)shadow, shadow_count);
+  else {
+    CME_REQUIRE(aligned16(params) && aligned16(grads), "sgd_flat: f32 arena must be 16-byte aligned");
+    sgd_flat_kernel<float><<<grid, 256, 0, s>>>((float*)params, (const float*)grads, count, (float)lr,
+                                                (__hip_bfloat16*)shadow, shadow_count);
+  }
+  CME_LAUNCH_CHECK(s);
+}
+
+void gemm(DType dt, bool tA, bool tB, int M, int N, int K, double alpha, const void* A, int lda, const void* B,
+          int ldb, double beta, void* C, int ldc, hipStream_t s) {
+  switch (dt) {
+    case DType::F32: launch_gemm<float>(tA, tB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, s); break;
+    case DType::F64: launch_gemm<double>(tA, tB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, s); break;
+    case DType::BF16:
+      launch_gemm<__hip_bfloat16>(tA, tB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, s);
+      break;
+  }
+}
+
+void convert_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  f32_to_bf16_kernel<<<grid, 256, 0, s>>>(src, (__hip_bfloat16*)dst, n);
+  CME_LAUNCH_CHECK(s);
+}
+
+}  // namespace cme
