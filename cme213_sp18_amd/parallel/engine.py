@@ -62,13 +62,36 @@ class FlatLayout:
                 flat[o[3]:o[3] + C])
 
 
+PATHS = ("auto", "split3", "split1", "mfma")
+
+
+def resolve_path(dtype: str, path: str = "auto") -> str:
+    """Compute path for a dtype.
+
+    * ``split3`` (f32 default): fp32 parameters, GEMMs on bf16 MFMA over an EXACT
+      3-plane bf16 split of the fp32 operands (csrc/mlp/mlp_split.h); needs inputs
+      that are exact in bf16 (raw 0..255 pixels).  2 kernels per step.
+    * ``split1`` (bf16 default): the same kernels with single bf16 planes (mixed precision).
+    * ``mfma``: plain f32 / f64 MFMA kernels (csrc/mlp/mlp_kernels.hip); the f64 parity
+      path and the f32 path for non-integer (normalised) inputs.  3 kernels per step.
+    """
+    if path not in PATHS:
+        raise ValueError(f"path must be one of {PATHS}")
+    if path == "auto":
+        return {"f32": "split3", "bf16": "split1", "f64": "mfma"}[dtype]
+    if path.startswith("split") and dtype == "f64":
+        raise ValueError("the split-bf16 path has fp32 parameters; use path='mfma' for f64")
+    return path
+
+
 class MlpEngine:
     def __init__(self, H=(784, 100, 10), dtype: str = "f32", max_cols: int = 800, device=None,
-                 backend: str = "hip", shift: bool = True, feature_major_copy: bool = True):
+                 backend: str = "hip", shift: bool = True, feature_major_copy: bool = True, path: str = "auto"):
         if dtype not in DTYPE_CODES:
             raise ValueError(f"dtype must be one of {list(DTYPE_CODES)}")
         self.P, self.H, self.C = (int(h) for h in H)
         self.dtype = dtype
+        self.path = resolve_path(dtype, path)
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
         if backend == "hip" and self.device.type != "cuda":
@@ -76,14 +99,12 @@ class MlpEngine:
         self.backend = backend
         self.shift = bool(shift)
         self.pdt = param_dtype(dtype)
-        self.gdt = gemm_dtype(dtype)
         self.layout = FlatLayout(self.P, self.H, self.C)
         dev = self.device
         self.params = torch.zeros(self.layout.total, dtype=self.pdt, device=dev)
         self.grads = torch.zeros(self.layout.total, dtype=self.pdt, device=dev)
         self.W1, self.b1, self.W2, self.b2 = self.layout.views(self.params)
         self.gW1, self.gb1, self.gW2, self.gb2 = self.layout.views(self.grads)
-        self.W1g = (torch.zeros(self.H, self.P, dtype=torch.bfloat16, device=dev) if dtype == "bf16" else self.W1)
         self.X = None
         self.XT = None
         self.labels = None
@@ -91,9 +112,23 @@ class MlpEngine:
         # keep a second, feature-major copy of the dataset ([P][N]) so the dW1 GEMM
         # reads its B operand K-contiguous (16-byte loads); +1x dataset bytes, which
         # is nothing next to 288 GB of HBM.
-        self.feature_major_copy = bool(feature_major_copy)
+        self.feature_major_copy = bool(feature_major_copy) or self.path.startswith("split")
+        self._configure_path()
         self._alloc_acts(max_cols)
         self._step = None
+
+    def _configure_path(self):
+        dev = self.device
+        self.np = {"split3": 3, "split1": 1}.get(self.path, 0)
+        if self.np:
+            self.gdt = torch.bfloat16
+            self.W1p = torch.zeros(self.np, self.H, self.P, dtype=torch.bfloat16, device=dev)
+            self.W1g = self.W1  # the torch backend reads the (exact) fp32 master
+        else:
+            self.gdt = gemm_dtype(self.dtype)
+            self.W1p = None
+            self.W1g = (torch.zeros(self.H, self.P, dtype=torch.bfloat16, device=dev)
+                        if self.dtype == "bf16" else self.W1)
 
     # ------------------------------------------------------------------ setup
     def _alloc_acts(self, max_cols: int):
@@ -102,7 +137,12 @@ class MlpEngine:
         self.a1 = torch.zeros(H, ld, dtype=self.pdt, device=dev)
         self.dZ1 = torch.zeros(H, ld, dtype=self.pdt, device=dev)
         self.D = torch.zeros(C, ld, dtype=self.pdt, device=dev)
-        self.dZ1g = torch.zeros(H, ld, dtype=torch.bfloat16, device=dev) if self.dtype == "bf16" else self.dZ1
+        if self.np:
+            self.dZ1p = torch.zeros(self.np, H, ld, dtype=torch.bfloat16, device=dev)
+            self.dZ1g = self.dZ1
+        else:
+            self.dZ1p = None
+            self.dZ1g = torch.zeros(H, ld, dtype=torch.bfloat16, device=dev) if self.dtype == "bf16" else self.dZ1
         nblk = (ld + 15) // 16
         self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
         self._step = None
@@ -117,11 +157,19 @@ class MlpEngine:
         self._normalize = bool(normalize)
         if normalize:
             xd = xd / 255.0
+        if self.path == "split3":
+            # the exact-split identity needs inputs that are exact in ONE bf16
+            exact = bool((xd.to(torch.bfloat16).to(xd.dtype) == xd).all().item())
+            if not exact:
+                self.path = "mfma"
+                self._configure_path()
+                self._alloc_acts(self.ld)
         self.X = xd.to(self.gdt).contiguous()
         self.XT = self.X.t().contiguous() if self.feature_major_copy else None
         self.labels = torch.as_tensor(np.asarray(labels, dtype=np.int32)).to(self.device).contiguous()
         self.num_samples = int(self.X.shape[0])
         self._step = None
+        self.refresh_shadow()
 
     def set_params(self, W1, b1, W2, b2):
         with torch.no_grad():
@@ -130,8 +178,19 @@ class MlpEngine:
             self.refresh_shadow()
 
     def refresh_shadow(self):
-        if self.dtype == "bf16":
-            self.W1g.copy_(self.W1.to(torch.bfloat16))
+        """Re-derive the low-precision copies of W1 (bf16 shadow or bf16 planes)."""
+        with torch.no_grad():
+            if self.np:
+                if self.backend == "hip":
+                    hip().split_planes(self.W1.data_ptr(), self.W1p.data_ptr(), self.H * self.P, self.np,
+                                       torch.cuda.current_stream(self.device).cuda_stream)
+                else:
+                    r = self.W1.clone()
+                    for p in range(self.np):
+                        self.W1p[p] = r.to(torch.bfloat16)
+                        r -= self.W1p[p].to(torch.float32)
+            elif self.dtype == "bf16":
+                self.W1g.copy_(self.W1.to(torch.bfloat16))
 
     def get_params(self):
         """Host float64 copies (W1, b1, W2, b2)."""
@@ -145,9 +204,11 @@ class MlpEngine:
             s = m.MlpStep()
             s.dt = DTYPE_CODES[self.dtype]
             s.P, s.H, s.C, s.ld = self.P, self.H, self.C, self.ld
-            s.X, s.labels = self.X.data_ptr(), self.labels.data_ptr()
-            s.XT = self.XT.data_ptr() if self.XT is not None else 0
-            s.N = self.num_samples
+            loaded = self.X is not None
+            s.X = self.X.data_ptr() if loaded else 0
+            s.labels = self.labels.data_ptr() if loaded else 0
+            s.XT = self.XT.data_ptr() if loaded and self.XT is not None else 0
+            s.N = self.num_samples if loaded else 0
             s.W1, s.b1, s.W2, s.b2 = (t.data_ptr() for t in (self.W1, self.b1, self.W2, self.b2))
             s.W1g = self.W1g.data_ptr()
             s.gW1, s.gb1, s.gW2, s.gb2 = (t.data_ptr() for t in (self.gW1, self.gb1, self.gW2, self.gb2))
@@ -155,6 +216,11 @@ class MlpEngine:
             s.loss = self.loss_buf.data_ptr()
             s.shift = int(self.shift)
             s.act = 1
+            if self.np:
+                s.split = 1
+                s.npw = s.npz = self.np
+                s.W1p = self.W1p.data_ptr()
+                s.dZ1p = self.dZ1p.data_ptr()
             self._step = s
         return self._step
 
@@ -177,7 +243,8 @@ class MlpEngine:
         """Same math as the HIP step in PyTorch ops (param dtype accumulation)."""
         with torch.no_grad():
             Xb = self.X[off:off + n].to(self.pdt)
-            W1g = self.W1g.to(self.pdt)
+            # the weights the kernels actually multiply: sum of the bf16 planes (== W1 for split3)
+            W1g = self.W1p.to(self.pdt).sum(0) if self.np else self.W1g.to(self.pdt)
             z1 = Xb @ W1g.t() + self.b1
             a1 = torch.sigmoid(z1)
             z2 = a1 @ self.W2.t() + self.b2
@@ -214,7 +281,11 @@ class MlpEngine:
 
     def sgd(self, lr: float):
         """params -= lr * grads over the whole flat arena (one fused kernel)."""
-        if self.backend == "hip":
+        if self.backend == "hip" and self.np:
+            hip().split_sgd(self.params.data_ptr(), self.grads.data_ptr(), self.layout.total, float(lr),
+                            self.W1p.data_ptr(), self.H * self.P, self.np,
+                            torch.cuda.current_stream(self.device).cuda_stream)
+        elif self.backend == "hip":
             stream = torch.cuda.current_stream(self.device).cuda_stream
             shadow = self.W1g.data_ptr() if self.dtype == "bf16" else 0
             hip().sgd_flat(DTYPE_CODES[self.dtype], self.params.data_ptr(), self.grads.data_ptr(),
@@ -244,13 +315,18 @@ class MlpEngine:
         out = torch.empty(n, dtype=torch.int32, device=self.device)
         chunk = chunk or max(self.ld, 4096)
         a1 = torch.empty(self.H, _round_up(chunk, 16), dtype=self.pdt, device=self.device)
+        if self.backend == "hip":
+            self._hip_step()
         for s in range(0, n, chunk):
             e = min(n, s + chunk)
             xb = xt[s:e].to(self.device).to(torch.float64 if self.dtype == "f64" else torch.float32)
             if getattr(self, "_normalize", False):
                 xb = xb / 255.0
             xb = xb.to(self.gdt).contiguous()
-            if self.backend == "hip":
+            if self.backend == "hip" and self.np:
+                self._hip_step().predict(xb.data_ptr(), e - s, a1.data_ptr(), a1.shape[1], out[s:e].data_ptr(),
+                                         torch.cuda.current_stream(self.device).cuda_stream)
+            elif self.backend == "hip":
                 m = hip()
                 st = torch.cuda.current_stream(self.device).cuda_stream
                 dt = DTYPE_CODES[self.dtype]

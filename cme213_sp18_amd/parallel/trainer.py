@@ -51,7 +51,7 @@ class TrainStats:
 class DataParallelTrainer:
     def __init__(self, nn, comm: Communicator | None = None, device=None, dtype: str = "f32",
                  batch_size: int = 800, backend: str = "hip", shift: bool = True, use_graphs: bool = True,
-                 normalize: bool = False):
+                 normalize: bool = False, path: str = "auto"):
         self.nn = nn
         self.comm = comm or NullComm()
         self.R = self.comm.world_size
@@ -61,7 +61,8 @@ class DataParallelTrainer:
         self.normalize = normalize
         self.use_graphs = bool(use_graphs) and backend == "hip" and (self.R == 1 or self.comm.graph_capturable)
         max_cols = max(1, self.B // self.R)
-        self.engine = MlpEngine(nn.H, dtype=dtype, max_cols=max_cols, device=device, backend=backend, shift=shift)
+        self.engine = MlpEngine(nn.H, dtype=dtype, max_cols=max_cols, device=device, backend=backend, shift=shift,
+                                path=path)
         self.engine.set_params(*nn.params)
         self._graphs: dict = {}
         self.iter = 0
@@ -113,13 +114,16 @@ class DataParallelTrainer:
     # -------------------------------------------------------------- graphs
     def _snapshot(self):
         e = self.engine
-        return e.params.clone(), (e.W1g.clone() if e.dtype == "bf16" else None)
+        return (e.params.clone(), (e.W1g.clone() if e.W1g is not e.W1 else None),
+                (e.W1p.clone() if e.W1p is not None else None))
 
     def _restore(self, snap):
         e = self.engine
         e.params.copy_(snap[0])
         if snap[1] is not None:
             e.W1g.copy_(snap[1])
+        if snap[2] is not None:
+            e.W1p.copy_(snap[2])
 
     def capture(self, plan: EpochPlan, lr: float, reg: float) -> torch.cuda.CUDAGraph:
         """Capture every step of ``plan`` into one HIP graph (state-neutral warm-up first)."""
@@ -220,9 +224,9 @@ class DataParallelTrainer:
 def parallel_train(nn, X, y, learning_rate: float, reg: float = 0.0, epochs: int = 15, batch_size: int = 800,
                    grad_check: bool = False, print_every: int = -1, debug: bool = False, comm=None, device=None,
                    dtype: str = "f32", backend: str = "hip", use_graphs: bool = True, shift: bool = True,
-                   outdir: str = "Outputs", normalize: bool = False) -> TrainStats:
+                   outdir: str = "Outputs", normalize: bool = False, path: str = "auto") -> TrainStats:
     """Reference-compatible entry point (inc/neural_network.h:45-48): trains ``nn`` in place."""
     tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=dtype, batch_size=batch_size, backend=backend,
-                             shift=shift, use_graphs=use_graphs, normalize=normalize)
+                             shift=shift, use_graphs=use_graphs, normalize=normalize, path=path)
     tr.load(X, y)
     return tr.train(epochs, learning_rate, reg, print_every=max(0, print_every), debug=debug, outdir=outdir)

@@ -10,6 +10,7 @@
 
 #include "common/hip_common.h"
 #include "mlp/mlp_kernels.h"
+#include "mlp/mlp_split.h"
 #include "suite/suite_kernels.h"
 
 namespace py = pybind11;
@@ -39,18 +40,61 @@ struct MlpStep {
   uintptr_t a1 = 0, D = 0, dZ1 = 0, dZ1g = 0;         // activations [rows][ld]
   uintptr_t loss = 0;                                 // float partials, >= head blocks
   int shift = 1, act = 1;
+  // split-bf16 path (mlp_split.h): X/XT are bf16, W1p/dZ1p hold npw/npz bf16 planes
+  int split = 0, npw = 3, npz = 3, fused_head = 0;
+  uintptr_t W1p = 0, dZ1p = 0;
+
+  cme::SplitStepArgs split_args(int64_t off, int n, double scale, double reg, double lr, int sgd,
+                                int with_loss) const {
+    cme::SplitStepArgs a;
+    a.P = P; a.H = H; a.C = C; a.n = n; a.ld = ld; a.npw = npw; a.npz = npz;
+    a.X = reinterpret_cast<const char*>(X) + (size_t)off * P * 2;
+    a.XT = reinterpret_cast<const char*>(XT) + (size_t)off * 2;
+    a.ldxt = (int)N;
+    a.labels = P_<int>(labels) + off;
+    a.W1 = P_<float>(W1); a.b1 = P_<float>(b1); a.W2 = P_<float>(W2); a.b2 = P_<float>(b2);
+    a.W1p = reinterpret_cast<void*>(W1p);
+    a.gW1 = P_<float>(gW1); a.gb1 = P_<float>(gb1); a.gW2 = P_<float>(gW2); a.gb2 = P_<float>(gb2);
+    a.a1 = P_<float>(a1); a.D = P_<float>(D); a.dZ1 = P_<float>(dZ1);
+    a.dZ1p = reinterpret_cast<void*>(dZ1p);
+    a.loss_partial = with_loss ? P_<float>(loss) : nullptr;
+    a.scale = scale; a.reg = reg; a.lr = lr; a.sgd = sgd; a.shift = shift; a.mode = 0;
+    return a;
+  }
 
   // Forward + backward for samples [off, off+n) of the resident dataset.
   // sgd=1 applies the update in place (single process); sgd=0 writes the
   // pre-scaled gradients into the bucket for the all-reduce.
-  void run(int64_t off, int n, double scale, double reg, double lr, int sgd, int with_loss, uintptr_t stream) {
+  // parts: bit0 = forward + head, bit1 = weight gradients / update (profiling hook; default both)
+  void run(int64_t off, int n, double scale, double reg, double lr, int sgd, int with_loss, uintptr_t stream,
+           int parts = 3) {
     CME_REQUIRE(n > 0 && n <= ld, "MlpStep.run: 0 < n <= ld required");
+    if (split) {
+      CME_REQUIRE(XT != 0 && W1p != 0 && dZ1p != 0, "MlpStep.run: split path needs XT, W1p, dZ1p");
+      const cme::SplitStepArgs a = split_args(off, n, scale, reg, lr, sgd, with_loss);
+      if (parts & 1) {
+        if (fused_head) {
+          cme::mlp_split_fwdhead(a, S(stream));
+        } else {  // tiled forward + the per-column head kernel (fp32 head)
+          cme::mlp_split_fwd1(a, S(stream));
+          cme::HeadArgs h{};
+          h.a1 = a.a1; h.lda = ld; h.W2 = a.W2; h.b2 = a.b2; h.labels = a.labels; h.H = H; h.C = C; h.n = n;
+          h.scale = scale; h.D = a.D; h.ldd = ld; h.dZ1 = a.dZ1; h.ldz = ld; h.dZ1_bf16 = nullptr;
+          h.dZ1_planes = a.dZ1p; h.npz = npz;
+          h.loss_partial = a.loss_partial; h.shift = shift; h.mode = cme::HEAD_TRAIN;
+          cme::mlp_head(DType::F32, h, S(stream));
+        }
+      }
+      if (parts & 2) cme::mlp_split_wgrad(a, S(stream));
+      return;
+    }
     const DType d = to_dt(dt);
     const size_t xe = d == DType::F64 ? 8 : (d == DType::BF16 ? 2 : 4);
     const void* Xb = reinterpret_cast<const char*>(X) + (size_t)off * P * xe;
     const int* lab = P_<int>(labels) + off;
-    cme::mlp_forward1(d, reinterpret_cast<void*>(W1g), reinterpret_cast<void*>(b1), Xb, P, H, n,
-                      reinterpret_cast<void*>(a1), ld, act, S(stream));
+    if (parts & 1)
+      cme::mlp_forward1(d, reinterpret_cast<void*>(W1g), reinterpret_cast<void*>(b1), Xb, P, H, n,
+                        reinterpret_cast<void*>(a1), ld, act, S(stream));
     cme::HeadArgs h{};
     h.a1 = reinterpret_cast<void*>(a1); h.lda = ld;
     h.W2 = reinterpret_cast<void*>(W2); h.b2 = reinterpret_cast<void*>(b2);
@@ -60,7 +104,7 @@ struct MlpStep {
     h.dZ1_bf16 = d == DType::BF16 ? reinterpret_cast<void*>(dZ1g) : nullptr;
     h.loss_partial = with_loss ? P_<float>(loss) : nullptr;
     h.shift = shift; h.mode = cme::HEAD_TRAIN;
-    cme::mlp_head(d, h, S(stream));
+    if (parts & 1) cme::mlp_head(d, h, S(stream));
     cme::WgradArgs w{};
     w.roles = 7;
     w.dZ1g = reinterpret_cast<void*>(d == DType::BF16 ? dZ1g : dZ1); w.ldz = ld;
@@ -76,7 +120,7 @@ struct MlpStep {
     w.gW1 = reinterpret_cast<void*>(gW1); w.gb1 = reinterpret_cast<void*>(gb1);
     w.gW2 = reinterpret_cast<void*>(gW2); w.gb2 = reinterpret_cast<void*>(gb2);
     w.W1_bf16 = d == DType::BF16 ? reinterpret_cast<void*>(W1g) : nullptr;
-    cme::mlp_wgrad(d, w, S(stream));
+    if (parts & 2) cme::mlp_wgrad(d, w, S(stream));
   }
 
   template <typename T>
@@ -193,8 +237,42 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("loss", &MlpStep::loss)
       .def_readwrite("shift", &MlpStep::shift)
       .def_readwrite("act", &MlpStep::act)
+      .def_readwrite("split", &MlpStep::split)
+      .def_readwrite("fused_head", &MlpStep::fused_head)
+      .def_readwrite("npw", &MlpStep::npw)
+      .def_readwrite("npz", &MlpStep::npz)
+      .def_readwrite("W1p", &MlpStep::W1p)
+      .def_readwrite("dZ1p", &MlpStep::dZ1p)
+      .def("predict",
+           [](const MlpStep& st, uintptr_t x, int n, uintptr_t a1buf, int lda, uintptr_t pred, uintptr_t s) {
+             // split path forward + argmax for n samples at x (bf16 [n][P]); a1buf: [H][lda] scratch
+             cme::SplitStepArgs a = st.split_args(0, n, 1.0, 0.0, 0.0, 0, 0);
+             a.X = reinterpret_cast<const void*>(x);
+             a.a1 = reinterpret_cast<float*>(a1buf);
+             a.ld = lda;
+             a.mode = cme::HEAD_PREDICT;
+             a.pred = reinterpret_cast<int*>(pred);
+             cme::mlp_split_fwdhead(a, S(s));
+           },
+           py::arg("x"), py::arg("n"), py::arg("a1buf"), py::arg("lda"), py::arg("pred"), py::arg("stream"))
       .def("run", &MlpStep::run, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"), py::arg("lr"),
-           py::arg("sgd"), py::arg("with_loss"), py::arg("stream"));
+           py::arg("sgd"), py::arg("with_loss"), py::arg("stream"), py::arg("parts") = 3);
+
+  m.def(
+      "split_planes",
+      [](uintptr_t W, uintptr_t planes, int64_t n, int np, uintptr_t s) {
+        cme::mlp_split_planes(P<const float>(W), P<void>(planes), n, np, S(s));
+      },
+      py::arg("W"), py::arg("planes"), py::arg("n"), py::arg("np"), py::arg("stream") = 0);
+  m.def(
+      "split_sgd",
+      [](uintptr_t params, uintptr_t grads, int64_t count, double lr, uintptr_t W1p, int64_t w1n, int npw,
+         uintptr_t s) {
+        cme::mlp_split_sgd(P<float>(params), P<const float>(grads), count, lr, P<void>(W1p), w1n, npw, S(s));
+      },
+      py::arg("params"), py::arg("grads"), py::arg("count"), py::arg("lr"), py::arg("W1p"), py::arg("w1n"),
+      py::arg("npw"), py::arg("stream") = 0);
+  m.def("split_fwdhead_blocks", &cme::mlp_split_fwdhead_blocks);
 
   bind_suite(m);
 }

@@ -36,6 +36,8 @@ struct HeadArgs {
   void* D;   int ldd;             // [C][ldd]
   void* dZ1; int ldz;             // [H][ldz]
   void* dZ1_bf16;                 // optional bf16 shadow of dZ1 for the bf16 weight-gradient GEMM
+  void* dZ1_planes = nullptr;     // optional exact bf16 planes of dZ1 ([npz][H][ldz]) for the split path
+  int npz = 0;
   float* loss_partial;            // optional: one sum of -log(yhat[label]) per workgroup
   int* pred;                      // predict mode: argmax labels [n]
   void* probs; int ldp;           // probs mode: [C][ldp]

@@ -74,8 +74,11 @@ constexpr int kHeadCols = 16;
 constexpr int kCMax = 16;
 constexpr int kHeadLdsMax = 64 * 1024;
 
-template <typename P, int NC, bool LDSW>
+template <typename P, int NC, bool LDSW, int HPT>
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
+  // HPT > 0: every thread owns at most HPT hidden units (H <= HPT * NPART); their
+  // a1 values are loaded ONCE (one burst, before the W2 staging barrier) and
+  // reused by both passes.  HPT == 0: generic loop for large H.
   constexpr int COLS = kHeadCols;
   constexpr int NPART = 256 / COLS;
   extern __shared__ __attribute__((aligned(16))) char head_dyn[];
@@ -92,7 +95,17 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   const int bcol = blockIdx.x * COLS + col;
   const bool valid = bcol < a.n;
   const int b = valid ? bcol : a.n - 1;  // clamped: loads stay in bounds, results discarded
+  const int lab = a.mode == HEAD_TRAIN ? a.labels[b] : 0;
 
+  P xa[HPT > 0 ? HPT : 1];
+  if constexpr (HPT > 0) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a1);
+#pragma unroll
+    for (int u = 0; u < HPT; ++u) {
+      const int h = part + u * NPART;
+      xa[u] = buf_load1<P>(rs, h < H ? (h * a.lda + b) * (int)sizeof(P) : kOOB);
+    }
+  }
   if constexpr (LDSW) {
     for (int i = t; i < H * NC; i += 256) {
       const int h = i / NC, c = i - h * NC;
@@ -109,7 +122,14 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   P z[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) z[c] = P(0);
-  {
+  if constexpr (HPT > 0) {
+#pragma unroll
+    for (int u = 0; u < HPT; ++u) {
+      const int h = min(part + u * NPART, H - 1);  // xa == 0 past H
+#pragma unroll
+      for (int c = 0; c < NC; ++c) z[c] += w2(c, h) * xa[u];
+    }
+  } else {
     int h = part;
     for (; h + 3 * NPART < H; h += 4 * NPART) {
       P x[4];
@@ -180,7 +200,6 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   }
 
   // ---- train: D = (yhat - onehot) * scale  (fused softmax + cross-entropy gradient)
-  const int lab = a.labels[b];
   float lpart = 0.f;
   if (a.loss_partial && part == 0 && valid) {
     P pl = P(0);
@@ -204,35 +223,36 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     if (t == 0) a.loss_partial[blockIdx.x] = lred[0] + lred[1] + lred[2] + lred[3];
   }
   // ---- pass 2: dZ1 = (W2^T D) .* a1 .* (1 - a1)
-  if (valid) {
-    P* dZ1 = static_cast<P*>(a.dZ1);
-    __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
-    int h = part;
-    for (; h + 3 * NPART < H; h += 4 * NPART) {
-      P x[4];
+  if (!valid) return;
+  P* dZ1 = static_cast<P*>(a.dZ1);
+  __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
+  __hip_bfloat16* dZp = static_cast<__hip_bfloat16*>(a.dZ1_planes);
+  const size_t pstride = (size_t)a.H * a.ldz;
+  auto emit = [&](int h, P x) {
+    P da = P(0);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = a1[(size_t)(h + u * NPART) * a.lda + bcol];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        P da = P(0);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) da += w2(c, h + u * NPART) * z[c];
-        const P dz = da * x[u] * (P(1) - x[u]);
-        const size_t zi = (size_t)(h + u * NPART) * a.ldz + bcol;
-        dZ1[zi] = dz;
-        if (dZlo) dZlo[zi] = __float2bfloat16((float)dz);
+    for (int c = 0; c < NC; ++c) da += w2(c, h) * z[c];
+    const P dz = da * x * (P(1) - x);
+    const size_t zi = (size_t)h * a.ldz + bcol;
+    dZ1[zi] = dz;
+    if (dZlo) dZlo[zi] = __float2bfloat16((float)dz);
+    if (dZp) {  // exact split into npz bf16 planes (mlp_split.h)
+      float r = (float)dz;
+      for (int p = 0; p < a.npz; ++p) {
+        const __hip_bfloat16 q = __float2bfloat16(r);
+        dZp[p * pstride + zi] = q;
+        r -= __bfloat162float(q);
       }
     }
-    for (; h < H; h += NPART) {
-      P da = P(0);
+  };
+  if constexpr (HPT > 0) {
 #pragma unroll
-      for (int c = 0; c < NC; ++c) da += w2(c, h) * z[c];
-      const P x = a1[(size_t)h * a.lda + bcol];
-      const P dz = da * x * (P(1) - x);
-      const size_t zi = (size_t)h * a.ldz + bcol;
-      dZ1[zi] = dz;
-      if (dZlo) dZlo[zi] = __float2bfloat16((float)dz);
+    for (int u = 0; u < HPT; ++u) {
+      const int h = part + u * NPART;
+      if (h < H) emit(h, xa[u]);
     }
+  } else {
+    for (int h = part; h < H; h += NPART) emit(h, a1[(size_t)h * a.lda + bcol]);
   }
 }
 
@@ -240,10 +260,13 @@ template <typename P, int NC>
 void launch_head(const HeadArgs& a, hipStream_t s) {
   const dim3 grid((a.n + kHeadCols - 1) / kHeadCols);
   const size_t lds = (size_t)a.H * NC * sizeof(P);
-  if (lds <= (size_t)kHeadLdsMax)
-    head_kernel<P, NC, true><<<grid, 256, lds, s>>>(a);
-  else
-    head_kernel<P, NC, false><<<grid, 256, 0, s>>>(a);
+  constexpr int NPART = 256 / kHeadCols;
+  if (lds <= (size_t)kHeadLdsMax) {
+    if (a.H <= 8 * NPART) head_kernel<P, NC, true, 8><<<grid, 256, lds, s>>>(a);
+    else head_kernel<P, NC, true, 0><<<grid, 256, lds, s>>>(a);
+  } else {
+    head_kernel<P, NC, false, 0><<<grid, 256, 0, s>>>(a);
+  }
 }
 
 // ----------------------------------------------------------------- K3: wgrad
@@ -314,15 +337,26 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradArgs a, int t1, in
                                                           (acc2_t*)smem);
     return;
   }
-  // ---- bias gradients: one wave per row; rows [0,H) -> db1 from dZ1, [H,H+C) -> db2 from D
+  // ---- bias gradients: one wave per row; rows [0,H) -> db1 from dZ1, [H,H+C) -> db2 from D.
+  // Burst of 16 coalesced buffer loads per lane (OOB -> 0 past n), then a wave reduction.
   const int row = (bid - t1 - t2) * kKS + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= a.H + a.C || !(a.roles & 4)) return;
   const bool first = row < a.H;
   const P* src = first ? static_cast<const P*>(a.dZ1) + (size_t)row * a.ldz
                        : static_cast<const P*>(a.D) + (size_t)(row - a.H) * a.ldd;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(src);
   P s = P(0);
-  for (int j = lane; j < a.n; j += 64) s += src[j];
+  for (int j0 = 0; j0 < a.n; j0 += 64 * 16) {
+    P v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = j0 + u * 64 + lane;
+      v[u] = buf_load1<P>(rs, j < a.n ? j * (int)sizeof(P) : kOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
   s = wave_sum(s);
   if (lane == 0) {
     P* bp = static_cast<P*>(first ? a.b1 : a.b2);

@@ -1,0 +1,62 @@
+// Split-bf16 fast path for the MLP step ("bf16 planes").
+//
+// gfx950 has no xf32/TF32 MFMA and its f32-input MFMA runs at the f32 VECTOR
+// rate (1/16 of bf16).  An fp32 value has a 24-bit significand = exactly three
+// bf16 significands, so w = w0 + w1 + w2 with w_i = bf16 EXACTLY
+// (w0 = rn_bf16(w), w1 = rn_bf16(w - w0), w2 = w - w0 - w1).  MNIST pixels are
+// integers 0..255, exact in ONE bf16.  Hence
+//      W1 . x  =  w0 . x + w1 . x + w2 . x
+// with every product exact and fp32 accumulation inside the bf16 MFMA: the
+// GEMM reads the same fp32 operands as an f32 GEMM and only the accumulation
+// order differs -- 3 v_mfma_f32_16x16x32_bf16 (48 cycles) instead of 8
+// v_mfma_f32_16x16x4_f32 (256 cycles) per 16x16x32 block.  The same identity
+// is used for dW1 = dZ1 . X^T with dZ1 split into 3 planes.
+// With npw = npz = 1 the identical kernels ARE the bf16 mixed-precision path.
+//
+// The step becomes TWO kernels:
+//   A  mlp_split_fwdhead : per 16-sample block, all of z1 (MFMA) -> sigmoid ->
+//                          z2 -> softmax -> D -> dZ1 (+ its planes); nothing
+//                          round-trips through another launch.
+//   B  mlp_split_wgrad   : dW1 (MFMA, planes) with fused reg + SGD + W1-plane
+//                          refresh, dW2 and bias gradients as extra roles.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace cme {
+
+struct SplitStepArgs {
+  int P = 784, H = 100, C = 10, n = 0, ld = 0;
+  int npw = 3, npz = 3;          // planes of W1 and of dZ1 (3: exact fp32, 1: bf16)
+  const void* X = nullptr;       // bf16 shard [n][P]
+  const void* XT = nullptr;      // bf16 feature-major shard (XT + off) [P][ldxt]
+  int ldxt = 0;
+  const int* labels = nullptr;   // shard
+  float *W1 = nullptr, *b1 = nullptr, *W2 = nullptr, *b2 = nullptr;  // fp32 master params
+  void* W1p = nullptr;           // bf16 planes [npw][H][P]
+  float *gW1 = nullptr, *gb1 = nullptr, *gW2 = nullptr, *gb2 = nullptr;
+  float *a1 = nullptr, *D = nullptr, *dZ1 = nullptr;  // [H][ld], [C][ld], [H][ld]
+  void* dZ1p = nullptr;          // bf16 planes [npz][H][ld]
+  float* loss_partial = nullptr; // one per fwdhead block (optional)
+  double scale = 1.0, reg = 0.0, lr = 0.0;
+  int sgd = 1, shift = 1;
+  int mode = 0;                  // HeadMode: 0 train, 1 predict (pred), 2 probs
+  int* pred = nullptr;
+  float* probs = nullptr;
+  int ldp = 0;
+};
+
+void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);
+// tiled forward only: a1 = sigmoid(W1 X + b1) (pair with mlp_head for the 3-kernel step)
+void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s);
+void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s);
+int mlp_split_fwdhead_blocks(int n);
+
+// planes[p][i] for i < n: exact np-way bf16 split of W[i] (np = 1: plain rounding).
+void mlp_split_planes(const float* W, void* planes, int64_t n, int np, hipStream_t s);
+// params[i] -= lr * grads[i]; then refresh the W1 planes (first w1_count params).
+void mlp_split_sgd(float* params, const float* grads, int64_t count, double lr, void* W1p, int64_t w1_count,
+                   int npw, hipStream_t s);
+
+}  // namespace cme

@@ -1,0 +1,426 @@
+// Split-bf16 MLP step kernels (see mlp_split.h for the numerics argument).
+#include "mlp_split.h"
+
+#include <algorithm>
+
+#include "mma_tile.h"
+
+namespace cme {
+
+namespace {
+
+using bf16 = __hip_bfloat16;
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// exact np-way split of an fp32 value into bf16 planes (np = 1: plain rounding)
+template <int NP>
+__device__ __forceinline__ void split_store(float v, bf16* base, size_t plane_stride, size_t idx) {
+  float r = v;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const bf16 h = __float2bfloat16(r);
+    base[p * plane_stride + idx] = h;
+    r -= __bfloat162float(h);
+  }
+}
+
+constexpr int kFHCols = 16;   // samples per workgroup
+constexpr int kFHMB = 8;      // 16-row MFMA blocks per H-chunk (128 hidden units)
+constexpr int kFHKS = 8;      // waves splitting K
+constexpr int kFHT = 64 * kFHKS;
+
+// ======================================================================
+// Kernel A: forward + head for 16 samples, all hidden units.
+// ======================================================================
+template <int NPW, int NPZ, int NC, bool VEC>
+__global__ __launch_bounds__(kFHT) void fwdhead_kernel(SplitStepArgs a) {
+  __shared__ __attribute__((aligned(16))) float red[kFHKS * kFHMB * 4 * 64];  // 64 KB split-K partials
+  __shared__ float a1s[kFHMB * 16][kFHCols + 1];  // a1 of the current H-chunk
+  __shared__ float w2s[kFHMB * 16][NC];           // W2^T of the current H-chunk
+  __shared__ float zs[kFHKS][NC][kFHCols];
+  __shared__ float Ds[NC][kFHCols];
+  __shared__ float lred[kFHKS];
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int col = t & 15;  // the column this thread owns in every epilogue element
+  const int H = a.H, C = a.C, P = a.P, ld = a.ld;
+  const int b0 = blockIdx.x * kFHCols;
+  const bool single = H <= kFHMB * 16;
+  const bf16* W1p = static_cast<const bf16*>(a.W1p);
+  const bf16* X = static_cast<const bf16*>(a.X);
+
+  float zp[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) zp[c] = 0.f;
+
+  for (int m0 = 0; m0 < H; m0 += kFHMB * 16) {
+    const int M = min(kFHMB * 16, H - m0);
+    for (int i = t; i < M * NC; i += kFHT) {
+      const int h = i / NC, c = i - h * NC;
+      w2s[h][c] = c < C ? a.W2[c * H + m0 + h] : 0.f;
+    }
+    // (w2s is first read in the epilogue, after wsk_tile's internal barrier)
+    auto epi = [&](int row, int gcol, float v) {  // gcol = global sample index (< n)
+      const float s = sigm(v + a.b1[m0 + row]);
+      a1s[row][gcol - b0] = s;
+      a.a1[(size_t)(m0 + row) * ld + gcol] = s;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) zp[c] += w2s[row][c] * s;
+    };
+    TileGeom g{M, a.n, P, 0, b0};
+    constexpr int U = NPW == 3 ? 1 : 2;  // keep one burst of loads <= ~100 VGPRs
+    wsk_tile<bf16, kFHMB, 1, kFHKS, true, true, VEC, U, NPW>(W1p + (size_t)m0 * P, P, X, P, g, epi, red,
+                                                             H * P * (int)sizeof(bf16));
+  }
+  // ---- z2 = W2 a1 + b2 for the 16 columns: reduce the per-thread partials
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    zp[c] += __shfl_xor(zp[c], 16, 64);
+    zp[c] += __shfl_xor(zp[c], 32, 64);
+  }
+  if (lane < kFHCols) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) zs[wave][c][lane] = zp[c];
+  }
+  __syncthreads();
+
+  float lpart = 0.f;
+  if (t < kFHCols) {
+    const int b = b0 + t;
+    const bool valid = b < a.n;
+    float z[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < kFHKS; ++w) s += zs[w][c][t];
+      z[c] = c < C ? s + a.b2[c] : 0.f;
+    }
+    if (a.mode == 1) {  // predict
+      if (valid) {
+        int best = 0;
+        float bv = z[0];
+#pragma unroll
+        for (int c = 1; c < NC; ++c)
+          if (c < C && z[c] > bv) { bv = z[c]; best = c; }
+        a.pred[b] = best;
+      }
+    } else {
+      float m = 0.f;
+      if (a.shift) {
+        m = z[0];
+#pragma unroll
+        for (int c = 1; c < NC; ++c) m = (c < C && z[c] > m) ? z[c] : m;
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        z[c] = c < C ? __expf(z[c] - m) : 0.f;
+        s += z[c];
+      }
+      const float inv = 1.f / s;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) z[c] *= inv;
+      if (a.mode == 2) {
+        if (valid) {
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+            if (c < C) a.probs[(size_t)c * a.ldp + b] = z[c];
+        }
+      } else {
+        const int lab = valid ? a.labels[b] : -1;
+        if (valid && a.loss_partial) {
+          float pl = 1.f;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) pl = c == lab ? z[c] : pl;
+          lpart = -__logf(pl);
+        }
+        const float sc = (float)a.scale;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const float d = valid ? (z[c] - (c == lab ? 1.f : 0.f)) * sc : 0.f;
+          Ds[c][t] = d;
+          if (valid && c < C) a.D[(size_t)c * ld + b] = d;
+        }
+      }
+    }
+  }
+  if (a.mode != 0) return;
+  if (a.loss_partial) {  // wave 0 holds every column's loss term
+    if (wave == 0) {
+      const float v = wave_sum(lpart);
+      if (lane == 0) a.loss_partial[blockIdx.x] = v;
+    }
+  }
+  __syncthreads();
+
+  // ---- dZ1 = (W2^T D) .* a1 .* (1 - a1), written in fp32 and as NPZ bf16 planes
+  const int b = b0 + col;
+  if (b >= a.n) return;
+  bf16* dZp = static_cast<bf16*>(a.dZ1p);
+  const size_t zstride = (size_t)H * ld;
+  float Dc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) Dc[c] = Ds[c][col];
+  for (int h = t >> 4; h < H; h += kFHT / kFHCols) {
+    float da = 0.f;
+    if (single) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) da += w2s[h][c] * Dc[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c < C) da += a.W2[c * H + h] * Dc[c];
+    }
+    const float x = single ? a1s[h][col] : a.a1[(size_t)h * ld + b];
+    const float dz = da * x * (1.f - x);
+    const size_t zi = (size_t)h * ld + b;
+    a.dZ1[zi] = dz;
+    split_store<NPZ>(dz, dZp, zstride, zi);
+  }
+}
+
+// ======================================================================
+// Kernel A1 (tiled): a1 = sigmoid(W1 X + b1) on 16x32 tiles, K split over 8
+// waves, W1 as NPW exact bf16 planes.  Used with the separate head kernel
+// (mlp_kernels.hip) -- cheaper than fwdhead_kernel because every workgroup
+// streams only 16 rows of W1 instead of all of it.
+// ======================================================================
+constexpr int kF1MB = 1, kF1NB = 2, kF1KS = 8;
+
+struct EpiSig {
+  const float* b1;
+  float* a1;
+  int ld;
+  __device__ __forceinline__ void operator()(int row, int col, float v) {
+    a1[(size_t)row * ld + col] = sigm(v + b1[row]);
+  }
+};
+
+template <int NPW, bool VEC>
+__global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) float red[kF1KS * kF1MB * kF1NB * 4 * 64];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  TileGeom g{a.H, a.n, a.P, (bid / tiles_n) * 16 * kF1MB, (bid % tiles_n) * 16 * kF1NB};
+  EpiSig epi{a.b1, a.a1, a.ld};
+  constexpr int U = 4;
+  wsk_tile<bf16, kF1MB, kF1NB, kF1KS, true, true, VEC, U, NPW>(static_cast<const bf16*>(a.W1p), a.P,
+                                                               static_cast<const bf16*>(a.X), a.P, g, epi, red,
+                                                               a.H * a.P * (int)sizeof(bf16));
+}
+
+// ======================================================================
+// Kernel B: dW1 (MFMA over dZ1 planes x X^T) + fused reg/SGD/plane refresh,
+//           dW2 and bias gradients as extra workgroup roles.
+// ======================================================================
+constexpr int kWMB = 1, kWNB = 2, kWKS = 8, kWT = 64 * kWKS;
+
+struct EpiW1 {
+  float* W1;
+  float* gW1;
+  bf16* W1p;
+  size_t plane;  // H*P
+  int P, sgd, npw;
+  float reg, lr;
+  __device__ __forceinline__ void operator()(int row, int col, float v) {
+    const size_t i = (size_t)row * P + col;
+    const float w = W1[i];
+    const float g = v + reg * w;
+    if (sgd) {
+      const float nw = w - lr * g;
+      W1[i] = nw;
+      if (npw == 3) split_store<3>(nw, W1p, plane, i);
+      else split_store<1>(nw, W1p, plane, i);
+    } else {
+      gW1[i] = g;
+    }
+  }
+};
+
+template <int NPZ, bool VEC>
+__global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
+  __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
+  const int bid = blockIdx.x;
+  const float reg = (float)a.reg, lr = (float)a.lr;
+  if (bid < t1) {  // ---- dW1 tile
+    const int tb = xcd_remap(bid, t1);
+    TileGeom g{a.H, a.P, a.n, (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
+    EpiW1 epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw, reg, lr};
+    constexpr int U = 4;
+    wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ>(static_cast<const bf16*>(a.dZ1p), a.ld,
+                                                              static_cast<const bf16*>(a.XT), a.ldxt, g, epi,
+                                                              red, a.H * a.ld * (int)sizeof(bf16));
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (bid < t1 + t2) {  // ---- dW2[c][h] = sum_b D[c][b] a1[h][b]: one wave per hidden unit h
+    const int h = (bid - t1) * kWKS + wv;
+    if (h >= a.H) return;
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.a1 + (size_t)h * a.ld);
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.D);
+    float acc[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc[c] = 0.f;
+    for (int j0 = 0; j0 < a.n; j0 += 64 * 4) {
+      float x[4], d[4][16];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j0 + u * 64 + lane;
+        const int ok = j < a.n;
+        x[u] = buf_load1<float>(ra, ok ? j * 4 : kOOB);
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          d[u][c] = buf_load1<float>(rd, (ok && c < a.C) ? (c * a.ld + j) * 4 : kOOB);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int c = 0; c < 16; ++c) acc[c] += d[u][c] * x[u];
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc[c] = wave_sum(acc[c]);
+    if (lane < a.C) {
+      float v = 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v = c == lane ? acc[c] : v;
+      const size_t i = (size_t)lane * a.H + h;
+      const float w = a.W2[i];
+      const float g = v + reg * w;
+      if (a.sgd) a.W2[i] = w - lr * g;
+      else a.gW2[i] = g;
+    }
+    return;
+  }
+  // ---- bias gradients: one wave per row; rows [0,H) -> db1 from dZ1, [H,H+C) -> db2 from D
+  const int row = (bid - t1 - t2) * kWKS + wv;
+  if (row >= a.H + a.C) return;
+  const bool first = row < a.H;
+  const float* src = first ? a.dZ1 + (size_t)row * a.ld : a.D + (size_t)(row - a.H) * a.ld;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(src);
+  float s = 0.f;
+  for (int j0 = 0; j0 < a.n; j0 += 64 * 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = j0 + u * 64 + lane;
+      v[u] = buf_load1<float>(rs, j < a.n ? j * 4 : kOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    float* bp = first ? a.b1 : a.b2;
+    const int r = first ? row : row - a.H;
+    if (a.sgd) bp[r] -= lr * s;
+    else (first ? a.gb1 : a.gb2)[r] = s;
+  }
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void planes_kernel(const float* __restrict__ W, bf16* __restrict__ p, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    split_store<NP>(W[i], p, (size_t)n, (size_t)i);
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void sgd_planes_kernel(float* __restrict__ prm, const float* __restrict__ g,
+                                                         int64_t n, float lr, bf16* __restrict__ planes,
+                                                         int64_t w1n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float v = prm[i] - lr * g[i];
+    prm[i] = v;
+    if (planes && i < w1n) split_store<NP>(v, planes, (size_t)w1n, (size_t)i);
+  }
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <int NPW, int NPZ, int NC>
+void launch_fwdhead(const SplitStepArgs& a, hipStream_t s) {
+  const bool vec = al16(a.X) && al16(a.W1p) && a.P % 8 == 0;
+  const dim3 grid(cdiv(a.n, kFHCols));
+  if (vec) fwdhead_kernel<NPW, NPZ, NC, true><<<grid, kFHT, 0, s>>>(a);
+  else fwdhead_kernel<NPW, NPZ, NC, false><<<grid, kFHT, 0, s>>>(a);
+}
+
+template <int NPW, int NPZ>
+void launch_fwdhead_nc(const SplitStepArgs& a, hipStream_t s) {
+  if (a.C == 10) launch_fwdhead<NPW, NPZ, 10>(a, s);
+  else launch_fwdhead<NPW, NPZ, 16>(a, s);
+}
+
+}  // namespace
+
+int mlp_split_fwdhead_blocks(int n) { return cdiv(n, kFHCols); }
+
+void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
+              "split path: operand too large for 32-bit buffer offsets");
+  const int tn = cdiv(a.n, 16 * kF1NB), tm = cdiv(a.H, 16 * kF1MB);
+  const bool vec = al16(a.X) && al16(a.W1p) && a.P % 8 == 0;
+  const dim3 grid(tm * tn);
+#define CME_F1(np)                                                                         \
+  if (vec) fwd1_split_kernel<np, true><<<grid, 64 * kF1KS, 0, s>>>(a, tn);                \
+  else fwd1_split_kernel<np, false><<<grid, 64 * kF1KS, 0, s>>>(a, tn);
+  if (a.npw == 3) { CME_F1(3) } else { CME_F1(1) }
+#undef CME_F1
+  CME_LAUNCH_CHECK(s);
+}
+
+void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  CME_REQUIRE(a.C >= 1 && a.C <= 16, "split path: 1 <= C <= 16");
+  CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
+  CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
+              "split path: operand too large for 32-bit buffer offsets");
+  if (a.npw == 3 && a.npz == 3) launch_fwdhead_nc<3, 3>(a, s);
+  else if (a.npw == 1 && a.npz == 1) launch_fwdhead_nc<1, 1>(a, s);
+  else if (a.npw == 1 && a.npz == 3) launch_fwdhead_nc<1, 3>(a, s);
+  else CME_REQUIRE(false, "split path: unsupported plane counts");
+  CME_LAUNCH_CHECK(s);
+}
+
+void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  CME_REQUIRE((int64_t)a.H * a.ld * 2 * a.npz < (int64_t)kOOB && (int64_t)a.P * a.ldxt * 2 < (int64_t)kOOB,
+              "split path: operand too large for 32-bit buffer offsets");
+  const int t1n = cdiv(a.P, 16 * kWNB), t1 = cdiv(a.H, 16 * kWMB) * t1n;
+  const int t2 = cdiv(a.H, kWKS);
+  const int tb = cdiv(a.H + a.C, kWKS);
+  const bool vec = al16(a.dZ1p) && al16(a.XT) && a.ld % 8 == 0 && a.ldxt % 8 == 0 && a.n % 8 == 0;
+  const dim3 grid(t1 + t2 + tb);
+#define CME_WG(npz)                                                                               \
+  if (vec) wgrad_split_kernel<npz, true><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);                    \
+  else wgrad_split_kernel<npz, false><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);
+  if (a.npz == 3) { CME_WG(3) } else { CME_WG(1) }
+#undef CME_WG
+  CME_LAUNCH_CHECK(s);
+}
+
+void mlp_split_planes(const float* W, void* planes, int64_t n, int np, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  if (np == 3) planes_kernel<3><<<grid, 256, 0, s>>>(W, (bf16*)planes, n);
+  else planes_kernel<1><<<grid, 256, 0, s>>>(W, (bf16*)planes, n);
+  CME_LAUNCH_CHECK(s);
+}
+
+void mlp_split_sgd(float* params, const float* grads, int64_t count, double lr, void* W1p, int64_t w1_count,
+                   int npw, hipStream_t s) {
+  if (count <= 0) return;
+  const int grid = (int)std::min<int64_t>(2048, (count + 255) / 256);
+  if (npw == 3)
+    sgd_planes_kernel<3><<<grid, 256, 0, s>>>(params, grads, count, (float)lr, (bf16*)W1p, w1_count);
+  else
+    sgd_planes_kernel<1><<<grid, 256, 0, s>>>(params, grads, count, (float)lr, (bf16*)W1p, w1_count);
+  CME_LAUNCH_CHECK(s);
+}
+
+}  // namespace cme

@@ -84,41 +84,57 @@ __device__ __forceinline__ T zero_val() { return T(0); }
 template <>
 __device__ __forceinline__ __hip_bfloat16 zero_val<__hip_bfloat16>() { return __float2bfloat16(0.f); }
 
+// Operand loads go through BUFFER loads (cdna_hip_programming.md §5.5 T8):
+// a wave-uniform 128-bit descriptor built from the kernel-argument pointer +
+// a 32-bit per-lane byte offset.  Anything outside the operand (row >= rmax,
+// k >= kend) gets the out-of-range offset kOOB and the hardware range check
+// returns ZERO -- no branches, no clamping, no select.  (A guarded load, or a
+// "load; ok ? v : 0" select that LLVM turns back into a guarded load, makes
+// hipcc branch around every load and wait vmcnt(0) per element -- measured:
+// a 10x100x800 dW2 took 17 us that way.)
+constexpr int kOOB = 0x7FFFFFF0;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, kOOB, 0x00020000);
+}
+
+template <typename T>
+__device__ __forceinline__ T buf_load1(__amdgpu_buffer_rsrc_t r, int off);
+template <>
+__device__ __forceinline__ float buf_load1<float>(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+template <>
+__device__ __forceinline__ double buf_load1<double>(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+template <>
+__device__ __forceinline__ __hip_bfloat16 buf_load1<__hip_bfloat16>(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(__hip_bfloat16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0));
+}
+
 // Load V logical elements X(r, k..k+V-1) of an operand stored either with k
-// contiguous (KCONTIG: X[r*ld + k]) or r contiguous (X[k*ld + r]); anything
-// outside r < rmax, k < kend reads as zero.
-//
-// Branch-free on purpose: the index is CLAMPED into range, the load is issued
-// unconditionally and the value is zeroed with a select.  A guarded load
-// ("if in range: load") makes hipcc branch around every load and wait
-// vmcnt(0) per element (cdna_hip_programming.md §5, trap (c)), which
-// serialises the whole K loop into dependent memory round trips.
-// VEC: caller guarantees 16-byte alignment of every full vector and that
-// kend is a multiple of V (so a vector is either fully in or fully out).
+// contiguous (KCONTIG: X[r*ld + k]) or r contiguous (X[k*ld + r]).
+// VEC: 16-byte vector loads; the caller guarantees 16-byte alignment of every
+// full vector and that kend is a multiple of V (a vector is fully in or out).
 template <typename T, int V, bool KCONTIG, bool VEC>
-__device__ __forceinline__ void load_frag(const T* __restrict__ base, int ld, int r, int rmax, int k,
-                                          int kend, T (&out)[V]) {
+__device__ __forceinline__ void load_frag(__amdgpu_buffer_rsrc_t rs, int ld, int r, int rmax, int k, int kend,
+                                          T (&out)[V], int base_off = 0) {
   const bool rok = r < rmax;
-  const int rc = rok ? r : rmax - 1;
   if constexpr (KCONTIG && VEC) {
     static_assert((V * sizeof(T)) % 16 == 0, "vector fragment must be a multiple of 16 B");
-    const bool ok = rok && k < kend;
-    const int kc = k < kend ? k : kend - V;
-    const T* p = base + (size_t)rc * ld + kc;
+    const int off = (rok && k < kend) ? (r * ld + k) * (int)sizeof(T) + base_off : kOOB;
 #pragma unroll
     for (int q = 0; q < (int)(V * sizeof(T) / 16); ++q) {
-      uint4 w = reinterpret_cast<const uint4*>(p)[q];
-      if (!ok) w = uint4{0, 0, 0, 0};
+      const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 16 * q, 0);
       __builtin_memcpy(reinterpret_cast<char*>(out) + 16 * q, &w, 16);
     }
   } else {
 #pragma unroll
     for (int j = 0; j < V; ++j) {
       const int kj = k + j;
-      const bool ok = rok && kj < kend;
-      const int kk = kj < kend ? kj : kend - 1;
-      const T v = KCONTIG ? base[(size_t)rc * ld + kk] : base[(size_t)kk * ld + rc];
-      out[j] = ok ? v : zero_val<T>();
+      const int idx = KCONTIG ? r * ld + kj : kj * ld + r;
+      out[j] = buf_load1<T>(rs, (rok && kj < kend) ? idx * (int)sizeof(T) + base_off : kOOB);
     }
   }
 }
@@ -132,10 +148,14 @@ struct TileGeom {
 // of C = A * B with K split across the waves.  On return, `epi(row, col, v)`
 // has been called exactly once for every in-bounds element of the tile.
 // `red` must point at >= KS*MB*NB*4*64 accumulators of LDS (unused if KS==1).
-template <typename T, int MB, int NB, int KS, bool AK, bool BK, bool VEC, int U, class Epi>
+//
+// NPA > 1: A is the exact sum of NPA planes stored `plane_bytes` apart
+// (A = A_0 + A_1 + ...; the split-bf16 representation of an fp32 operand,
+// see mlp_split.hip) and every plane is multiplied into the same accumulator.
+template <typename T, int MB, int NB, int KS, bool AK, bool BK, bool VEC, int U, int NPA = 1, class Epi>
 __device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const T* __restrict__ B, int ldb,
                                          TileGeom g, Epi& epi,
-                                         typename MmaTraits<T>::acc_t* __restrict__ red) {
+                                         typename MmaTraits<T>::acc_t* __restrict__ red, int plane_bytes = 0) {
   using Tr = MmaTraits<T>;
   using accv_t = typename Tr::accv_t;
   using acc_t = typename Tr::acc_t;
@@ -151,23 +171,26 @@ __device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = accv_t{0, 0, 0, 0};
 
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A), rsB = make_rsrc(B);
   const int nch = (g.K + KC - 1) / KC;
   const int cpw = (nch + KS - 1) / KS;
   const int kbeg = wave * cpw * KC;
   const int kend = min(g.K, (wave + 1) * cpw * KC);
 
   for (int kc = kbeg; kc < kend; kc += KC * U) {
-    T af[U][MB][V];
+    T af[U][NPA][MB][V];
     T bf[U][NB][V];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = kc + u * KC + V * grp;
 #pragma unroll
-      for (int i = 0; i < MB; ++i)
-        load_frag<T, V, AK, VEC>(A, lda, g.m0 + 16 * i + c, g.M, k, kend, af[u][i]);
+      for (int p = 0; p < NPA; ++p)
+#pragma unroll
+        for (int i = 0; i < MB; ++i)
+          load_frag<T, V, AK, VEC>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, af[u][p][i], p * plane_bytes);
 #pragma unroll
       for (int j = 0; j < NB; ++j)
-        load_frag<T, V, BK, VEC>(B, ldb, g.n0 + 16 * j + c, g.N, k, kend, bf[u][j]);
+        load_frag<T, V, BK, VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, bf[u][j]);
     }
     // Keep every load of this burst ahead of the first MFMA: without the fence
     // the scheduler sinks each load next to its consumer to save VGPRs, which
@@ -177,9 +200,11 @@ __device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int i = 0; i < MB; ++i)
+      for (int p = 0; p < NPA; ++p)
 #pragma unroll
-        for (int j = 0; j < NB; ++j) Tr::mma(af[u][i], bf[u][j], acc[i][j]);
+        for (int i = 0; i < MB; ++i)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) Tr::mma(af[u][p][i], bf[u][j], acc[i][j]);
   }
 
   if constexpr (KS == 1) {

@@ -78,27 +78,34 @@ def test_forward1_bias_sigmoid(dt, H, n):
     assert (a1[:, :n].double().cpu() - ref).abs().max().item() < tol
 
 
-def _engine_pair(dt, H=100, n=800, N=1600):
+CFGS = [("f64", "mfma"), ("f32", "split3"), ("f32", "mfma"), ("bf16", "split1"), ("bf16", "mfma")]
+TOL = {("f64", "mfma"): 1e-11, ("f32", "split3"): 2e-4, ("f32", "mfma"): 2e-4, ("bf16", "split1"): 3e-2,
+       ("bf16", "mfma"): 3e-2}
+
+
+def _engine_pair(dt, H=100, n=800, N=1600, path="auto"):
     x, y = synthetic_mnist(N, seed=3)
     nn = NeuralNetwork([784, H, 10])
     engines = []
     for backend in ("hip", "torch"):
-        e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", backend=backend)
+        e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", backend=backend, path=path)
         e.set_params(*nn.params)
         e.load_dataset(x, y)
         engines.append(e)
     return engines
 
 
-@pytest.mark.parametrize("dt", ["f64", "f32", "bf16"])
+@pytest.mark.parametrize("dt,path", CFGS)
 @pytest.mark.parametrize("n", [800, 100, 37])
-def test_step_gradients_match_torch(dt, n):
-    hipe, te = _engine_pair(dt, n=max(n, 16))
+@pytest.mark.parametrize("H", [100, 300])
+def test_step_gradients_match_torch(dt, path, n, H):
+    hipe, te = _engine_pair(dt, n=max(n, 16), path=path, H=H)
+    assert hipe.path == path
     scale, reg = 1.0 / n, 1e-4
     for e in (hipe, te):
         e.run(64, n, scale, reg, 0.0, sgd=False, with_loss=True)
     torch.cuda.synchronize()
-    tol = {"f64": 1e-11, "f32": 2e-4, "bf16": 3e-2}[dt]
+    tol = TOL[(dt, path)]
     for name in ("gW1", "gb1", "gW2", "gb2"):
         assert _rel(getattr(hipe, name), getattr(te, name)) < tol, name
     assert abs(hipe.loss_sum() - te.loss_sum()) / te.loss_sum() < 1e-4
@@ -108,25 +115,46 @@ def test_step_gradients_match_torch(dt, n):
         assert _rel(a, b) < max(tol, 1e-5), name
 
 
-@pytest.mark.parametrize("dt", ["f64", "f32", "bf16"])
-def test_fused_sgd_matches_torch(dt):
-    hipe, te = _engine_pair(dt)
+@pytest.mark.parametrize("dt,path", CFGS)
+def test_fused_sgd_matches_torch(dt, path):
+    hipe, te = _engine_pair(dt, path=path)
     for it in range(5):
         for e in (hipe, te):
             e.run(800 * (it % 2), 800, 1 / 800, 1e-4, 0.01, sgd=True)
     torch.cuda.synchronize()
     tol = {"f64": 1e-11, "f32": 1e-5, "bf16": 1e-2}[dt]
     assert _rel(hipe.params, te.params) < tol
+    if hipe.W1p is not None:  # the bf16 planes must track the fp32 master exactly (split3) / rounded (split1)
+        recon = hipe.W1p.float().sum(0)
+        if path == "split3":
+            assert torch.equal(recon, hipe.W1)
+        else:
+            assert torch.equal(recon, hipe.W1.to(torch.bfloat16).float())
 
 
-def test_predict_matches_cpu_oracle():
+@pytest.mark.parametrize("dt,path", CFGS)
+def test_dp_grads_then_sgd_matches_fused(dt, path):
+    """sgd=0 (gradient bucket) + the flat SGD kernel == the fused in-place update."""
+    a, _ = _engine_pair(dt, path=path)
+    b, _ = _engine_pair(dt, path=path)
+    a.run(0, 800, 1 / 800, 1e-4, 0.01, sgd=True)
+    b.run(0, 800, 1 / 800, 1e-4, 0.0, sgd=False)
+    b.sgd(0.01)
+    torch.cuda.synchronize()
+    assert _rel(a.params, b.params) < (1e-13 if dt == "f64" else 1e-6)
+    if a.W1p is not None:
+        assert torch.equal(a.W1p, b.W1p)
+
+
+@pytest.mark.parametrize("dt,path", CFGS)
+def test_predict_matches_cpu_oracle(dt, path):
     x, y = synthetic_mnist(3000, seed=5)
     nn = NeuralNetwork([784, 100, 10])
-    e = MlpEngine(nn.H, dtype="f64", max_cols=800, device="cuda")
+    e = MlpEngine(nn.H, dtype=dt, max_cols=800, device="cuda", path=path)
     e.set_params(*nn.params)
     pg = e.predict(x)
     pc = cpu_mlp.predict(nn, x)
-    assert (pg == pc).mean() > 0.999
+    assert (pg == pc).mean() > (0.999 if dt != "bf16" else 0.98)
 
 
 @pytest.mark.parametrize("dt", ["f64", "f32"])
@@ -156,6 +184,31 @@ def test_gpu_f64_matches_cpu_oracle_reference_threshold():
     t.load(x, y)
     t.train(1, 0.025, 1e-4)
     assert checkNNErrors(seq, par, "/tmp/cme_nnerrors.txt", verbose=False)
+
+
+def test_split3_gemm_accuracy_is_fp32_class():
+    """The exact 3-plane bf16 split must be as accurate as a plain fp32 GEMM (vs fp64)."""
+    x, y = synthetic_mnist(1600, seed=9)
+    nn = NeuralNetwork([784, 100, 10])
+    errs = {}
+    ref = None
+    for path in ("split3", "mfma"):
+        e = MlpEngine(nn.H, dtype="f32", max_cols=800, device="cuda", path=path)
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        e.run(0, 800, 1 / 800, 1e-4, 0.0, sgd=False)
+        torch.cuda.synchronize()
+        if ref is None:
+            t = MlpEngine(nn.H, dtype="f64", max_cols=800, device="cuda", path="mfma")
+            t.set_params(*nn.params)
+            t.load_dataset(x, y)
+            t.run(0, 800, 1 / 800, 1e-4, 0.0, sgd=False)
+            torch.cuda.synchronize()
+            ref = t
+        errs[path] = {k: _rel(getattr(e, k), getattr(ref, k)) for k in ("gW1", "gW2", "gb1", "gb2")}
+        errs[path]["a1"] = _rel(e.a1[:, :800], ref.a1[:, :800])
+    for k in errs["mfma"]:
+        assert errs["split3"][k] < max(4 * errs["mfma"][k], 1e-6), (k, errs)
 
 
 def test_gpu_f32_close_to_cpu_oracle():
