@@ -109,6 +109,7 @@ class MlpEngine:
         self.XT = None
         self.labels = None
         self._normalize = False
+        self.xscale = 1.0
         # keep a second, feature-major copy of the dataset ([P][N]) so the dW1 GEMM
         # reads its B operand K-contiguous (16-byte loads); +1x dataset bytes, which
         # is nothing next to 288 GB of HBM.
@@ -148,23 +149,34 @@ class MlpEngine:
         self._step = None
 
     def load_dataset(self, x, labels, normalize: bool = False):
-        """Upload the training set once (uint8 or float [N][P]) in the GEMM dtype."""
+        """Upload the training set once ([N][P] uint8 or float) and keep it resident.
+
+        Split paths keep the RAW uint8 pixels (1 byte/element; widened to bf16
+        exactly inside the GEMM kernels, normalisation folded into the epilogues
+        as ``xscale``), plus a feature-major uint8 copy for the dW1 GEMM.  The
+        mfma path stores the (optionally normalised) values in the GEMM dtype.
+        """
         x = torch.as_tensor(np.ascontiguousarray(x) if isinstance(x, np.ndarray) else x)
         if x.ndim != 2 or x.shape[1] != self.P:
             raise ValueError(f"expected [N][{self.P}] samples, got {tuple(x.shape)}")
         xd = x.to(self.device)
-        xd = xd.to(torch.float64 if self.dtype == "f64" else torch.float32)
         self._normalize = bool(normalize)
-        if normalize:
-            xd = xd / 255.0
-        if self.path == "split3":
-            # the exact-split identity needs inputs that are exact in ONE bf16
-            exact = bool((xd.to(torch.bfloat16).to(xd.dtype) == xd).all().item())
-            if not exact:
+        if self.np:
+            raw = xd.to(torch.float32)
+            exact = bool(((raw == raw.round()) & (raw >= 0) & (raw <= 255)).all().item())
+            if not exact:  # the split kernels need raw 0..255 pixels; fall back to the plain MFMA path
                 self.path = "mfma"
                 self._configure_path()
                 self._alloc_acts(self.ld)
-        self.X = xd.to(self.gdt).contiguous()
+        if self.np:
+            self.xscale = 1.0 / 255.0 if normalize else 1.0
+            self.X = raw.to(torch.uint8).contiguous()
+        else:
+            self.xscale = 1.0
+            xd = xd.to(torch.float64 if self.dtype == "f64" else torch.float32)
+            if normalize:
+                xd = xd / 255.0
+            self.X = xd.to(self.gdt).contiguous()
         self.XT = self.X.t().contiguous() if self.feature_major_copy else None
         self.labels = torch.as_tensor(np.asarray(labels, dtype=np.int32)).to(self.device).contiguous()
         self.num_samples = int(self.X.shape[0])
@@ -218,6 +230,7 @@ class MlpEngine:
             s.act = 1
             if self.np:
                 s.split = 1
+                s.xscale = float(self.xscale)
                 s.npw = s.npz = self.np
                 s.W1p = self.W1p.data_ptr()
                 s.dZ1p = self.dZ1p.data_ptr()
@@ -242,7 +255,7 @@ class MlpEngine:
     def _torch_step(self, off, n, scale, reg, lr, sgd, with_loss):
         """Same math as the HIP step in PyTorch ops (param dtype accumulation)."""
         with torch.no_grad():
-            Xb = self.X[off:off + n].to(self.pdt)
+            Xb = self.X[off:off + n].to(self.pdt) * self.xscale
             # the weights the kernels actually multiply: sum of the bf16 planes (== W1 for split3)
             W1g = self.W1p.to(self.pdt).sum(0) if self.np else self.W1g.to(self.pdt)
             z1 = Xb @ W1g.t() + self.b1
@@ -319,10 +332,16 @@ class MlpEngine:
             self._hip_step()
         for s in range(0, n, chunk):
             e = min(n, s + chunk)
-            xb = xt[s:e].to(self.device).to(torch.float64 if self.dtype == "f64" else torch.float32)
-            if getattr(self, "_normalize", False):
-                xb = xb / 255.0
-            xb = xb.to(self.gdt).contiguous()
+            if self.np:  # raw uint8 pixels, scaled inside the kernel
+                raw = xt[s:e].to(self.device).to(torch.float32)
+                if not bool(((raw == raw.round()) & (raw >= 0) & (raw <= 255)).all().item()):
+                    raise ValueError("split-path predict needs raw 0..255 pixel inputs")
+                xb = raw.to(torch.uint8).contiguous()
+            else:
+                xb = xt[s:e].to(self.device).to(torch.float64 if self.dtype == "f64" else torch.float32)
+                if self._normalize:
+                    xb = xb / 255.0
+                xb = xb.to(self.gdt).contiguous()
             if self.backend == "hip" and self.np:
                 self._hip_step().predict(xb.data_ptr(), e - s, a1.data_ptr(), a1.shape[1], out[s:e].data_ptr(),
                                          torch.cuda.current_stream(self.device).cuda_stream)
@@ -336,7 +355,8 @@ class MlpEngine:
                            self.b2.data_ptr(), H=self.H, C=self.C, n=e - s, pred=out[s:e].data_ptr(), stream=st)
             else:
                 with torch.no_grad():
-                    z1 = xb.to(self.pdt) @ self.W1g.to(self.pdt).t() + self.b1
+                    W1e = self.W1p.to(self.pdt).sum(0) if self.np else self.W1g.to(self.pdt)
+                    z1 = (xb.to(self.pdt) * self.xscale) @ W1e.t() + self.b1
                     z2 = torch.sigmoid(z1) @ self.W2.t() + self.b2
                     out[s:e] = z2.argmax(dim=1).to(torch.int32)
         return out.cpu().numpy()

@@ -42,14 +42,17 @@ struct MlpStep {
   int shift = 1, act = 1;
   // split-bf16 path (mlp_split.h): X/XT are bf16, W1p/dZ1p hold npw/npz bf16 planes
   int split = 0, npw = 3, npz = 3, fused_head = 0;
+  uintptr_t stamps = 0;  // diagnostics only
+  float xscale = 1.f;    // split path: inputs are uint8 * xscale
   uintptr_t W1p = 0, dZ1p = 0;
 
   cme::SplitStepArgs split_args(int64_t off, int n, double scale, double reg, double lr, int sgd,
                                 int with_loss) const {
     cme::SplitStepArgs a;
     a.P = P; a.H = H; a.C = C; a.n = n; a.ld = ld; a.npw = npw; a.npz = npz;
-    a.X = reinterpret_cast<const char*>(X) + (size_t)off * P * 2;
-    a.XT = reinterpret_cast<const char*>(XT) + (size_t)off * 2;
+    a.X = reinterpret_cast<const char*>(X) + (size_t)off * P;  // uint8 dataset
+    a.XT = reinterpret_cast<const char*>(XT) + (size_t)off;
+    a.xscale = xscale;
     a.ldxt = (int)N;
     a.labels = P_<int>(labels) + off;
     a.W1 = P_<float>(W1); a.b1 = P_<float>(b1); a.W2 = P_<float>(W2); a.b2 = P_<float>(b2);
@@ -59,6 +62,7 @@ struct MlpStep {
     a.dZ1p = reinterpret_cast<void*>(dZ1p);
     a.loss_partial = with_loss ? P_<float>(loss) : nullptr;
     a.scale = scale; a.reg = reg; a.lr = lr; a.sgd = sgd; a.shift = shift; a.mode = 0;
+    a.stamps = reinterpret_cast<unsigned long long*>(stamps);
     return a;
   }
 
@@ -239,6 +243,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("act", &MlpStep::act)
       .def_readwrite("split", &MlpStep::split)
       .def_readwrite("fused_head", &MlpStep::fused_head)
+      .def_readwrite("stamps", &MlpStep::stamps)
+      .def_readwrite("xscale", &MlpStep::xscale)
       .def_readwrite("npw", &MlpStep::npw)
       .def_readwrite("npz", &MlpStep::npz)
       .def_readwrite("W1p", &MlpStep::W1p)

@@ -35,9 +35,13 @@ struct EpiBiasAct {
   P* __restrict__ out;
   int ldo;
   int act;  // 0 none, 1 sigmoid, 2 relu
+  P pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int, bool ok) {
+    pre[q] = buf_load1<P>(make_rsrc(bias), ok ? row * (int)sizeof(P) : kOOB);
+  }
   template <typename A>
-  __device__ __forceinline__ void operator()(int row, int col, A v) {
-    P z = P(v) + bias[row];
+  __device__ __forceinline__ void operator()(int q, int row, int col, A v) {
+    P z = P(v) + pre[q];
     if (act == 1) z = sigmoid_<P>(z);
     else if (act == 2) z = z > P(0) ? z : P(0);
     out[(size_t)row * ldo + col] = z;
@@ -59,7 +63,7 @@ __global__ __launch_bounds__(kThreads) void fwd1_kernel(const T* __restrict__ W1
   __shared__ acc_t red[kKS * kFwdMB * kFwdNB * 4 * 64];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   TileGeom g{H, n, Pdim, (bid / tiles_n) * 16 * kFwdMB, (bid % tiles_n) * 16 * kFwdNB};
-  EpiBiasAct<P> epi{b1, a1, lda, act};
+  EpiBiasAct<P> epi{b1, a1, lda, act, {}};
   constexpr int U = unroll_for<T>();
   wsk_tile<T, kFwdMB, kFwdNB, kKS, true, true, VEC, U>(W1, Pdim, X, Pdim, g, epi, red);
 }
@@ -278,10 +282,14 @@ struct EpiWgrad {
   int ldw;
   P reg, lr;
   int sgd;
+  P pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
+    pre[q] = buf_load1<P>(make_rsrc(W), ok ? (row * ldw + col) * (int)sizeof(P) : kOOB);
+  }
   template <typename A>
-  __device__ __forceinline__ void operator()(int row, int col, A v) {
+  __device__ __forceinline__ void operator()(int q, int row, int col, A v) {
     const size_t i = (size_t)row * ldw + col;
-    const P w = W[i];
+    const P w = pre[q];
     const P gr = P(v) + reg * w;
     if (sgd) {
       const P nw = w - lr * gr;
@@ -311,7 +319,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradArgs a, int t1, in
     const int tb = xcd_remap(bid, t1);
     TileGeom g{a.H, a.P, a.n, (tb / t1n) * 16 * kW1MB, (tb % t1n) * 16 * kW1NB};
     EpiWgrad<P> epi{static_cast<P*>(a.W1), static_cast<P*>(a.gW1),
-                    static_cast<__hip_bfloat16*>(a.W1_bf16), a.P, reg, lr, a.sgd};
+                    static_cast<__hip_bfloat16*>(a.W1_bf16), a.P, reg, lr, a.sgd, {}};
     const T* A = static_cast<const T*>(a.dZ1g);
     constexpr int U = unroll_for<T>();
     if (a.XT) {  // B(k=b, n=p) = XT[p*ldxt + b]: K-contiguous, 16-byte loads
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradArgs a, int t1, in
     if (!(a.roles & 2)) return;
     const int tb = bid - t1;
     TileGeom g{a.C, a.H, a.n, (tb / t2n) * 16 * kW2MB, (tb % t2n) * 16 * kW2NB};
-    EpiWgrad<P> epi{static_cast<P*>(a.W2), static_cast<P*>(a.gW2), nullptr, a.H, reg, lr, a.sgd};
+    EpiWgrad<P> epi{static_cast<P*>(a.W2), static_cast<P*>(a.gW2), nullptr, a.H, reg, lr, a.sgd, {}};
     constexpr int U = unroll_for<P>();
     wsk_tile<P, kW2MB, kW2NB, kKS, true, true, false, U>(static_cast<const P*>(a.D), a.ldd,
                                                           static_cast<const P*>(a.a1), a.lda, g, epi,
@@ -420,11 +428,15 @@ struct EpiColMajor {
   T* __restrict__ C;
   int ldc;
   T alpha, beta;
+  T pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
+    pre[q] = buf_load1<T>(make_rsrc(C), (ok && beta != T(0)) ? (row + col * ldc) * (int)sizeof(T) : kOOB);
+  }
   template <typename A>
-  __device__ __forceinline__ void operator()(int row, int col, A v) {
+  __device__ __forceinline__ void operator()(int q, int row, int col, A v) {
     const size_t i = (size_t)row + (size_t)col * ldc;
     T r = alpha * T(v);
-    if (beta != T(0)) r += beta * C[i];
+    if (beta != T(0)) r += beta * pre[q];
     C[i] = r;
   }
 };
@@ -433,10 +445,15 @@ struct EpiColMajor<__hip_bfloat16> {
   __hip_bfloat16* __restrict__ C;
   int ldc;
   float alpha, beta;
-  __device__ __forceinline__ void operator()(int row, int col, float v) {
+  float pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
+    pre[q] = __bfloat162float(
+        buf_load1<__hip_bfloat16>(make_rsrc(C), (ok && beta != 0.f) ? (row + col * ldc) * 2 : kOOB));
+  }
+  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     const size_t i = (size_t)row + (size_t)col * ldc;
     float r = alpha * v;
-    if (beta != 0.f) r += beta * __bfloat162float(C[i]);
+    if (beta != 0.f) r += beta * pre[q];
     C[i] = __float2bfloat16(r);
   }
 };

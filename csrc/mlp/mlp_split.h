@@ -29,9 +29,10 @@ namespace cme {
 struct SplitStepArgs {
   int P = 784, H = 100, C = 10, n = 0, ld = 0;
   int npw = 3, npz = 3;          // planes of W1 and of dZ1 (3: exact fp32, 1: bf16)
-  const void* X = nullptr;       // bf16 shard [n][P]
-  const void* XT = nullptr;      // bf16 feature-major shard (XT + off) [P][ldxt]
+  const void* X = nullptr;       // uint8 shard [n][P] (raw pixels, exact in bf16)
+  const void* XT = nullptr;      // uint8 feature-major shard (XT + off) [P][ldxt]
   int ldxt = 0;
+  float xscale = 1.f;            // inputs are X * xscale (1/255 = normalised); applied in the epilogues
   const int* labels = nullptr;   // shard
   float *W1 = nullptr, *b1 = nullptr, *W2 = nullptr, *b2 = nullptr;  // fp32 master params
   void* W1p = nullptr;           // bf16 planes [npw][H][P]
@@ -45,6 +46,7 @@ struct SplitStepArgs {
   int* pred = nullptr;
   float* probs = nullptr;
   int ldp = 0;
+  unsigned long long* stamps = nullptr;  // diagnostics: per-wave s_memrealtime stamps (see mma_tile.h)
 };
 
 void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);

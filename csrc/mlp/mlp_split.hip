@@ -33,7 +33,7 @@ constexpr int kFHT = 64 * kFHKS;
 // ======================================================================
 // Kernel A: forward + head for 16 samples, all hidden units.
 // ======================================================================
-template <int NPW, int NPZ, int NC, bool VEC>
+template <int NPW, int NPZ, int NC, int VEC>
 __global__ __launch_bounds__(kFHT) void fwdhead_kernel(SplitStepArgs a) {
   __shared__ __attribute__((aligned(16))) float red[kFHKS * kFHMB * 4 * 64];  // 64 KB split-K partials
   __shared__ float a1s[kFHMB * 16][kFHCols + 1];  // a1 of the current H-chunk
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(kFHT) void fwdhead_kernel(SplitStepArgs a) {
   const int b0 = blockIdx.x * kFHCols;
   const bool single = H <= kFHMB * 16;
   const bf16* W1p = static_cast<const bf16*>(a.W1p);
-  const bf16* X = static_cast<const bf16*>(a.X);
+  const uint8_t* X = static_cast<const uint8_t*>(a.X);
 
   float zp[NC];
 #pragma unroll
@@ -61,16 +61,29 @@ __global__ __launch_bounds__(kFHT) void fwdhead_kernel(SplitStepArgs a) {
       w2s[h][c] = c < C ? a.W2[c * H + m0 + h] : 0.f;
     }
     // (w2s is first read in the epilogue, after wsk_tile's internal barrier)
-    auto epi = [&](int row, int gcol, float v) {  // gcol = global sample index (< n)
-      const float s = sigm(v + a.b1[m0 + row]);
-      a1s[row][gcol - b0] = s;
-      a.a1[(size_t)(m0 + row) * ld + gcol] = s;
+    struct EpiFH {
+      const float* b1;
+      float* a1g;
+      float (*a1s)[kFHCols + 1];
+      float (*w2s)[NC];
+      float* zp;
+      int ld, b0;
+      float xscale;
+      float pre[kEpiMaxQ];
+      __device__ __forceinline__ void prefetch(int q, int row, int, bool ok) {
+        pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
+      }
+      __device__ __forceinline__ void operator()(int q, int row, int gcol, float v) {  // gcol: sample < n
+        const float s = sigm(v * xscale + pre[q]);
+        a1s[row][gcol - b0] = s;
+        a1g[(size_t)row * ld + gcol] = s;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) zp[c] += w2s[row][c] * s;
-    };
+        for (int c = 0; c < NC; ++c) zp[c] += w2s[row][c] * s;
+      }
+    } epi{a.b1 + m0, a.a1 + (size_t)m0 * ld, a1s, w2s, zp, ld, b0, a.xscale, {}};
     TileGeom g{M, a.n, P, 0, b0};
     constexpr int U = NPW == 3 ? 1 : 2;  // keep one burst of loads <= ~100 VGPRs
-    wsk_tile<bf16, kFHMB, 1, kFHKS, true, true, VEC, U, NPW>(W1p + (size_t)m0 * P, P, X, P, g, epi, red,
+    wsk_tile<bf16, kFHMB, 1, kFHKS, true, true, VEC, U, NPW, uint8_t>(W1p + (size_t)m0 * P, P, X, P, g, epi, red,
                                                              H * P * (int)sizeof(bf16));
   }
   // ---- z2 = W2 a1 + b2 for the 16 columns: reduce the per-thread partials
@@ -193,21 +206,26 @@ struct EpiSig {
   const float* b1;
   float* a1;
   int ld;
-  __device__ __forceinline__ void operator()(int row, int col, float v) {
-    a1[(size_t)row * ld + col] = sigm(v + b1[row]);
+  float xscale;
+  float pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int, bool ok) {
+    pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
+  }
+  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
+    a1[(size_t)row * ld + col] = sigm(v * xscale + pre[q]);
   }
 };
 
-template <int NPW, bool VEC>
+template <int NPW, int VEC>
 __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a, int tiles_n) {
   __shared__ __attribute__((aligned(16))) float red[kF1KS * kF1MB * kF1NB * 4 * 64];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   TileGeom g{a.H, a.n, a.P, (bid / tiles_n) * 16 * kF1MB, (bid % tiles_n) * 16 * kF1NB};
-  EpiSig epi{a.b1, a.a1, a.ld};
+  EpiSig epi{a.b1, a.a1, a.ld, a.xscale, {}};
   constexpr int U = 4;
-  wsk_tile<bf16, kF1MB, kF1NB, kF1KS, true, true, VEC, U, NPW>(static_cast<const bf16*>(a.W1p), a.P,
-                                                               static_cast<const bf16*>(a.X), a.P, g, epi, red,
-                                                               a.H * a.P * (int)sizeof(bf16));
+  wsk_tile<bf16, kF1MB, kF1NB, kF1KS, true, true, VEC, U, NPW, uint8_t>(static_cast<const bf16*>(a.W1p), a.P,
+                                                               static_cast<const uint8_t*>(a.X), a.P, g, epi, red,
+                                                               a.H * a.P * (int)sizeof(bf16), a.stamps);
 }
 
 // ======================================================================
@@ -222,11 +240,15 @@ struct EpiW1 {
   bf16* W1p;
   size_t plane;  // H*P
   int P, sgd, npw;
-  float reg, lr;
-  __device__ __forceinline__ void operator()(int row, int col, float v) {
+  float reg, lr, xscale;
+  float pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
+    pre[q] = buf_load1<float>(make_rsrc(W1), ok ? (row * P + col) * 4 : kOOB);
+  }
+  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     const size_t i = (size_t)row * P + col;
-    const float w = W1[i];
-    const float g = v + reg * w;
+    const float w = pre[q];
+    const float g = v * xscale + reg * w;
     if (sgd) {
       const float nw = w - lr * g;
       W1[i] = nw;
@@ -238,7 +260,7 @@ struct EpiW1 {
   }
 };
 
-template <int NPZ, bool VEC>
+template <int NPZ, int VEC>
 __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
   const int bid = blockIdx.x;
@@ -246,11 +268,11 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   if (bid < t1) {  // ---- dW1 tile
     const int tb = xcd_remap(bid, t1);
     TileGeom g{a.H, a.P, a.n, (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
-    EpiW1 epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw, reg, lr};
+    EpiW1 epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw, reg, lr, a.xscale, {}};
     constexpr int U = 4;
-    wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ>(static_cast<const bf16*>(a.dZ1p), a.ld,
-                                                              static_cast<const bf16*>(a.XT), a.ldxt, g, epi,
-                                                              red, a.H * a.ld * (int)sizeof(bf16));
+    wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
+                                                              static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
+                                                              red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
     return;
   }
   const int lane = threadIdx.x & 63;
@@ -260,6 +282,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     if (h >= a.H) return;
     const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.a1 + (size_t)h * a.ld);
     const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.D);
+    const float wpre = buf_load1<float>(make_rsrc(a.W2), lane < a.C ? (lane * a.H + h) * 4 : kOOB);
     float acc[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) acc[c] = 0.f;
@@ -286,7 +309,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
 #pragma unroll
       for (int c = 0; c < 16; ++c) v = c == lane ? acc[c] : v;
       const size_t i = (size_t)lane * a.H + h;
-      const float w = a.W2[i];
+      const float w = wpre;
       const float g = v + reg * w;
       if (a.sgd) a.W2[i] = w - lr * g;
       else a.gW2[i] = g;
@@ -299,6 +322,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   const bool first = row < a.H;
   const float* src = first ? a.dZ1 + (size_t)row * a.ld : a.D + (size_t)(row - a.H) * a.ld;
   const __amdgpu_buffer_rsrc_t rs = make_rsrc(src);
+  const float bpre = buf_load1<float>(make_rsrc(first ? a.b1 : a.b2), (first ? row : row - a.H) * 4);
   float s = 0.f;
   for (int j0 = 0; j0 < a.n; j0 += 64 * 16) {
     float v[16];
@@ -314,7 +338,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   if (lane == 0) {
     float* bp = first ? a.b1 : a.b2;
     const int r = first ? row : row - a.H;
-    if (a.sgd) bp[r] -= lr * s;
+    if (a.sgd) bp[r] = bpre - lr * s;
     else (first ? a.gb1 : a.gb2)[r] = s;
   }
 }
@@ -340,13 +364,14 @@ __global__ __launch_bounds__(256) void sgd_planes_kernel(float* __restrict__ prm
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+inline bool al4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
 
 template <int NPW, int NPZ, int NC>
 void launch_fwdhead(const SplitStepArgs& a, hipStream_t s) {
-  const bool vec = al16(a.X) && al16(a.W1p) && a.P % 8 == 0;
+  const bool vec = al4(a.X) && al16(a.W1p) && a.P % 8 == 0;
   const dim3 grid(cdiv(a.n, kFHCols));
-  if (vec) fwdhead_kernel<NPW, NPZ, NC, true><<<grid, kFHT, 0, s>>>(a);
-  else fwdhead_kernel<NPW, NPZ, NC, false><<<grid, kFHT, 0, s>>>(a);
+  if (vec) fwdhead_kernel<NPW, NPZ, NC, 1><<<grid, kFHT, 0, s>>>(a);
+  else fwdhead_kernel<NPW, NPZ, NC, 0><<<grid, kFHT, 0, s>>>(a);
 }
 
 template <int NPW, int NPZ>
@@ -363,12 +388,13 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
   CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
               "split path: operand too large for 32-bit buffer offsets");
+  CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
   const int tn = cdiv(a.n, 16 * kF1NB), tm = cdiv(a.H, 16 * kF1MB);
-  const bool vec = al16(a.X) && al16(a.W1p) && a.P % 8 == 0;
+  const bool vec = al4(a.X) && al16(a.W1p) && a.P % 8 == 0;
   const dim3 grid(tm * tn);
 #define CME_F1(np)                                                                         \
-  if (vec) fwd1_split_kernel<np, true><<<grid, 64 * kF1KS, 0, s>>>(a, tn);                \
-  else fwd1_split_kernel<np, false><<<grid, 64 * kF1KS, 0, s>>>(a, tn);
+  if (vec) fwd1_split_kernel<np, 1><<<grid, 64 * kF1KS, 0, s>>>(a, tn);                   \
+  else fwd1_split_kernel<np, 0><<<grid, 64 * kF1KS, 0, s>>>(a, tn);
   if (a.npw == 3) { CME_F1(3) } else { CME_F1(1) }
 #undef CME_F1
   CME_LAUNCH_CHECK(s);
@@ -389,16 +415,19 @@ void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s) {
 
 void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
-  CME_REQUIRE((int64_t)a.H * a.ld * 2 * a.npz < (int64_t)kOOB && (int64_t)a.P * a.ldxt * 2 < (int64_t)kOOB,
+  CME_REQUIRE((int64_t)a.H * a.ld * 2 * a.npz < (int64_t)kOOB && (int64_t)a.P * a.ldxt < (int64_t)kOOB,
               "split path: operand too large for 32-bit buffer offsets");
   const int t1n = cdiv(a.P, 16 * kWNB), t1 = cdiv(a.H, 16 * kWMB) * t1n;
   const int t2 = cdiv(a.H, kWKS);
   const int tb = cdiv(a.H + a.C, kWKS);
-  const bool vec = al16(a.dZ1p) && al16(a.XT) && a.ld % 8 == 0 && a.ldxt % 8 == 0 && a.n % 8 == 0;
+  // dZ1 planes: 16-byte vectors when n % 8 == 0, 8-byte halves when n % 4 == 0; XT bytes need 4-byte rows
+  const bool base_ok = al16(a.dZ1p) && al4(a.XT) && a.ld % 8 == 0 && a.ldxt % 4 == 0;
+  const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? 1 : (a.n % 4 == 0 ? 2 : 0));
   const dim3 grid(t1 + t2 + tb);
 #define CME_WG(npz)                                                                               \
-  if (vec) wgrad_split_kernel<npz, true><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);                    \
-  else wgrad_split_kernel<npz, false><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);
+  if (vec == 1) wgrad_split_kernel<npz, 1><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);                  \
+  else if (vec == 2) wgrad_split_kernel<npz, 2><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);             \
+  else wgrad_split_kernel<npz, 0><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);
   if (a.npz == 3) { CME_WG(3) } else { CME_WG(1) }
 #undef CME_WG
   CME_LAUNCH_CHECK(s);

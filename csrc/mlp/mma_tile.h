@@ -26,6 +26,8 @@
 
 #include "../common/hip_common.h"
 
+#include <type_traits>
+
 namespace cme {
 
 template <typename T>
@@ -117,11 +119,14 @@ __device__ __forceinline__ __hip_bfloat16 buf_load1<__hip_bfloat16>(__amdgpu_buf
 // contiguous (KCONTIG: X[r*ld + k]) or r contiguous (X[k*ld + r]).
 // VEC: 16-byte vector loads; the caller guarantees 16-byte alignment of every
 // full vector and that kend is a multiple of V (a vector is fully in or out).
-template <typename T, int V, bool KCONTIG, bool VEC>
+template <typename T, int V, bool KCONTIG, int VEC>
 __device__ __forceinline__ void load_frag(__amdgpu_buffer_rsrc_t rs, int ld, int r, int rmax, int k, int kend,
                                           T (&out)[V], int base_off = 0) {
+  // VEC == 1: 16-byte loads, every vector fully in or out (kend % V == 0)
+  // VEC == 2: two 8-byte halves with separate range checks (kend % (V/2) == 0)
+  // VEC == 0: element loads
   const bool rok = r < rmax;
-  if constexpr (KCONTIG && VEC) {
+  if constexpr (KCONTIG && VEC == 1) {
     static_assert((V * sizeof(T)) % 16 == 0, "vector fragment must be a multiple of 16 B");
     const int off = (rok && k < kend) ? (r * ld + k) * (int)sizeof(T) + base_off : kOOB;
 #pragma unroll
@@ -129,6 +134,16 @@ __device__ __forceinline__ void load_frag(__amdgpu_buffer_rsrc_t rs, int ld, int
       const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 16 * q, 0);
       __builtin_memcpy(reinterpret_cast<char*>(out) + 16 * q, &w, 16);
     }
+  } else if constexpr (KCONTIG && VEC == 2) {
+    constexpr int HV = V / 2;  // elements per 8-byte half
+    static_assert(HV * sizeof(T) == 8, "half-vector path expects 8-byte halves");
+    const int base = (r * ld + k) * (int)sizeof(T) + base_off;
+    const int o0 = (rok && k + HV <= kend) ? base : kOOB;
+    const int o1 = (rok && k + V <= kend) ? base + 8 : kOOB;
+    const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(rs, o0, 0, 0);
+    const auto w1 = __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, 0);
+    __builtin_memcpy(reinterpret_cast<char*>(out), &w0, 8);
+    __builtin_memcpy(reinterpret_cast<char*>(out) + 8, &w1, 8);
   } else {
 #pragma unroll
     for (int j = 0; j < V; ++j) {
@@ -138,6 +153,51 @@ __device__ __forceinline__ void load_frag(__amdgpu_buffer_rsrc_t rs, int ld, int
     }
   }
 }
+
+// B operand stored as uint8 (raw MNIST pixels, exact in bf16): 8 bytes per lane
+// (two 4-byte buffer loads, OOB -> 0) widened to 8 bf16 in registers.  Halves
+// the operand bytes of a bf16 copy; the per-CU L2->L1 fill rate (~70 GB/s) is
+// what bounds these small GEMMs.  VEC: 4-byte aligned rows, kend % 8 == 0.
+__device__ __forceinline__ unsigned int u8x2_to_bf16x2(unsigned int w, int hi) {
+  // bytes (2*hi, 2*hi+1) of w -> two bf16 (upper halves of the exact floats)
+  const float f0 = (float)((w >> (16 * hi)) & 0xffu);
+  const float f1 = (float)((w >> (16 * hi + 8)) & 0xffu);
+  return (__builtin_bit_cast(unsigned int, f0) >> 16) | (__builtin_bit_cast(unsigned int, f1) & 0xffff0000u);
+}
+
+template <int VEC>
+__device__ __forceinline__ void load_frag_u8(__amdgpu_buffer_rsrc_t rs, int ld, int r, int rmax, int k, int kend,
+                                             __hip_bfloat16 (&out)[8]) {
+  // VEC != 0: two 4-byte loads, each range-checked on its own (kend % 4 == 0, rows 4-byte aligned)
+  const bool rok = r < rmax;
+  unsigned int w[4];
+  if constexpr (VEC != 0) {
+    const int base = r * ld + k;
+    const unsigned int lo = __builtin_amdgcn_raw_buffer_load_b32(rs, (rok && k + 4 <= kend) ? base : kOOB, 0, 0);
+    const unsigned int hi = __builtin_amdgcn_raw_buffer_load_b32(rs, (rok && k + 8 <= kend) ? base + 4 : kOOB, 0, 0);
+    w[0] = u8x2_to_bf16x2(lo, 0);
+    w[1] = u8x2_to_bf16x2(lo, 1);
+    w[2] = u8x2_to_bf16x2(hi, 0);
+    w[3] = u8x2_to_bf16x2(hi, 1);
+  } else {
+    unsigned int b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      b[j] = __builtin_amdgcn_raw_buffer_load_b8(rs, (rok && k + j < kend) ? r * ld + k + j : kOOB, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = u8x2_to_bf16x2(b[2 * q] | (b[2 * q + 1] << 8), 0);
+  }
+  __builtin_memcpy(out, w, 16);
+}
+
+constexpr int kEpiMaxQ = 16;  // max output elements per thread in a tile epilogue
+
+// Epilogue protocol used by wsk_tile:
+//   epi.prefetch(q, row, col, valid)  -- before the K loop (issue independent loads)
+//   epi(q, row, col, value)           -- once per in-bounds output element
+struct EpiNoPrefetch {
+  __device__ __forceinline__ void prefetch(int, int, int, bool) {}
+};
 
 struct TileGeom {
   int M, N, K;
@@ -152,10 +212,18 @@ struct TileGeom {
 // NPA > 1: A is the exact sum of NPA planes stored `plane_bytes` apart
 // (A = A_0 + A_1 + ...; the split-bf16 representation of an fp32 operand,
 // see mlp_split.hip) and every plane is multiplied into the same accumulator.
-template <typename T, int MB, int NB, int KS, bool AK, bool BK, bool VEC, int U, int NPA = 1, class Epi>
-__device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const T* __restrict__ B, int ldb,
+//
+// stamps != nullptr (diagnostic builds only): lane 0 of every wave records
+// s_memrealtime (100 MHz wall clock) at entry, after the K loop, after the
+// reduction barrier and at the end: stamps[(block*KS + wave)*4 + i].
+//
+// TB = uint8_t (with T = bf16): the B operand is raw bytes, widened in registers.
+template <typename T, int MB, int NB, int KS, bool AK, bool BK, int VEC, int U, int NPA = 1, typename TB = T,
+          class Epi>
+__device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const TB* __restrict__ B, int ldb,
                                          TileGeom g, Epi& epi,
-                                         typename MmaTraits<T>::acc_t* __restrict__ red, int plane_bytes = 0) {
+                                         typename MmaTraits<T>::acc_t* __restrict__ red, int plane_bytes = 0,
+                                         unsigned long long* stamps = nullptr) {
   using Tr = MmaTraits<T>;
   using accv_t = typename Tr::accv_t;
   using acc_t = typename Tr::acc_t;
@@ -165,11 +233,49 @@ __device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const
   const int wave = threadIdx.x >> 6;
   const int c = lane & 15, grp = lane >> 4;
 
+  unsigned long long* st = stamps ? stamps + ((size_t)blockIdx.x * KS + wave) * 4 : nullptr;
+  auto stamp = [&](int i) {
+    if (st) {
+      const unsigned long long tt = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) st[i] = tt;
+    }
+  };
+  stamp(0);
   accv_t acc[MB][NB];
 #pragma unroll
   for (int i = 0; i < MB; ++i)
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = accv_t{0, 0, 0, 0};
+
+  // Output elements owned by this thread in the epilogue: q = 0..NQ-1.
+  constexpr int E = MB * NB * 4 * 64;  // accumulators per wave
+  constexpr int NQ = KS == 1 ? MB * NB * 4 : (E + 64 * KS - 1) / (64 * KS);
+  static_assert(NQ <= kEpiMaxQ, "epilogue prefetch slots exceeded");
+  auto coord = [&](int q, int& row, int& col, int& e) -> bool {
+    if constexpr (KS == 1) {
+      const int i = q / (NB * 4), j = (q / 4) % NB, r = q % 4;
+      row = g.m0 + 16 * i + Tr::row(grp, r);
+      col = g.n0 + 16 * j + c;
+      e = 0;
+    } else {
+      e = threadIdx.x + q * 64 * KS;
+      const int ln = e & 63, r = (e >> 6) & 3, blk = e >> 8;
+      const int i = blk / NB, j = blk % NB;
+      row = g.m0 + 16 * i + Tr::row(ln >> 4, r);
+      col = g.n0 + 16 * j + (ln & 15);
+      if (e >= E) return false;
+    }
+    return row < g.M && col < g.N;
+  };
+  // Epilogue operands that do not depend on the GEMM (bias, the weight being
+  // updated, ...) are fetched now, so their latency hides under the K loop
+  // instead of adding a dependent round trip after the reduction.
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    int row, col, e;
+    const bool ok = coord(q, row, col, e);
+    epi.prefetch(q, row, col, ok);
+  }
 
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A), rsB = make_rsrc(B);
   const int nch = (g.K + KC - 1) / KC;
@@ -189,8 +295,14 @@ __device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const
         for (int i = 0; i < MB; ++i)
           load_frag<T, V, AK, VEC>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, af[u][p][i], p * plane_bytes);
 #pragma unroll
-      for (int j = 0; j < NB; ++j)
-        load_frag<T, V, BK, VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, bf[u][j]);
+      for (int j = 0; j < NB; ++j) {
+        if constexpr (std::is_same_v<TB, uint8_t>) {
+          static_assert(std::is_same_v<T, __hip_bfloat16> && BK, "u8 B operand: bf16 MFMA, K-contiguous");
+          load_frag_u8<VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, bf[u][j]);
+        } else {
+          load_frag<T, V, BK, VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, bf[u][j]);
+        }
+      }
     }
     // Keep every load of this burst ahead of the first MFMA: without the fence
     // the scheduler sinks each load next to its consumer to save VGPRs, which
@@ -207,19 +319,24 @@ __device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const
           for (int j = 0; j < NB; ++j) Tr::mma(af[u][p][i], bf[u][j], acc[i][j]);
   }
 
-  if constexpr (KS == 1) {
+  if (st) {  // make the K-loop stamp wait for the MFMA results
+    float sink = 0.f;
 #pragma unroll
     for (int i = 0; i < MB; ++i)
 #pragma unroll
-      for (int j = 0; j < NB; ++j)
+      for (int j = 0; j < NB; ++j) sink += (float)acc[i][j][0];
+    asm volatile("" ::"v"(sink));
+  }
+  stamp(1);
+  if constexpr (KS == 1) {
+    stamp(2);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = g.m0 + 16 * i + Tr::row(grp, r);
-          const int col = g.n0 + 16 * j + c;
-          if (row < g.M && col < g.N) epi(row, col, acc[i][j][r]);
-        }
+    for (int q = 0; q < NQ; ++q) {
+      int row, col, e;
+      if (coord(q, row, col, e)) epi(q, row, col, acc[q / (NB * 4)][(q / 4) % NB][q % 4]);
+    }
+    stamp(3);
   } else {
-    constexpr int E = MB * NB * 4 * 64;  // accumulators per wave
 #pragma unroll
     for (int i = 0; i < MB; ++i)
 #pragma unroll
@@ -227,16 +344,20 @@ __device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[wave * E + (((i * NB + j) * 4 + r) << 6) + lane] = acc[i][j][r];
     __syncthreads();
-    for (int e = threadIdx.x; e < E; e += 64 * KS) {
-      acc_t s = red[e];
+    stamp(2);
 #pragma unroll
-      for (int w = 1; w < KS; ++w) s += red[w * E + e];
-      const int ln = e & 63, r = (e >> 6) & 3, blk = e >> 8;
-      const int i = blk / NB, j = blk % NB;
-      const int row = g.m0 + 16 * i + Tr::row(ln >> 4, r);
-      const int col = g.n0 + 16 * j + (ln & 15);
-      if (row < g.M && col < g.N) epi(row, col, s);
+    for (int q = 0; q < NQ; ++q) {
+      int row, col, e;
+      const bool ok = coord(q, row, col, e);
+      if (e < E) {
+        acc_t s = red[e];
+#pragma unroll
+        for (int w = 1; w < KS; ++w) s += red[w * E + e];
+        if (ok) epi(q, row, col, s);
+      }
     }
+    if (st) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(3);
     __syncthreads();  // `red` may be reused by the caller
   }
 }

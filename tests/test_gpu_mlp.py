@@ -83,14 +83,14 @@ TOL = {("f64", "mfma"): 1e-11, ("f32", "split3"): 2e-4, ("f32", "mfma"): 2e-4, (
        ("bf16", "mfma"): 3e-2}
 
 
-def _engine_pair(dt, H=100, n=800, N=1600, path="auto"):
+def _engine_pair(dt, H=100, n=800, N=1600, path="auto", normalize=False):
     x, y = synthetic_mnist(N, seed=3)
     nn = NeuralNetwork([784, H, 10])
     engines = []
     for backend in ("hip", "torch"):
         e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", backend=backend, path=path)
         e.set_params(*nn.params)
-        e.load_dataset(x, y)
+        e.load_dataset(x, y, normalize=normalize)
         engines.append(e)
     return engines
 
@@ -113,6 +113,18 @@ def test_step_gradients_match_torch(dt, path, n, H):
         a = getattr(hipe, name)[:, :n]
         b = getattr(te, name)[:, :n]
         assert _rel(a, b) < max(tol, 1e-5), name
+
+
+@pytest.mark.parametrize("dt,path", [("f32", "split3"), ("bf16", "split1"), ("f32", "mfma")])
+def test_normalized_inputs_match_torch(dt, path):
+    """normalize=True: split paths keep raw uint8 pixels and fold 1/255 into the epilogues."""
+    hipe, te = _engine_pair(dt, path=path, normalize=True)
+    assert hipe.path == path
+    for e in (hipe, te):
+        e.run(0, 800, 1 / 800, 1e-4, 0.0, sgd=False)
+    torch.cuda.synchronize()
+    for name in ("gW1", "gb1", "gW2", "gb2"):
+        assert _rel(getattr(hipe, name), getattr(te, name)) < TOL[(dt, path)], name
 
 
 @pytest.mark.parametrize("dt,path", CFGS)
