@@ -8,15 +8,17 @@ synchronize on both sides; the max time over ranks is reported; rank 0 prints
 one JSON line.
 
 What a step is (the reference's ``parallel_train`` inner loop,
-fpcode/neural_network.cpp:449-555): one synchronous SGD update on a global
-batch of 800 synthetic MNIST-shaped images (random-init 784-100-10 weights,
-seeded as the reference does), split across the N ranks
-(``n = 800 / N`` columns each, strong scaling like the reference), forward +
-backward on every rank, gradient all-reduce over RCCL, SGD update.  Nothing
-is skipped inside the timed region.  Steps cycle over the 67 full batches of
-the 54,000-image training split; steps are replayed from a captured HIP graph.
+fpcode/neural_network.cpp:449-555): one synchronous SGD update -- forward +
+backward of the 784-100-10 MLP (random-init weights, seeded as the reference
+does) on every rank, gradient all-reduce over RCCL, SGD update -- on
+synthetic MNIST-shaped images resident on every GPU.  Nothing is skipped
+inside the timed region.  Steps cycle over the full batches of the 54,000-image
+training split and are replayed from a captured HIP graph.
 
-``--scaling weak`` keeps 800 images per GPU instead (global batch 800*N).
+Scaling (default ``weak``): every GPU processes 800 images per step, so the
+global batch is 800*N (N=8 -> 6400, the BASELINE's 8-GPU batch); at N=1 this
+is exactly batch=800.  ``--scaling strong`` instead splits a global batch of
+800 across the N ranks (n = 800/N each), the reference's ``-b 800`` semantics.
 """
 from __future__ import annotations
 
@@ -38,7 +40,7 @@ def parse(argv=None):
     ap.add_argument("--hidden", type=int, default=100)
     ap.add_argument("--batch", type=int, default=800, help="global batch (strong) or per-GPU batch (weak)")
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
-    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"])
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--train-size", type=int, default=54000)
@@ -83,8 +85,13 @@ def main(argv=None) -> int:
 
     warm_plans, timed_plans = plans_for(a.warmup), plans_for(a.steps)
     if tr.use_graphs:  # capture outside the timed region (graphs are cached by plan)
-        for p in {tuple(p.steps): p for p in warm_plans + timed_plans}.values():
-            tr.capture(p, lr, reg)
+        try:
+            for p in {tuple(p.steps): p for p in warm_plans + timed_plans}.values():
+                tr.capture(p, lr, reg)
+        except Exception as ex:  # pragma: no cover - depends on the collective backend
+            print(f"warning: HIP graph capture failed ({ex!r}); running eager steps", file=sys.stderr)
+            tr.use_graphs = False
+            tr._graphs.clear()
     for p in warm_plans:
         tr.run_plan(p, lr, reg)
     torch.cuda.synchronize(device)

@@ -93,7 +93,7 @@ class DataParallelTrainer:
             e.sgd(lr)
             return
         scale = 1.0 / (n * self.R)
-        if self.R == 1:
+        if isinstance(self.comm, NullComm):  # single process: SGD fused into the weight-gradient kernel
             e.run(off, n, scale, reg, lr, sgd=True, with_loss=with_loss)
         else:
             e.run(off, n, scale, reg / self.R, lr, sgd=False, with_loss=with_loss)

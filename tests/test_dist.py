@@ -1,0 +1,104 @@
+"""Data-parallel semantics without a cluster: gloo multi-process (world_size 2)
+and the in-process LoopbackComm, both against the single-process result."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from cme213_sp18_amd import NeuralNetwork
+from cme213_sp18_amd.parallel import DataParallelTrainer, LoopbackComm, MlpEngine
+from cme213_sp18_amd.parallel.launcher import spawn
+from cme213_sp18_amd.utils.data import synthetic_mnist
+
+from .dist_workers import allreduce_worker, dp_train_worker
+
+
+def _single(H, N, batch, epochs, lr, reg, dtype="f64"):
+    x, y = synthetic_mnist(N, seed=11)
+    nn = NeuralNetwork([784, H, 10])
+    tr = DataParallelTrainer(nn, device="cpu", dtype=dtype, batch_size=batch, backend="torch", use_graphs=False)
+    tr.load(x, y)
+    st = tr.train(epochs, lr, reg, print_every=2, log=lambda *_: None)
+    return nn, st
+
+
+def test_gloo_allreduce_broadcast(tmp_path):
+    spawn(allreduce_worker, 2, args=(str(tmp_path),), backend="gloo")
+    for r in range(2):
+        v = np.load(tmp_path / f"ar{r}.npy")
+        np.testing.assert_array_equal(v[:5], 3.0)
+        assert v[5] == 10.0
+        np.testing.assert_array_equal(v[6:], 1.0)
+
+
+def test_gloo_dp_equals_single_process(tmp_path):
+    """R=2 ranks, global batch 800 (400 columns each), pre-scaled SUM all-reduce
+    == single-process training on the same global batches (checkNNErrors-grade)."""
+    H, N, B, E, lr, reg = 24, 2400, 800, 2, 0.05, 1e-4
+    spawn(dp_train_worker, 2, args=(str(tmp_path), H, N, B, E, lr, reg, "f64"), backend="gloo")
+    ref, st = _single(H, N, B, E, lr, reg)
+    r0 = np.load(tmp_path / "rank0.npz")
+    r1 = np.load(tmp_path / "rank1.npz")
+    for k, i in (("W0", 0), ("W1", 1)):
+        np.testing.assert_array_equal(r0[k], r1[k])  # replicas stay bit-identical
+        assert np.abs(r0[k] - ref.W[i]).max() / np.abs(ref.W[i]).max() < 1e-12
+    for k, i in (("b0", 0), ("b1", 1)):
+        assert np.abs(r0[k] - ref.b[i]).max() <= 1e-12 * max(1.0, np.abs(ref.b[i]).max())
+    np.testing.assert_allclose(r0["losses"], st.losses, rtol=1e-6)  # loss is computed globally
+    assert int(r0["images"]) == st.images
+
+
+def _loopback_run(world, H, N, B, E, lr, reg):
+    comms = LoopbackComm.create(world)
+    x, y = synthetic_mnist(N, seed=11)
+    results = [None] * world
+
+    def work(r):
+        torch.set_num_threads(1)
+        nn = NeuralNetwork([784, H, 10])
+        tr = DataParallelTrainer(nn, comm=comms[r], device="cpu", dtype="f64", batch_size=B, backend="torch",
+                                 use_graphs=False)
+        tr.load(x, y)
+        tr.train(E, lr, reg)
+        results[r] = nn
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return results
+
+
+def test_loopback_world4_matches_single():
+    H, N, B, E, lr, reg = 16, 1600, 800, 1, 0.05, 1e-4
+    res = _loopback_run(4, H, N, B, E, lr, reg)
+    ref, _ = _single(H, N, B, E, lr, reg)
+    for nn in res:
+        assert np.abs(nn.W[0] - ref.W[0]).max() / np.abs(ref.W[0]).max() < 1e-12
+
+
+def test_remainder_columns_are_dropped_like_reference():
+    """B=801, R=2: n = floor(801/2) = 400 per rank; column 800 of each batch is
+    dropped and D is scaled by 1/(n*R) = 1/800 (fpcode/neural_network.cpp:458,330)."""
+    H, N, B, lr, reg = 12, 1602, 801, 0.05, 1e-4
+    res = _loopback_run(2, H, N, B, 1, lr, reg)
+    x, y = synthetic_mnist(N, seed=11)
+    nn = NeuralNetwork([784, H, 10])
+    e = MlpEngine(nn.H, dtype="f64", max_cols=800, device="cpu", backend="torch")
+    e.set_params(*nn.params)
+    e.load_dataset(x, y)
+    for start in (0, 801):  # ceil(1602/801) = 2 batches
+        e.run(start, 800, 1.0 / 800, reg, lr, sgd=True)
+    W1 = e.get_params()[0]
+    assert np.abs(res[0].W[0] - W1).max() / np.abs(W1).max() < 1e-12
+
+
+def test_shard_math():
+    nn = NeuralNetwork([784, 8, 10])
+    comms = LoopbackComm.create(3)
+    trs = [DataParallelTrainer(nn, comm=c, device="cpu", dtype="f64", backend="torch", use_graphs=False)
+           for c in comms]
+    assert [t.shard(800, 800) for t in trs] == [(800, 266), (1066, 266), (1332, 266)]
+    assert [t.shard(0, 2) for t in trs] == [(0, 0), (0, 0), (0, 0)]
