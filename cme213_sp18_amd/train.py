@@ -1,0 +1,122 @@
+"""CLI driver -- the reference's ``main()`` (fpcode/main.cpp:34-276).
+
+    python -m cme213_sp18_amd.train -g 1                      # grade preset 1 (fp64 parity)
+    python -m cme213_sp18_amd.train -n 100 -e 5 -p 10         # f32 split-bf16 engine, print loss
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        -m cme213_sp18_amd.train --preset 8gpu_wide           # one rank per GPU, RCCL
+
+Flow: bootstrap (one process per GPU, device = LOCAL_RANK) -> data (identical on
+every rank, uploaded once per GPU) -> optional sequential fp64 CPU training on
+rank 0 (-s) -> data-parallel GPU training -> rank 0 evaluates on the dev split,
+writes test-set predictions, and with -g/-d compares against the CPU run.
+Grade 4 runs the GEMM benchmark instead.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+from .config import TrainConfig, parse_config
+
+
+def log0(rank: int, *a):
+    if rank == 0:
+        print(*a, flush=True)
+
+
+def run(cfg: TrainConfig) -> dict:
+    import torch
+
+    from .models import mlp
+    from .models.mlp import NeuralNetwork
+    from .parallel.launcher import init_distributed, shutdown
+    from .parallel.trainer import DataParallelTrainer
+    from .utils.checkpoint import checkNNErrors, load_checkpoint, save_checkpoint
+    from .utils.common import precision, save_label
+    from .utils.data import load_dataset
+
+    backend = cfg.backend
+    if backend == "hip" and not torch.cuda.is_available():
+        backend = "torch"
+    comm, device = init_distributed("gloo" if backend == "torch" else None)
+    rank, world = comm.rank, comm.world_size
+    try:
+        log0(rank, f"Number of processes = {world}")
+        log0(rank, f"Device = {device} ({torch.cuda.get_device_name(device) if device.type == 'cuda' else 'cpu'})")
+        if cfg.grade == 4:
+            if rank == 0:
+                from .ops.gemm import benchmark_gemm
+
+                benchmark_gemm(device=device)
+            return {}
+        log0(rank, f"num_neuron={cfg.num_neuron}, reg={cfg.reg}, learning_rate={cfg.learning_rate}, "
+                   f"num_epochs={cfg.num_epochs}, batch_size={cfg.batch_size}, dtype={cfg.dtype}")
+        t = time.perf_counter()
+        ds = load_dataset(cfg.data, cfg.data_dir, cfg.num_train, cfg.num_test, cfg.seed)
+        log0(rank, f"Loaded {ds.source}: train {ds.x_train.shape[0]}, dev {ds.x_dev.shape[0]}, "
+                   f"test {ds.x_test.shape[0]} ({time.perf_counter() - t:.2f}s)")
+        os.makedirs(cfg.outdir, exist_ok=True)
+        meta = {}
+        if cfg.resume:
+            nn, meta = load_checkpoint(cfg.resume)
+            log0(rank, f"Resumed from {cfg.resume}: {meta}")
+        else:
+            nn = NeuralNetwork(cfg.H)
+        seq_nn = nn.copy()
+        xs = ds.x_train / 255.0 if cfg.normalize else ds.x_train
+        xd = ds.x_dev / 255.0 if cfg.normalize else ds.x_dev
+        out = {}
+        if rank == 0 and cfg.run_seq:
+            log0(rank, "Start Sequential Training")
+            t = time.perf_counter()
+            mlp.train(seq_nn, xs, ds.y_train, cfg.learning_rate, cfg.reg, cfg.num_epochs, cfg.batch_size,
+                      False, cfg.print_every, cfg.debug, cfg.outdir, cfg.softmax_shift, cfg.ckpt_precision)
+            out["seq_seconds"] = time.perf_counter() - t
+            log0(rank, f"Time for Sequential Training: {out['seq_seconds']:.6f} seconds")
+            out["seq_dev_precision"] = precision(mlp.predict(seq_nn, xd, cfg.softmax_shift), ds.y_dev)
+            log0(rank, f"Precision on validation set for sequential training = {out['seq_dev_precision']}")
+        comm.barrier()  # the parallel run's debug diff reads the CPU snapshots
+        log0(rank, "\nStart Parallel Training")
+        tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,
+                                 backend=backend, shift=cfg.softmax_shift, use_graphs=cfg.use_graphs,
+                                 normalize=cfg.normalize, path=cfg.path)
+        tr.load(ds.x_train, ds.y_train)
+        st = tr.train(cfg.num_epochs, cfg.learning_rate, cfg.reg, print_every=cfg.print_every, debug=cfg.debug,
+                      outdir=cfg.outdir, log=lambda m: log0(rank, m))
+        out.update(par_seconds=st.seconds, images_per_sec=st.images_per_sec, engine_path=tr.engine.path)
+        log0(rank, f"Time for Parallel Training: {st.seconds:.6f} seconds ({st.images_per_sec:,.0f} images/s, "
+                   f"engine path {tr.engine.path})")
+        if rank == 0:
+            out["par_dev_precision"] = precision(tr.predict(ds.x_dev), ds.y_dev)
+            log0(rank, f"Precision on validation set for parallel training = {out['par_dev_precision']}")
+            pred = tr.predict(ds.x_test)
+            save_label(os.path.join(cfg.outdir, "Pred_testset.txt"), pred)
+            if ds.y_test is not None:
+                out["par_test_precision"] = precision(pred, ds.y_test)
+            if cfg.ckpt_dir:
+                save_checkpoint(nn, cfg.ckpt_dir, meta={"epochs": cfg.num_epochs + meta.get("epochs", 0),
+                                                        "lr": cfg.learning_rate, "reg": cfg.reg,
+                                                        "seed": cfg.seed, "dtype": cfg.dtype})
+            if (cfg.grade or cfg.debug) and cfg.run_seq:
+                log0(rank, "\nGrading mode on. Checking for correctness")
+                out["correct"] = checkNNErrors(seq_nn, nn, os.path.join(cfg.outdir, "NNErrors.txt"))
+        comm.barrier()
+        return out
+    finally:
+        shutdown()
+
+
+def main(argv=None) -> int:
+    cfg = parse_config(argv)
+    out = run(cfg)
+    if out and int(os.environ.get("RANK", "0")) == 0:
+        print(json.dumps({k: (float(v) if isinstance(v, (np.floating,)) else v) for k, v in out.items()}))
+    return 0 if out.get("correct", True) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -191,6 +191,7 @@ std::vector<double> train(NetView net, const double* X, const int* labels, int N
         const double l = loss(net, yc.data(), labels + s, n, o.reg);
         losses.push_back(l);
         std::printf("Loss at iteration %d of epoch %d/%d = %.10g\n", iter, epoch, o.epochs, l);
+        std::fflush(stdout);
       }
       for (int64_t i = 0; i < (int64_t)H * P; ++i) net.W1[i] -= o.lr * dW1[i];
       for (int64_t i = 0; i < (int64_t)C * H; ++i) net.W2[i] -= o.lr * dW2[i];
