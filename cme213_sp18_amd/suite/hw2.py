@@ -1,0 +1,174 @@
+"""hw2: byte-shift cipher streaming and CSR PageRank on gfx950.
+
+Reference capabilities:
+  * shift_char / shift_int / shift_int2 kernels     hw2code/shift.cu:13-42
+  * shift driver (Moby Dick doubled, exact compare)  hw2code/main_q1.cu:74-224
+  * PageRank pull kernel + 6-iteration ping-pong     hw2code/pagerank.cu:9-136
+  * host propagate / iterate, graph generator,       hw2code/main_q2.cu:30-148
+    ULP-100 check and the bytes model                hw2code/main_q2.cu:224-226
+
+MI355X design: the wide shift variants move 4/8/16 bytes per lane (dwordx4
+loads saturate HBM with far fewer waves) and add with carry isolation, so they
+are exact for every byte value -- the reference's packed add was only correct
+for ASCII (byte + shift < 256).  PageRank is a thread-per-row CSR SpMV with a
+lanes-per-row variant for long rows.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..utils.common import ulp_distance
+from ._dev import EventTimer, host, kernels, require_cuda, stream_handle
+
+SHIFT_WIDTHS = (1, 4, 8, 16)
+PAGERANK_ITERS = 6          # main_q2.cu:153
+PAGERANK_MAX_ULPS = 100     # main_q2.cu:27
+
+
+# --------------------------------------------------------------- shift cipher
+def shift_host(text: np.ndarray, shift: int) -> np.ndarray:
+    """Host reference: byte-wise add mod 256 (main_q1.cu:40-72 compares against this)."""
+    return (np.asarray(text, np.uint8) + np.uint8(shift & 255)).astype(np.uint8)
+
+
+def shift_gpu(inp: torch.Tensor, shift: int, width: int = 16, out: torch.Tensor | None = None,
+              block: int = 256, grid_cap: int = 1 << 20) -> torch.Tensor:
+    """``out = inp + shift`` byte-wise with ``width`` bytes per lane (1/4/8/16)."""
+    require_cuda(inp)
+    if inp.dtype != torch.uint8:
+        raise TypeError("shift_gpu: uint8 input")
+    if width not in SHIFT_WIDTHS:
+        raise ValueError(f"shift_gpu: width must be one of {SHIFT_WIDTHS}")
+    if width > 1 and inp.data_ptr() % width:
+        raise ValueError("shift_gpu: input must be aligned to the lane width")
+    if out is None:
+        out = torch.empty_like(inp)
+    kernels().shift_bytes(inp.data_ptr(), out.data_ptr(), inp.numel(), shift & 255, width, block, grid_cap,
+                          stream_handle())
+    return out
+
+
+def doubled_text(text: bytes | np.ndarray, doublings: int) -> np.ndarray:
+    """The driver's input sizes: the text doubled ``doublings`` times (main_q1.cu:116-122)."""
+    t = np.frombuffer(text, np.uint8) if isinstance(text, (bytes, bytearray)) else np.asarray(text, np.uint8)
+    return np.tile(t, 1 << doublings) if doublings else t.copy()
+
+
+def benchmark_shift(text: np.ndarray, shift: int = 1, reps: int = 20, widths=SHIFT_WIDTHS) -> dict:
+    """Time every width on one input; returns {'bytes', 'ms': {w: ms}, 'gbps': {w: GB/s}} and checks exactness."""
+    dev = torch.device("cuda")
+    d_in = torch.from_numpy(np.ascontiguousarray(text, np.uint8)).to(dev)
+    d_out = torch.empty_like(d_in)
+    ref = torch.from_numpy(shift_host(text, shift)).to(dev)
+    res = {"bytes": int(d_in.numel()), "ms": {}, "gbps": {}}
+    for w in widths:
+        shift_gpu(d_in, shift, w, d_out)  # warm
+        with EventTimer() as t:
+            for _ in range(reps):
+                shift_gpu(d_in, shift, w, d_out)
+        ms = t.ms / reps
+        if not torch.equal(d_out, ref):
+            raise AssertionError(f"shift width {w}: GPU output differs from host reference")
+        d_out.zero_()  # main_q1.cu memsets the output between kernels
+        res["ms"][w] = ms
+        res["gbps"][w] = 2 * d_in.numel() / (ms * 1e-3) / 1e9
+    return res
+
+
+# --------------------------------------------------------------- PageRank
+class Graph:
+    """CSR graph in the reference's layout (main_q2.cu:87-120)."""
+
+    def __init__(self, indptr, edges, inv_deg, values):
+        self.indptr = np.ascontiguousarray(indptr, np.uint32)
+        self.edges = np.ascontiguousarray(edges, np.uint32)
+        self.inv_deg = np.ascontiguousarray(inv_deg, np.float32)
+        self.values = np.ascontiguousarray(values, np.float32)
+
+    @property
+    def num_nodes(self) -> int:
+        return len(self.values)
+
+
+def generate_graph(num_nodes: int, avg_edges: int, seed: int = 0) -> Graph:
+    """Deterministic degree ramp 1,1,..,2,2,..,2*avg-1 with uniformly random sources
+    (main_q2.cu:87-120; the reference seeds rand() with time(), we take a seed)."""
+    nodes_per_block = num_nodes // (avg_edges * 2 - 1) + 1
+    deg = (np.arange(num_nodes, dtype=np.int64) // nodes_per_block + 1).astype(np.uint32)
+    indptr = np.zeros(num_nodes + 1, np.uint32)
+    np.cumsum(deg, out=indptr[1:])
+    edges = np.random.default_rng(seed).integers(0, num_nodes, int(indptr[-1]), dtype=np.uint32)
+    inv = (1.0 / deg.astype(np.float32)).astype(np.float32)
+    vals = np.full(num_nodes, 1.0 / num_nodes, np.float32)
+    return Graph(indptr, edges, inv, vals)
+
+
+def pagerank_host(g: Graph, iters: int = PAGERANK_ITERS) -> np.ndarray:
+    """Host iterate (main_q2.cu:49-85), OpenMP-parallel over nodes in the native runtime."""
+    return host().pagerank(g.indptr, g.edges, g.inv_deg, g.values, iters)
+
+
+class DeviceGraph:
+    def __init__(self, g: Graph, device="cuda"):
+        t = lambda a: torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).to(device)
+        self.n = g.num_nodes
+        self.num_edges = len(g.edges)
+        self.indptr, self.edges, self.inv = t(g.indptr), t(g.edges), t(g.inv_deg)
+        self.a = t(g.values)
+        self.b = torch.empty_like(self.a)
+        self.initial = self.a.clone()
+
+    def reset(self):
+        self.a.copy_(self.initial)
+
+    def propagate(self, src, dst, variant: int = 2):
+        kernels().pagerank_propagate(self.indptr.data_ptr(), self.edges.data_ptr(), src.data_ptr(), dst.data_ptr(),
+                                     self.inv.data_ptr(), self.n, variant, stream_handle())
+
+    def iterate(self, iters: int = PAGERANK_ITERS, variant: int = 2) -> torch.Tensor:
+        """Ping-pong ``iters`` propagations (pagerank.cu:100-117); returns the final buffer."""
+        src, dst = self.a, self.b
+        for _ in range(iters):
+            self.propagate(src, dst, variant)
+            src, dst = dst, src
+        return src
+
+
+def pagerank_gpu(g: Graph, iters: int = PAGERANK_ITERS, variant: int = 2) -> np.ndarray:
+    return DeviceGraph(g).iterate(iters, variant).cpu().numpy()
+
+
+def pagerank_bytes(num_nodes: int, avg_edges: int, iters: int = PAGERANK_ITERS) -> int:
+    """The reference's traffic model (main_q2.cu:224-226)."""
+    uint_bytes = 2 * num_nodes * iters * (1 + avg_edges) * 4
+    float_bytes = num_nodes * iters * (1 + 2 * avg_edges) * 4
+    return uint_bytes + float_bytes
+
+
+def check_pagerank(gpu: np.ndarray, cpu: np.ndarray, max_ulps: int = PAGERANK_MAX_ULPS) -> int:
+    """Number of nodes differing by more than ``max_ulps`` ULP (main_q2.cu:122-148)."""
+    return int(np.count_nonzero(ulp_distance(np.asarray(gpu, np.float32), np.asarray(cpu, np.float32)) > max_ulps))
+
+
+def benchmark_pagerank(nodes=(1 << 15, 1 << 16, 1 << 17, 1 << 18, 1 << 19, 1 << 20), edges=range(2, 20),
+                       iters: int = PAGERANK_ITERS, reps: int = 5, check: bool = True, variant: int = 2) -> list[dict]:
+    """The GB/s sweep of main_q2.cu:151-233 (nodes 2^15..2^20 x avg edges 2..19)."""
+    rows = []
+    for e in edges:
+        for n in nodes:
+            g = generate_graph(n, e, seed=n * 31 + e)
+            dg = DeviceGraph(g)
+            dg.iterate(iters, variant)
+            dg.reset()
+            with EventTimer() as t:
+                for _ in range(reps):
+                    dg.iterate(iters, variant)
+            ms = t.ms / reps
+            bad = 0
+            if check:
+                dg.reset()
+                bad = check_pagerank(dg.iterate(iters, variant).cpu().numpy(), pagerank_host(g, iters))
+            rows.append({"nodes": n, "avg_edges": e, "ms": ms, "gbps": pagerank_bytes(n, e, iters) / (ms * 1e-3) / 1e9,
+                         "mismatches": bad})
+    return rows
