@@ -26,6 +26,24 @@ MIN_PERIOD = 4        # create_cipher.cu:166, solve_cipher.cu:77
 SHIFT_SEED = 123      # create_cipher.cu:207
 
 
+# relative letter frequencies of English text (a..z), used for synthetic plaintext
+ENGLISH_FREQ = np.array([8.17, 1.49, 2.78, 4.25, 12.70, 2.23, 2.02, 6.09, 6.97, 0.15, 0.77, 4.03, 2.41, 6.75, 7.51,
+                         1.93, 0.10, 5.99, 6.33, 9.06, 2.76, 0.98, 2.36, 0.15, 1.97, 0.07])
+
+
+def synthetic_english(n: int, seed: int = 0) -> bytes:
+    """``n`` bytes of English-like text: letters drawn with English frequencies, ~10% capitals,
+    words of 1-9 letters separated by spaces/punctuation (stand-in for the reference's Moby Dick)."""
+    rng = np.random.default_rng(seed)
+    p = ENGLISH_FREQ / ENGLISH_FREQ.sum()
+    out = (97 + rng.choice(26, n, p=p)).astype(np.uint8)
+    out[rng.random(n) < 0.1] -= 32
+    gaps = np.cumsum(rng.integers(2, 11, n // 2 + 1))
+    gaps = gaps[gaps < n]
+    out[gaps] = rng.choice(np.frombuffer(b"     ,.;\n", np.uint8), gaps.size)
+    return out.tobytes()
+
+
 def _t(a) -> torch.Tensor:
     if isinstance(a, torch.Tensor):
         return a if a.is_cuda else a.cuda()

@@ -195,3 +195,12 @@ def test_vigenere_host_roundtrip(wrap):
 def test_make_shifts_rejects_short_period():
     with pytest.raises(ValueError):
         hw4.make_shifts(3)
+
+
+def test_synthetic_english_ioc_separates_period():
+    t = hw4.sanitize_host(hw4.synthetic_english(200_000, seed=1))
+    x = hw4.vigenere_host(t, hw4.make_shifts(6), 1, True)
+    s = np.arange(4, 20)
+    m = np.array([np.count_nonzero(x[:-k] == x[k:]) for k in s])
+    ioc = hw4.index_of_coincidence(m, len(x), s)
+    assert list(s[ioc > hw4.IOC_THRESHOLD]) == [6, 12, 18]
