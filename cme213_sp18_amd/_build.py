@@ -44,7 +44,7 @@ def _hip_sources() -> list[Path]:
 
 
 def _cpu_sources() -> list[Path]:
-    return sorted((CSRC / "cpu").glob("*.cpp")) + [CSRC / "bindings_cpu.cpp"]
+    return sorted((CSRC / "cpu").glob("*.cpp")) + [CSRC / "bindings_cpu.cpp", CSRC / "bindings_suite_cpu.cpp"]
 
 
 def _headers_mtime() -> float:
