@@ -10,7 +10,8 @@ one JSON line.
 What a step is (the reference's ``parallel_train`` inner loop,
 fpcode/neural_network.cpp:449-555): one synchronous SGD update -- forward +
 backward of the 784-100-10 MLP (random-init weights, seeded as the reference
-does) on every rank, gradient all-reduce over RCCL, SGD update -- on
+does) on every rank, gradient all-reduce (xGMI peer kernel with the SGD
+fused in, or RCCL with ``--allreduce rccl``), SGD update -- on
 synthetic MNIST-shaped images resident on every GPU.  Nothing is skipped
 inside the timed region.  Steps cycle over the full batches of the 54,000-image
 training split and are replayed from a captured HIP graph.
@@ -43,6 +44,8 @@ def parse(argv=None):
     ap.add_argument("--scaling", default="weak", choices=["strong", "weak"])
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
+                    help="gradient sync for N>1: xGMI peer kernel with fused SGD (auto/xgmi) or RCCL all-reduce")
     ap.add_argument("--train-size", type=int, default=54000)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -68,7 +71,7 @@ def main(argv=None) -> int:
     x, y = synthetic_mnist(a.train_size, seed=0)  # identical on every rank, no broadcast
     nn = NeuralNetwork([784, a.hidden, 10])
     tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=global_batch,
-                             backend=a.backend, use_graphs=not a.no_graphs)
+                             backend=a.backend, use_graphs=not a.no_graphs, allreduce=a.allreduce)
     tr.load(x, y)
     full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == global_batch]
     if not full:
@@ -106,8 +109,10 @@ def main(argv=None) -> int:
     dt = time.perf_counter() - t0
     dt = comm.allreduce_scalar(dt, op="max")
 
-    # sanity: parameters finite after training
+    # sanity: parameters finite after training, peer waits never timed out
     ok = bool(torch.isfinite(tr.engine.params).all().item())
+    if tr.xgmi is not None:
+        tr.xgmi.check()
     images = a.steps * global_batch
     value = images / dt
     if rank == 0:
@@ -126,7 +131,7 @@ def main(argv=None) -> int:
             "data": "synthetic (MNIST-shaped 784-dim uint8 images, random-init weights)",
             "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": global_batch, "seq_len": None,
                        "parallelism": f"dp{R}", "per_gpu_batch": global_batch // R, "backend": a.backend,
-                       "hip_graphs": tr.use_graphs, "params_finite": ok},
+                       "hip_graphs": tr.use_graphs, "allreduce": tr.allreduce_impl, "params_finite": ok},
         }
         print(json.dumps(rec), flush=True)
     shutdown()

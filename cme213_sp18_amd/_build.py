@@ -38,8 +38,8 @@ def _pybind_includes() -> list[str]:
 
 
 def _hip_sources() -> list[Path]:
-    srcs = sorted((CSRC / "mlp").glob("*.hip")) + sorted((CSRC / "suite").glob("*.hip"))
-    srcs += [CSRC / "bindings_hip.cpp", CSRC / "suite" / "suite_bindings.cpp"]
+    srcs = [s for d in ("mlp", "suite", "comm") for s in sorted((CSRC / d).glob("*.hip"))]
+    srcs += [CSRC / "bindings_hip.cpp", CSRC / "suite" / "suite_bindings.cpp", CSRC / "comm" / "comm_bindings.cpp"]
     return srcs
 
 

@@ -39,6 +39,7 @@ class TrainConfig:
     use_graphs: bool = True
     softmax_shift: bool = True
     ckpt_precision: int = 12
+    allreduce: str = "auto"     # auto | xgmi (peer kernel, SGD fused) | rccl
 
     @property
     def H(self):
@@ -59,7 +60,7 @@ GRADE_PRESETS = {
 NAMED_PRESETS = {
     "cpu_plumbing": dict(num_neuron=100, batch_size=800, backend="torch", dtype="f64", run_seq=True),
     "1gpu_fp32": dict(num_neuron=100, batch_size=800, dtype="f32"),
-    "4gpu_rccl": dict(num_neuron=100, batch_size=800, dtype="f32"),
+    "4gpu_rccl": dict(num_neuron=100, batch_size=800, dtype="f32", allreduce="rccl"),
     "8gpu_wide": dict(num_neuron=4096, batch_size=6400, dtype="f32"),
     "8gpu_bf16": dict(num_neuron=1024, batch_size=800, dtype="bf16"),
 }
@@ -93,6 +94,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-graphs", dest="use_graphs", action="store_false", default=None)
     ap.add_argument("--no-softmax-shift", dest="softmax_shift", action="store_false", default=None)
     ap.add_argument("--ckpt-precision", type=int)
+    ap.add_argument("--allreduce", choices=["auto", "xgmi", "rccl"])
     return ap
 
 

@@ -51,7 +51,7 @@ class TrainStats:
 class DataParallelTrainer:
     def __init__(self, nn, comm: Communicator | None = None, device=None, dtype: str = "f32",
                  batch_size: int = 800, backend: str = "hip", shift: bool = True, use_graphs: bool = True,
-                 normalize: bool = False, path: str = "auto"):
+                 normalize: bool = False, path: str = "auto", allreduce: str = "auto"):
         self.nn = nn
         self.comm = comm or NullComm()
         self.R = self.comm.world_size
@@ -60,12 +60,60 @@ class DataParallelTrainer:
         self.dtype = dtype
         self.normalize = normalize
         self.use_graphs = bool(use_graphs) and backend == "hip" and (self.R == 1 or self.comm.graph_capturable)
+        self.allreduce_mode = allreduce
         max_cols = max(1, self.B // self.R)
         self.engine = MlpEngine(nn.H, dtype=dtype, max_cols=max_cols, device=device, backend=backend, shift=shift,
                                 path=path)
         self.engine.set_params(*nn.params)
         self._graphs: dict = {}
         self.iter = 0
+        self.xgmi = self._setup_xgmi(allreduce)
+        self.allreduce_impl = "none" if self.R == 1 else ("xgmi" if self.xgmi is not None else self.comm.name)
+
+    def _setup_xgmi(self, mode: str):
+        """Peer-to-peer fused all-reduce+SGD (parallel/xgmi.py) when every rank is a GPU on this node.
+        mode: auto (use it if the self-test passes), xgmi (require it), rccl/off (never)."""
+        from .comm import TorchDistComm
+
+        if mode not in ("auto", "xgmi", "rccl", "off"):
+            raise ValueError("allreduce must be auto, xgmi, rccl or off")
+        e = self.engine
+        eligible = (self.R > 1 and isinstance(self.comm, TorchDistComm) and e.device.type == "cuda"
+                    and e.backend == "hip" and e.params.dtype in (torch.float32, torch.float64))
+        if mode in ("rccl", "off") or not eligible:
+            if mode == "xgmi" and not eligible:
+                raise RuntimeError("xgmi all-reduce needs >1 GPU ranks of the hip backend")
+            return None
+        from .xgmi import XgmiBucket, same_node
+
+        if mode == "auto" and (not same_node(self.R) or self.R > 8):
+            return None
+        try:
+            xb = XgmiBucket(self.comm.group, self.rank, self.R, e.params.numel(), e.params.dtype, e.device)
+        except Exception as ex:  # IPC unavailable: every rank sees the same failure at the same point
+            if mode == "xgmi":
+                raise
+            print(f"[rank {self.rank}] xgmi all-reduce unavailable ({ex}); using {self.comm.name}", flush=True)
+            return None
+        if not xb.ok:
+            xb.close()
+            if mode == "xgmi":
+                raise RuntimeError("xgmi all-reduce self-test failed")
+            return None
+        return xb
+
+    def _allreduce_sgd(self, lr: float) -> None:
+        e = self.engine
+        if self.xgmi is None:
+            self.comm.allreduce_(e.grads)
+            e.sgd(lr)
+            return
+        planes, np_ = None, 0
+        if e.np:  # split paths: refresh the exact bf16 planes of W1
+            planes, np_ = e.W1p, e.np
+        elif e.dtype == "bf16":  # bf16 path: single-rounded shadow of W1
+            planes, np_ = e.W1g, 1
+        self.xgmi.sgd_(e.grads, e.params, lr, planes, np_, e.H * e.P)
 
     # ---------------------------------------------------------------- data
     def load(self, x_train, y_train):
@@ -89,16 +137,14 @@ class DataParallelTrainer:
         off, n = self.shard(start, length)
         if n == 0:  # fewer columns than ranks: only the regulariser contributes
             e.reg_only_grads(reg / self.R)
-            self.comm.allreduce_(e.grads)
-            e.sgd(lr)
+            self._allreduce_sgd(lr)
             return
         scale = 1.0 / (n * self.R)
         if isinstance(self.comm, NullComm):  # single process: SGD fused into the weight-gradient kernel
             e.run(off, n, scale, reg, lr, sgd=True, with_loss=with_loss)
         else:
             e.run(off, n, scale, reg / self.R, lr, sgd=False, with_loss=with_loss)
-            self.comm.allreduce_(e.grads)
-            e.sgd(lr)
+            self._allreduce_sgd(lr)
 
     def step_loss(self, start: int, length: int, lr: float, reg: float) -> float:
         """One step that also returns the (pre-update) global loss -- reference
@@ -202,6 +248,8 @@ class DataParallelTrainer:
                     stats.images += (ln // self.R) * self.R
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
+            if self.xgmi is not None:
+                self.xgmi.check()
             self.comm.barrier()
         finally:
             if err_file is not None:
@@ -224,9 +272,11 @@ class DataParallelTrainer:
 def parallel_train(nn, X, y, learning_rate: float, reg: float = 0.0, epochs: int = 15, batch_size: int = 800,
                    grad_check: bool = False, print_every: int = -1, debug: bool = False, comm=None, device=None,
                    dtype: str = "f32", backend: str = "hip", use_graphs: bool = True, shift: bool = True,
-                   outdir: str = "Outputs", normalize: bool = False, path: str = "auto") -> TrainStats:
+                   outdir: str = "Outputs", normalize: bool = False, path: str = "auto",
+                   allreduce: str = "auto") -> TrainStats:
     """Reference-compatible entry point (inc/neural_network.h:45-48): trains ``nn`` in place."""
     tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=dtype, batch_size=batch_size, backend=backend,
-                             shift=shift, use_graphs=use_graphs, normalize=normalize, path=path)
+                             shift=shift, use_graphs=use_graphs, normalize=normalize, path=path,
+                             allreduce=allreduce)
     tr.load(X, y)
     return tr.train(epochs, learning_rate, reg, print_every=max(0, print_every), debug=debug, outdir=outdir)

@@ -1,0 +1,98 @@
+"""xGMI peer-to-peer all-reduce with the SGD update fused in (one kernel per step).
+
+The data-parallel step's gradient bucket is small (318 KB at H=100), so a ring
+all-reduce is latency bound.  :class:`XgmiBucket` maps every rank's gradient
+buffer into every other rank over IPC (dmabuf; ``HSA_ENABLE_IPC_MODE_LEGACY=0``)
+and one kernel per step copies, signals, waits, sums the R gradients in rank
+order straight from the peers' HBM and applies ``params -= lr * sum`` (plus the
+bf16 W1 plane refresh).  See csrc/comm/xgmi_allreduce.hip for the protocol.
+
+It replaces the reference's 4 x MPI_Allreduce on host buffers + host SGD
+(fpcode/neural_network.cpp:496-541).  The handles are exchanged through any
+torch.distributed group (nccl or gloo), so the mechanism is testable with
+several processes sharing ONE GPU.  A self-test at construction compares the
+result with the expected sum on every rank; on any failure the caller falls
+back to the RCCL path.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from .._native import DTYPE_CODES, hip
+
+
+def same_node(world: int) -> bool:
+    lws = os.environ.get("LOCAL_WORLD_SIZE")
+    return lws is not None and int(lws) == world
+
+
+class XgmiBucket:
+    MODE_SGD = 0
+    MODE_ALLREDUCE = 1
+
+    def __init__(self, group, rank: int, world: int, numel: int, dtype: torch.dtype, device, self_test: bool = True):
+        import torch.distributed as dist
+
+        if world > hip().comm.MAX_RANKS:
+            raise ValueError(f"xGMI all-reduce supports at most {hip().comm.MAX_RANKS} ranks")
+        if dtype not in (torch.float32, torch.float64):
+            raise TypeError("xGMI bucket: float32 or float64")
+        self.rank, self.world, self.numel, self.dtype = rank, world, int(numel), dtype
+        self.device = torch.device(device)
+        self.code = 1 if dtype == torch.float64 else 0
+        with torch.cuda.device(self.device):
+            self.c = hip().comm.XgmiComm(rank, world, self.numel, 8 if self.code else 4)
+            mine = self.c.handles()
+            allh = [None] * world
+            dist.all_gather_object(allh, mine, group=group)
+            self.c.open([(bytes(a), bytes(b)) for a, b in allh])
+        self.ok = True
+        if self_test:
+            self.ok = self._self_test(group)
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _self_test(self, group) -> bool:
+        import torch.distributed as dist
+
+        n = self.numel
+        base = torch.arange(n, dtype=torch.float64, device=self.device) % 1000
+        g = ((self.rank + 1) * 0.25 + base / 1024).to(self.dtype)
+        exp = sum(((r + 1) * 0.25 + base / 1024).to(self.dtype).double() for r in range(self.world))
+        good = True
+        for _ in range(3):  # exercises both buffer halves and the epoch counters
+            t = g.clone()
+            self.allreduce_(t)
+            torch.cuda.synchronize(self.device)
+            good &= bool(torch.allclose(t.double(), exp, rtol=1e-6, atol=0)) and self.error() == 0
+        flag = torch.tensor([1 if good else 0], dtype=torch.int32,
+                            device=self.device if dist.get_backend(group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        return bool(flag.item())
+
+    def allreduce_(self, t: torch.Tensor) -> None:
+        """In-place SUM of a contiguous tensor of exactly ``numel`` elements."""
+        assert t.numel() == self.numel and t.dtype == self.dtype and t.is_contiguous()
+        self.c.run(self.code, t.data_ptr(), 0, 0.0, 0, 0, 0, self.MODE_ALLREDUCE, self.numel, self._stream())
+
+    def sgd_(self, grads: torch.Tensor, params: torch.Tensor, lr: float, planes: torch.Tensor | None = None,
+             np_: int = 0, w1n: int = 0) -> None:
+        """params -= lr * sum_ranks(grads); refresh bf16 planes ([np_][w1n]) of the first w1n params."""
+        assert grads.numel() == self.numel == params.numel()
+        pl = planes.data_ptr() if planes is not None else 0
+        self.c.run(self.code, grads.data_ptr(), params.data_ptr(), float(lr), pl, np_ if pl else 0, w1n,
+                   self.MODE_SGD, self.numel, self._stream())
+
+    def error(self) -> int:
+        return int(self.c.error())
+
+    def check(self) -> None:
+        if self.error():
+            raise RuntimeError("xGMI all-reduce: a peer wait timed out (a rank stalled or died)")
+
+    def close(self) -> None:
+        self.c.close()

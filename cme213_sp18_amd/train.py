@@ -83,11 +83,12 @@ def run(cfg: TrainConfig) -> dict:
         log0(rank, "\nStart Parallel Training")
         tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,
                                  backend=backend, shift=cfg.softmax_shift, use_graphs=cfg.use_graphs,
-                                 normalize=cfg.normalize, path=cfg.path)
+                                 normalize=cfg.normalize, path=cfg.path, allreduce=cfg.allreduce)
         tr.load(ds.x_train, ds.y_train)
         st = tr.train(cfg.num_epochs, cfg.learning_rate, cfg.reg, print_every=cfg.print_every, debug=cfg.debug,
                       outdir=cfg.outdir, log=lambda m: log0(rank, m))
-        out.update(par_seconds=st.seconds, images_per_sec=st.images_per_sec, engine_path=tr.engine.path)
+        out.update(par_seconds=st.seconds, images_per_sec=st.images_per_sec, engine_path=tr.engine.path,
+                   allreduce=tr.allreduce_impl)
         log0(rank, f"Time for Parallel Training: {st.seconds:.6f} seconds ({st.images_per_sec:,.0f} images/s, "
                    f"engine path {tr.engine.path})")
         if rank == 0:

@@ -134,6 +134,7 @@ struct MlpStep {
 }  // namespace
 
 void bind_suite(py::module_& m);  // suite_bindings.cpp
+void bind_comm(py::module_& m);   // comm/comm_bindings.cpp
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "cme213_sp18_amd gfx950 HIP kernels (MFMA MLP engine + homework kernel suite)";
@@ -281,4 +282,5 @@ PYBIND11_MODULE(_hip, m) {
   m.def("split_fwdhead_blocks", &cme::mlp_split_fwdhead_blocks);
 
   bind_suite(m);
+  bind_comm(m);
 }

@@ -1,0 +1,129 @@
+// pybind11 bindings for the xGMI peer all-reduce: IPC buffer ownership,
+// handle export/import and the launch (submodule `_hip.comm`).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../common/hip_common.h"
+#include "xgmi_allreduce.h"
+
+namespace py = pybind11;
+
+namespace cme::comm {
+
+namespace {
+
+py::bytes handle_bytes(void* p) {
+  hipIpcMemHandle_t h;
+  HIP_CHECK(hipIpcGetMemHandle(&h, p));
+  return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void* open_handle(const std::string& b) {
+  CME_REQUIRE(b.size() == sizeof(hipIpcMemHandle_t), "xgmi: bad IPC handle size");
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, b.data(), sizeof(h));
+  void* p = nullptr;
+  HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  return p;
+}
+
+// Owns this rank's IPC buffers and the peers' mappings.
+class XgmiComm {
+ public:
+  XgmiComm(int rank, int world, int64_t n, int elt_bytes) {
+    CME_REQUIRE(world >= 1 && world <= kMaxRanks, "XgmiComm: 1 <= world <= 8");
+    CME_REQUIRE(rank >= 0 && rank < world, "XgmiComm: bad rank");
+    CME_REQUIRE(elt_bytes == 4 || elt_bytes == 8, "XgmiComm: f32 or f64");
+    d_.rank = rank;
+    d_.world = world;
+    d_.n = n;
+    d_.npad = xgmi_padded_count(n);
+    nblocks_ = std::max<int64_t>(1, xgmi_num_blocks(n));
+    HIP_CHECK(hipMalloc(&d_.mybuf, 2 * d_.npad * elt_bytes));
+    HIP_CHECK(hipMemset(d_.mybuf, 0, 2 * d_.npad * elt_bytes));
+    // flag page: uncached so the peers' system-scope stores are seen without cache maintenance
+    HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_.myflags), flag_bytes(), hipDeviceMallocUncached));
+    HIP_CHECK(hipMemset(d_.myflags, 0, flag_bytes()));
+    HIP_CHECK(hipMalloc(&d_.epochs, nblocks_ * sizeof(uint32_t)));
+    HIP_CHECK(hipMemset(d_.epochs, 0, nblocks_ * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&d_.err, sizeof(int)));
+    HIP_CHECK(hipMemset(d_.err, 0, sizeof(int)));
+    HIP_CHECK(hipDeviceSynchronize());
+    d_.peers[rank] = d_.mybuf;
+    d_.peerflags[rank] = d_.myflags;
+  }
+  ~XgmiComm() { close(); }
+
+  py::tuple handles() const { return py::make_tuple(handle_bytes(d_.mybuf), handle_bytes(d_.myflags)); }
+
+  void open(const std::vector<std::pair<std::string, std::string>>& all) {
+    CME_REQUIRE((int)all.size() == d_.world, "XgmiComm.open: need one handle pair per rank");
+    for (int r = 0; r < d_.world; ++r) {
+      if (r == d_.rank) continue;
+      d_.peers[r] = open_handle(all[r].first);
+      d_.peerflags[r] = static_cast<uint32_t*>(open_handle(all[r].second));
+      opened_.push_back(d_.peers[r]);
+      opened_.push_back(d_.peerflags[r]);
+    }
+    ready_ = true;
+  }
+
+  void run(int dtype, uintptr_t grads, uintptr_t params, double lr, uintptr_t planes, int np, int64_t w1n, int mode,
+           int64_t n, uintptr_t stream) {
+    CME_REQUIRE(ready_ || d_.world == 1, "XgmiComm.run: open() the peer handles first");
+    CME_REQUIRE(n == d_.n, "XgmiComm.run: element count differs from the one the buffers were sized for");
+    xgmi_allreduce(d_, dtype, reinterpret_cast<const void*>(grads), reinterpret_cast<void*>(params), lr,
+                   reinterpret_cast<void*>(planes), np, w1n, mode, reinterpret_cast<hipStream_t>(stream));
+  }
+
+  int error() const {
+    int e = 0;
+    HIP_CHECK(hipMemcpy(&e, d_.err, sizeof(int), hipMemcpyDeviceToHost));
+    return e;
+  }
+
+  void close() {
+    for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+    opened_.clear();
+    if (d_.mybuf) (void)hipFree(d_.mybuf);
+    if (d_.myflags) (void)hipFree(d_.myflags);
+    if (d_.epochs) (void)hipFree(d_.epochs);
+    if (d_.err) (void)hipFree(d_.err);
+    d_ = XgmiDesc{};
+    ready_ = false;
+  }
+
+  int64_t nblocks() const { return nblocks_; }
+
+ private:
+  size_t flag_bytes() const { return (size_t)nblocks_ * kMaxRanks * sizeof(uint32_t); }
+  XgmiDesc d_;
+  int64_t nblocks_ = 0;
+  bool ready_ = false;
+  std::vector<void*> opened_;
+};
+
+}  // namespace
+
+}  // namespace cme::comm
+
+void bind_comm(py::module_& m) {
+  using cme::comm::XgmiComm;
+  auto sm = m.def_submodule("comm", "xGMI peer-to-peer all-reduce (IPC buffers, SGD fused)");
+  py::class_<XgmiComm>(sm, "XgmiComm")
+      .def(py::init<int, int, int64_t, int>(), py::arg("rank"), py::arg("world"), py::arg("n"), py::arg("elt_bytes"))
+      .def("handles", &XgmiComm::handles)
+      .def("open", &XgmiComm::open)
+      .def("run", &XgmiComm::run, py::arg("dtype"), py::arg("grads"), py::arg("params"), py::arg("lr"),
+           py::arg("planes"), py::arg("np"), py::arg("w1n"), py::arg("mode"), py::arg("n"), py::arg("stream"))
+      .def("error", &XgmiComm::error)
+      .def("close", &XgmiComm::close)
+      .def_property_readonly("nblocks", &XgmiComm::nblocks);
+  sm.attr("MODE_SGD") = cme::comm::kModeSgd;
+  sm.attr("MODE_ALLREDUCE") = cme::comm::kModeAllReduce;
+  sm.attr("MAX_RANKS") = cme::comm::kMaxRanks;
+}

@@ -1,0 +1,35 @@
+// Peer-to-peer (xGMI) all-reduce for small gradient buckets, SGD fused.
+// See xgmi_allreduce.hip for the protocol.  The IPC plumbing (allocation,
+// handle export/import) lives in xgmi_ipc.cpp; Python drives the handle
+// exchange through any torch.distributed group (cme213_sp18_amd/parallel/xgmi.py).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace cme::comm {
+
+constexpr int kMaxRanks = 8;  // one xGMI hive
+constexpr int kModeSgd = 0;        // params -= lr * sum(grads)   (+ bf16 plane/shadow refresh)
+constexpr int kModeAllReduce = 1;  // grads  := sum(grads)
+
+struct XgmiDesc {
+  int rank = 0, world = 1;
+  int64_t n = 0, npad = 0;            // elements, padded elements per buffer half
+  void* mybuf = nullptr;              // [2][npad] my IPC data buffer
+  void* peers[kMaxRanks] = {};        // every rank's data buffer as mapped here (peers[rank] == mybuf)
+  uint32_t* myflags = nullptr;        // [nblocks][kMaxRanks] uncached, IPC-exported
+  uint32_t* peerflags[kMaxRanks] = {};
+  uint32_t* epochs = nullptr;         // [nblocks] local
+  int* err = nullptr;                 // set to 1 when a wait timed out
+};
+
+int64_t xgmi_padded_count(int64_t n);
+int64_t xgmi_num_blocks(int64_t n);
+
+// dtype: 0 f32, 1 f64.  planes: bf16 [np][w1n] refreshed from the first w1n params (np 1 or 3), or null.
+void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* params, double lr, void* planes, int np,
+                    int64_t w1n, int mode, hipStream_t s);
+
+}  // namespace cme::comm

@@ -59,3 +59,82 @@ def nccl_graph_worker(out_dir):
         np.savez(os.path.join(out_dir, "nccl.npz"), a=nn.W[0], b=ref.W[0], a1=nn.b[0], b1=ref.b[0])
     finally:
         dist.destroy_process_group()
+
+
+def xgmi_worker(rank, world, comm, device, out_dir):
+    """Several processes on ONE GPU: the xGMI peer all-reduce through IPC handles
+    exchanged over gloo (same code path as 8 GPUs, minus the links)."""
+    from cme213_sp18_amd.parallel.xgmi import XgmiBucket
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    res = {}
+    # plain all-reduce: sizes around the vector / chunk / grid-stride edges, both halves, fp32 + fp64
+    for dt in (torch.float32, torch.float64):
+        for n in (1, 3, 1024, 79_510, 600 * 1024 + 3):
+            xb = XgmiBucket(comm.group, rank, world, n, dt, dev)
+            worst = 0.0
+            base = torch.arange(n, device=dev, dtype=torch.float64) % 977
+            for it in range(5):
+                g = (base * 1e-3 * (rank + 1) + it).to(dt)
+                xb.allreduce_(g)
+                exp = sum((base * 1e-3 * (r + 1) + it).to(dt).double() for r in range(world))
+                worst = max(worst, float(((g.double() - exp).abs() / exp.abs().clamp_min(1)).max()))
+            torch.cuda.synchronize()
+            res[f"ar_{dt}_{n}"] = worst
+            res[f"ok_{dt}_{n}"] = float(xb.ok and xb.error() == 0)
+            xb.close()
+    # fused SGD with exact bf16 planes, replayed from a HIP graph
+    n, w1n = 5000, 3136
+    gen = torch.Generator(device="cpu").manual_seed(7)
+    p0 = torch.randn(n, generator=gen).to(dev)
+    grads = (torch.randn(n, generator=gen) * (rank + 1)).to(dev)
+    params = p0.clone()
+    planes = torch.zeros(3, w1n, dtype=torch.bfloat16, device=dev)
+    xb = XgmiBucket(comm.group, rank, world, n, torch.float32, dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        xb.sgd_(grads, params, 0.01, planes, 3, w1n)  # eager step 1
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        xb.sgd_(grads, params, 0.01, planes, 3, w1n)
+    for _ in range(4):
+        graph.replay()
+    torch.cuda.synchronize()
+    # every rank's grads: regenerate them to build the expected update
+    gsum = torch.zeros(n, dtype=torch.float64)
+    for r in range(world):
+        gg = torch.Generator(device="cpu").manual_seed(7)
+        torch.randn(n, generator=gg)
+        gsum += (torch.randn(n, generator=gg) * (r + 1)).double()
+    exp = p0.double().cpu() - 5 * 0.01 * gsum
+    res["sgd_err"] = float((params.double().cpu() - exp).abs().max())
+    res["planes_exact"] = float(torch.equal(planes.float().sum(0), params[:w1n]))
+    res["sgd_ok"] = float(xb.error() == 0)
+    xb.close()
+    # the trainer: xgmi fused path vs the gloo all-reduce path, same data and seeds
+    from cme213_sp18_amd import NeuralNetwork
+    from cme213_sp18_amd.parallel import DataParallelTrainer
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    x, y = synthetic_mnist(3200, seed=3)
+    out = {}
+    for mode in ("xgmi", "off"):
+        nn = NeuralNetwork([784, 100, 10])
+        tr = DataParallelTrainer(nn, comm=comm, device=dev, batch_size=800, use_graphs=False, allreduce=mode)
+        assert (tr.xgmi is not None) == (mode == "xgmi")
+        tr.load(x, y)
+        tr.train(2, 0.05, 1e-4)
+        out[mode] = nn.W[0].copy(), nn.W[1].copy()
+    res["trainer_w1_diff"] = float(np.abs(out["xgmi"][0] - out["off"][0]).max())
+    res["trainer_w2_diff"] = float(np.abs(out["xgmi"][1] - out["off"][1]).max())
+    np.savez(os.path.join(out_dir, f"xgmi{rank}.npz"), **{k: np.array(v) for k, v in res.items()})
+
+
+def xgmi_spawn_main(out_dir, world):
+    from cme213_sp18_amd.parallel.launcher import spawn
+
+    spawn(xgmi_worker, world, (out_dir,), backend="gloo")

@@ -1,0 +1,28 @@
+"""xGMI peer all-reduce (IPC + one fused kernel) with 2 and 4 processes sharing the GPU."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_allreduce_multiprocess(tmp_path, world):
+    code = f"import sys; sys.path.insert(0, {ROOT!r}); from tests.dist_workers import xgmi_spawn_main; " \
+           f"xgmi_spawn_main({str(tmp_path)!r}, {world})"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    for rank in range(world):
+        z = dict(np.load(tmp_path / f"xgmi{rank}.npz"))
+        for k, v in z.items():
+            if k.startswith("ok_") or k in ("sgd_ok", "planes_exact"):
+                assert float(v) == 1.0, (rank, k)
+            elif k.startswith("ar_"):
+                assert float(v) < (1e-6 if "float32" in k else 1e-14), (rank, k, float(v))
+        assert float(z["sgd_err"]) < 1e-4
+        assert float(z["trainer_w1_diff"]) < 1e-5 and float(z["trainer_w2_diff"]) < 1e-5
