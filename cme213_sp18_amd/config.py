@@ -40,6 +40,10 @@ class TrainConfig:
     softmax_shift: bool = True
     ckpt_precision: int = 12
     allreduce: str = "auto"     # auto | xgmi (peer kernel, SGD fused) | rccl
+    comm_timeout: float = 300.0  # seconds before a stuck collective fails the job
+    fault_inject: str = ""      # "rank:step" -- raise on that rank at that step (failure-detection test hook)
+    log_json: str = ""          # rank-0 JSON-lines event log
+    ckpt_every: int = 0         # epochs between checkpoints (needs --ckpt-dir); 0 = only at the end
 
     @property
     def H(self):
@@ -95,6 +99,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-softmax-shift", dest="softmax_shift", action="store_false", default=None)
     ap.add_argument("--ckpt-precision", type=int)
     ap.add_argument("--allreduce", choices=["auto", "xgmi", "rccl"])
+    ap.add_argument("--comm-timeout", type=float)
+    ap.add_argument("--fault-inject", help="rank:step")
+    ap.add_argument("--log-json")
+    ap.add_argument("--ckpt-every", type=int)
     return ap
 
 

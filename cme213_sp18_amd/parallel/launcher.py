@@ -32,8 +32,12 @@ def env_world() -> tuple[int, int, int]:
 def init_distributed(backend: str | None = None, timeout_s: float = 600.0) -> tuple[Communicator, torch.device]:
     """Initialise the process group from env vars; returns (communicator, device)."""
     rank, local_rank, world = env_world()
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
-    if use_gpu:
+    if os.environ.get("CME_SHARED_GPU") == "1":
+        # rehearsal mode: every rank on cuda:0 with a gloo group (RCCL refuses two ranks on one GPU);
+        # exercises the multi-rank GPU code paths (xGMI peer kernel, sharding, bench) on a 1-GPU box
+        torch.cuda.set_device(0)
+        device, backend, use_gpu = torch.device("cuda", 0), "gloo", False
+    elif (use_gpu := torch.cuda.is_available() and backend != "gloo"):
         ndev = torch.cuda.device_count()
         if local_rank >= ndev:
             raise RuntimeError(f"LOCAL_RANK {local_rank} has no GPU to bind to ({ndev} visible)")

@@ -31,6 +31,10 @@ from .comm import Communicator, NullComm
 from .engine import MlpEngine
 
 
+class FaultInjected(RuntimeError):
+    """Raised by ``train(fault=(rank, step))`` -- the failure-detection test hook."""
+
+
 @dataclass
 class EpochPlan:
     steps: list  # [(start, length)]
@@ -203,9 +207,14 @@ class DataParallelTrainer:
 
     # ---------------------------------------------------------------- train
     def train(self, epochs: int, lr: float, reg: float, print_every: int = 0, debug: bool = False,
-              outdir: str = "Outputs", log=print) -> TrainStats:
+              outdir: str = "Outputs", log=print, on_event=None, fault: tuple[int, int] | None = None) -> TrainStats:
         """Full training loop (neural_network.cpp:446-555).  Eager steps where the
-        host must look at a step (loss printing / debug diffs), graphs elsewhere."""
+        host must look at a step (loss printing / debug diffs), graphs elsewhere.
+
+        on_event(dict): structured progress records (loss, epoch) for JSON-lines logs.
+        fault=(rank, step): raise FaultInjected on that rank when the global step
+        counter reaches ``step`` (before it runs) -- tests that a failing rank
+        takes the job down instead of leaving its peers hung."""
         from ..utils.checkpoint import write_diff_gpu_cpu
 
         stats = TrainStats()
@@ -222,21 +231,35 @@ class DataParallelTrainer:
             torch.cuda.synchronize(dev)
         self.comm.barrier()
         t0 = time.perf_counter()
+        def maybe_fault(first: int, count: int):
+            if fault is not None and fault[0] == self.rank and first <= fault[1] < first + count:
+                raise FaultInjected(f"injected fault on rank {self.rank} at step {fault[1]}")
+
         try:
             for epoch in range(epochs):
                 if not host_needed:
+                    maybe_fault(self.iter, len(plan.steps))
                     self.run_plan(plan, lr, reg)
                     self.iter += len(plan.steps)
                     stats.steps += len(plan.steps)
                     stats.images += sum((ln // self.R) * self.R for _, ln in plan.steps)
+                    if on_event is not None:
+                        if dev.type == "cuda":
+                            torch.cuda.synchronize(dev)
+                        el = time.perf_counter() - t0
+                        on_event({"event": "epoch", "epoch": epoch, "iter": self.iter, "seconds": el,
+                                  "images_per_s": stats.images / el if el > 0 else None})
                     continue
                 for bi, (s, ln) in enumerate(plan.steps):
                     it = self.iter
+                    maybe_fault(it, 1)
                     if print_every > 0 and it % print_every == 0:
                         l = self.step_loss(s, ln, lr, reg)
                         stats.losses.append(l)
                         if self.rank == 0:
                             log(f"Loss at iteration {it} of epoch {epoch}/{epochs} = {l:.10g}")
+                        if on_event is not None:
+                            on_event({"event": "loss", "iter": it, "epoch": epoch, "loss": l})
                     else:
                         self.step(s, ln, lr, reg)
                     print_flag = (bi == 0) if print_every <= 0 else (it % print_every == 0)

@@ -28,6 +28,31 @@ def log0(rank: int, *a):
         print(*a, flush=True)
 
 
+class JsonLog:
+    """Rank-0 JSON-lines event log: config, losses, epochs, summary."""
+
+    def __init__(self, path: str, rank: int):
+        self.fh = open(path, "a") if path and rank == 0 else None
+        self.t0 = time.time()
+
+    def __call__(self, rec: dict) -> None:
+        if self.fh is not None:
+            rec = {"t": round(time.time() - self.t0, 6), **rec}
+            self.fh.write(json.dumps(rec, default=float) + "\n")
+            self.fh.flush()
+
+    def close(self):
+        if self.fh is not None:
+            self.fh.close()
+
+
+def parse_fault(spec: str):
+    if not spec:
+        return None
+    r, s = spec.split(":")
+    return int(r), int(s)
+
+
 def run(cfg: TrainConfig) -> dict:
     import torch
 
@@ -42,9 +67,12 @@ def run(cfg: TrainConfig) -> dict:
     backend = cfg.backend
     if backend == "hip" and not torch.cuda.is_available():
         backend = "torch"
-    comm, device = init_distributed("gloo" if backend == "torch" else None)
+    comm, device = init_distributed("gloo" if backend == "torch" else None, timeout_s=cfg.comm_timeout)
     rank, world = comm.rank, comm.world_size
+    jlog = JsonLog(cfg.log_json, rank)
     try:
+        jlog({"event": "config", "world": world, "device": str(device), **{
+            k: v for k, v in vars(cfg).items() if isinstance(v, (int, float, str, bool))}})
         log0(rank, f"Number of processes = {world}")
         log0(rank, f"Device = {device} ({torch.cuda.get_device_name(device) if device.type == 'cuda' else 'cpu'})")
         if cfg.grade == 4:
@@ -85,8 +113,29 @@ def run(cfg: TrainConfig) -> dict:
                                  backend=backend, shift=cfg.softmax_shift, use_graphs=cfg.use_graphs,
                                  normalize=cfg.normalize, path=cfg.path, allreduce=cfg.allreduce)
         tr.load(ds.x_train, ds.y_train)
-        st = tr.train(cfg.num_epochs, cfg.learning_rate, cfg.reg, print_every=cfg.print_every, debug=cfg.debug,
-                      outdir=cfg.outdir, log=lambda m: log0(rank, m))
+        fault = parse_fault(cfg.fault_inject)
+        ckpt_meta = lambda done: {"epochs": done + meta.get("epochs", 0), "lr": cfg.learning_rate, "reg": cfg.reg,
+                                  "seed": cfg.seed, "dtype": cfg.dtype, "iter": tr.iter}
+        seg = cfg.ckpt_every if (cfg.ckpt_every > 0 and cfg.ckpt_dir) else cfg.num_epochs
+        done, st = 0, None
+        while done < cfg.num_epochs or st is None:  # train in checkpoint segments
+            k = min(seg, cfg.num_epochs - done)
+            s1 = tr.train(k, cfg.learning_rate, cfg.reg, print_every=cfg.print_every, debug=cfg.debug,
+                          outdir=cfg.outdir, log=lambda m: log0(rank, m), on_event=jlog, fault=fault)
+            st = s1 if st is None else st
+            if st is not s1:
+                st.seconds += s1.seconds
+                st.steps += s1.steps
+                st.images += s1.images
+                st.losses += s1.losses
+            done += k
+            if cfg.ckpt_dir and done < cfg.num_epochs:
+                if rank == 0:
+                    save_checkpoint(nn, cfg.ckpt_dir, meta=ckpt_meta(done))
+                    jlog({"event": "checkpoint", "dir": cfg.ckpt_dir, "epochs": done})
+                comm.barrier()
+            if k == 0:
+                break
         out.update(par_seconds=st.seconds, images_per_sec=st.images_per_sec, engine_path=tr.engine.path,
                    allreduce=tr.allreduce_impl)
         log0(rank, f"Time for Parallel Training: {st.seconds:.6f} seconds ({st.images_per_sec:,.0f} images/s, "
@@ -99,15 +148,27 @@ def run(cfg: TrainConfig) -> dict:
             if ds.y_test is not None:
                 out["par_test_precision"] = precision(pred, ds.y_test)
             if cfg.ckpt_dir:
-                save_checkpoint(nn, cfg.ckpt_dir, meta={"epochs": cfg.num_epochs + meta.get("epochs", 0),
-                                                        "lr": cfg.learning_rate, "reg": cfg.reg,
-                                                        "seed": cfg.seed, "dtype": cfg.dtype})
+                save_checkpoint(nn, cfg.ckpt_dir, meta=ckpt_meta(cfg.num_epochs))
             if (cfg.grade or cfg.debug) and cfg.run_seq:
                 log0(rank, "\nGrading mode on. Checking for correctness")
                 out["correct"] = checkNNErrors(seq_nn, nn, os.path.join(cfg.outdir, "NNErrors.txt"))
+        jlog({"event": "summary", **{k: v for k, v in out.items() if isinstance(v, (int, float, str, bool))}})
         comm.barrier()
         return out
+    except BaseException as ex:
+        # failure detection: report, then leave without waiting on peers -- torchrun's agent (or the
+        # collective timeout) takes the rest of the job down instead of leaving it hung
+        import traceback
+
+        traceback.print_exc()
+        print(f"[rank {rank}] FATAL: {type(ex).__name__}: {ex}", file=sys.stderr, flush=True)
+        jlog({"event": "fatal", "rank": rank, "error": f"{type(ex).__name__}: {ex}"})
+        jlog.close()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(3)
     finally:
+        jlog.close()
         shutdown()
 
 
