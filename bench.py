@@ -44,8 +44,12 @@ def parse(argv=None):
     ap.add_argument("--scaling", default="weak", choices=["strong", "weak"])
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
-                    help="gradient sync for N>1: xGMI peer kernel with fused SGD (auto/xgmi) or RCCL all-reduce")
+    ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl", "host"],
+                    help="gradient sync for N>1: xGMI peer kernel with fused SGD (auto/xgmi), RCCL all-reduce, "
+                         "or host-staged gloo (reference-equivalent)")
+    ap.add_argument("--mode", default="optimized", choices=["optimized", "reference"],
+                    help="reference: the reference's execution model on MI355X -- unfused PyTorch/hipBLAS ops, "
+                         "no graphs, host-staged gradient all-reduce (for comparison only)")
     ap.add_argument("--train-size", type=int, default=54000)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -53,6 +57,8 @@ def parse(argv=None):
 
 def main(argv=None) -> int:
     a = parse(argv)
+    if a.mode == "reference":
+        a.backend, a.no_graphs, a.allreduce = "torch", True, "host"
     import numpy as np
     import torch
 
@@ -131,6 +137,7 @@ def main(argv=None) -> int:
             "data": "synthetic (MNIST-shaped 784-dim uint8 images, random-init weights)",
             "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": global_batch, "seq_len": None,
                        "parallelism": f"dp{R}", "per_gpu_batch": global_batch // R, "backend": a.backend,
+                       "mode": a.mode,
                        "hip_graphs": tr.use_graphs, "allreduce": tr.allreduce_impl, "params_finite": ok},
         }
         print(json.dumps(rec), flush=True)

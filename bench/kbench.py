@@ -73,7 +73,8 @@ def main(argv=None):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
                 row = {"dtype": dt, "path": e.path + ("+fh" if fused else ""), "H": H, "n": n}
-                for name, fn in (("fwd_head", part(1)), ("wgrad_sgd", part(2)), ("wgrad_grads", part(2, 0)),
+                for name, fn in (("fwd_head", part(1)), ("fwd1", part(1 | 4)), ("head", part(1 | 8)),
+                                 ("wgrad_sgd", part(2)), ("wgrad_grads", part(2, 0)),
                                  ("step_fused", part(3)), ("sgd_flat", lambda: e.sgd(0.0))):
                     row[name + "_us"] = round(timeit(fn, a.reps), 3)
                 flops = 2 * n * (784 * H * 2 + 10 * H * 3)

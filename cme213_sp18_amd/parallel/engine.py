@@ -144,6 +144,10 @@ class MlpEngine:
         else:
             self.dZ1p = None
             self.dZ1g = torch.zeros(H, ld, dtype=torch.bfloat16, device=dev) if self.dtype == "bf16" else self.dZ1
+        # wide layers: scratch for the split-H z2 partial sums of the two-kernel head
+        self.z2buf = None
+        if self.backend == "hip" and H >= 512 and self.pdt == torch.float32:
+            self.z2buf = torch.zeros(int(hip().head_big_scratch_floats(H, ld)), dtype=torch.float32, device=dev)
         nblk = (ld + 15) // 16
         self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
         self._step = None
@@ -234,6 +238,8 @@ class MlpEngine:
                 s.npw = s.npz = self.np
                 s.W1p = self.W1p.data_ptr()
                 s.dZ1p = self.dZ1p.data_ptr()
+            if self.z2buf is not None:
+                s.z2p = self.z2buf.data_ptr()
             self._step = s
         return self._step
 

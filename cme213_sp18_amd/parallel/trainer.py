@@ -72,15 +72,25 @@ class DataParallelTrainer:
         self._graphs: dict = {}
         self.iter = 0
         self.xgmi = self._setup_xgmi(allreduce)
-        self.allreduce_impl = "none" if self.R == 1 else ("xgmi" if self.xgmi is not None else self.comm.name)
+        self.allreduce_impl = "none" if self.R == 1 else (
+            "xgmi" if self.xgmi is not None else "host-gloo" if allreduce == "host" else self.comm.name)
 
     def _setup_xgmi(self, mode: str):
         """Peer-to-peer fused all-reduce+SGD (parallel/xgmi.py) when every rank is a GPU on this node.
         mode: auto (use it if the self-test passes), xgmi (require it), rccl/off (never)."""
         from .comm import TorchDistComm
 
-        if mode not in ("auto", "xgmi", "rccl", "off"):
-            raise ValueError("allreduce must be auto, xgmi, rccl or off")
+        if mode not in ("auto", "xgmi", "rccl", "off", "host"):
+            raise ValueError("allreduce must be auto, xgmi, rccl, host or off")
+        if mode == "host":
+            # reference-equivalent sync: gradients staged through host memory and summed over a
+            # gloo group, as the reference's MPI_Allreduce on host buffers (neural_network.cpp:496-536)
+            self.use_graphs = False
+            if self.R > 1:
+                import torch.distributed as dist
+
+                self._host_group = dist.new_group(backend="gloo")
+            return None
         e = self.engine
         eligible = (self.R > 1 and isinstance(self.comm, TorchDistComm) and e.device.type == "cuda"
                     and e.backend == "hip" and e.params.dtype in (torch.float32, torch.float64))
@@ -108,6 +118,15 @@ class DataParallelTrainer:
 
     def _allreduce_sgd(self, lr: float) -> None:
         e = self.engine
+        if self.allreduce_mode == "host":
+            if self.R > 1:
+                import torch.distributed as dist
+
+                g = e.grads.cpu()
+                dist.all_reduce(g, group=self._host_group)
+                e.grads.copy_(g)
+            e.sgd(lr)
+            return
         if self.xgmi is None:
             self.comm.allreduce_(e.grads)
             e.sgd(lr)
@@ -144,7 +163,7 @@ class DataParallelTrainer:
             self._allreduce_sgd(lr)
             return
         scale = 1.0 / (n * self.R)
-        if isinstance(self.comm, NullComm):  # single process: SGD fused into the weight-gradient kernel
+        if isinstance(self.comm, NullComm) and self.allreduce_mode != "host":  # 1 process: SGD fused into wgrad
             e.run(off, n, scale, reg, lr, sgd=True, with_loss=with_loss)
         else:
             e.run(off, n, scale, reg / self.R, lr, sgd=False, with_loss=with_loss)

@@ -43,6 +43,7 @@ struct MlpStep {
   // split-bf16 path (mlp_split.h): X/XT are bf16, W1p/dZ1p hold npw/npz bf16 planes
   int split = 0, npw = 3, npz = 3, fused_head = 0;
   uintptr_t stamps = 0;  // diagnostics only
+  uintptr_t z2p = 0;     // wide-layer head scratch (head_big_scratch_floats), 0: column head
   float xscale = 1.f;    // split path: inputs are uint8 * xscale
   uintptr_t W1p = 0, dZ1p = 0;
 
@@ -69,7 +70,8 @@ struct MlpStep {
   // Forward + backward for samples [off, off+n) of the resident dataset.
   // sgd=1 applies the update in place (single process); sgd=0 writes the
   // pre-scaled gradients into the bucket for the all-reduce.
-  // parts: bit0 = forward + head, bit1 = weight gradients / update (profiling hook; default both)
+  // parts: bit0 = forward + head, bit1 = weight gradients / update (profiling hook; default both);
+  //        with bit0: +4 skips the head (forward GEMM only), +8 skips the forward GEMM (head only)
   void run(int64_t off, int n, double scale, double reg, double lr, int sgd, int with_loss, uintptr_t stream,
            int parts = 3) {
     CME_REQUIRE(n > 0 && n <= ld, "MlpStep.run: 0 < n <= ld required");
@@ -80,13 +82,14 @@ struct MlpStep {
         if (fused_head) {
           cme::mlp_split_fwdhead(a, S(stream));
         } else {  // tiled forward + the per-column head kernel (fp32 head)
-          cme::mlp_split_fwd1(a, S(stream));
+          if (!(parts & 8)) cme::mlp_split_fwd1(a, S(stream));
           cme::HeadArgs h{};
           h.a1 = a.a1; h.lda = ld; h.W2 = a.W2; h.b2 = a.b2; h.labels = a.labels; h.H = H; h.C = C; h.n = n;
           h.scale = scale; h.D = a.D; h.ldd = ld; h.dZ1 = a.dZ1; h.ldz = ld; h.dZ1_bf16 = nullptr;
           h.dZ1_planes = a.dZ1p; h.npz = npz;
           h.loss_partial = a.loss_partial; h.shift = shift; h.mode = cme::HEAD_TRAIN;
-          cme::mlp_head(DType::F32, h, S(stream));
+          h.z2part = P_<float>(z2p);
+          if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
         }
       }
       if (parts & 2) cme::mlp_split_wgrad(a, S(stream));
@@ -108,6 +111,7 @@ struct MlpStep {
     h.dZ1_bf16 = d == DType::BF16 ? reinterpret_cast<void*>(dZ1g) : nullptr;
     h.loss_partial = with_loss ? P_<float>(loss) : nullptr;
     h.shift = shift; h.mode = cme::HEAD_TRAIN;
+    h.z2part = P_<float>(z2p);
     if (parts & 1) cme::mlp_head(d, h, S(stream));
     cme::WgradArgs w{};
     w.roles = 7;
@@ -167,6 +171,7 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("loss") = 0, py::arg("pred") = 0, py::arg("probs") = 0, py::arg("ldp") = 0,
       py::arg("shift") = 1, py::arg("stream") = 0);
   m.def("mlp_head_num_blocks", &cme::mlp_head_num_blocks);
+  m.def("head_big_scratch_floats", &cme::head_big_scratch_floats);
 
   m.def(
       "mlp_wgrad",
@@ -246,6 +251,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("fused_head", &MlpStep::fused_head)
       .def_readwrite("stamps", &MlpStep::stamps)
       .def_readwrite("xscale", &MlpStep::xscale)
+      .def_readwrite("z2p", &MlpStep::z2p)
       .def_readwrite("npw", &MlpStep::npw)
       .def_readwrite("npz", &MlpStep::npz)
       .def_readwrite("W1p", &MlpStep::W1p)

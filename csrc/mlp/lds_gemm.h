@@ -1,0 +1,194 @@
+// LDS double-buffered MFMA tile engine for the WIDE MLP configs (H >= 512:
+// BASELINE configs 4 and 5, 784-4096-10 and 784-1024-10).
+//
+// At H=100 the step's GEMMs are too small for operand reuse and the
+// wave-split-K engine (mma_tile.h) wins; at H=4096 the same tiles re-read W1
+// 25x and X 256x through L2 (~640 MB per step) -- there the classic blocked
+// GEMM is the right shape (cdna_hip_programming.md §5):
+//   * C[m][n] = sum_k A[m][k] B[n][k], both operands K-contiguous ("NT");
+//     A = NPA exact bf16 planes (split-fp32, see mlp_split.h), B = uint8 pixels
+//     (exact in bf16, converted at fragment read) or bf16.
+//   * BM x BN workgroup tile, 4 waves as 2x2, each wave (BM/2)x(BN/2) built from
+//     16x16 blocks of v_mfma_f32_16x16x32_bf16; BK = 64 per stage.
+//   * global -> VGPR -> LDS staging with 16-byte buffer loads (out-of-range
+//     rows / k return zero: no edge branches), two LDS buffers: the loads of
+//     stage k+1 are in flight while stage k is multiplied, ONE barrier per stage.
+//   * LDS rows padded (+16 B) so the 16-row fragment reads spread over the banks.
+//   * XCD-aware tile order (tiles sharing A rows land on one XCD's L2).
+#pragma once
+
+#include "mma_tile.h"
+
+namespace cme {
+
+namespace lg {
+
+constexpr int kBK = 64;
+constexpr int kThreads = 256;
+constexpr int kARow = kBK * 2 + 16;  // bytes per A row in LDS (bf16, padded)
+
+template <typename TB>
+struct BTraits;
+template <>
+struct BTraits<uint8_t> {
+  static constexpr int kRow = kBK + 16;       // bytes per B row in LDS
+  static constexpr int kChunksPerRow = kBK / 16;
+};
+template <>
+struct BTraits<__hip_bfloat16> {
+  static constexpr int kRow = kBK * 2 + 16;
+  static constexpr int kChunksPerRow = kBK * 2 / 16;
+};
+
+template <int BM, int BN, int NPA, typename TB>
+constexpr int lds_bytes() {
+  return 2 * (NPA * BM * kARow + BN * BTraits<TB>::kRow);
+}
+
+__device__ __forceinline__ bf16x8_t u8x8_to_bf16(uint2 w) {
+  // bytes -> bf16 exactly: bf16(x) for 0 <= x <= 255 via the float bit pattern
+  bf16x8_t r;
+  const uint32_t lo = w.x, hi = w.y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = (__bf16)(float)((lo >> (8 * j)) & 255u);
+    r[4 + j] = (__bf16)(float)((hi >> (8 * j)) & 255u);
+  }
+  return r;
+}
+
+}  // namespace lg
+
+// One BM x BN output tile at (m0, n0).  `lds` must hold lg::lds_bytes<...>()
+// bytes (16-byte aligned).  Requirements (checked by the launcher): K % 16 == 0,
+// lda % 8 == 0 (bf16) and ldb % 16 == 0 bytes, 16-byte aligned operand bases.
+// epi(row, col, v) is called for every in-range element of the tile.
+template <int BM, int BN, int NPA, typename TB, class Epi>
+__device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__ A, int lda, int plane_bytes,
+                                              const TB* __restrict__ B, int ldb, int M, int N, int K, int m0, int n0,
+                                              Epi& epi, char* __restrict__ lds) {
+  using namespace lg;
+  constexpr int WM = BM / 2, WN = BN / 2, MB = WM / 16, NB = WN / 16;
+  constexpr int BROW = BTraits<TB>::kRow, BCPR = BTraits<TB>::kChunksPerRow;
+  constexpr int A_CHUNKS = BM * (kBK * 2 / 16);  // 16-byte chunks per plane per stage
+  constexpr int B_CHUNKS = BN * BCPR;
+  constexpr int AJ = (A_CHUNKS + kThreads - 1) / kThreads, BJ = (B_CHUNKS + kThreads - 1) / kThreads;
+  static_assert(A_CHUNKS % kThreads == 0 && B_CHUNKS % kThreads == 0, "tile/thread mismatch");
+  constexpr int A_BUF = NPA * BM * kARow, B_BUF = BN * BROW;
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(A), rb = make_rsrc(B);
+  char* ldsA = lds;
+  char* ldsB = lds + 2 * A_BUF;
+
+  // per-thread staging coordinates (fixed across stages)
+  int a_off[AJ], a_lds[AJ], b_off[BJ], b_lds[BJ];
+  bool a_ok[AJ], b_ok[BJ];
+#pragma unroll
+  for (int j = 0; j < AJ; ++j) {
+    const int c = t + j * kThreads, r = c >> 3, kc = c & 7;  // 8 chunks of 8 bf16 per row
+    a_ok[j] = m0 + r < M;
+    a_off[j] = ((m0 + r) * lda + kc * 8) * 2;
+    a_lds[j] = r * kARow + kc * 16;
+  }
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) {
+    const int c = t + j * kThreads, r = c / BCPR, kc = c % BCPR;
+    b_ok[j] = n0 + r < N;
+    b_off[j] = (n0 + r) * ldb * (int)sizeof(TB) + kc * 16;
+    b_lds[j] = r * BROW + kc * 16;
+  }
+
+  uint4 ra_reg[NPA][AJ], rb_reg[BJ];
+  auto load_stage = [&](int k0) {
+    const int kb = k0 * 2;  // byte offset of k0 in an A row
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const int kc = (t + j * kThreads) & 7;
+      const bool ok = a_ok[j] && k0 + kc * 8 < K;
+#pragma unroll
+      for (int p = 0; p < NPA; ++p) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? a_off[j] + kb + p * plane_bytes : kOOB, 0, 0);
+        __builtin_memcpy(&ra_reg[p][j], &w, 16);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+      const int kc = (t + j * kThreads) % BCPR;
+      constexpr int EPC = 16 / (int)sizeof(TB);  // elements per chunk
+      const bool ok = b_ok[j] && k0 + kc * EPC < K;
+      const auto w = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? b_off[j] + k0 * (int)sizeof(TB) : kOOB, 0, 0);
+      __builtin_memcpy(&rb_reg[j], &w, 16);
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < NPA; ++p)
+#pragma unroll
+      for (int j = 0; j < AJ; ++j)
+        *reinterpret_cast<uint4*>(ldsA + buf * A_BUF + p * BM * kARow + a_lds[j]) = ra_reg[p][j];
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) *reinterpret_cast<uint4*>(ldsB + buf * B_BUF + b_lds[j]) = rb_reg[j];
+  };
+
+  f32x4 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K + kBK - 1) / kBK;
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load_stage((kt + 1) * kBK);
+    const char* sA = ldsA + buf * A_BUF + (wr * WM + fr) * kARow;
+    const char* sB = ldsB + buf * B_BUF + (wc * WN + fr) * BROW;
+#pragma unroll
+    for (int kk = 0; kk < kBK / 32; ++kk) {
+      bf16x8_t bf[NB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        if constexpr (sizeof(TB) == 1) {
+          const uint2 w = *reinterpret_cast<const uint2*>(sB + nb * 16 * BROW + kk * 32 + fg * 8);
+          bf[nb] = lg::u8x8_to_bf16(w);
+        } else {
+          bf[nb] = *reinterpret_cast<const bf16x8_t*>(sB + nb * 16 * BROW + (kk * 32 + fg * 8) * 2);
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < NPA; ++p) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+          const bf16x8_t af =
+              *reinterpret_cast<const bf16x8_t*>(sA + p * BM * kARow + mb * 16 * kARow + (kk * 32 + fg * 8) * 2);
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[nb], acc[mb][nb], 0, 0, 0);
+        }
+      }
+    }
+    if (kt + 1 < nk) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C layout of 16x16 f32 MFMA -- lane holds col fr, rows 4*fg + i
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wr * WM + mb * 16 + 4 * fg + i;
+        const int col = n0 + wc * WN + nb * 16 + fr;
+        if (row < M && col < N) epi(row, col, acc[mb][nb][i]);
+      }
+}
+
+}  // namespace cme

@@ -43,7 +43,12 @@ struct HeadArgs {
   void* probs; int ldp;           // probs mode: [C][ldp]
   int shift;                      // 1: max-shifted softmax; 0: reference form (common.cpp:13-18)
   int mode;
+  // wide layers (H >= 512, fp32 params, train mode): scratch of head_big_scratch_floats(H, n) floats for
+  // the split-H z2 partial sums; when set, the head runs as two grid-wide kernels instead of one
+  // column-parallel kernel whose per-thread loop over H is serial
+  float* z2part = nullptr;
 };
+int64_t head_big_scratch_floats(int H, int n);
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t stream);
 int mlp_head_num_blocks(int n);
 

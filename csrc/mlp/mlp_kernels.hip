@@ -273,6 +273,164 @@ void launch_head(const HeadArgs& a, hipStream_t s) {
   }
 }
 
+// ------------------------------------------------ K2 for wide layers (H >= 512)
+// z2 = W2 a1 split over H-chunks (partial sums, deterministic), then one pass
+// that finishes softmax / D / loss per column and writes dZ1 (+ planes) for
+// its (H-chunk x 64-column) block: the whole chip works on both phases.
+constexpr int kHBCols = 64, kHBRows = 256, kHBMinH = 512;
+inline int hb_cdiv(int a, int b) { return (a + b - 1) / b; }
+
+inline int hb_cols_pad(int n) { return hb_cdiv(n, kHBCols) * kHBCols; }
+
+template <int NC>
+__device__ __forceinline__ void hb_stage_w2(const float* __restrict__ W2, int C, int H, int h0,
+                                            float (*w2s)[kHBRows]) {
+  for (int i = threadIdx.x; i < NC * kHBRows; i += 256) {
+    const int c = i / kHBRows, hh = i - c * kHBRows;
+    w2s[c][hh] = (c < C && h0 + hh < H) ? W2[(size_t)c * H + h0 + hh] : 0.f;
+  }
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void head_big_z2_kernel(HeadArgs a, int ncb) {
+  __shared__ float w2s[NC][kHBRows];
+  __shared__ float red[4][NC][kHBCols];
+  const int cb = blockIdx.x % ncb, ch = blockIdx.x / ncb;
+  const int t = threadIdx.x, col = t & 63, hq = t >> 6;
+  const int h0 = ch * kHBRows;
+  hb_stage_w2<NC>(static_cast<const float*>(a.W2), a.C, a.H, h0, w2s);
+  __syncthreads();
+  const int bcol = cb * kHBCols + col;
+  const bool ok = bcol < a.n;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.a1);
+  float z[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) z[c] = 0.f;
+#pragma unroll 2
+  for (int j0 = 0; j0 < 64; j0 += 16) {
+    float x[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int h = h0 + hq * 64 + j0 + u;
+      x[u] = buf_load1<float>(ra, (ok && h < a.H) ? (h * a.lda + bcol) * 4 : kOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) z[c] += w2s[c][hq * 64 + j0 + u] * x[u];
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) red[hq][c][col] = z[c];
+  __syncthreads();
+  const int ldz = ncb * kHBCols;
+  for (int i = t; i < NC * kHBCols; i += 256) {
+    const int c = i / kHBCols, cc = i - c * kHBCols;
+    a.z2part[((size_t)ch * NC + c) * ldz + cb * kHBCols + cc] = red[0][c][cc] + red[1][c][cc] + red[2][c][cc] + red[3][c][cc];
+  }
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void head_big_dz_kernel(HeadArgs a, int ncb, int nch) {
+  __shared__ float w2s[NC][kHBRows];
+  __shared__ float ds[NC][kHBCols];
+  __shared__ float lsum[kHBCols];
+  const int cb = blockIdx.x % ncb, ch = blockIdx.x / ncb;
+  const int t = threadIdx.x, col = t & 63, hq = t >> 6;
+  const int h0 = ch * kHBRows;
+  hb_stage_w2<NC>(static_cast<const float*>(a.W2), a.C, a.H, h0, w2s);
+  const int bcol = cb * kHBCols + col;
+  const bool ok = bcol < a.n;
+  if (t < kHBCols) {  // finish z2 -> softmax -> D for this column (every H-chunk block recomputes it)
+    const int ldz = ncb * kHBCols;
+    const float* b2 = static_cast<const float*>(a.b2);
+    float z[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) z[c] = c < a.C ? b2[c] : 0.f;
+    for (int k = 0; k < nch; ++k)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) z[c] += a.z2part[((size_t)k * NC + c) * ldz + bcol];
+    float m = 0.f;
+    if (a.shift) {
+      m = z[0];
+#pragma unroll
+      for (int c = 1; c < NC; ++c) m = (c < a.C && z[c] > m) ? z[c] : m;
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      z[c] = c < a.C ? __expf(z[c] - m) : 0.f;
+      sum += z[c];
+    }
+    const float inv = 1.f / sum;
+    const int lab = ok ? a.labels[bcol] : 0;
+    float pl = 1.f;
+    const float sc = (float)a.scale;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float y = z[c] * inv;
+      pl = c == lab ? y : pl;
+      const float d = (y - (c == lab ? 1.f : 0.f)) * sc;
+      ds[c][col] = (ok && c < a.C) ? d : 0.f;
+      if (ch == 0 && ok && c < a.C) static_cast<float*>(a.D)[(size_t)c * a.ldd + bcol] = d;
+    }
+    lsum[col] = ok ? -__logf(pl) : 0.f;
+  }
+  __syncthreads();
+  if (ch == 0 && a.loss_partial && t < kHBCols / 16) {  // the column head's partial layout: one per 16 columns
+    const int g = cb * (kHBCols / 16) + t;
+    if (g * 16 < a.n) {
+      float s = 0.f;
+      for (int k = 0; k < 16; ++k) s += lsum[t * 16 + k];
+      a.loss_partial[g] = s;
+    }
+  }
+  if (!ok) return;
+  // dZ1 = (W2^T D) .* a1 .* (1 - a1) for rows [h0, h0 + 256) of this column
+  float dcol[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) dcol[c] = ds[c][col];
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.a1);
+  float* dZ1 = static_cast<float*>(a.dZ1);
+  __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
+  __hip_bfloat16* dZp = static_cast<__hip_bfloat16*>(a.dZ1_planes);
+  const size_t pstride = (size_t)a.H * a.ldz;
+  for (int j0 = 0; j0 < 64; j0 += 16) {
+    float x[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int h = h0 + hq * 64 + j0 + u;
+      x[u] = buf_load1<float>(ra, h < a.H ? (h * a.lda + bcol) * 4 : kOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int hl = hq * 64 + j0 + u, h = h0 + hl;
+      if (h >= a.H) break;
+      float da = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) da += w2s[c][hl] * dcol[c];
+      const float dz = da * x[u] * (1.f - x[u]);
+      const size_t zi = (size_t)h * a.ldz + bcol;
+      dZ1[zi] = dz;
+      if (dZlo) dZlo[zi] = __float2bfloat16(dz);
+      if (dZp) {
+        float r = dz;
+        for (int p = 0; p < a.npz; ++p) {
+          const __hip_bfloat16 q = __float2bfloat16(r);
+          dZp[p * pstride + zi] = q;
+          r -= __bfloat162float(q);
+        }
+      }
+    }
+  }
+}
+
+template <int NC>
+void launch_head_big(const HeadArgs& a, hipStream_t s) {
+  const int ncb = hb_cdiv(a.n, kHBCols), nch = hb_cdiv(a.H, kHBRows);
+  head_big_z2_kernel<NC><<<ncb * nch, 256, 0, s>>>(a, ncb);
+  head_big_dz_kernel<NC><<<ncb * nch, 256, 0, s>>>(a, ncb, nch);
+}
+
 // ----------------------------------------------------------------- K3: wgrad
 template <typename P>
 struct EpiWgrad {
@@ -555,9 +713,18 @@ void mlp_forward1(DType dt, const void* W1g, const void* b1, const void* X, int 
 
 int mlp_head_num_blocks(int n) { return cdiv(n, kHeadCols); }
 
+int64_t head_big_scratch_floats(int H, int n) { return (int64_t)cdiv(H, kHBRows) * kCMax * hb_cols_pad(n); }
+
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
   CME_REQUIRE(a.C >= 1 && a.C <= kCMax, "mlp_head: 1 <= C <= 16 required");
+  if (a.z2part && dt != DType::F64 && a.mode == HEAD_TRAIN && a.H >= kHBMinH) {
+    CME_REQUIRE((int64_t)a.H * a.lda < (int64_t)kOOB / 4, "mlp_head: a1 too large for 32-bit buffer offsets");
+    if (a.C == 10) launch_head_big<10>(a, s);
+    else launch_head_big<16>(a, s);
+    CME_LAUNCH_CHECK(s);
+    return;
+  }
   if (dt == DType::F64) {
     if (a.C == 10) launch_head<double, 10>(a, s);
     else launch_head<double, 16>(a, s);

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 
+#include "lds_gemm.h"
 #include "mma_tile.h"
 
 namespace cme {
@@ -362,9 +363,126 @@ __global__ __launch_bounds__(256) void sgd_planes_kernel(float* __restrict__ prm
   }
 }
 
+// ======================================================================
+// Wide configs (H >= 512): LDS double-buffered blocked GEMMs (lds_gemm.h)
+// for a1 = sigmoid(W1 X + b1) and dW1 = dZ1 X^T (+ reg / SGD / planes).
+// ======================================================================
+struct EpiSigBig {
+  const float* b1;
+  float* a1;
+  int ld;
+  float xscale;
+  __device__ __forceinline__ void operator()(int row, int col, float v) {
+    a1[(size_t)row * ld + col] = sigm(v * xscale + b1[row]);
+  }
+};
+
+struct EpiW1Big {
+  float* W1;
+  float* gW1;
+  bf16* W1p;
+  size_t plane;
+  int P, sgd, npw;
+  float reg, lr, xscale;
+  __device__ __forceinline__ void operator()(int row, int col, float v) {
+    const size_t i = (size_t)row * P + col;
+    const float w = W1[i];
+    const float g = v * xscale + reg * w;
+    if (sgd) {
+      const float nw = w - lr * g;
+      W1[i] = nw;
+      if (npw == 3) split_store<3>(nw, W1p, plane, i);
+      else split_store<1>(nw, W1p, plane, i);
+    } else {
+      gW1[i] = g;
+    }
+  }
+};
+
+template <int BM, int BN, int NPW>
+__global__ __launch_bounds__(lg::kThreads) void fwd1_big_kernel(SplitStepArgs a, int tn) {
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  EpiSigBig epi{a.b1, a.a1, a.ld, a.xscale};
+  lds_gemm_tile<BM, BN, NPW, uint8_t>(static_cast<const bf16*>(a.W1p), a.P, a.H * a.P * (int)sizeof(bf16),
+                                      static_cast<const uint8_t*>(a.X), a.P, a.H, a.n, a.P, (id / tn) * BM,
+                                      (id % tn) * BN, epi, lds_dyn);
+}
+
+template <int BM, int BN, int NPZ>
+__global__ __launch_bounds__(lg::kThreads) void wgrad_big_kernel(SplitStepArgs a, int tn) {
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  EpiW1Big epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw,
+               (float)a.reg, (float)a.lr, a.xscale};
+  lds_gemm_tile<BM, BN, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
+                                      static_cast<const uint8_t*>(a.XT), a.ldxt, a.H, a.P, a.n, (id / tn) * BM,
+                                      (id % tn) * BN, epi, lds_dyn);
+}
+
+template <auto Kern>
+void set_lds_limit(int bytes) {
+  static bool done = false;  // one attribute call per kernel instantiation
+  if (!done) {
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(Kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  bytes));
+    done = true;
+  }
+}
+
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 inline bool al4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
+
+constexpr int kBigMinH = 512;
+bool big_path_disabled() {  // CME_NO_BIG_GEMM=1: force the wave-split-K kernels (A/B tests)
+  static const bool v = [] {
+    const char* e = std::getenv("CME_NO_BIG_GEMM");
+    return e && e[0] == '1';
+  }();
+  return v;
+}  // below this the wave-split-K kernels win (too few tiles to fill the chip)
+
+// true when the LDS-staged GEMM path applies: wide hidden layer and 16-byte aligned K-contiguous rows
+bool big_fwd_ok(const SplitStepArgs& a) {
+  return a.H >= kBigMinH && a.P % 16 == 0 && al16(a.W1p) && al16(a.X);
+}
+bool big_wgrad_ok(const SplitStepArgs& a) {
+  return a.H >= kBigMinH && a.n % 16 == 0 && a.ld % 8 == 0 && a.ldxt % 16 == 0 && al16(a.dZ1p) && al16(a.XT);
+}
+
+// 128x128 tiles when that still gives ~200+ workgroups, else 64x64
+template <int NP>
+void launch_fwd1_big(const SplitStepArgs& a, hipStream_t s) {
+  const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
+  if (t128 >= 192) {
+    constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
+    set_lds_limit<fwd1_big_kernel<128, 128, NP>>(L);
+    const int tn = cdiv(a.n, 128);
+    fwd1_big_kernel<128, 128, NP><<<t128, lg::kThreads, L, s>>>(a, tn);
+  } else {
+    constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
+    set_lds_limit<fwd1_big_kernel<64, 64, NP>>(L);
+    const int tn = cdiv(a.n, 64);
+    fwd1_big_kernel<64, 64, NP><<<cdiv(a.H, 64) * tn, lg::kThreads, L, s>>>(a, tn);
+  }
+}
+
+template <int NP>
+void launch_wgrad_big(const SplitStepArgs& a, hipStream_t s) {
+  const int t128 = cdiv(a.H, 128) * cdiv(a.P, 128);
+  if (t128 >= 192) {
+    constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
+    set_lds_limit<wgrad_big_kernel<128, 128, NP>>(L);
+    const int tn = cdiv(a.P, 128);
+    wgrad_big_kernel<128, 128, NP><<<t128, lg::kThreads, L, s>>>(a, tn);
+  } else {
+    constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
+    set_lds_limit<wgrad_big_kernel<64, 64, NP>>(L);
+    const int tn = cdiv(a.P, 64);
+    wgrad_big_kernel<64, 64, NP><<<cdiv(a.H, 64) * tn, lg::kThreads, L, s>>>(a, tn);
+  }
+}
 
 template <int NPW, int NPZ, int NC>
 void launch_fwdhead(const SplitStepArgs& a, hipStream_t s) {
@@ -389,6 +507,12 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
   CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
               "split path: operand too large for 32-bit buffer offsets");
   CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
+  if (big_fwd_ok(a) && !big_path_disabled()) {
+    if (a.npw == 3) launch_fwd1_big<3>(a, s);
+    else launch_fwd1_big<1>(a, s);
+    CME_LAUNCH_CHECK(s);
+    return;
+  }
   const int tn = cdiv(a.n, 16 * kF1NB), tm = cdiv(a.H, 16 * kF1MB);
   const bool vec = al4(a.X) && al16(a.W1p) && a.P % 8 == 0;
   const dim3 grid(tm * tn);
@@ -417,7 +541,12 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
   CME_REQUIRE((int64_t)a.H * a.ld * 2 * a.npz < (int64_t)kOOB && (int64_t)a.P * a.ldxt < (int64_t)kOOB,
               "split path: operand too large for 32-bit buffer offsets");
-  const int t1n = cdiv(a.P, 16 * kWNB), t1 = cdiv(a.H, 16 * kWMB) * t1n;
+  const bool big = big_wgrad_ok(a) && !big_path_disabled();
+  if (big) {  // dW1 as a blocked GEMM; dW2 + bias roles stay in the split kernel below (t1 = 0)
+    if (a.npz == 3) launch_wgrad_big<3>(a, s);
+    else launch_wgrad_big<1>(a, s);
+  }
+  const int t1n = cdiv(a.P, 16 * kWNB), t1 = big ? 0 : cdiv(a.H, 16 * kWMB) * t1n;
   const int t2 = cdiv(a.H, kWKS);
   const int tb = cdiv(a.H + a.C, kWKS);
   // dZ1 planes: 16-byte vectors when n % 8 == 0, 8-byte halves when n % 4 == 0; XT bytes need 4-byte rows

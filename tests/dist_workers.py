@@ -5,7 +5,7 @@ import numpy as np
 import torch
 
 
-def dp_train_worker(rank, world, comm, device, out_dir, H, N, batch, epochs, lr, reg, dtype):
+def dp_train_worker(rank, world, comm, device, out_dir, H, N, batch, epochs, lr, reg, dtype, allreduce="auto"):
     torch.set_num_threads(2)
     from cme213_sp18_amd import NeuralNetwork
     from cme213_sp18_amd.parallel import DataParallelTrainer
@@ -14,7 +14,7 @@ def dp_train_worker(rank, world, comm, device, out_dir, H, N, batch, epochs, lr,
     x, y = synthetic_mnist(N, seed=11)
     nn = NeuralNetwork([784, H, 10])
     tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=dtype, batch_size=batch, backend="torch",
-                             use_graphs=False)
+                             use_graphs=False, allreduce=allreduce)
     tr.load(x, y)
     st = tr.train(epochs, lr, reg, print_every=2, log=lambda *_: None)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), W0=nn.W[0], W1=nn.W[1], b0=nn.b[0], b1=nn.b[1],

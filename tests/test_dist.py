@@ -32,11 +32,13 @@ def test_gloo_allreduce_broadcast(tmp_path):
         np.testing.assert_array_equal(v[6:], 1.0)
 
 
-def test_gloo_dp_equals_single_process(tmp_path):
+@pytest.mark.parametrize("allreduce", ["auto", "host"])
+def test_gloo_dp_equals_single_process(tmp_path, allreduce):
     """R=2 ranks, global batch 800 (400 columns each), pre-scaled SUM all-reduce
-    == single-process training on the same global batches (checkNNErrors-grade)."""
+    (device collective, or host-staged as the reference) == single-process training
+    on the same global batches (checkNNErrors-grade)."""
     H, N, B, E, lr, reg = 24, 2400, 800, 2, 0.05, 1e-4
-    spawn(dp_train_worker, 2, args=(str(tmp_path), H, N, B, E, lr, reg, "f64"), backend="gloo")
+    spawn(dp_train_worker, 2, args=(str(tmp_path), H, N, B, E, lr, reg, "f64", allreduce), backend="gloo")
     ref, st = _single(H, N, B, E, lr, reg)
     r0 = np.load(tmp_path / "rank0.npz")
     r1 = np.load(tmp_path / "rank1.npz")

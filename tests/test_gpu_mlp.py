@@ -234,3 +234,26 @@ def test_gpu_f32_close_to_cpu_oracle():
     t.train(2, 0.01, 1e-4)
     for i in range(2):
         assert np.abs(par.W[i] - seq.W[i]).max() / np.abs(seq.W[i]).max() < 1e-4
+
+
+@pytest.mark.parametrize("dt,path", [("f32", "split3"), ("bf16", "split1"), ("f32", "mfma"), ("bf16", "mfma")])
+@pytest.mark.parametrize("H,n", [(512, 800), (1024, 800), (1024, 100), (4096, 800), (4096, 160), (700, 37)])
+def test_wide_step_matches_torch(dt, path, H, n):
+    """H >= 512 takes the LDS double-buffered blocked GEMMs (lds_gemm.h) for a1 and dW1
+    (n % 16 != 0 keeps the wave-split-K dW1) and the two-kernel split-H head:
+    gradients, loss and the fused SGD vs PyTorch."""
+    hipe, te = _engine_pair(dt, H=H, n=n, N=2 * n + 64, path=path)
+    for e in (hipe, te):
+        e.run(64, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
+    torch.cuda.synchronize()
+    tol = TOL[(dt, path)]
+    for name in ("gW1", "gb1", "gW2", "gb2"):
+        assert _rel(getattr(hipe, name), getattr(te, name)) < tol, name
+    assert _rel(hipe.a1[:, :n], te.a1[:, :n]) < max(tol, 1e-5)
+    assert abs(hipe.loss_sum() - te.loss_sum()) / te.loss_sum() < 1e-4
+    for e in (hipe, te):
+        e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+    torch.cuda.synchronize()
+    assert _rel(hipe.params, te.params) < (1e-5 if dt == "f32" else 1e-2)
+    if path == "split3":
+        assert torch.equal(hipe.W1p.float().sum(0), hipe.W1)
