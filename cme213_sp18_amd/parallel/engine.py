@@ -258,6 +258,21 @@ class MlpEngine:
         else:
             self._torch_step(off, n, scale, reg, lr, sgd, with_loss)
 
+    def run_forward_head(self, off: int, n: int, scale: float, with_loss: bool = False):
+        """Forward + head only (a1, D, dZ1 and its planes); the weight gradients follow via run_wgrad."""
+        self._hip_step().run(int(off), int(n), float(scale), 0.0, 0.0, 0, int(bool(with_loss)),
+                             torch.cuda.current_stream(self.device).cuda_stream, 1)
+
+    def run_wgrad(self, off: int, n: int, scale: float, reg: float, parts: int, row0: int = 0, rows: int = -1):
+        """Gradient pieces into ``self.grads`` (split paths): parts bit0 = dW1 rows [row0, row0+rows),
+        bit1 = dW2 + bias gradients."""
+        self._hip_step().run_wgrad(int(off), int(n), float(scale), float(reg), 0.0, 0, int(parts), int(row0),
+                                   int(rows), torch.cuda.current_stream(self.device).cuda_stream)
+
+    @property
+    def supports_bucketed_wgrad(self) -> bool:
+        return self.backend == "hip" and bool(self.np)
+
     def _torch_step(self, off, n, scale, reg, lr, sgd, with_loss):
         """Same math as the HIP step in PyTorch ops (param dtype accumulation)."""
         with torch.no_grad():

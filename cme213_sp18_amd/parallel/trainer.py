@@ -31,6 +31,10 @@ from .comm import Communicator, NullComm
 from .engine import MlpEngine
 
 
+XGMI_AUTO_MAX_BYTES = 2 << 20  # allreduce="auto" uses the xGMI one-shot kernel up to this bucket size
+BUCKET_BYTES = 4 << 20         # dW1 all-reduce chunk of the overlapped RCCL backward
+
+
 class FaultInjected(RuntimeError):
     """Raised by ``train(fault=(rank, step))`` -- the failure-detection test hook."""
 
@@ -55,7 +59,7 @@ class TrainStats:
 class DataParallelTrainer:
     def __init__(self, nn, comm: Communicator | None = None, device=None, dtype: str = "f32",
                  batch_size: int = 800, backend: str = "hip", shift: bool = True, use_graphs: bool = True,
-                 normalize: bool = False, path: str = "auto", allreduce: str = "auto"):
+                 normalize: bool = False, path: str = "auto", allreduce: str = "auto", overlap: bool = True):
         self.nn = nn
         self.comm = comm or NullComm()
         self.R = self.comm.world_size
@@ -72,6 +76,9 @@ class DataParallelTrainer:
         self._graphs: dict = {}
         self.iter = 0
         self.xgmi = self._setup_xgmi(allreduce)
+        self._bucketed = (self.R > 1 and self.xgmi is None and allreduce != "host" and overlap
+                          and self.engine.supports_bucketed_wgrad and self.engine.device.type == "cuda")
+        self._comm_stream = torch.cuda.Stream(self.engine.device) if self._bucketed else None
         self.allreduce_impl = "none" if self.R == 1 else (
             "xgmi" if self.xgmi is not None else "host-gloo" if allreduce == "host" else self.comm.name)
 
@@ -101,6 +108,10 @@ class DataParallelTrainer:
         from .xgmi import XgmiBucket, same_node
 
         if mode == "auto" and (not same_node(self.R) or self.R > 8):
+            return None
+        # one-shot: every rank pulls all R-1 peer buckets over its links -- the win for latency-bound
+        # buckets (318 KB at H=100); past a few MB the ring/tree of RCCL moves fewer bytes per link
+        if mode == "auto" and e.params.numel() * e.params.element_size() > XGMI_AUTO_MAX_BYTES:
             return None
         try:
             xb = XgmiBucket(self.comm.group, self.rank, self.R, e.params.numel(), e.params.dtype, e.device)
@@ -165,9 +176,43 @@ class DataParallelTrainer:
         scale = 1.0 / (n * self.R)
         if isinstance(self.comm, NullComm) and self.allreduce_mode != "host":  # 1 process: SGD fused into wgrad
             e.run(off, n, scale, reg, lr, sgd=True, with_loss=with_loss)
+        elif self._bucketed:
+            self._step_bucketed(off, n, scale, reg / self.R, lr, with_loss)
         else:
             e.run(off, n, scale, reg / self.R, lr, sgd=False, with_loss=with_loss)
             self._allreduce_sgd(lr)
+
+    def _buckets(self):
+        """dW1 row chunks of ~BUCKET_BYTES (multiples of 128 rows, the blocked-GEMM tile)."""
+        e = self.engine
+        w1_bytes = e.H * e.P * e.params.element_size()
+        k = max(1, min(8, -(-w1_bytes // BUCKET_BYTES)))
+        rows = -(-e.H // k)
+        rows = -(-rows // 128) * 128
+        return [(r0, min(rows, e.H - r0)) for r0 in range(0, e.H, rows)]
+
+    def _step_bucketed(self, off, n, scale, reg, lr, with_loss):
+        """Backward with the gradient all-reduce overlapped (RCCL path): the small
+        [b1|W2|b2] bucket goes out first, then every dW1 row chunk as soon as its blocked GEMM has
+        finished, on a side stream while the next chunk is still being computed."""
+        e = self.engine
+        cur = torch.cuda.current_stream(e.device)
+        cs = self._comm_stream
+        e.run_forward_head(off, n, scale, with_loss)
+        e.run_wgrad(off, n, scale, reg, parts=2)
+        w1n = e.H * e.P
+        pieces = [(e.grads[w1n:], None)] + [(e.grads[r0 * e.P:(r0 + rows) * e.P], (r0, rows))
+                                            for r0, rows in self._buckets()]
+        for view, rng in pieces:
+            if rng is not None:
+                e.run_wgrad(off, n, scale, reg, parts=1, row0=rng[0], rows=rng[1])
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            cs.wait_event(ev)
+            with torch.cuda.stream(cs):
+                self.comm.allreduce_(view)
+        cur.wait_stream(cs)
+        e.sgd(lr)
 
     def step_loss(self, start: int, length: int, lr: float, reg: float) -> float:
         """One step that also returns the (pre-update) global loss -- reference

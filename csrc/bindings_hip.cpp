@@ -131,6 +131,20 @@ struct MlpStep {
     if (parts & 2) cme::mlp_wgrad(d, w, S(stream));
   }
 
+  // Weight-gradient pieces of a step whose forward + head already ran (parts=1): used by the
+  // trainer to overlap per-bucket all-reduces with the rest of the backward pass.
+  // parts bit0 = dW1 rows [row0, row0+rows), bit1 = dW2 + bias gradients.  Split paths only.
+  void run_wgrad(int64_t off, int n, double scale, double reg, double lr, int sgd, int parts, int row0, int rows,
+                 uintptr_t stream) {
+    CME_REQUIRE(split, "MlpStep.run_wgrad: split (bf16-plane) paths only");
+    CME_REQUIRE(n > 0 && n <= ld, "MlpStep.run_wgrad: 0 < n <= ld required");
+    cme::SplitStepArgs a = split_args(off, n, scale, reg, lr, sgd, 0);
+    a.wg_parts = parts;
+    a.w1_row0 = row0;
+    a.w1_rows = rows;
+    cme::mlp_split_wgrad(a, S(stream));
+  }
+
   template <typename T>
   static T* P_(uintptr_t p) { return reinterpret_cast<T*>(p); }
 };
@@ -252,6 +266,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("stamps", &MlpStep::stamps)
       .def_readwrite("xscale", &MlpStep::xscale)
       .def_readwrite("z2p", &MlpStep::z2p)
+      .def("run_wgrad", &MlpStep::run_wgrad, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"),
+           py::arg("lr"), py::arg("sgd"), py::arg("parts"), py::arg("row0"), py::arg("rows"), py::arg("stream"))
       .def_readwrite("npw", &MlpStep::npw)
       .def_readwrite("npz", &MlpStep::npz)
       .def_readwrite("W1p", &MlpStep::W1p)

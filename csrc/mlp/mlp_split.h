@@ -47,6 +47,9 @@ struct SplitStepArgs {
   float* probs = nullptr;
   int ldp = 0;
   unsigned long long* stamps = nullptr;  // diagnostics: per-wave s_memrealtime stamps (see mma_tile.h)
+  // weight-gradient launch selection (bucketed all-reduce overlap): wg_parts bit0 = dW1 rows
+  // [w1_row0, w1_row0 + w1_rows) (w1_rows < 0: all), bit1 = dW2 + bias gradients
+  int wg_parts = 3, w1_row0 = 0, w1_rows = -1;
 };
 
 void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);

@@ -268,7 +268,8 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   const float reg = (float)a.reg, lr = (float)a.lr;
   if (bid < t1) {  // ---- dW1 tile
     const int tb = xcd_remap(bid, t1);
-    TileGeom g{a.H, a.P, a.n, (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
+    const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
+    TileGeom g{r1, a.P, a.n, a.w1_row0 + (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
     EpiW1 epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw, reg, lr, a.xscale, {}};
     constexpr int U = 4;
     wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
@@ -415,9 +416,10 @@ __global__ __launch_bounds__(lg::kThreads) void wgrad_big_kernel(SplitStepArgs a
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   EpiW1Big epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw,
                (float)a.reg, (float)a.lr, a.xscale};
+  const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
   lds_gemm_tile<BM, BN, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
-                                      static_cast<const uint8_t*>(a.XT), a.ldxt, a.H, a.P, a.n, (id / tn) * BM,
-                                      (id % tn) * BN, epi, lds_dyn);
+                                      static_cast<const uint8_t*>(a.XT), a.ldxt, r1, a.P, a.n,
+                                      a.w1_row0 + (id / tn) * BM, (id % tn) * BN, epi, lds_dyn);
 }
 
 template <auto Kern>
@@ -470,7 +472,8 @@ void launch_fwd1_big(const SplitStepArgs& a, hipStream_t s) {
 
 template <int NP>
 void launch_wgrad_big(const SplitStepArgs& a, hipStream_t s) {
-  const int t128 = cdiv(a.H, 128) * cdiv(a.P, 128);
+  const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
+  const int t128 = cdiv(rows, 128) * cdiv(a.P, 128);
   if (t128 >= 192) {
     constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
     set_lds_limit<wgrad_big_kernel<128, 128, NP>>(L);
@@ -480,7 +483,7 @@ void launch_wgrad_big(const SplitStepArgs& a, hipStream_t s) {
     constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
     set_lds_limit<wgrad_big_kernel<64, 64, NP>>(L);
     const int tn = cdiv(a.P, 64);
-    wgrad_big_kernel<64, 64, NP><<<cdiv(a.H, 64) * tn, lg::kThreads, L, s>>>(a, tn);
+    wgrad_big_kernel<64, 64, NP><<<cdiv(rows, 64) * tn, lg::kThreads, L, s>>>(a, tn);
   }
 }
 
@@ -541,14 +544,21 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
   CME_REQUIRE((int64_t)a.H * a.ld * 2 * a.npz < (int64_t)kOOB && (int64_t)a.P * a.ldxt < (int64_t)kOOB,
               "split path: operand too large for 32-bit buffer offsets");
+  CME_REQUIRE(a.w1_row0 >= 0 && (a.w1_rows < 0 || a.w1_row0 + a.w1_rows <= a.H), "wgrad: bad dW1 row range");
   const bool big = big_wgrad_ok(a) && !big_path_disabled();
-  if (big) {  // dW1 as a blocked GEMM; dW2 + bias roles stay in the split kernel below (t1 = 0)
+  const bool do_w1 = (a.wg_parts & 1) && a.w1_rows != 0, do_roles = (a.wg_parts & 2) != 0;
+  if (big && do_w1) {  // dW1 as a blocked GEMM; dW2 + bias roles stay in the split kernel below (t1 = 0)
     if (a.npz == 3) launch_wgrad_big<3>(a, s);
     else launch_wgrad_big<1>(a, s);
   }
-  const int t1n = cdiv(a.P, 16 * kWNB), t1 = big ? 0 : cdiv(a.H, 16 * kWMB) * t1n;
-  const int t2 = cdiv(a.H, kWKS);
-  const int tb = cdiv(a.H + a.C, kWKS);
+  const int w1rows = a.w1_rows < 0 ? a.H : a.w1_rows;
+  const int t1n = cdiv(a.P, 16 * kWNB), t1 = (big || !do_w1) ? 0 : cdiv(w1rows, 16 * kWMB) * t1n;
+  const int t2 = do_roles ? cdiv(a.H, kWKS) : 0;
+  const int tb = do_roles ? cdiv(a.H + a.C, kWKS) : 0;
+  if (t1 + t2 + tb == 0) {
+    CME_LAUNCH_CHECK(s);
+    return;
+  }
   // dZ1 planes: 16-byte vectors when n % 8 == 0, 8-byte halves when n % 4 == 0; XT bytes need 4-byte rows
   const bool base_ok = al16(a.dZ1p) && al4(a.XT) && a.ld % 8 == 0 && a.ldxt % 4 == 0;
   const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? 1 : (a.n % 4 == 0 ? 2 : 0));

@@ -131,6 +131,21 @@ def xgmi_worker(rank, world, comm, device, out_dir):
         out[mode] = nn.W[0].copy(), nn.W[1].copy()
     res["trainer_w1_diff"] = float(np.abs(out["xgmi"][0] - out["off"][0]).max())
     res["trainer_w2_diff"] = float(np.abs(out["xgmi"][1] - out["off"][1]).max())
+    # overlapped bucketed backward (dW1 row chunks all-reduced on a side stream) vs one bucket
+    import cme213_sp18_amd.parallel.trainer as trmod
+
+    trmod.BUCKET_BYTES = 256 << 10  # force several chunks (incl. a partial one)
+    for H in (300, 1024):
+        outs = {}
+        for overlap in (True, False):
+            nn = NeuralNetwork([784, H, 10])
+            tr = DataParallelTrainer(nn, comm=comm, device=dev, batch_size=800, use_graphs=False, allreduce="rccl",
+                                     overlap=overlap)
+            assert tr._bucketed == overlap and len(tr._buckets()) > 1
+            tr.load(x, y)
+            tr.train(2, 0.05, 1e-4)
+            outs[overlap] = np.concatenate([nn.W[0].ravel(), nn.W[1].ravel(), nn.b[0].ravel(), nn.b[1].ravel()])
+        res[f"bucketed_diff_{H}"] = float(np.abs(outs[True] - outs[False]).max())
     np.savez(os.path.join(out_dir, f"xgmi{rank}.npz"), **{k: np.array(v) for k, v in res.items()})
 
 

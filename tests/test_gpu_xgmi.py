@@ -26,3 +26,5 @@ def test_xgmi_allreduce_multiprocess(tmp_path, world):
                 assert float(v) < (1e-6 if "float32" in k else 1e-14), (rank, k, float(v))
         assert float(z["sgd_err"]) < 1e-4
         assert float(z["trainer_w1_diff"]) < 1e-5 and float(z["trainer_w2_diff"]) < 1e-5
+        for H in (300, 1024):  # 2 ranks: a+b is exact in any order -> bitwise; 4 ranks: rounding only
+            assert float(z[f"bucketed_diff_{H}"]) <= (0.0 if world == 2 else 1e-6), (H, float(z[f"bucketed_diff_{H}"]))
