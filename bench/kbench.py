@@ -36,13 +36,19 @@ def main(argv=None):
     x, y = synthetic_mnist(8000, seed=0)
     results = []
 
+    join = None
+
     def timeit(fn, reps):
         fn()
+        if join is not None:
+            join()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for _ in range(reps):
                 fn()
+            if join is not None:
+                join()
         g.replay()
         torch.cuda.synchronize()
         best = float("inf")
@@ -66,6 +72,7 @@ def main(argv=None):
                 e.set_params(*nn.params)
                 e.load_dataset(x, y)
                 step = e._hip_step()
+                join = e.join
                 step.fused_head = int(fused)
                 st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
 
@@ -73,6 +80,10 @@ def main(argv=None):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
                 row = {"dtype": dt, "path": e.path + ("+fh" if fused else ""), "H": H, "n": n}
+                if e.np:  # split paths: the weight-gradient launch's two halves on their own
+                    for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
+                        row[name + "_us"] = round(timeit(
+                            lambda prt=prt: step.run_wgrad(0, n, 1.0 / n, 1e-4, 0.0, 0, prt, 0, -1, st()), a.reps), 3)
                 for name, fn in (("fwd_head", part(1)), ("fwd1", part(1 | 4)), ("head", part(1 | 8)),
                                  ("wgrad_sgd", part(2)), ("wgrad_grads", part(2, 0)),
                                  ("step_fused", part(3)), ("sgd_flat", lambda: e.sgd(0.0))):

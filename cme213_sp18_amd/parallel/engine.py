@@ -86,7 +86,8 @@ def resolve_path(dtype: str, path: str = "auto") -> str:
 
 class MlpEngine:
     def __init__(self, H=(784, 100, 10), dtype: str = "f32", max_cols: int = 800, device=None,
-                 backend: str = "hip", shift: bool = True, feature_major_copy: bool = True, path: str = "auto"):
+                 backend: str = "hip", shift: bool = True, feature_major_copy: bool = True, path: str = "auto",
+                 overlap_roles: bool = False):
         if dtype not in DTYPE_CODES:
             raise ValueError(f"dtype must be one of {list(DTYPE_CODES)}")
         self.P, self.H, self.C = (int(h) for h in H)
@@ -115,6 +116,15 @@ class MlpEngine:
         # is nothing next to 288 GB of HBM.
         self.feature_major_copy = bool(feature_major_copy) or self.path.startswith("split")
         self._configure_path()
+        # split paths: the dW2/db2 role kernel runs on a side stream, concurrently with dW1 and the
+        # next step's forward GEMM (a1 is double-buffered so that forward cannot overwrite it early)
+        import os
+
+        # measured: a second stream inside the HIP graph costs more than it hides at these kernel
+        # sizes (20 -> 34 us/step), so it is off unless asked for (CME_ROLE_OVERLAP=1)
+        self.overlap_roles = ((bool(overlap_roles) or os.environ.get("CME_ROLE_OVERLAP") == "1")
+                              and backend == "hip" and self.device.type == "cuda")
+        self._aux_stream = None
         self._alloc_acts(max_cols)
         self._step = None
 
@@ -136,6 +146,8 @@ class MlpEngine:
         self.ld = _round_up(max(int(max_cols), 1), 16)
         dev, H, C, ld = self.device, self.H, self.C, self.ld
         self.a1 = torch.zeros(H, ld, dtype=self.pdt, device=dev)
+        self._a1bufs = [self.a1, torch.zeros_like(self.a1)] if (self.overlap_roles and self.np) else None
+        self._a1k = 0
         self.dZ1 = torch.zeros(H, ld, dtype=self.pdt, device=dev)
         self.D = torch.zeros(C, ld, dtype=self.pdt, device=dev)
         if self.np:
@@ -149,6 +161,14 @@ class MlpEngine:
         if self.backend == "hip" and H >= 512 and self.pdt == torch.float32:
             self.z2buf = torch.zeros(int(hip().head_big_scratch_floats(H, ld)), dtype=torch.float32, device=dev)
         nblk = (ld + 15) // 16
+        # optional (CME_HEAD_PARTIALS=1, needs CME_NO_BIAS_COL=1): the head leaves per-16-column partials
+        # of dW2|db1|db2 for the weight-gradient launch to reduce; the default instead overlaps the
+        # dW2/db2 role kernel with dW1 on a side stream and takes db1 from the dW1 GEMM
+        import os
+
+        self.gpart = None
+        if self.backend == "hip" and self.np and H <= 128 and os.environ.get("CME_HEAD_PARTIALS") == "1":
+            self.gpart = torch.zeros(nblk * (C * H + H + C), dtype=torch.float32, device=dev)
         self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
         self._step = None
 
@@ -181,13 +201,21 @@ class MlpEngine:
             if normalize:
                 xd = xd / 255.0
             self.X = xd.to(self.gdt).contiguous()
-        self.XT = self.X.t().contiguous() if self.feature_major_copy else None
+        import os
+
+        if self.feature_major_copy and self.np and os.environ.get("CME_NO_BIAS_COL") != "1":
+            # + an all-ones feature row: the dW1 GEMM's extra column is db1 (no separate bias reduction)
+            self.XT = torch.cat([self.X.t(), torch.ones(1, self.X.shape[0], dtype=self.X.dtype, device=self.device)])
+            self.XT = self.XT.contiguous()
+        else:
+            self.XT = self.X.t().contiguous() if self.feature_major_copy else None
         self.labels = torch.as_tensor(np.asarray(labels, dtype=np.int32)).to(self.device).contiguous()
         self.num_samples = int(self.X.shape[0])
         self._step = None
         self.refresh_shadow()
 
     def set_params(self, W1, b1, W2, b2):
+        self.join()
         with torch.no_grad():
             for dst, src in ((self.W1, W1), (self.b1, b1), (self.W2, W2), (self.b2, b2)):
                 dst.copy_(torch.as_tensor(np.asarray(src)).to(dst.dtype))
@@ -195,6 +223,7 @@ class MlpEngine:
 
     def refresh_shadow(self):
         """Re-derive the low-precision copies of W1 (bf16 shadow or bf16 planes)."""
+        self.join()
         with torch.no_grad():
             if self.np:
                 if self.backend == "hip":
@@ -208,8 +237,14 @@ class MlpEngine:
             elif self.dtype == "bf16":
                 self.W1g.copy_(self.W1.to(torch.bfloat16))
 
+    def join(self):
+        """Make the current stream wait for an outstanding side-stream role kernel (W2/b2 update)."""
+        if self._step is not None and self.backend == "hip":
+            self._step.join(torch.cuda.current_stream(self.device).cuda_stream)
+
     def get_params(self):
         """Host float64 copies (W1, b1, W2, b2)."""
+        self.join()
         return tuple(t.detach().to("cpu", torch.float64).numpy().copy()
                      for t in (self.W1, self.b1, self.W2, self.b2))
 
@@ -240,6 +275,14 @@ class MlpEngine:
                 s.dZ1p = self.dZ1p.data_ptr()
             if self.z2buf is not None:
                 s.z2p = self.z2buf.data_ptr()
+            if self.gpart is not None:
+                s.gpart = self.gpart.data_ptr()
+            if self.np and self.XT is not None and self.XT.shape[0] == self.P + 1:
+                s.bias_col = 1
+                if self._a1bufs is not None:
+                    if self._aux_stream is None:
+                        self._aux_stream = torch.cuda.Stream(self.device)
+                    s.stream2 = self._aux_stream.cuda_stream
             self._step = s
         return self._step
 
@@ -253,8 +296,13 @@ class MlpEngine:
         if off < 0 or off + n > self.num_samples:
             raise IndexError("batch slice outside the resident dataset")
         if self.backend == "hip":
-            self._hip_step().run(int(off), int(n), float(scale), float(reg), float(lr), int(bool(sgd)),
-                                 int(bool(with_loss)), torch.cuda.current_stream(self.device).cuda_stream)
+            st = self._hip_step()
+            if self._a1bufs is not None and st.stream2:  # alternate a1 buffers (roles may still read the last)
+                self._a1k ^= 1
+                self.a1 = self._a1bufs[self._a1k]
+                st.a1 = self.a1.data_ptr()
+            st.run(int(off), int(n), float(scale), float(reg), float(lr), int(bool(sgd)), int(bool(with_loss)),
+                   torch.cuda.current_stream(self.device).cuda_stream)
         else:
             self._torch_step(off, n, scale, reg, lr, sgd, with_loss)
 
@@ -315,6 +363,7 @@ class MlpEngine:
 
     def sgd(self, lr: float):
         """params -= lr * grads over the whole flat arena (one fused kernel)."""
+        self.join()
         if self.backend == "hip" and self.np:
             hip().split_sgd(self.params.data_ptr(), self.grads.data_ptr(), self.layout.total, float(lr),
                             self.W1p.data_ptr(), self.H * self.P, self.np,
@@ -344,6 +393,7 @@ class MlpEngine:
     # --------------------------------------------------------------- predict
     def predict(self, x, chunk: int | None = None) -> np.ndarray:
         """argmax labels for samples ``x`` ([N][P], host or device); GPU forward."""
+        self.join()
         xt = torch.as_tensor(np.ascontiguousarray(x) if isinstance(x, np.ndarray) else x)
         n = int(xt.shape[0])
         out = torch.empty(n, dtype=torch.int32, device=self.device)

@@ -192,17 +192,19 @@ class DataParallelTrainer:
         return [(r0, min(rows, e.H - r0)) for r0 in range(0, e.H, rows)]
 
     def _step_bucketed(self, off, n, scale, reg, lr, with_loss):
-        """Backward with the gradient all-reduce overlapped (RCCL path): the small
-        [b1|W2|b2] bucket goes out first, then every dW1 row chunk as soon as its blocked GEMM has
-        finished, on a side stream while the next chunk is still being computed."""
+        """Backward with the gradient all-reduce overlapped (RCCL path): every dW1 row
+        chunk is all-reduced on a side stream as soon as its GEMM has finished, while the next chunk
+        is still being computed; the small [b1|W2|b2] bucket follows the last chunk."""
         e = self.engine
         cur = torch.cuda.current_stream(e.device)
         cs = self._comm_stream
         e.run_forward_head(off, n, scale, with_loss)
         e.run_wgrad(off, n, scale, reg, parts=2)
         w1n = e.H * e.P
-        pieces = [(e.grads[w1n:], None)] + [(e.grads[r0 * e.P:(r0 + rows) * e.P], (r0, rows))
-                                            for r0, rows in self._buckets()]
+        # dW1 row chunks first (each all-reduced while the next is computed); the small tail bucket
+        # [b1|W2|b2] last, because db1 comes out of the dW1 GEMMs (all-ones feature column)
+        pieces = [(e.grads[r0 * e.P:(r0 + rows) * e.P], (r0, rows)) for r0, rows in self._buckets()]
+        pieces.append((e.grads[w1n:], None))
         for view, rng in pieces:
             if rng is not None:
                 e.run_wgrad(off, n, scale, reg, parts=1, row0=rng[0], rows=rng[1])
@@ -228,6 +230,7 @@ class DataParallelTrainer:
     # -------------------------------------------------------------- graphs
     def _snapshot(self):
         e = self.engine
+        e.join()
         return (e.params.clone(), (e.W1g.clone() if e.W1g is not e.W1 else None),
                 (e.W1p.clone() if e.W1p is not None else None))
 
@@ -250,6 +253,7 @@ class DataParallelTrainer:
         side.wait_stream(torch.cuda.current_stream(self.engine.device))
         with torch.cuda.stream(side):  # warm-up: lazy kernel loads, communicator init
             self.step(*plan.steps[0], lr, reg)
+            self.engine.join()
         torch.cuda.current_stream(self.engine.device).wait_stream(side)
         torch.cuda.synchronize(self.engine.device)
         self._restore(snap)
@@ -258,6 +262,7 @@ class DataParallelTrainer:
         with torch.cuda.graph(g):
             for s, ln in plan.steps:
                 self.step(s, ln, lr, reg)
+            self.engine.join()  # every side-stream role kernel rejoins before the capture ends
         torch.cuda.synchronize(self.engine.device)
         self._graphs[key] = g
         return g
@@ -268,6 +273,7 @@ class DataParallelTrainer:
         else:
             for s, ln in plan.steps:
                 self.step(s, ln, lr, reg)
+            self.engine.join()
 
     # ---------------------------------------------------------------- train
     def train(self, epochs: int, lr: float, reg: float, print_every: int = 0, debug: bool = False,

@@ -41,14 +41,37 @@ class XgmiBucket:
         if dtype not in (torch.float32, torch.float64):
             raise TypeError("xGMI bucket: float32 or float64")
         self.rank, self.world, self.numel, self.dtype = rank, world, int(numel), dtype
+        self.group = group
         self.device = torch.device(device)
         self.code = 1 if dtype == torch.float64 else 0
+        self.c = None
         with torch.cuda.device(self.device):
-            self.c = hip().comm.XgmiComm(rank, world, self.numel, 8 if self.code else 4)
-            mine = self.c.handles()
+            # every step that can fail on one rank is followed by a collective agreement, so a local
+            # IPC failure makes ALL ranks give up together instead of leaving peers in a collective
+            mine, err = None, None
+            try:
+                self.c = hip().comm.XgmiComm(rank, world, self.numel, 8 if self.code else 4)
+                mine = self.c.handles()
+            except Exception as ex:  # noqa: BLE001 - reported collectively below
+                err = f"rank {rank}: {ex}"
             allh = [None] * world
-            dist.all_gather_object(allh, mine, group=group)
-            self.c.open([(bytes(a), bytes(b)) for a, b in allh])
+            dist.all_gather_object(allh, (mine, err), group=group)
+            errs = [e for _, e in allh if e]
+            if errs:
+                if self.c is not None:
+                    self.c.close()
+                    self.c = None
+                raise RuntimeError("xGMI IPC setup failed: " + "; ".join(errs))
+            try:
+                self.c.open([(bytes(h[0]), bytes(h[1])) for h, _ in allh])
+                err = None
+            except Exception as ex:  # noqa: BLE001
+                err = f"rank {rank}: {ex}"
+            errs = [None] * world
+            dist.all_gather_object(errs, err, group=group)
+            if any(errs):
+                self.close()
+                raise RuntimeError("xGMI IPC open failed: " + "; ".join(e for e in errs if e))
         self.ok = True
         if self_test:
             self.ok = self._self_test(group)
@@ -95,4 +118,12 @@ class XgmiBucket:
             raise RuntimeError("xGMI all-reduce: a peer wait timed out (a rank stalled or died)")
 
     def close(self) -> None:
+        """Collective: unmap the peers everywhere, barrier, then free this rank's buffers."""
+        import torch.distributed as dist
+
+        if self.c is None:
+            return
+        self.c.close_peers()
+        dist.barrier(group=self.group)
         self.c.close()
+        self.c = None

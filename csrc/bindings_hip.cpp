@@ -44,6 +44,24 @@ struct MlpStep {
   int split = 0, npw = 3, npz = 3, fused_head = 0;
   uintptr_t stamps = 0;  // diagnostics only
   uintptr_t z2p = 0;     // wide-layer head scratch (head_big_scratch_floats), 0: column head
+  uintptr_t gpart = 0;   // small-layer gradient partials (split path, H <= 128), 0: recompute in wgrad
+  int bias_col = 0;      // XT has an all-ones feature row P: db1 comes out of the dW1 GEMM
+  // second stream for the dW2/db2 role kernel (split path, bias_col): it runs concurrently with dW1
+  // and the next step's forward GEMM; the next head (which reads W2) waits for it
+  uintptr_t stream2 = 0;
+  hipEvent_t ev_head = nullptr, ev_roles = nullptr;
+  bool roles_pending = false;
+
+  ~MlpStep() {
+    if (ev_head) (void)hipEventDestroy(ev_head);
+    if (ev_roles) (void)hipEventDestroy(ev_roles);
+  }
+  void join(uintptr_t stream) {  // make `stream` wait for an outstanding role kernel on stream2
+    if (roles_pending) {
+      HIP_CHECK(hipStreamWaitEvent(S(stream), ev_roles, 0));
+      roles_pending = false;
+    }
+  }
   float xscale = 1.f;    // split path: inputs are uint8 * xscale
   uintptr_t W1p = 0, dZ1p = 0;
 
@@ -64,6 +82,11 @@ struct MlpStep {
     a.loss_partial = with_loss ? P_<float>(loss) : nullptr;
     a.scale = scale; a.reg = reg; a.lr = lr; a.sgd = sgd; a.shift = shift; a.mode = 0;
     a.stamps = reinterpret_cast<unsigned long long*>(stamps);
+    a.bias_col = bias_col;
+    if (gpart && !bias_col && !fused_head && H <= cme::kHeadPartialMaxH) {  // db1 would be computed twice
+      a.gpart = P_<float>(gpart);
+      a.gblocks = cme::mlp_head_num_blocks(n);
+    }
     return a;
   }
 
@@ -89,10 +112,33 @@ struct MlpStep {
           h.dZ1_planes = a.dZ1p; h.npz = npz;
           h.loss_partial = a.loss_partial; h.shift = shift; h.mode = cme::HEAD_TRAIN;
           h.z2part = P_<float>(z2p);
+          h.gpart = const_cast<float*>(a.gpart);
+          join(stream);  // the head reads W2 / b2, updated by the previous step's role kernel
           if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
         }
       }
-      if (parts & 2) cme::mlp_split_wgrad(a, S(stream));
+      if (parts & 2) {
+        if (stream2 && bias_col && !a.gpart) {
+          if (!ev_head) {
+            HIP_CHECK(hipEventCreateWithFlags(&ev_head, hipEventDisableTiming));
+            HIP_CHECK(hipEventCreateWithFlags(&ev_roles, hipEventDisableTiming));
+          }
+          join(stream);
+          HIP_CHECK(hipEventRecord(ev_head, S(stream)));
+          HIP_CHECK(hipStreamWaitEvent(S(stream2), ev_head, 0));
+          cme::SplitStepArgs r = a;
+          r.wg_parts = 2;  // dW2 + db2 on the side stream
+          cme::mlp_split_wgrad(r, S(stream2));
+          HIP_CHECK(hipEventRecord(ev_roles, S(stream2)));
+          roles_pending = true;
+          cme::SplitStepArgs w = a;
+          w.wg_parts = 1;  // dW1 + db1 (+ SGD, planes) on the main stream
+          cme::mlp_split_wgrad(w, S(stream));
+          if (!sgd) join(stream);  // gradient bucket complete before the all-reduce
+        } else {
+          cme::mlp_split_wgrad(a, S(stream));
+        }
+      }
       return;
     }
     const DType d = to_dt(dt);
@@ -266,6 +312,11 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("stamps", &MlpStep::stamps)
       .def_readwrite("xscale", &MlpStep::xscale)
       .def_readwrite("z2p", &MlpStep::z2p)
+      .def_readwrite("gpart", &MlpStep::gpart)
+      .def_readwrite("bias_col", &MlpStep::bias_col)
+      .def_readwrite("stream2", &MlpStep::stream2)
+      .def("join", &MlpStep::join, py::arg("stream"))
+      .def_property_readonly("roles_pending", [](const MlpStep& s) { return s.roles_pending; })
       .def("run_wgrad", &MlpStep::run_wgrad, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"),
            py::arg("lr"), py::arg("sgd"), py::arg("parts"), py::arg("row0"), py::arg("rows"), py::arg("stream"))
       .def_readwrite("npw", &MlpStep::npw)

@@ -16,9 +16,18 @@ namespace cme::comm {
 
 namespace {
 
-py::bytes handle_bytes(void* p) {
+constexpr size_t kIpcGranule = 2u << 20;
+size_t round_alloc(size_t b) { return (b + kIpcGranule - 1) / kIpcGranule * kIpcGranule; }
+
+py::bytes handle_bytes(void* p, const char* what) {
   hipIpcMemHandle_t h;
-  HIP_CHECK(hipIpcGetMemHandle(&h, p));
+  const hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) {
+    char buf[256];
+    std::snprintf(buf, sizeof(buf), "hipIpcGetMemHandle(%s) failed: %s (is HSA_ENABLE_IPC_MODE_LEGACY=0 set?)",
+                  what, hipGetErrorString(e));
+    throw std::runtime_error(buf);
+  }
   return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
 }
 
@@ -43,11 +52,15 @@ class XgmiComm {
     d_.n = n;
     d_.npad = xgmi_padded_count(n);
     nblocks_ = std::max<int64_t>(1, xgmi_num_blocks(n));
-    HIP_CHECK(hipMalloc(&d_.mybuf, 2 * d_.npad * elt_bytes));
-    HIP_CHECK(hipMemset(d_.mybuf, 0, 2 * d_.npad * elt_bytes));
+    // IPC export needs a dedicated allocation: small requests can be sub-allocated from a pooled
+    // chunk by the runtime, and hipIpcGetMemHandle then rejects the pointer -- round up to 2 MiB
+    const size_t data_bytes = round_alloc(2 * d_.npad * elt_bytes);
+    HIP_CHECK(hipMalloc(&d_.mybuf, data_bytes));
+    HIP_CHECK(hipMemset(d_.mybuf, 0, data_bytes));
     // flag page: uncached so the peers' system-scope stores are seen without cache maintenance
-    HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_.myflags), flag_bytes(), hipDeviceMallocUncached));
-    HIP_CHECK(hipMemset(d_.myflags, 0, flag_bytes()));
+    HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_.myflags), round_alloc(flag_bytes()),
+                                    hipDeviceMallocUncached));
+    HIP_CHECK(hipMemset(d_.myflags, 0, round_alloc(flag_bytes())));
     HIP_CHECK(hipMalloc(&d_.epochs, nblocks_ * sizeof(uint32_t)));
     HIP_CHECK(hipMemset(d_.epochs, 0, nblocks_ * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&d_.err, sizeof(int)));
@@ -58,7 +71,9 @@ class XgmiComm {
   }
   ~XgmiComm() { close(); }
 
-  py::tuple handles() const { return py::make_tuple(handle_bytes(d_.mybuf), handle_bytes(d_.myflags)); }
+  py::tuple handles() const {
+    return py::make_tuple(handle_bytes(d_.mybuf, "data"), handle_bytes(d_.myflags, "flags"));
+  }
 
   void open(const std::vector<std::pair<std::string, std::string>>& all) {
     CME_REQUIRE((int)all.size() == d_.world, "XgmiComm.open: need one handle pair per rank");
@@ -86,9 +101,22 @@ class XgmiComm {
     return e;
   }
 
-  void close() {
+  // teardown in two phases across the group: every rank unmaps its peers (close_peers), a barrier,
+  // then every rank frees its own buffers (close) -- never free while a peer still maps them
+  void close_peers() {
+    if (!opened_.empty()) HIP_CHECK(hipDeviceSynchronize());
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
     opened_.clear();
+    for (int r = 0; r < d_.world; ++r)
+      if (r != d_.rank) {
+        d_.peers[r] = nullptr;
+        d_.peerflags[r] = nullptr;
+      }
+    ready_ = false;
+  }
+
+  void close() {
+    close_peers();
     if (d_.mybuf) (void)hipFree(d_.mybuf);
     if (d_.myflags) (void)hipFree(d_.myflags);
     if (d_.epochs) (void)hipFree(d_.epochs);
@@ -122,6 +150,7 @@ void bind_comm(py::module_& m) {
            py::arg("planes"), py::arg("np"), py::arg("w1n"), py::arg("mode"), py::arg("n"), py::arg("stream"))
       .def("error", &XgmiComm::error)
       .def("close", &XgmiComm::close)
+      .def("close_peers", &XgmiComm::close_peers)
       .def_property_readonly("nblocks", &XgmiComm::nblocks);
   sm.attr("MODE_SGD") = cme::comm::kModeSgd;
   sm.attr("MODE_ALLREDUCE") = cme::comm::kModeAllReduce;

@@ -29,7 +29,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kVec = 4;                       // elements per thread
 constexpr int kChunk = kThreads * kVec;       // elements per block
-constexpr int64_t kMaxGrid = 512;             // resident on any gfx950 part
+constexpr int64_t kMaxGrid = 256;             // one block per CU: always resident, even with several ranks per GPU
 constexpr uint32_t kSpinLimit = 1u << 22;     // ~seconds, then flag an error instead of hanging
 
 template <typename T>
@@ -48,6 +48,31 @@ struct Args {
   int np;
   int rank, world, mode;
 };
+
+constexpr int kSysCoherent = 1 | 16;  // buffer-load cache policy sc0 | sc1 (system coherent)
+
+// load sizeof(U) bytes at byte offset `off` of a peer buffer, system coherent
+template <typename U>
+__device__ __forceinline__ U peer_load(const void* base, int64_t off) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                                                      0x7FFFFFFF, 0x00020000);
+  U out;
+  if constexpr (sizeof(U) == 4) {
+    const auto w = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, kSysCoherent);
+    __builtin_memcpy(&out, &w, 4);
+  } else if constexpr (sizeof(U) == 8) {
+    const auto w = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, kSysCoherent);
+    __builtin_memcpy(&out, &w, 8);
+  } else {
+    static_assert(sizeof(U) % 16 == 0, "vector peer loads are multiples of 16 bytes");
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(U) / 16); ++q) {
+      const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off + 16 * q, 0, kSysCoherent);
+      __builtin_memcpy(reinterpret_cast<char*>(&out) + 16 * q, &w, 16);
+    }
+  }
+  return out;
+}
 
 template <int NP>
 __device__ __forceinline__ void store_planes(float v, __hip_bfloat16* base, int64_t stride, int64_t i) {
@@ -84,18 +109,37 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
   const int64_t half = (int64_t)(epoch & 1u) * a.npad;
   const int64_t i0 = c * kChunk + (int64_t)t * kVec;
 
-  // 1. local gradients -> my IPC buffer (this step's half)
+  // 1. local gradients -> my IPC buffer (this step's half), stored WRITE-THROUGH (sc0 sc1) so the
+  //    bytes are in memory, not in this XCD's L2, once the store has retired; every wave drains its
+  //    stores (vmcnt(0)) before the barrier that precedes the flag stores
   using V = T __attribute__((ext_vector_type(kVec)));
   const bool full = i0 + kVec <= a.n;  // every vector but the last partial one
+  const __amdgpu_buffer_rsrc_t rmine = __builtin_amdgcn_make_buffer_rsrc(a.mybuf, (short)0, 0x7FFFFFFF, 0x00020000);
   if (full) {
-    *reinterpret_cast<V*>(a.mybuf + half + i0) = *reinterpret_cast<const V*>(a.grads + i0);
+    const V v = *reinterpret_cast<const V*>(a.grads + i0);
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(V) / 16); ++q) {
+      uint4 w;
+      __builtin_memcpy(&w, reinterpret_cast<const char*>(&v) + 16 * q, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, w),
+                                             rmine, (int)((half + i0) * (int64_t)sizeof(T)) + 16 * q, 0,
+                                             kSysCoherent);
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < kVec; ++k)
-      if (i0 + k < a.n) a.mybuf[half + i0 + k] = a.grads[i0 + k];
+      if (i0 + k < a.n) {
+        const T x = a.grads[i0 + k];
+        if constexpr (sizeof(T) == 8) {
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x),
+                                                rmine, (int)((half + i0 + k) * 8), 0, kSysCoherent);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), rmine, (int)((half + i0 + k) * 4), 0,
+                                                kSysCoherent);
+        }
+      }
   }
-  __syncthreads();
-  if (t == 0) __threadfence_system();  // release at system scope: write the L2 back so peers can read it
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   // 2. signal every peer that my chunk c of this epoch is ready
@@ -116,18 +160,25 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire: drop stale cached peer lines
 
-  // 4. sum the R gradients of my elements in rank order, 5. update
+  // 4. sum the R gradients of my elements in rank order, 5. update.
+  //    Peer data is read with system-coherent loads (sc0 sc1): a line of a peer buffer cached by this
+  //    agent two epochs ago must not be served again (a peer mapped on the SAME device is ordinary
+  //    local memory to the L2, which a system-scope acquire does not invalidate).
   if (full) {
-    V acc = __builtin_nontemporal_load(reinterpret_cast<const V*>(a.peers[0] + half + i0));
-    for (int r = 1; r < a.world; ++r)
-      acc += __builtin_nontemporal_load(reinterpret_cast<const V*>(a.peers[r] + half + i0));
+    V acc;
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r) {
+      if (r >= a.world) break;
+      V v = peer_load<V>(a.peers[r], (half + i0) * (int64_t)sizeof(T));
+      acc = r == 0 ? v : acc + v;
+    }
 #pragma unroll
     for (int k = 0; k < kVec; ++k) update_one(a, i0 + k, acc[k]);
   } else {
     for (int k = 0; k < kVec; ++k) {
       if (i0 + k >= a.n) break;
-      T acc = a.peers[0][half + i0 + k];
-      for (int r = 1; r < a.world; ++r) acc += a.peers[r][half + i0 + k];
+      T acc = peer_load<T>(a.peers[0], (half + i0 + k) * (int64_t)sizeof(T));
+      for (int r = 1; r < a.world; ++r) acc += peer_load<T>(a.peers[r], (half + i0 + k) * (int64_t)sizeof(T));
       update_one(a, i0 + k, acc);
     }
   }

@@ -47,7 +47,12 @@ struct HeadArgs {
   // the split-H z2 partial sums; when set, the head runs as two grid-wide kernels instead of one
   // column-parallel kernel whose per-thread loop over H is serial
   float* z2part = nullptr;
+  // small layers (H <= 128, fp32, train): per-block partial sums of the OTHER gradients, so the
+  // weight-gradient launch only reduces them: gpart[blk][C*H + H + C] = (dW2 [C][H] | db1 [H] | db2 [C])
+  // over this block's 16 columns (mlp_head_num_blocks(n) blocks)
+  float* gpart = nullptr;
 };
+constexpr int kHeadPartialMaxH = 128;
 int64_t head_big_scratch_floats(int H, int n);
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t stream);
 int mlp_head_num_blocks(int n);

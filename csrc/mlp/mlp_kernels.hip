@@ -226,12 +226,59 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     __syncthreads();
     if (t == 0) a.loss_partial[blockIdx.x] = lred[0] + lred[1] + lred[2] + lred[3];
   }
+  // ---- partial dW2 / db2 over this block's 16 columns (reduced by the weight-gradient launch):
+  //      stage a1 and D of the block in LDS, then every thread does whole 16-term dot products
+  //      (cross-lane shuffles of 80 values per thread cost ~13 us here; LDS staging ~0.3 us)
+  const bool gp = HPT > 0 && a.gpart != nullptr;
+  const int gstride = C * H + H + C;
+  float* gpb = gp ? a.gpart + (size_t)blockIdx.x * gstride : nullptr;
+  __shared__ float gs_x[HPT > 0 ? HPT * NPART : 1][COLS + 1];
+  __shared__ float gs_d[NC][COLS + 1];
+  if constexpr (HPT > 0) {
+    if (gp) {
+#pragma unroll
+      for (int u = 0; u < HPT; ++u) gs_x[part + u * NPART][col] = valid ? (float)xa[u] : 0.f;
+      if (part == 0) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) gs_d[c][col] = valid ? (float)z[c] : 0.f;
+      }
+      __syncthreads();
+      for (int e = t; e < C * H + C; e += 256) {
+        float acc = 0.f;
+        if (e < C * H) {
+          const int c = e / H, h = e - c * H;
+#pragma unroll
+          for (int k = 0; k < COLS; ++k) acc += gs_d[c][k] * gs_x[h][k];
+          gpb[e] = acc;
+        } else {
+          const int c = e - C * H;
+#pragma unroll
+          for (int k = 0; k < COLS; ++k) acc += gs_d[c][k];
+          gpb[C * H + H + c] = acc;
+        }
+      }
+      __syncthreads();  // gs_x is reused for dZ1 below
+    }
+  }
   // ---- pass 2: dZ1 = (W2^T D) .* a1 .* (1 - a1)
-  if (!valid) return;
+  if (!valid && !gp) return;
   P* dZ1 = static_cast<P*>(a.dZ1);
   __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
   __hip_bfloat16* dZp = static_cast<__hip_bfloat16*>(a.dZ1_planes);
   const size_t pstride = (size_t)a.H * a.ldz;
+  auto emit_store = [&](int h, P dz) {
+    const size_t zi = (size_t)h * a.ldz + bcol;
+    dZ1[zi] = dz;
+    if (dZlo) dZlo[zi] = __float2bfloat16((float)dz);
+    if (dZp) {  // exact split into npz bf16 planes (mlp_split.h)
+      float r = (float)dz;
+      for (int p = 0; p < a.npz; ++p) {
+        const __hip_bfloat16 q = __float2bfloat16(r);
+        dZp[p * pstride + zi] = q;
+        r -= __bfloat162float(q);
+      }
+    }
+  };
   auto emit = [&](int h, P x) {
     P da = P(0);
 #pragma unroll
@@ -250,6 +297,29 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     }
   };
   if constexpr (HPT > 0) {
+    if (gp) {  // dZ1 as usual, plus its 16-column partial row sums (db1) through LDS
+#pragma unroll
+      for (int u = 0; u < HPT; ++u) {
+        const int h = part + u * NPART;
+        P dz = P(0);
+        if (valid && h < H) {
+          P da = P(0);
+#pragma unroll
+          for (int c = 0; c < NC; ++c) da += w2(c, h) * z[c];
+          dz = da * xa[u] * (P(1) - xa[u]);
+          emit_store(h, dz);
+        }
+        gs_x[h][col] = (float)dz;
+      }
+      __syncthreads();
+      if (t < H) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < COLS; ++k) acc += gs_x[t][k];
+        gpb[C * H + t] = acc;
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < HPT; ++u) {
       const int h = part + u * NPART;

@@ -50,6 +50,15 @@ struct SplitStepArgs {
   // weight-gradient launch selection (bucketed all-reduce overlap): wg_parts bit0 = dW1 rows
   // [w1_row0, w1_row0 + w1_rows) (w1_rows < 0: all), bit1 = dW2 + bias gradients
   int wg_parts = 3, w1_row0 = 0, w1_rows = -1;
+  // when the head produced per-block partial sums of dW2 / db1 / db2 (HeadArgs::gpart), the
+  // weight-gradient launch reduces those instead of recomputing them from D and a1
+  const float* gpart = nullptr;
+  int gblocks = 0;
+  // XT carries an extra all-ones feature row P: the dW1 GEMM's column P is then sum_b dZ1[h][b] = db1[h]
+  // (exact, same planes), so db1 / b1 come out of the dW1 launch and the role kernel only does dW2 / db2
+  int bias_col = 0;
+  // role selection inside the weight-gradient launch (bit0 dW2, bit1 db1, bit2 db2); 7 = all
+  int role_mask = 7;
 };
 
 void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);

@@ -235,6 +235,24 @@ __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a,
 // ======================================================================
 constexpr int kWMB = 1, kWNB = 2, kWKS = 8, kWT = 64 * kWKS;
 
+struct EpiW2 {
+  float* W2;
+  float* gW2;
+  int H, sgd;
+  float reg, lr;
+  float pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
+    pre[q] = buf_load1<float>(make_rsrc(W2), ok ? (row * H + col) * 4 : kOOB);
+  }
+  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
+    const size_t i = (size_t)row * H + col;
+    const float w = pre[q];
+    const float g = v + reg * w;
+    if (sgd) W2[i] = w - lr * g;
+    else gW2[i] = g;
+  }
+};
+
 struct EpiW1 {
   float* W1;
   float* gW1;
@@ -243,10 +261,17 @@ struct EpiW1 {
   int P, sgd, npw;
   float reg, lr, xscale;
   float pre[kEpiMaxQ];
+  float* b1;
+  float* gb1;
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
-    pre[q] = buf_load1<float>(make_rsrc(W1), ok ? (row * P + col) * 4 : kOOB);
+    pre[q] = buf_load1<float>(make_rsrc(W1), (ok && col < P) ? (row * P + col) * 4 : kOOB);
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
+    if (col == P) {  // the all-ones feature: db1[row] (no input scale, no regulariser)
+      if (sgd) b1[row] -= lr * v;
+      else gb1[row] = v;
+      return;
+    }
     const size_t i = (size_t)row * P + col;
     const float w = pre[q];
     const float g = v * xscale + reg * w;
@@ -269,57 +294,60 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   if (bid < t1) {  // ---- dW1 tile
     const int tb = xcd_remap(bid, t1);
     const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
-    TileGeom g{r1, a.P, a.n, a.w1_row0 + (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
-    EpiW1 epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw, reg, lr, a.xscale, {}};
+    TileGeom g{r1, a.P + a.bias_col, a.n, a.w1_row0 + (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
+    EpiW1 epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw, reg, lr, a.xscale, {},
+              a.b1, a.gb1};
     constexpr int U = 4;
     wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
                                                               static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
                                                               red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
     return;
   }
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (bid < t1 + t2) {  // ---- dW2[c][h] = sum_b D[c][b] a1[h][b]: one wave per hidden unit h
-    const int h = (bid - t1) * kWKS + wv;
-    if (h >= a.H) return;
-    const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.a1 + (size_t)h * a.ld);
-    const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.D);
-    const float wpre = buf_load1<float>(make_rsrc(a.W2), lane < a.C ? (lane * a.H + h) * 4 : kOOB);
-    float acc[16];
+  if (a.gpart) {  // ---- reduce the head's per-block partials of dW2 | db1 | db2, then update
+    const int tot = a.C * a.H + a.H + a.C;
+    const int e = (bid - t1) * kWT + threadIdx.x;
+    if (e >= tot) return;
+    float s = 0.f;
+    int b = 0;
+    for (; b + 8 <= a.gblocks; b += 8) {
+      float v[8];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) acc[c] = 0.f;
-    for (int j0 = 0; j0 < a.n; j0 += 64 * 4) {
-      float x[4], d[4][16];
+      for (int u = 0; u < 8; ++u) v[u] = a.gpart[(size_t)(b + u) * tot + e];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j0 + u * 64 + lane;
-        const int ok = j < a.n;
-        x[u] = buf_load1<float>(ra, ok ? j * 4 : kOOB);
-#pragma unroll
-        for (int c = 0; c < 16; ++c)
-          d[u][c] = buf_load1<float>(rd, (ok && c < a.C) ? (c * a.ld + j) * 4 : kOOB);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int c = 0; c < 16; ++c) acc[c] += d[u][c] * x[u];
+      for (int u = 0; u < 8; ++u) s += v[u];
     }
-#pragma unroll
-    for (int c = 0; c < 16; ++c) acc[c] = wave_sum(acc[c]);
-    if (lane < a.C) {
-      float v = 0.f;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) v = c == lane ? acc[c] : v;
-      const size_t i = (size_t)lane * a.H + h;
-      const float w = wpre;
-      const float g = v + reg * w;
-      if (a.sgd) a.W2[i] = w - lr * g;
-      else a.gW2[i] = g;
+    for (; b < a.gblocks; ++b) s += a.gpart[(size_t)b * tot + e];
+    if (e < a.C * a.H) {
+      const float w = a.W2[e];
+      const float g = s + reg * w;
+      if (a.sgd) a.W2[e] = w - lr * g;
+      else a.gW2[e] = g;
+    } else if (e < a.C * a.H + a.H) {
+      const int h = e - a.C * a.H;
+      if (a.sgd) a.b1[h] -= lr * s;
+      else a.gb1[h] = s;
+    } else {
+      const int c = e - a.C * a.H - a.H;
+      if (a.sgd) a.b2[c] -= lr * s;
+      else a.gb2[c] = s;
     }
     return;
   }
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (bid < t1 + t2) {  // ---- dW2 = D a1^T on MFMA (exact f32 16x16x4): one 16x16 tile per workgroup,
+    //                        the 8 waves split K = batch; fused reg + SGD (or gradient) epilogue
+    const int tb = bid - t1;
+    TileGeom g{a.C, a.H, a.n, 0, tb * 16};
+    EpiW2 epi{a.W2, a.gW2, a.H, a.sgd, reg, lr, {}};
+    if (a.n % 4 == 0)
+      wsk_tile<float, 1, 1, kWKS, true, true, 1, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red);
+    else
+      wsk_tile<float, 1, 1, kWKS, true, true, 0, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red);
+    return;
+  }
   // ---- bias gradients: one wave per row; rows [0,H) -> db1 from dZ1, [H,H+C) -> db2 from D
-  const int row = (bid - t1 - t2) * kWKS + wv;
+  const int row = (bid - t1 - t2) * kWKS + wv + (a.bias_col ? a.H : 0);  // db1 fused into dW1: db2 rows only
   if (row >= a.H + a.C) return;
   const bool first = row < a.H;
   const float* src = first ? a.dZ1 + (size_t)row * a.ld : a.D + (size_t)(row - a.H) * a.ld;
@@ -385,7 +413,14 @@ struct EpiW1Big {
   size_t plane;
   int P, sgd, npw;
   float reg, lr, xscale;
+  float* b1;
+  float* gb1;
   __device__ __forceinline__ void operator()(int row, int col, float v) {
+    if (col == P) {  // all-ones feature row of XT: db1
+      if (sgd) b1[row] -= lr * v;
+      else gb1[row] = v;
+      return;
+    }
     const size_t i = (size_t)row * P + col;
     const float w = W1[i];
     const float g = v * xscale + reg * w;
@@ -415,10 +450,10 @@ __global__ __launch_bounds__(lg::kThreads) void wgrad_big_kernel(SplitStepArgs a
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   EpiW1Big epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw,
-               (float)a.reg, (float)a.lr, a.xscale};
+               (float)a.reg, (float)a.lr, a.xscale, a.b1, a.gb1};
   const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
   lds_gemm_tile<BM, BN, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
-                                      static_cast<const uint8_t*>(a.XT), a.ldxt, r1, a.P, a.n,
+                                      static_cast<const uint8_t*>(a.XT), a.ldxt, r1, a.P + a.bias_col, a.n,
                                       a.w1_row0 + (id / tn) * BM, (id % tn) * BN, epi, lds_dyn);
 }
 
@@ -473,16 +508,17 @@ void launch_fwd1_big(const SplitStepArgs& a, hipStream_t s) {
 template <int NP>
 void launch_wgrad_big(const SplitStepArgs& a, hipStream_t s) {
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
-  const int t128 = cdiv(rows, 128) * cdiv(a.P, 128);
+  const int NW = a.P + a.bias_col;
+  const int t128 = cdiv(rows, 128) * cdiv(NW, 128);
   if (t128 >= 192) {
     constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
     set_lds_limit<wgrad_big_kernel<128, 128, NP>>(L);
-    const int tn = cdiv(a.P, 128);
+    const int tn = cdiv(NW, 128);
     wgrad_big_kernel<128, 128, NP><<<t128, lg::kThreads, L, s>>>(a, tn);
   } else {
     constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
     set_lds_limit<wgrad_big_kernel<64, 64, NP>>(L);
-    const int tn = cdiv(a.P, 64);
+    const int tn = cdiv(NW, 64);
     wgrad_big_kernel<64, 64, NP><<<cdiv(rows, 64) * tn, lg::kThreads, L, s>>>(a, tn);
   }
 }
@@ -552,9 +588,9 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
     else launch_wgrad_big<1>(a, s);
   }
   const int w1rows = a.w1_rows < 0 ? a.H : a.w1_rows;
-  const int t1n = cdiv(a.P, 16 * kWNB), t1 = (big || !do_w1) ? 0 : cdiv(w1rows, 16 * kWMB) * t1n;
-  const int t2 = do_roles ? cdiv(a.H, kWKS) : 0;
-  const int tb = do_roles ? cdiv(a.H + a.C, kWKS) : 0;
+  const int t1n = cdiv(a.P + a.bias_col, 16 * kWNB), t1 = (big || !do_w1) ? 0 : cdiv(w1rows, 16 * kWMB) * t1n;
+  const int t2 = !do_roles ? 0 : (a.gpart ? cdiv(a.C * a.H + a.H + a.C, kWT) : cdiv(a.H, 16));
+  const int tb = (do_roles && !a.gpart) ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
   if (t1 + t2 + tb == 0) {
     CME_LAUNCH_CHECK(s);
     return;
