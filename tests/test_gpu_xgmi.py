@@ -28,3 +28,11 @@ def test_xgmi_allreduce_multiprocess(tmp_path, world):
         assert float(z["trainer_w1_diff"]) < 1e-5 and float(z["trainer_w2_diff"]) < 1e-5
         for H in (300, 1024):  # 2 ranks: a+b is exact in any order -> bitwise; 4 ranks: rounding only
             assert float(z[f"bucketed_diff_{H}"]) <= (0.0 if world == 2 else 1e-6), (H, float(z[f"bucketed_diff_{H}"]))
+
+
+def test_xgmi_stress_four_ranks():
+    """Many back-to-back all-reduces (both buffer halves, all epochs) with 4 ranks on one GPU: no stale reads."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "stress_xgmi.py"), "4", "10"],
+                       capture_output=True, text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "bad_elements=0" in r.stdout, r.stdout[-2000:]
