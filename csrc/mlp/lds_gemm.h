@@ -11,9 +11,11 @@
 //   * BM x BN workgroup tile, 4 waves as 2x2, each wave (BM/2)x(BN/2) built from
 //     16x16 blocks of v_mfma_f32_16x16x32_bf16; BK = 64 per stage.
 //   * global -> VGPR -> LDS staging with 16-byte buffer loads (out-of-range
-//     rows / k return zero: no edge branches), two LDS buffers: the loads of
-//     stage k+1 are in flight while stage k is multiplied, ONE barrier per stage.
-//   * LDS rows padded (+16 B) so the 16-row fragment reads spread over the banks.
+//     rows / k return zero: no edge branches), two LDS buffers and two register
+//     stages: the loads of stage k+2 are in flight while stages k and k+1 are
+//     multiplied, ONE barrier per stage.
+//   * A rows padded +32 B: the 16-row ds_read_b128 fragment reads are bank-conflict
+//     free (modelled per the gfx950 lane groups); B rows +16 B (ds_read_b64).
 //   * XCD-aware tile order (tiles sharing A rows land on one XCD's L2).
 #pragma once
 
@@ -25,7 +27,7 @@ namespace lg {
 
 constexpr int kBK = 64;
 constexpr int kThreads = 256;
-constexpr int kARow = kBK * 2 + 16;  // bytes per A row in LDS (bf16, padded)
+constexpr int kARow = kBK * 2 + 32;  // bytes per A row in LDS (bf16, +32 B: conflict-free ds_read_b128 fragments)
 
 template <typename TB>
 struct BTraits;
@@ -103,8 +105,10 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
     b_lds[j] = r * BROW + kc * 16;
   }
 
-  uint4 ra_reg[NPA][AJ], rb_reg[BJ];
-  auto load_stage = [&](int k0) {
+  // two register stages: the loads of K-stage k+2 are issued before stage k is multiplied and are
+  // only consumed (written to LDS) after stage k+1 -- two compute phases of cover for L2 latency
+  uint4 ra_reg[2][NPA][AJ], rb_reg[2][BJ];
+  auto load_stage = [&](int k0, uint4 (&rA)[NPA][AJ], uint4 (&rB)[BJ]) {
     const int kb = k0 * 2;  // byte offset of k0 in an A row
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
@@ -113,7 +117,7 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
 #pragma unroll
       for (int p = 0; p < NPA; ++p) {
         const auto w = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? a_off[j] + kb + p * plane_bytes : kOOB, 0, 0);
-        __builtin_memcpy(&ra_reg[p][j], &w, 16);
+        __builtin_memcpy(&rA[p][j], &w, 16);
       }
     }
 #pragma unroll
@@ -122,17 +126,17 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
       constexpr int EPC = 16 / (int)sizeof(TB);  // elements per chunk
       const bool ok = b_ok[j] && k0 + kc * EPC < K;
       const auto w = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? b_off[j] + k0 * (int)sizeof(TB) : kOOB, 0, 0);
-      __builtin_memcpy(&rb_reg[j], &w, 16);
+      __builtin_memcpy(&rB[j], &w, 16);
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf, const uint4 (&rA)[NPA][AJ], const uint4 (&rB)[BJ]) {
 #pragma unroll
     for (int p = 0; p < NPA; ++p)
 #pragma unroll
       for (int j = 0; j < AJ; ++j)
-        *reinterpret_cast<uint4*>(ldsA + buf * A_BUF + p * BM * kARow + a_lds[j]) = ra_reg[p][j];
+        *reinterpret_cast<uint4*>(ldsA + buf * A_BUF + p * BM * kARow + a_lds[j]) = rA[p][j];
 #pragma unroll
-    for (int j = 0; j < BJ; ++j) *reinterpret_cast<uint4*>(ldsB + buf * B_BUF + b_lds[j]) = rb_reg[j];
+    for (int j = 0; j < BJ; ++j) *reinterpret_cast<uint4*>(ldsB + buf * B_BUF + b_lds[j]) = rB[j];
   };
 
   f32x4 acc[MB][NB];
@@ -141,13 +145,7 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + kBK - 1) / kBK;
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_stage((kt + 1) * kBK);
+  auto compute = [&](int buf) {
     const char* sA = ldsA + buf * A_BUF + (wr * WM + fr) * kARow;
     const char* sB = ldsB + buf * B_BUF + (wc * WN + fr) * BROW;
 #pragma unroll
@@ -162,20 +160,49 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
           bf[nb] = *reinterpret_cast<const bf16x8_t*>(sB + nb * 16 * BROW + (kk * 32 + fg * 8) * 2);
         }
       }
+      // issue every A fragment read of this k-step before the first MFMA: one LDS round trip per
+      // k-step instead of one per fragment (the reads are independent; counted lgkmcnt waits)
+      bf16x8_t af[NPA][MB];
 #pragma unroll
-      for (int p = 0; p < NPA; ++p) {
+      for (int p = 0; p < NPA; ++p)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) {
-          const bf16x8_t af =
+        for (int mb = 0; mb < MB; ++mb)
+          af[p][mb] =
               *reinterpret_cast<const bf16x8_t*>(sA + p * BM * kARow + mb * 16 * kARow + (kk * 32 + fg * 8) * 2);
 #pragma unroll
+      for (int p = 0; p < NPA; ++p)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
           for (int nb = 0; nb < NB; ++nb)
-            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[nb], acc[mb][nb], 0, 0, 0);
-        }
-      }
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[p][mb], bf[nb], acc[mb][nb], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_stage(buf ^ 1);
-    __syncthreads();
+  };
+
+  const int nk = (K + kBK - 1) / kBK;
+  load_stage(0, ra_reg[0], rb_reg[0]);
+  if (nk > 1) load_stage(kBK, ra_reg[1], rb_reg[1]);
+  store_stage(0, ra_reg[0], rb_reg[0]);
+  __syncthreads();
+  // stage kt lives in LDS buffer kt&1 and (before its store) in register set kt&1
+  // LDS-only barrier: __syncthreads() would also drain vmcnt, i.e. wait for the stage-(k+2) global
+  // loads that are meant to stay in flight across it (cdna_hip_programming.md §5, "Pipelining
+  // across barriers"); the LDS writes only need lgkmcnt(0) before the s_barrier
+  auto lds_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto step = [&](int kt, uint4 (&rA_cur)[NPA][AJ], uint4 (&rB_cur)[BJ], uint4 (&rA_nxt)[NPA][AJ],
+                  uint4 (&rB_nxt)[BJ]) {
+    if (kt + 2 < nk) load_stage((kt + 2) * kBK, rA_cur, rB_cur);  // set kt&1 is free again
+    compute(kt & 1);
+    if (kt + 1 < nk) store_stage((kt + 1) & 1, rA_nxt, rB_nxt);
+    lds_barrier();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, ra_reg[0], rb_reg[0], ra_reg[1], rb_reg[1]);
+    if (kt + 1 < nk) step(kt + 1, ra_reg[1], rb_reg[1], ra_reg[0], rb_reg[0]);
   }
 
   // epilogue: C layout of 16x16 f32 MFMA -- lane holds col fr, rows 4*fg + i
