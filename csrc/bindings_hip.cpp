@@ -177,6 +177,46 @@ struct MlpStep {
     if (parts & 2) cme::mlp_wgrad(d, w, S(stream));
   }
 
+  // ---- lookahead steps (single process; see cme213_sp18_amd/parallel/lookahead.py)
+  // prologue: zbuf = xscale * (W1 . X[off:off+n])  (pre-activation without bias)
+  void la_prologue(int64_t off, int n, uintptr_t zbuf, uintptr_t stream) {
+    CME_REQUIRE(split && bias_col, "lookahead: split path with the all-ones XT feature");
+    cme::SplitStepArgs a = split_args(off, n, 1.0, 0.0, 0.0, 1, 0);
+    cme::mlp_split_fwd_raw(a, P_<float>(zbuf), a.xscale, S(stream));
+  }
+  // launch L2 of step (off, n): head on zcur (pre-activation + b1 -> sigmoid, written back) and, when
+  // n_next > 0, the raw forward An = W1 . X[off_next:off_next+n_next] into abuf
+  void la_l2(int64_t off, int n, double scale, int with_loss, uintptr_t zcur, int64_t off_next, int n_next,
+             uintptr_t abuf, uintptr_t stream) {
+    CME_REQUIRE(split && bias_col, "lookahead: split path with the all-ones XT feature");
+    const cme::SplitStepArgs a = split_args(off, n, scale, 0.0, 0.0, 1, with_loss);
+    cme::HeadArgs h{};
+    h.a1 = reinterpret_cast<void*>(zcur); h.lda = ld; h.W2 = a.W2; h.b2 = a.b2; h.labels = a.labels; h.H = H;
+    h.C = C; h.n = n; h.scale = scale; h.D = a.D; h.ldd = ld; h.dZ1 = a.dZ1; h.ldz = ld; h.dZ1_bf16 = nullptr;
+    h.dZ1_planes = a.dZ1p; h.npz = npz; h.loss_partial = a.loss_partial; h.shift = shift;
+    h.mode = cme::HEAD_TRAIN; h.b1_pre = a.b1;
+    cme::SplitStepArgs f = split_args(n_next > 0 ? off_next : off, n_next > 0 ? n_next : n, 1.0, 0.0, 0.0, 1, 0);
+    cme::mlp_lookahead_l2(f, P_<float>(abuf), h, n_next > 0, S(stream));
+  }
+  // launch L1 of step (off, n): dW1/db1/dW2/db2 with the fused SGD and, when n_next > 0, the next
+  // step's pre-activation z_next = c1 * abuf - c2 * dZ1 . GT^T  (GT [n_next][ldg] fp32 Gram matrix)
+  void la_l1(int64_t off, int n, double scale, double reg, double lr, uintptr_t zcur, int n_next, uintptr_t GT,
+             int ldg, uintptr_t abuf, uintptr_t znext, double c1, double c2, uintptr_t stream) {
+    CME_REQUIRE(split && bias_col, "lookahead: split path with the all-ones XT feature");
+    cme::SplitStepArgs a = split_args(off, n, scale, reg, lr, 1, 0);
+    a.a1 = P_<float>(zcur);  // the head wrote the activated a1 back there (dW2 reads it)
+    if (n_next > 0) {
+      a.GTn = P_<float>(GT);
+      a.ldg = ldg;
+      a.n_next = n_next;
+      a.An = P_<float>(abuf);
+      a.z1n = P_<float>(znext);
+      a.c1 = (float)c1;
+      a.c2 = (float)c2;
+    }
+    cme::mlp_split_wgrad(a, S(stream));
+  }
+
   // Weight-gradient pieces of a step whose forward + head already ran (parts=1): used by the
   // trainer to overlap per-bucket all-reduces with the rest of the backward pass.
   // parts bit0 = dW1 rows [row0, row0+rows), bit1 = dW2 + bias gradients.  Split paths only.
@@ -317,6 +357,9 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("stream2", &MlpStep::stream2)
       .def("join", &MlpStep::join, py::arg("stream"))
       .def_property_readonly("roles_pending", [](const MlpStep& s) { return s.roles_pending; })
+      .def("la_prologue", &MlpStep::la_prologue)
+      .def("la_l2", &MlpStep::la_l2)
+      .def("la_l1", &MlpStep::la_l1)
       .def("run_wgrad", &MlpStep::run_wgrad, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"),
            py::arg("lr"), py::arg("sgd"), py::arg("parts"), py::arg("row0"), py::arg("rows"), py::arg("stream"))
       .def_readwrite("npw", &MlpStep::npw)

@@ -51,9 +51,17 @@ struct HeadArgs {
   // weight-gradient launch only reduces them: gpart[blk][C*H + H + C] = (dW2 [C][H] | db1 [H] | db2 [C])
   // over this block's 16 columns (mlp_head_num_blocks(n) blocks)
   float* gpart = nullptr;
+  // lookahead step (fp32, H <= 128): a1 holds z1 - b1 (no activation); the head adds b1_pre and applies
+  // the sigmoid, writing the activated a1 back
+  const float* b1_pre = nullptr;
 };
 constexpr int kHeadPartialMaxH = 128;
 int64_t head_big_scratch_floats(int H, int n);
+
+struct SplitStepArgs;
+// lookahead step launch "L2": this step's head (a1 given as pre-activation, h.b1_pre) + the next
+// step's raw forward GEMM An = W1 . X_next (f: next step's args; with_next = false on the last step)
+void mlp_lookahead_l2(const SplitStepArgs& f, float* Aout, const HeadArgs& h, bool with_next, hipStream_t s);
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t stream);
 int mlp_head_num_blocks(int n);
 

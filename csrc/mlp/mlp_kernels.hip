@@ -1,6 +1,7 @@
 // Fused MLP step kernels for MI355X (gfx950).  See mlp_kernels.h for the
 // step decomposition and mma_tile.h for the MFMA tile engine.
 #include "mlp_kernels.h"
+#include "mlp_split.h"
 
 #include "mma_tile.h"
 
@@ -79,24 +80,25 @@ constexpr int kCMax = 16;
 constexpr int kHeadLdsMax = 64 * 1024;
 
 template <typename P, int NC, bool LDSW, int HPT>
-__global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
+__device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, const int t, char* head_dyn,
+                                           P (*zred)[NC][kHeadCols], float* lred,
+                                           float (*gs_x)[kHeadCols + 1], float (*gs_d)[kHeadCols + 1]) {
+  // One head block (kHeadCols columns, 256 threads) -- vb: the block index, t: thread in [0, 256).
+  // Called by head_kernel (one block per workgroup) and by the lookahead step kernel (two per
+  // 512-thread workgroup); every barrier below is reached by all threads of the workgroup.
   // HPT > 0: every thread owns at most HPT hidden units (H <= HPT * NPART); their
   // a1 values are loaded ONCE (one burst, before the W2 staging barrier) and
   // reused by both passes.  HPT == 0: generic loop for large H.
   constexpr int COLS = kHeadCols;
   constexpr int NPART = 256 / COLS;
-  extern __shared__ __attribute__((aligned(16))) char head_dyn[];
-  __shared__ P zred[4][NC][COLS];
-  __shared__ float lred[4];
-
   const P* __restrict__ a1 = static_cast<const P*>(a.a1);
   const P* __restrict__ W2 = static_cast<const P*>(a.W2);
   const P* __restrict__ b2 = static_cast<const P*>(a.b2);
   P* ws = reinterpret_cast<P*>(head_dyn);
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int lane = t & 63, wave = t >> 6;
   const int col = t % COLS, part = t / COLS;
   const int H = a.H, C = a.C;
-  const int bcol = blockIdx.x * COLS + col;
+  const int bcol = vb * COLS + col;
   const bool valid = bcol < a.n;
   const int b = valid ? bcol : a.n - 1;  // clamped: loads stay in bounds, results discarded
   const int lab = a.mode == HEAD_TRAIN ? a.labels[b] : 0;
@@ -108,6 +110,18 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     for (int u = 0; u < HPT; ++u) {
       const int h = part + u * NPART;
       xa[u] = buf_load1<P>(rs, h < H ? (h * a.lda + b) * (int)sizeof(P) : kOOB);
+    }
+    if (a.b1_pre) {  // lookahead step: a1 holds the pre-activation without bias; finish it here
+      const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.b1_pre);
+      P* a1w = const_cast<P*>(a1);
+#pragma unroll
+      for (int u = 0; u < HPT; ++u) {
+        const int h = part + u * NPART;
+        const P bb = (P)buf_load1<float>(rb, h < H ? h * 4 : kOOB);
+        const P v = P(1) / (P(1) + dev_exp<P>(-(xa[u] + bb)));
+        xa[u] = h < H ? v : P(0);
+        if (valid && h < H) a1w[(size_t)h * a.lda + bcol] = v;
+      }
     }
   }
   if constexpr (LDSW) {
@@ -224,16 +238,14 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
     const float v = wave_sum(lpart);
     if (lane == 0) lred[wave] = v;
     __syncthreads();
-    if (t == 0) a.loss_partial[blockIdx.x] = lred[0] + lred[1] + lred[2] + lred[3];
+    if (t == 0 && vb * COLS < a.n) a.loss_partial[vb] = lred[0] + lred[1] + lred[2] + lred[3];
   }
   // ---- partial dW2 / db2 over this block's 16 columns (reduced by the weight-gradient launch):
   //      stage a1 and D of the block in LDS, then every thread does whole 16-term dot products
   //      (cross-lane shuffles of 80 values per thread cost ~13 us here; LDS staging ~0.3 us)
   const bool gp = HPT > 0 && a.gpart != nullptr;
   const int gstride = C * H + H + C;
-  float* gpb = gp ? a.gpart + (size_t)blockIdx.x * gstride : nullptr;
-  __shared__ float gs_x[HPT > 0 ? HPT * NPART : 1][COLS + 1];
-  __shared__ float gs_d[NC][COLS + 1];
+  float* gpb = gp ? a.gpart + (size_t)vb * gstride : nullptr;
   if constexpr (HPT > 0) {
     if (gp) {
 #pragma unroll
@@ -328,6 +340,52 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   } else {
     for (int h = part; h < H; h += NPART) emit(h, a1[(size_t)h * a.lda + bcol]);
   }
+}
+
+template <typename P, int NC, bool LDSW, int HPT>
+__global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char head_dyn[];
+  __shared__ P zred[4][NC][kHeadCols];
+  __shared__ float lred[4];
+  __shared__ float gs_x[HPT > 0 ? HPT * (256 / kHeadCols) : 1][kHeadCols + 1];
+  __shared__ float gs_d[NC][kHeadCols + 1];
+  head_block<P, NC, LDSW, HPT>(a, blockIdx.x, threadIdx.x, head_dyn, zred, lred, gs_x, gs_d);
+}
+
+// ------------------------------------------- lookahead step, launch "L2" (see parallel/lookahead.py)
+// Workgroups [0, ntiles): raw forward tiles An = W1 . X_next for the NEXT step (W1 already updated by
+// the previous launch).  The rest: two head blocks each (512 threads = 2 x 256) for THIS step, whose
+// a1 arrives as a pre-activation (HeadArgs::b1_pre).  Both halves are independent; the critical path
+// (head) and the off-path GEMM share one launch.
+struct EpiScaleStoreK {
+  float* out;
+  int ld;
+  __device__ __forceinline__ void prefetch(int, int, int, bool) {}
+  __device__ __forceinline__ void operator()(int, int row, int col, float v) { out[(size_t)row * ld + col] = v; }
+};
+
+template <int NC, int NPW>
+__global__ __launch_bounds__(512) void lookahead_l2_kernel(SplitStepArgs f, float* Aout, HeadArgs h, int ntiles,
+                                                          int tiles_n) {
+  __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];
+  extern __shared__ __attribute__((aligned(16))) char l2_dyn[];
+  __shared__ float zred[2][4][NC][kHeadCols];
+  __shared__ float lred[2][4];
+  __shared__ float gs_x[2][8 * (256 / kHeadCols)][kHeadCols + 1];
+  __shared__ float gs_d[2][NC][kHeadCols + 1];
+  if ((int)blockIdx.x < ntiles) {
+    const int bid = xcd_remap(blockIdx.x, ntiles);
+    TileGeom g{f.H, f.n, f.P, (bid / tiles_n) * 16, (bid % tiles_n) * 32};
+    EpiScaleStoreK epi{Aout, f.ld};
+    wsk_tile<__hip_bfloat16, 1, 2, 8, true, true, 1, 4, NPW, uint8_t>(
+        static_cast<const __hip_bfloat16*>(f.W1p), f.P, static_cast<const uint8_t*>(f.X), f.P, g, epi, red,
+        f.H * f.P * (int)sizeof(__hip_bfloat16));
+    return;
+  }
+  const int half = threadIdx.x >> 8;
+  const int vb = 2 * ((int)blockIdx.x - ntiles) + half;
+  head_block<float, NC, true, 8>(h, vb, threadIdx.x & 255, l2_dyn + half * h.H * NC * (int)sizeof(float),
+                                 zred[half], lred[half], gs_x[half], gs_d[half]);
 }
 
 template <typename P, int NC>
@@ -782,6 +840,28 @@ void mlp_forward1(DType dt, const void* W1g, const void* b1, const void* X, int 
 }
 
 int mlp_head_num_blocks(int n) { return cdiv(n, kHeadCols); }
+
+void mlp_lookahead_l2(const SplitStepArgs& f, float* Aout, const HeadArgs& h, bool with_next, hipStream_t s) {
+  CME_REQUIRE(h.H <= 8 * (256 / kHeadCols) && h.C <= kCMax && h.b1_pre && h.mode == HEAD_TRAIN,
+              "lookahead: H <= 128, train-mode head with b1_pre");
+  CME_REQUIRE(reinterpret_cast<uintptr_t>(f.X) % 4 == 0 && reinterpret_cast<uintptr_t>(f.W1p) % 16 == 0 &&
+                  f.P % 8 == 0,
+              "lookahead: aligned operands");
+  const int tiles_n = cdiv(f.n, 32), ntiles = with_next ? cdiv(f.H, 16) * tiles_n : 0;
+  const int nwg = ntiles + cdiv(cdiv(h.n, kHeadCols), 2);
+  const int NC = h.C <= 10 ? 10 : 16;
+  const size_t dyn = 2 * (size_t)h.H * NC * sizeof(float);
+#define CME_L2(nc, np) lookahead_l2_kernel<nc, np><<<nwg, 512, dyn, s>>>(f, Aout, h, ntiles, tiles_n)
+  if (NC == 10) {
+    if (f.npw == 3) CME_L2(10, 3);
+    else CME_L2(10, 1);
+  } else {
+    if (f.npw == 3) CME_L2(16, 3);
+    else CME_L2(16, 1);
+  }
+#undef CME_L2
+  CME_LAUNCH_CHECK(s);
+}
 
 int64_t head_big_scratch_floats(int H, int n) { return (int64_t)cdiv(H, kHBRows) * kCMax * hb_cols_pad(n); }
 

@@ -59,12 +59,22 @@ struct SplitStepArgs {
   int bias_col = 0;
   // role selection inside the weight-gradient launch (bit0 dW2, bit1 db1, bit2 db2); 7 = all
   int role_mask = 7;
+  // lookahead (single process, see parallel/lookahead.py): the same launch also computes the NEXT
+  // step's pre-activation  z1n = c1 * An - c2 * (dZ1 . GTn^T)  on extra tiles, where An = W1 X_next
+  // (raw), GTn[j][k] = x_next_j . x_k (exact integer Gram of the two batches, fp32); zero tiles: off
+  const float* GTn = nullptr;
+  int ldg = 0, n_next = 0;
+  const float* An = nullptr;
+  float* z1n = nullptr;
+  float c1 = 0.f, c2 = 0.f;
 };
 
 void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);
 // tiled forward only: a1 = sigmoid(W1 X + b1) (pair with mlp_head for the 3-kernel step)
 void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s);
 void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s);
+// raw forward tiles An = W1 . X (no bias / activation) into `out` [H][ld], times `scale`
+void mlp_split_fwd_raw(const SplitStepArgs& a, float* out, float scale, hipStream_t s);
 int mlp_split_fwdhead_blocks(int n);
 
 // planes[p][i] for i < n: exact np-way bf16 split of W[i] (np = 1: plain rounding).

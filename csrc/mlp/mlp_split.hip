@@ -217,6 +217,25 @@ struct EpiSig {
   }
 };
 
+struct EpiScaleStore {
+  float* out;
+  int ld;
+  float s;
+  __device__ __forceinline__ void prefetch(int, int, int, bool) {}
+  __device__ __forceinline__ void operator()(int, int row, int col, float v) { out[(size_t)row * ld + col] = v * s; }
+};
+
+template <int NPW, int VEC>
+__global__ __launch_bounds__(64 * kF1KS) void fwd_raw_kernel(SplitStepArgs a, int tiles_n, float* out, float scale) {
+  __shared__ __attribute__((aligned(16))) float red[kF1KS * kF1MB * kF1NB * 4 * 64];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  TileGeom g{a.H, a.n, a.P, (bid / tiles_n) * 16 * kF1MB, (bid % tiles_n) * 16 * kF1NB};
+  EpiScaleStore epi{out, a.ld, scale};
+  wsk_tile<bf16, kF1MB, kF1NB, kF1KS, true, true, VEC, 4, NPW, uint8_t>(static_cast<const bf16*>(a.W1p), a.P,
+                                                               static_cast<const uint8_t*>(a.X), a.P, g, epi, red,
+                                                               a.H * a.P * (int)sizeof(bf16));
+}
+
 template <int NPW, int VEC>
 __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a, int tiles_n) {
   __shared__ __attribute__((aligned(16))) float red[kF1KS * kF1MB * kF1NB * 4 * 64];
@@ -250,6 +269,20 @@ struct EpiW2 {
     const float g = v + reg * w;
     if (sgd) W2[i] = w - lr * g;
     else gW2[i] = g;
+  }
+};
+
+struct EpiCombine {
+  const float* An;
+  float* z1n;
+  int ld;
+  float c1, c2;
+  float pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
+    pre[q] = buf_load1<float>(make_rsrc(An), ok ? (row * ld + col) * 4 : kOOB);
+  }
+  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
+    z1n[(size_t)row * ld + col] = c1 * pre[q] - c2 * v;
   }
 };
 
@@ -287,9 +320,20 @@ struct EpiW1 {
 };
 
 template <int NPZ, int VEC>
-__global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
+__global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2, int tc,
+                                                          int tcn) {
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
-  const int bid = blockIdx.x;
+  if ((int)blockIdx.x < tc) {  // ---- lookahead: next step's pre-activation (critical path: first ids)
+    const int tb = blockIdx.x;
+    TileGeom g{a.H, a.n_next, a.n, (tb / tcn) * 16 * kWMB, (tb % tcn) * 16 * kWNB};
+    EpiCombine epi{a.An, a.z1n, a.ld, a.c1, a.c2, {}};
+    if (VEC == 1)
+      wsk_tile<float, kWMB, kWNB, kWKS, true, true, 1, 8>(a.dZ1, a.ld, a.GTn, a.ldg, g, epi, red);
+    else
+      wsk_tile<float, kWMB, kWNB, kWKS, true, true, 0, 8>(a.dZ1, a.ld, a.GTn, a.ldg, g, epi, red);
+    return;
+  }
+  const int bid = blockIdx.x - tc;
   const float reg = (float)a.reg, lr = (float)a.lr;
   if (bid < t1) {  // ---- dW1 tile
     const int tb = xcd_remap(bid, t1);
@@ -563,6 +607,21 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
   CME_LAUNCH_CHECK(s);
 }
 
+void mlp_split_fwd_raw(const SplitStepArgs& a, float* out, float scale, hipStream_t s) {
+  if (a.n <= 0) return;
+  CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
+  const int tn = cdiv(a.n, 16 * kF1NB), tm = cdiv(a.H, 16 * kF1MB);
+  const bool vec = al4(a.X) && al16(a.W1p) && a.P % 8 == 0;
+  if (a.npw == 3) {
+    if (vec) fwd_raw_kernel<3, 1><<<tm * tn, 64 * kF1KS, 0, s>>>(a, tn, out, scale);
+    else fwd_raw_kernel<3, 0><<<tm * tn, 64 * kF1KS, 0, s>>>(a, tn, out, scale);
+  } else {
+    if (vec) fwd_raw_kernel<1, 1><<<tm * tn, 64 * kF1KS, 0, s>>>(a, tn, out, scale);
+    else fwd_raw_kernel<1, 0><<<tm * tn, 64 * kF1KS, 0, s>>>(a, tn, out, scale);
+  }
+  CME_LAUNCH_CHECK(s);
+}
+
 void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
   CME_REQUIRE(a.C >= 1 && a.C <= 16, "split path: 1 <= C <= 16");
@@ -591,18 +650,23 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   const int t1n = cdiv(a.P + a.bias_col, 16 * kWNB), t1 = (big || !do_w1) ? 0 : cdiv(w1rows, 16 * kWMB) * t1n;
   const int t2 = !do_roles ? 0 : (a.gpart ? cdiv(a.C * a.H + a.H + a.C, kWT) : cdiv(a.H, 16));
   const int tb = (do_roles && !a.gpart) ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
-  if (t1 + t2 + tb == 0) {
+  if (t1 + t2 + tb == 0 && !a.GTn) {
     CME_LAUNCH_CHECK(s);
     return;
   }
   // dZ1 planes: 16-byte vectors when n % 8 == 0, 8-byte halves when n % 4 == 0; XT bytes need 4-byte rows
   const bool base_ok = al16(a.dZ1p) && al4(a.XT) && a.ld % 8 == 0 && a.ldxt % 4 == 0;
   const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? 1 : (a.n % 4 == 0 ? 2 : 0));
-  const dim3 grid(t1 + t2 + tb);
+  const int tcn = a.GTn ? cdiv(a.n_next, 16 * kWNB) : 0;
+  const int tc = a.GTn ? cdiv(a.H, 16 * kWMB) * tcn : 0;
+  if (a.GTn)
+    CME_REQUIRE(a.n % 4 == 0 && a.ldg % 4 == 0 && a.ld % 4 == 0 && al16(a.GTn) && al16(a.dZ1) && vec == 1,
+                "lookahead: 16-byte aligned fp32 operands with n % 4 == 0");
+  const dim3 grid(tc + t1 + t2 + tb);
 #define CME_WG(npz)                                                                               \
-  if (vec == 1) wgrad_split_kernel<npz, 1><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);                  \
-  else if (vec == 2) wgrad_split_kernel<npz, 2><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);             \
-  else wgrad_split_kernel<npz, 0><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);
+  if (vec == 1) wgrad_split_kernel<npz, 1><<<grid, kWT, 0, s>>>(a, t1, t1n, t2, tc, tcn);         \
+  else if (vec == 2) wgrad_split_kernel<npz, 2><<<grid, kWT, 0, s>>>(a, t1, t1n, t2, tc, tcn);    \
+  else wgrad_split_kernel<npz, 0><<<grid, kWT, 0, s>>>(a, t1, t1n, t2, tc, tcn);
   if (a.npz == 3) { CME_WG(3) } else { CME_WG(1) }
 #undef CME_WG
   CME_LAUNCH_CHECK(s);
