@@ -131,22 +131,29 @@ class Grid:
         np.savetxt(path, self.to_host(), fmt="%.8g")
 
 
-def gpu_step(grid: Grid, p: SimParams, variant: int) -> None:
+def gpu_step(grid: Grid, p: SimParams, variant: int, fused: bool = True) -> None:
+    """One time step: BC on the border + stencil on the interior -- one fused launch (default), or the
+    reference's two launches (BC kernel then stencil kernel, gpuStencil.cu:113-131)."""
     k = kernels()
     s = stream_handle()
-    k.stencil_bc(grid.next.data_ptr(), grid.curr.data_ptr(), p.gx, p.gy, p.border, p.bc_scale, s)
-    k.stencil_step(grid.next.data_ptr(), grid.curr.data_ptr(), p.gx, p.gy, p.order, p.xcfl, p.ycfl, variant, s)
+    if fused:
+        k.stencil_step_bc(grid.next.data_ptr(), grid.curr.data_ptr(), p.gx, p.gy, p.order, p.xcfl, p.ycfl, variant,
+                          p.bc_scale, s)
+    else:
+        k.stencil_bc(grid.next.data_ptr(), grid.curr.data_ptr(), p.gx, p.gy, p.border, p.bc_scale, s)
+        k.stencil_step(grid.next.data_ptr(), grid.curr.data_ptr(), p.gx, p.gy, p.order, p.xcfl, p.ycfl, variant, s)
     grid.swap()
 
 
-def gpu_computation(host_grid: np.ndarray, p: SimParams, variant: str | int = "shared") -> tuple[np.ndarray, float]:
+def gpu_computation(host_grid: np.ndarray, p: SimParams, variant: str | int = "shared",
+                    fused: bool = True) -> tuple[np.ndarray, float]:
     """Run ``iters`` steps on the GPU; returns (final grid, milliseconds)."""
     v = VARIANTS[variant] if isinstance(variant, str) else int(variant)
     g = Grid(host_grid)
     require_cuda(g.curr)
     with EventTimer() as t:
         for _ in range(p.iters):
-            gpu_step(g, p, v)
+            gpu_step(g, p, v, fused)
     return g.to_host(), t.ms
 
 

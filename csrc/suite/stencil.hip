@@ -52,11 +52,11 @@ __device__ __forceinline__ float apply_stencil(float center, FX fx, FY fy, float
 }
 
 template <int ORDER>
-__global__ __launch_bounds__(256) void stencil_global(float* __restrict__ next, const float* __restrict__ curr,
-                                                      int gx, int nx, int ny, float xcfl, float ycfl) {
+__device__ __forceinline__ void stencil_global_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
+                                                    int nx, int ny, float xcfl, float ycfl, int bx, int by) {
   constexpr int B = Coef<ORDER>::B;
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  const int y = blockIdx.y * 4 + threadIdx.y;
+  const int x = bx * 64 + threadIdx.x;
+  const int y = by * 4 + threadIdx.y;
   if (x >= nx || y >= ny) return;
   const int64_t i = (int64_t)(y + B) * gx + (x + B);
   const float* c = curr + i;
@@ -65,12 +65,12 @@ __global__ __launch_bounds__(256) void stencil_global(float* __restrict__ next, 
 }
 
 template <int ORDER, int ROWS>
-__global__ __launch_bounds__(256) void stencil_loop(float* __restrict__ next, const float* __restrict__ curr,
-                                                    int gx, int nx, int ny, float xcfl, float ycfl) {
+__device__ __forceinline__ void stencil_loop_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
+                                                  int nx, int ny, float xcfl, float ycfl, int bx, int by) {
   constexpr int B = Coef<ORDER>::B;
   constexpr int WIN = 2 * B + 1;
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  const int y0 = (blockIdx.y * 4 + threadIdx.y) * ROWS;
+  const int x = bx * 64 + threadIdx.x;
+  const int y0 = (by * 4 + threadIdx.y) * ROWS;
   if (x >= nx || y0 >= ny) return;
   const int64_t col = x + B;
   float win[WIN];  // column window rows y-B .. y+B (grid coordinates y0 .. y0+2B)
@@ -93,12 +93,12 @@ __global__ __launch_bounds__(256) void stencil_loop(float* __restrict__ next, co
 constexpr int kTX = 64, kTY = 16;
 
 template <int ORDER>
-__global__ __launch_bounds__(256) void stencil_lds(float* __restrict__ next, const float* __restrict__ curr, int gx,
-                                                   int gy, int nx, int ny, float xcfl, float ycfl) {
+__device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
+                                                 int gy, int nx, int ny, float xcfl, float ycfl, int tbx, int tby) {
   constexpr int B = Coef<ORDER>::B;
   constexpr int W = kTX + 2 * B, Hh = kTY + 2 * B;
   __shared__ float tile[Hh][W + 1];
-  const int bx = blockIdx.x * kTX, by = blockIdx.y * kTY;  // interior-coordinate origin
+  const int bx = tbx * kTX, by = tby * kTY;  // interior-coordinate origin
   // stage the tile + halo: grid rows by .. by+Hh-1, cols bx .. bx+W-1 (grid coordinates)
   for (int idx = threadIdx.y * 64 + threadIdx.x; idx < Hh * W; idx += 256) {
     const int r = idx / W, cc = idx - r * W;
@@ -118,14 +118,14 @@ __global__ __launch_bounds__(256) void stencil_lds(float* __restrict__ next, con
   }
 }
 
-__global__ __launch_bounds__(256) void stencil_bc_kernel(float* __restrict__ next, const float* __restrict__ curr,
-                                                         int gx, int gy, int b, float scale) {
-  // border strips: rows [0,b) and [gy-b,gy) (full width), columns [0,b) and [gx-b,gx) of the middle rows
+// border strips: rows [0,b) and [gy-b,gy) (full width), columns [0,b) and [gx-b,gx) of the middle rows;
+// `first`/`stride` enumerate the border cells over the calling threads
+__device__ __forceinline__ void bc_cells(float* __restrict__ next, const float* __restrict__ curr, int gx, int gy,
+                                         int b, float scale, int64_t first, int64_t stride) {
   const int64_t n_top = (int64_t)gx * b;
   const int64_t n_side = (int64_t)(gy - 2 * b) * b;
   const int64_t total = 2 * n_top + 2 * n_side;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+  for (int64_t t = first; t < total; t += stride) {
     int64_t idx;
     if (t < n_top) idx = t;
     else if (t < 2 * n_top) idx = (t - n_top) + (int64_t)gx * (gy - b);
@@ -140,32 +140,66 @@ __global__ __launch_bounds__(256) void stencil_bc_kernel(float* __restrict__ nex
   }
 }
 
-template <int ORDER>
-void launch(float* next, const float* curr, int gx, int gy, float xcfl, float ycfl, int variant, hipStream_t s) {
+__global__ __launch_bounds__(256) void stencil_bc_kernel(float* __restrict__ next, const float* __restrict__ curr,
+                                                         int gx, int gy, int b, float scale) {
+  bc_cells(next, curr, gx, gy, b, scale, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+           (int64_t)gridDim.x * blockDim.x);
+}
+
+// Fused iteration: workgroups [0, nint) run the interior variant, the remaining nbc workgroups apply the
+// boundary condition -- one launch per time step instead of two (the reference launched BC + stencil).
+template <int ORDER, int VARIANT>
+__global__ __launch_bounds__(256) void stencil_fused(float* __restrict__ next, const float* __restrict__ curr, int gx,
+                                                     int gy, int nx, int ny, float xcfl, float ycfl, int nbx, int nint,
+                                                     float scale) {
+  const int id = blockIdx.x;
+  if (id >= nint) {
+    const int64_t tid = (int64_t)(id - nint) * 256 + threadIdx.y * 64 + threadIdx.x;
+    bc_cells(next, curr, gx, gy, Coef<ORDER>::B, scale, tid, (int64_t)(gridDim.x - nint) * 256);
+    return;
+  }
+  const int bx = id % nbx, by = id / nbx;
+  if constexpr (VARIANT == 0) stencil_global_body<ORDER>(next, curr, gx, nx, ny, xcfl, ycfl, bx, by);
+  else if constexpr (VARIANT == 1) stencil_loop_body<ORDER, 8>(next, curr, gx, nx, ny, xcfl, ycfl, bx, by);
+  else stencil_lds_body<ORDER>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by);
+}
+
+template <int ORDER, int VARIANT>
+void launch_v(float* next, const float* curr, int gx, int gy, float xcfl, float ycfl, float scale, bool with_bc,
+              hipStream_t s) {
   constexpr int B = Coef<ORDER>::B;
   const int nx = gx - 2 * B, ny = gy - 2 * B;
-  const dim3 block(64, 4);
-  if (variant == 0) {
-    stencil_global<ORDER><<<dim3((nx + 63) / 64, (ny + 3) / 4), block, 0, s>>>(next, curr, gx, nx, ny, xcfl, ycfl);
-  } else if (variant == 1) {
-    constexpr int ROWS = 8;
-    stencil_loop<ORDER, ROWS>
-        <<<dim3((nx + 63) / 64, (ny + 4 * ROWS - 1) / (4 * ROWS)), block, 0, s>>>(next, curr, gx, nx, ny, xcfl, ycfl);
-  } else {
-    stencil_lds<ORDER><<<dim3((nx + kTX - 1) / kTX, (ny + kTY - 1) / kTY), block, 0, s>>>(next, curr, gx, gy, nx, ny,
-                                                                                         xcfl, ycfl);
-  }
+  const int rows_per_block = VARIANT == 0 ? 4 : (VARIANT == 1 ? 4 * 8 : kTY);
+  const int nbx = (nx + 63) / 64, nby = (ny + rows_per_block - 1) / rows_per_block;
+  const int nint = nbx * nby;
+  const int64_t bc_cells_total = 2 * ((int64_t)gx * B + (int64_t)(gy - 2 * B) * B);
+  const int nbc = with_bc ? (int)std::min<int64_t>((bc_cells_total + 255) / 256, 1024) : 0;
+  stencil_fused<ORDER, VARIANT><<<nint + nbc, dim3(64, 4), 0, s>>>(next, curr, gx, gy, nx, ny, xcfl, ycfl, nbx, nint,
+                                                                   scale);
+}
+
+template <int ORDER>
+void launch(float* next, const float* curr, int gx, int gy, float xcfl, float ycfl, int variant, float scale,
+            bool with_bc, hipStream_t s) {
+  if (variant == 0) launch_v<ORDER, 0>(next, curr, gx, gy, xcfl, ycfl, scale, with_bc, s);
+  else if (variant == 1) launch_v<ORDER, 1>(next, curr, gx, gy, xcfl, ycfl, scale, with_bc, s);
+  else launch_v<ORDER, 2>(next, curr, gx, gy, xcfl, ycfl, scale, with_bc, s);
 }
 
 }  // namespace
 
 void stencil_step(float* next, const float* curr, int gx, int gy, int order, float xcfl, float ycfl, int variant,
                   hipStream_t s) {
+  stencil_step_bc(next, curr, gx, gy, order, xcfl, ycfl, variant, 1.f, false, s);
+}
+
+void stencil_step_bc(float* next, const float* curr, int gx, int gy, int order, float xcfl, float ycfl, int variant,
+                     float scale, bool with_bc, hipStream_t s) {
   CME_REQUIRE(variant >= 0 && variant <= 2, "stencil_step: variant 0 (global), 1 (loop), 2 (lds)");
   switch (order) {
-    case 2: launch<2>(next, curr, gx, gy, xcfl, ycfl, variant, s); break;
-    case 4: launch<4>(next, curr, gx, gy, xcfl, ycfl, variant, s); break;
-    case 8: launch<8>(next, curr, gx, gy, xcfl, ycfl, variant, s); break;
+    case 2: launch<2>(next, curr, gx, gy, xcfl, ycfl, variant, scale, with_bc, s); break;
+    case 4: launch<4>(next, curr, gx, gy, xcfl, ycfl, variant, scale, with_bc, s); break;
+    case 8: launch<8>(next, curr, gx, gy, xcfl, ycfl, variant, scale, with_bc, s); break;
     default: CME_REQUIRE(false, "stencil_step: order must be 2, 4 or 8");
   }
   CME_LAUNCH_CHECK(s);

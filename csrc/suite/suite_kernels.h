@@ -33,6 +33,9 @@ void pagerank_propagate(const uint32_t* indptr, const uint32_t* edges, const flo
 // next(interior) = Stencil<order>(curr); variant 0 global, 1 register-blocked loop, 2 LDS tile
 void stencil_step(float* next, const float* curr, int gx, int gy, int order, float xcfl, float ycfl,
                   int variant, hipStream_t s);
+// one launch per time step: interior stencil AND next(border) = curr(border) * scale (with_bc)
+void stencil_step_bc(float* next, const float* curr, int gx, int gy, int order, float xcfl, float ycfl, int variant,
+                     float scale, bool with_bc, hipStream_t s);
 // next(border) = curr(border) * scale  (border width b)
 void stencil_bc(float* next, const float* curr, int gx, int gy, int b, float scale, hipStream_t s);
 

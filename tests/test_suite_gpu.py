@@ -129,3 +129,13 @@ def test_cipher_roundtrip(period, wrap):
     assert k == period
     assert np.array_equal(rec % 26, shifts % 26)
     assert torch.equal(plain, clean)
+
+
+@pytest.mark.parametrize("variant", ["global", "block", "shared"])
+@pytest.mark.parametrize("order", [2, 8])
+def test_stencil_fused_bc_equals_two_launches(variant, order):
+    p = hw3.SimParams(300, 211, 1.0, 1.0, 7, order)
+    g0 = hw3.init_grid(p)
+    a, _ = hw3.gpu_computation(g0, p, variant, fused=True)
+    b, _ = hw3.gpu_computation(g0, p, variant, fused=False)
+    assert np.array_equal(a, b)
