@@ -117,8 +117,7 @@ def main(argv=None) -> int:
 
     # sanity: parameters finite after training, peer waits never timed out
     ok = bool(torch.isfinite(tr.engine.params).all().item())
-    if tr.xgmi is not None:
-        tr.xgmi.check()
+    tr.check_comm()
     images = a.steps * global_batch
     value = images / dt
     if rank == 0:

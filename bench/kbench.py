@@ -88,6 +88,25 @@ def main(argv=None):
                                  ("wgrad_sgd", part(2)), ("wgrad_grads", part(2, 0)),
                                  ("step_fused", part(3)), ("sgd_flat", lambda: e.sgd(0.0))):
                     row[name + "_us"] = round(timeit(fn, a.reps), 3)
+                slots = e.fused_allreduce_slots()
+                if slots:  # wgrad with the xGMI all-reduce fused in, world 1 (the flag protocol, no peers)
+                    from cme213_sp18_amd._native import hip as _hip
+
+                    xc = _hip().comm.XgmiComm(0, 1, e.params.numel(), 4, slots)
+
+                    class _B:  # minimal bucket view for attach_xgmi
+                        c = xc
+
+                    e.attach_xgmi(_B)
+                    row["wgrad_xgmi1_us"] = round(timeit(part(2, 2), a.reps), 3)
+                    row["step_xgmi1_us"] = round(timeit(part(3, 2), a.reps), 3)
+                    torch.cuda.synchronize()
+                    row["xgmi1_sep_us"] = round(timeit(lambda: xc.run(0, e.grads.data_ptr(), e.params.data_ptr(), 0.0,
+                                                                      e.W1p.data_ptr(), e.np, e.H * e.P, 0,
+                                                                      e.params.numel(), st()), a.reps), 3)
+                    row["xgmi1_err"] = xc.error()
+                    e.attach_xgmi(None)
+                    xc.close()
                 flops = 2 * n * (784 * H * 2 + 10 * H * 3)
                 row["step_tflops"] = round(flops / (row["step_fused_us"] * 1e-6) / 1e12, 3)
                 print(json.dumps(row), flush=True)

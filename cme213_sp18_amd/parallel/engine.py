@@ -127,6 +127,7 @@ class MlpEngine:
         self._aux_stream = None
         self._alloc_acts(max_cols)
         self._step = None
+        self._xgmi_fuse = None
 
     def _configure_path(self):
         dev = self.device
@@ -283,12 +284,40 @@ class MlpEngine:
                     if self._aux_stream is None:
                         self._aux_stream = torch.cuda.Stream(self.device)
                     s.stream2 = self._aux_stream.cuda_stream
+            if self._xgmi_fuse is not None and s.bias_col:
+                s.set_xgmi(*self._xgmi_fuse)
             self._step = s
         return self._step
 
-    def run(self, off: int, n: int, scale: float, reg: float, lr: float, sgd: bool, with_loss: bool = False):
+    # ------------------------------------------------ xGMI all-reduce fused into the wgrad launch
+    def fused_allreduce_slots(self) -> int:
+        """Flag slots (one per wgrad workgroup tile) the fused data-parallel step needs; 0 when this
+        engine cannot run it (split path, H <= 128, all-ones XT feature, no head partials)."""
+        import os
+
+        bias_feature = (self.XT.shape[0] == self.P + 1 if self.XT is not None   # loaded, or will be
+                        else self.feature_major_copy and os.environ.get("CME_NO_BIAS_COL") != "1")
+        if not (self.backend == "hip" and self.np and self.H <= 128 and self.device.type == "cuda"
+                and self.gpart is None and bias_feature):
+            return 0
+        return max(0, int(hip().mlp_split_fused_tiles(self.P, self.H, 1 << 30)))
+
+    def attach_xgmi(self, bucket) -> None:
+        """Bind an open XgmiBucket (created with flag_slots >= fused_allreduce_slots()) to the step;
+        ``None`` detaches.  run(..., sgd=2) then all-reduces and applies SGD inside the wgrad launch."""
+        if bucket is None:
+            self._xgmi_fuse = None
+            if self._step is not None:
+                self._step.set_xgmi(0, 0, 0, 0, 0)
+            return
+        o = self.layout.offsets
+        self._xgmi_fuse = (int(bucket.c.desc_address), int(bucket.c.nblocks), int(o[1]), int(o[2]), int(o[3]))
+        self._hip_step().set_xgmi(*self._xgmi_fuse)
+
+    def run(self, off: int, n: int, scale: float, reg: float, lr: float, sgd, with_loss: bool = False):
         """Forward + backward on samples [off, off+n).  sgd=True: update params in
-        place; else write pre-scaled gradients into ``self.grads``."""
+        place; False: write pre-scaled gradients into ``self.grads``; 2: all-reduce over the attached
+        xGMI bucket and update inside the wgrad launch (attach_xgmi)."""
         if self.X is None:
             raise RuntimeError("load_dataset() first")
         if n > self.ld:
@@ -301,7 +330,8 @@ class MlpEngine:
                 self._a1k ^= 1
                 self.a1 = self._a1bufs[self._a1k]
                 st.a1 = self.a1.data_ptr()
-            st.run(int(off), int(n), float(scale), float(reg), float(lr), int(bool(sgd)), int(bool(with_loss)),
+            st.run(int(off), int(n), float(scale), float(reg), float(lr), 2 if sgd == 2 else int(bool(sgd)),
+                   int(bool(with_loss)),
                    torch.cuda.current_stream(self.device).cuda_stream)
         else:
             self._torch_step(off, n, scale, reg, lr, sgd, with_loss)

@@ -21,6 +21,7 @@ What changes (MI355X-first):
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -77,6 +78,27 @@ class DataParallelTrainer:
         self._graphs: dict = {}
         self.iter = 0
         self.xgmi = self._setup_xgmi(allreduce)
+        # the same all-reduce fused into the wgrad launch (one kernel less per step, tiles reduced as
+        # they finish): own IPC bucket with one flag slot per wgrad tile; enabled by load() once a
+        # bitwise comparison with the separate-kernel step has passed on every rank
+        self._xgmi_fused = None
+        self.fused_allreduce = False
+        if self.xgmi is not None and os.environ.get("CME_XGMI_FUSED", "1") != "0":
+            slots = self.engine.fused_allreduce_slots()
+            if slots and self.engine.params.dtype == torch.float32 and self._fused_fits(slots):
+                from .xgmi import XgmiBucket
+
+                try:
+                    xb = XgmiBucket(self.comm.group, self.rank, self.R, self.engine.params.numel(),
+                                    torch.float32, self.engine.device, flag_slots=slots)
+                    if xb.ok:
+                        self._xgmi_fused = xb
+                    else:
+                        xb.close()
+                except RuntimeError as ex:  # raised on every rank together (collective setup)
+                    print(f"[rank {self.rank}] fused xgmi bucket unavailable ({ex})", flush=True)
+        if self.xgmi is not None and bool(use_graphs) and backend == "hip":
+            self.use_graphs = True  # the xGMI steps are pure device work: capturable whatever the group
         self._bucketed = (self.R > 1 and self.xgmi is None and allreduce != "host" and overlap
                           and self.engine.supports_bucketed_wgrad and self.engine.device.type == "cuda")
         self._comm_stream = torch.cuda.Stream(self.engine.device) if self._bucketed else None
@@ -134,6 +156,45 @@ class DataParallelTrainer:
             return None
         return xb
 
+    def _fused_fits(self, tiles: int) -> bool:
+        """Every wgrad tile waits for the same tile of its peers, so all tiles of all ranks SHARING a
+        GPU must be resident at once (2 workgroups of 512 threads per CU at the kernel's occupancy).
+        One rank per GPU always fits (~180 tiles at H=100 on 256 CUs); the several-ranks-on-one-GPU
+        rehearsal only with 2 ranks.  Collective."""
+        import torch.distributed as dist
+
+        dev = self.engine.device
+        props = torch.cuda.get_device_properties(dev)
+        ident = str(getattr(props, "uuid", "")) or f"{os.environ.get('HIP_VISIBLE_DEVICES', '')}:{dev.index}"
+        ids = [None] * self.R
+        dist.all_gather_object(ids, (os.uname().nodename, ident), group=self.comm.group)
+        sharing = sum(1 for x in ids if x == ids[self.rank])
+        return self._all_true(sharing * tiles <= 2 * props.multi_processor_count)
+
+    def _all_true(self, v: bool) -> bool:
+        import torch.distributed as dist
+
+        out = [None] * self.R
+        dist.all_gather_object(out, bool(v), group=self.comm.group)
+        return all(out)
+
+    def check_comm(self) -> None:
+        """Raise if a peer wait of an xGMI all-reduce timed out (a rank stalled or died)."""
+        for b in (self.xgmi, self._xgmi_fused):
+            if b is not None:
+                b.check()
+
+    def close(self) -> None:
+        """Collective: release the xGMI IPC buckets (every rank must call it)."""
+        self.engine.attach_xgmi(None)
+        for name in ("_xgmi_fused", "xgmi"):
+            b = getattr(self, name)
+            if b is not None:
+                b.close()
+                setattr(self, name, None)
+        self.fused_allreduce = False
+        self._graphs.clear()
+
     def _allreduce_sgd(self, lr: float) -> None:
         e = self.engine
         if self.allreduce_mode == "host":
@@ -162,11 +223,53 @@ class DataParallelTrainer:
         self.N = self.engine.num_samples
         self._graphs.clear()
         self._la = None
+        if self._xgmi_fused is not None:
+            self.fused_allreduce = self._check_fused()
+            self.allreduce_impl = "xgmi-fused" if self.fused_allreduce else "xgmi"
         if self.lookahead:
             from .lookahead import LookaheadRunner
 
             if LookaheadRunner.supported(self.engine):
                 self._la = LookaheadRunner(self.engine)
+
+    def _check_fused(self) -> bool:
+        """One step from the same state through both all-reduce paths (separate xGMI kernel, and
+        fused into wgrad); enable the fused one only if every rank gets bitwise-identical parameters
+        and bf16 planes.  The state is restored afterwards.  Collective."""
+        e = self.engine
+        if e.fused_allreduce_slots() == 0 or self.N < self.R:
+            e.attach_xgmi(None)
+            return False
+        snap = self._snapshot()
+        off, n = self.shard(0, min(self.B, self.N))
+        scale, reg, lr = 1.0 / (n * self.R), 1e-3 / self.R, 0.05
+        e.attach_xgmi(None)
+        e.run(off, n, scale, reg, lr, sgd=False)
+        self._allreduce_sgd(lr)
+        ref = (e.params.clone(), e.W1p.clone())
+        self._restore(snap)
+        ok = True
+        try:
+            e.attach_xgmi(self._xgmi_fused)
+            for _ in range(3):  # both buffer halves, and back to the first
+                self._restore(snap)
+                e.run(off, n, scale, reg, lr, sgd=2)
+                torch.cuda.synchronize(e.device)
+                ok &= bool(torch.equal(e.params, ref[0]) and torch.equal(e.W1p, ref[1]))
+            ok &= self._xgmi_fused.error() == 0 and self.xgmi.error() == 0
+        except RuntimeError as ex:
+            print(f"[rank {self.rank}] fused xgmi step failed: {ex}", flush=True)
+            ok = False
+        self._restore(snap)
+        torch.cuda.synchronize(e.device)
+        ok = self._all_true(ok)
+        if not ok:
+            e.attach_xgmi(None)
+            self._xgmi_fused.close()  # collective; also drops its error flag
+            self._xgmi_fused = None
+            if self.rank == 0:
+                print("[xgmi] fused all-reduce self-check failed; using the separate kernel", flush=True)
+        return ok
 
     def _uses_lookahead(self, plan: EpochPlan) -> bool:
         from .lookahead import LookaheadRunner
@@ -202,6 +305,8 @@ class DataParallelTrainer:
         scale = 1.0 / (n * self.R)
         if isinstance(self.comm, NullComm) and self.allreduce_mode != "host":  # 1 process: SGD fused into wgrad
             e.run(off, n, scale, reg, lr, sgd=True, with_loss=with_loss)
+        elif self.fused_allreduce:
+            e.run(off, n, scale, reg / self.R, lr, sgd=2, with_loss=with_loss)
         elif self._bucketed:
             self._step_bucketed(off, n, scale, reg / self.R, lr, with_loss)
         else:
@@ -365,8 +470,7 @@ class DataParallelTrainer:
                     stats.images += (ln // self.R) * self.R
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
-            if self.xgmi is not None:
-                self.xgmi.check()
+            self.check_comm()
             self.comm.barrier()
         finally:
             if err_file is not None:

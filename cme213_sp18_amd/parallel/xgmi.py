@@ -33,7 +33,8 @@ class XgmiBucket:
     MODE_SGD = 0
     MODE_ALLREDUCE = 1
 
-    def __init__(self, group, rank: int, world: int, numel: int, dtype: torch.dtype, device, self_test: bool = True):
+    def __init__(self, group, rank: int, world: int, numel: int, dtype: torch.dtype, device, self_test: bool = True,
+                 flag_slots: int = 0):
         import torch.distributed as dist
 
         if world > hip().comm.MAX_RANKS:
@@ -50,7 +51,7 @@ class XgmiBucket:
             # IPC failure makes ALL ranks give up together instead of leaving peers in a collective
             mine, err = None, None
             try:
-                self.c = hip().comm.XgmiComm(rank, world, self.numel, 8 if self.code else 4)
+                self.c = hip().comm.XgmiComm(rank, world, self.numel, 8 if self.code else 4, int(flag_slots))
                 mine = self.c.handles()
             except Exception as ex:  # noqa: BLE001 - reported collectively below
                 err = f"rank {rank}: {ex}"

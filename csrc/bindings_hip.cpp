@@ -8,6 +8,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstdlib>
+
+#include "comm/xgmi_allreduce.h"
 #include "common/hip_common.h"
 #include "mlp/mlp_kernels.h"
 #include "mlp/mlp_split.h"
@@ -62,6 +65,39 @@ struct MlpStep {
       roles_pending = false;
     }
   }
+  // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
+  cme::XgmiFuse xf;
+  void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2) {
+    if (!desc) {
+      xf = cme::XgmiFuse{};
+      return;
+    }
+    CME_REQUIRE(split && bias_col && XT, "MlpStep.set_xgmi: split path with the all-ones XT feature only");
+    CME_REQUIRE(cme::mlp_split_fused_tiles(P, H, (int)std::min<int64_t>(slots, 1 << 30)) > 0,
+                "MlpStep.set_xgmi: the bucket has fewer flag slots than the wgrad launch has tiles");
+    const auto* d = reinterpret_cast<const cme::comm::XgmiDesc*>(desc);
+    CME_REQUIRE(d->world >= 1 && d->world <= 8 && d->mybuf && d->n >= off_b2 + C,
+                "MlpStep.set_xgmi: bucket not open or smaller than the flat gradient");
+    cme::XgmiFuse f;
+    f.mybuf = d->mybuf;
+    for (int r = 0; r < d->world; ++r) {
+      CME_REQUIRE(d->peers[r] && d->peerflags[r], "MlpStep.set_xgmi: peer handles not opened");
+      f.peers[r] = d->peers[r];
+      f.peerflags[r] = d->peerflags[r];
+    }
+    f.myflags = d->myflags;
+    f.epochs = d->epochs;
+    f.err = d->err;
+    f.rank = d->rank;
+    f.world = d->world;
+    f.npad = d->npad;
+    f.off_b1 = off_b1;
+    f.off_W2 = off_W2;
+    f.off_b2 = off_b2;
+    const char* v = std::getenv("CME_XF_VARIANT");
+    f.variant = v ? std::atoi(v) : 0;
+    xf = f;
+  }
   float xscale = 1.f;    // split path: inputs are uint8 * xscale
   uintptr_t W1p = 0, dZ1p = 0;
 
@@ -92,7 +128,8 @@ struct MlpStep {
 
   // Forward + backward for samples [off, off+n) of the resident dataset.
   // sgd=1 applies the update in place (single process); sgd=0 writes the
-  // pre-scaled gradients into the bucket for the all-reduce.
+  // pre-scaled gradients into the bucket for the all-reduce; sgd=2 all-reduces over xGMI and applies
+  // the update inside the wgrad launch (set_xgmi, split path).
   // parts: bit0 = forward + head, bit1 = weight gradients / update (profiling hook; default both);
   //        with bit0: +4 skips the head (forward GEMM only), +8 skips the forward GEMM (head only)
   void run(int64_t off, int n, double scale, double reg, double lr, int sgd, int with_loss, uintptr_t stream,
@@ -100,7 +137,11 @@ struct MlpStep {
     CME_REQUIRE(n > 0 && n <= ld, "MlpStep.run: 0 < n <= ld required");
     if (split) {
       CME_REQUIRE(XT != 0 && W1p != 0 && dZ1p != 0, "MlpStep.run: split path needs XT, W1p, dZ1p");
-      const cme::SplitStepArgs a = split_args(off, n, scale, reg, lr, sgd, with_loss);
+      cme::SplitStepArgs a = split_args(off, n, scale, reg, lr, sgd == 2 ? 0 : sgd, with_loss);
+      if (sgd == 2) {  // all-reduce + SGD inside the wgrad launch
+        CME_REQUIRE(xf.world > 0, "MlpStep.run(sgd=2): set_xgmi() first");
+        a.xf = xf;
+      }
       if (parts & 1) {
         if (fused_head) {
           cme::mlp_split_fwdhead(a, S(stream));
@@ -118,7 +159,7 @@ struct MlpStep {
         }
       }
       if (parts & 2) {
-        if (stream2 && bias_col && !a.gpart) {
+        if (stream2 && bias_col && !a.gpart && sgd != 2) {
           if (!ev_head) {
             HIP_CHECK(hipEventCreateWithFlags(&ev_head, hipEventDisableTiming));
             HIP_CHECK(hipEventCreateWithFlags(&ev_roles, hipEventDisableTiming));
@@ -141,6 +182,7 @@ struct MlpStep {
       }
       return;
     }
+    CME_REQUIRE(sgd != 2, "MlpStep.run(sgd=2): split paths only");
     const DType d = to_dt(dt);
     const size_t xe = d == DType::F64 ? 8 : (d == DType::BF16 ? 2 : 4);
     const void* Xb = reinterpret_cast<const char*>(X) + (size_t)off * P * xe;
@@ -356,6 +398,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("bias_col", &MlpStep::bias_col)
       .def_readwrite("stream2", &MlpStep::stream2)
       .def("join", &MlpStep::join, py::arg("stream"))
+      .def("set_xgmi", &MlpStep::set_xgmi, py::arg("desc"), py::arg("slots"), py::arg("off_b1"), py::arg("off_W2"),
+           py::arg("off_b2"))
       .def_property_readonly("roles_pending", [](const MlpStep& s) { return s.roles_pending; })
       .def("la_prologue", &MlpStep::la_prologue)
       .def("la_l2", &MlpStep::la_l2)
@@ -396,6 +440,7 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("params"), py::arg("grads"), py::arg("count"), py::arg("lr"), py::arg("W1p"), py::arg("w1n"),
       py::arg("npw"), py::arg("stream") = 0);
   m.def("split_fwdhead_blocks", &cme::mlp_split_fwdhead_blocks);
+  m.def("mlp_split_fused_tiles", &cme::mlp_split_fused_tiles, py::arg("P"), py::arg("H"), py::arg("cap"));
 
   bind_suite(m);
   bind_comm(m);

@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -43,7 +44,9 @@ void* open_handle(const std::string& b) {
 // Owns this rank's IPC buffers and the peers' mappings.
 class XgmiComm {
  public:
-  XgmiComm(int rank, int world, int64_t n, int elt_bytes) {
+  // flag_slots: minimum number of [kMaxRanks]-word flag rows (a kernel that signals per workgroup tile
+  // -- the wgrad launch with the all-reduce fused in -- needs one per tile; default one per chunk)
+  XgmiComm(int rank, int world, int64_t n, int elt_bytes, int64_t flag_slots = 0) {
     CME_REQUIRE(world >= 1 && world <= kMaxRanks, "XgmiComm: 1 <= world <= 8");
     CME_REQUIRE(rank >= 0 && rank < world, "XgmiComm: bad rank");
     CME_REQUIRE(elt_bytes == 4 || elt_bytes == 8, "XgmiComm: f32 or f64");
@@ -51,7 +54,7 @@ class XgmiComm {
     d_.world = world;
     d_.n = n;
     d_.npad = xgmi_padded_count(n);
-    nblocks_ = std::max<int64_t>(1, xgmi_num_blocks(n));
+    nblocks_ = std::max<int64_t>({1, xgmi_num_blocks(n), flag_slots});
     // ONE dedicated allocation per rank, [data: 2 x npad | flags: nblocks x 8 words], exported with one
     // IPC handle.  Rounded to 2 MiB so the runtime never sub-allocates it (hipIpcGetMemHandle rejects
     // sub-allocated pointers); plain device memory -- hipDeviceMallocUncached pages do not export
@@ -122,6 +125,10 @@ class XgmiComm {
   }
 
   int64_t nblocks() const { return nblocks_; }
+  int64_t npad() const { return d_.npad; }
+  // address of the descriptor, for a kernel that fuses this all-reduce in (MlpStep.set_xgmi); valid
+  // while this object is open
+  uintptr_t desc_address() const { return reinterpret_cast<uintptr_t>(&d_); }
 
  private:
   size_t flag_bytes() const { return (size_t)nblocks_ * kMaxRanks * sizeof(uint32_t); }
@@ -140,7 +147,8 @@ void bind_comm(py::module_& m) {
   using cme::comm::XgmiComm;
   auto sm = m.def_submodule("comm", "xGMI peer-to-peer all-reduce (IPC buffers, SGD fused)");
   py::class_<XgmiComm>(sm, "XgmiComm")
-      .def(py::init<int, int, int64_t, int>(), py::arg("rank"), py::arg("world"), py::arg("n"), py::arg("elt_bytes"))
+      .def(py::init<int, int, int64_t, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("n"),
+           py::arg("elt_bytes"), py::arg("flag_slots") = 0)
       .def("handles", &XgmiComm::handles)
       .def("open", &XgmiComm::open)
       .def("run", &XgmiComm::run, py::arg("dtype"), py::arg("grads"), py::arg("params"), py::arg("lr"),
@@ -148,7 +156,9 @@ void bind_comm(py::module_& m) {
       .def("error", &XgmiComm::error)
       .def("close", &XgmiComm::close)
       .def("close_peers", &XgmiComm::close_peers)
-      .def_property_readonly("nblocks", &XgmiComm::nblocks);
+      .def_property_readonly("nblocks", &XgmiComm::nblocks)
+      .def_property_readonly("npad", &XgmiComm::npad)
+      .def_property_readonly("desc_address", &XgmiComm::desc_address);
   sm.attr("MODE_SGD") = cme::comm::kModeSgd;
   sm.attr("MODE_ALLREDUCE") = cme::comm::kModeAllReduce;
   sm.attr("MAX_RANKS") = cme::comm::kMaxRanks;

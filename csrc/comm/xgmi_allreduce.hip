@@ -48,7 +48,7 @@ struct Args {
   __hip_bfloat16* planes;
   int np;
   int rank, world, mode;
-  int variant;  // diagnostics (CME_XGMI_VARIANT): bit0 extra system release fence after the stores
+  int variant;  // diagnostics (CME_XGMI_VARIANT): bit1 extra acquire fence (L2 invalidate)
 };
 
 constexpr int kSysCoherent = 1 | 16;  // buffer-load cache policy sc0 | sc1 (system coherent)
@@ -143,17 +143,12 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (a.variant & 1) {
-    if (t == 0) {
-      __threadfence_system();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-  }
 
-  // 2. signal every peer that my chunk c of this epoch is ready
+  // 2. signal every peer that my chunk c of this epoch is ready: a system-scope RELEASE store (L2
+  //    write-back before the flag) by the signalling lanes of wave 0; the barrier above makes every
+  //    wave's stores part of what it releases
   if (t < a.world)
-    __hip_atomic_store(a.peerflags[t] + c * kMaxRanks + a.rank, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.peerflags[t] + c * kMaxRanks + a.rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   // 3. wait for every peer's chunk c (bounded)
   if (t < a.world) {
     uint32_t spins = 0;
@@ -167,12 +162,13 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
     }
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire: drop stale cached peer lines
+  if (a.variant & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // diagnostics: full L2 invalidate
 
   // 4. sum the R gradients of my elements in rank order, 5. update.
-  //    Peer data is read with system-coherent loads (sc0 sc1): a line of a peer buffer cached by this
-  //    agent two epochs ago must not be served again (a peer mapped on the SAME device is ordinary
-  //    local memory to the L2, which a system-scope acquire does not invalidate).
+  //    Peer data is read with system-coherent loads (sc0 sc1), i.e. as relaxed system-scope atomics,
+  //    issued only after the peer's release-ordered flag was observed: no acquire fence (an L2
+  //    invalidation per block) is needed -- and a line of a peer buffer cached by this agent two
+  //    epochs ago is never served again (a peer mapped on the SAME device is local memory to the L2).
   if (full) {
     V acc;
 #pragma unroll

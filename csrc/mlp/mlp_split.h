@@ -26,6 +26,23 @@
 
 namespace cme {
 
+// Gradient all-reduce fused into the weight-gradient launch (data parallel over xGMI, one process per
+// GPU): every gradient tile is written into this step's half of the rank's IPC buffer, published,
+// and, once every peer has published the same tile, summed in rank order and applied (SGD + bf16
+// planes) by the same workgroup.  world == 0: off.  Buffers/handles: csrc/comm (XgmiComm).
+struct XgmiFuse {
+  void* mybuf = nullptr;
+  const void* peers[8] = {};
+  uint32_t* myflags = nullptr;
+  uint32_t* peerflags[8] = {};
+  uint32_t* epochs = nullptr;
+  int* err = nullptr;
+  int rank = 0, world = 0;
+  int64_t npad = 0;
+  int64_t off_b1 = 0, off_W2 = 0, off_b2 = 0;  // flat-arena offsets ([W1|b1|W2|b2], 64-aligned)
+  int variant = 0;  // diagnostics (CME_XF_VARIANT): bit0 relaxed flag store, bit1 extra acquire fence
+};
+
 struct SplitStepArgs {
   int P = 784, H = 100, C = 10, n = 0, ld = 0;
   int npw = 3, npz = 3;          // planes of W1 and of dZ1 (3: exact fp32, 1: bf16)
@@ -67,7 +84,12 @@ struct SplitStepArgs {
   const float* An = nullptr;
   float* z1n = nullptr;
   float c1 = 0.f, c2 = 0.f;
+  XgmiFuse xf;
 };
+
+// flag slots (workgroup tiles) of the fused-all-reduce wgrad launch for a P-H layer with the all-ones
+// feature; -1 when above `cap`
+int mlp_split_fused_tiles(int P, int H, int cap);
 
 void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);
 // tiled forward only: a1 = sigmoid(W1 X + b1) (pair with mlp_head for the 3-kernel step)

@@ -248,16 +248,95 @@ __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a,
                                                                a.H * a.P * (int)sizeof(bf16), a.stamps);
 }
 
+
+// ---- gradient all-reduce fused into the wgrad launch (XgmiFuse, see mlp_split.h) ------------------
+// Protocol per gradient tile (same as csrc/comm/xgmi_allreduce.hip per chunk): epoch e = epochs[tile]+1;
+// the tile's gradients go WRITE-THROUGH (sc0 sc1) into half e&1 of my IPC buffer; drain, barrier,
+// system-scope release flag store into every peer's slot [tile][rank]; bounded wait for every peer's
+// flag; rank-order sum with system-coherent loads (bit-identical on every rank).  Double
+// buffering + per-tile epochs: half e&1 of a tile is rewritten only after every peer passed e-1.
+constexpr int kXfSys = 1 | 16;  // cache policy sc0 | sc1: system coherent
+constexpr uint32_t kXfSpinLimit = 1u << 22;
+
+__device__ __forceinline__ void xf_store(float* base, int64_t idx, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), make_rsrc(base), (int)(idx * 4), 0, kXfSys);
+}
+
+__device__ __forceinline__ float xf_load(const void* base, int64_t idx) {
+  const auto w = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(base), (int)(idx * 4), 0, kXfSys);
+  return __builtin_bit_cast(float, w);
+}
+
+__device__ __forceinline__ uint32_t xf_begin(const XgmiFuse& x, int tile, uint32_t* s_ep) {
+  if (threadIdx.x == 0) *s_ep = x.epochs[tile] + 1;
+  __syncthreads();
+  return *s_ep;
+}
+
+// every thread's gradient stores of this tile are complete -> publish, wait for the peers
+__device__ __forceinline__ void xf_exchange(const XgmiFuse& x, int tile, uint32_t ep) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < x.world) {
+    if (x.variant & 1)
+      __hip_atomic_store(x.peerflags[t] + tile * 8 + x.rank, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      __hip_atomic_store(x.peerflags[t] + tile * 8 + x.rank, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t spins = 0;
+    const uint32_t* f = x.myflags + tile * 8 + t;
+    while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) < 0) {
+      if (++spins > kXfSpinLimit) {
+        atomicExch(x.err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  // no acquire fence: every peer datum is read with system-coherent loads (xf_load) issued after the
+  // flag was observed; a full L2 invalidation per tile measured +9 us per step (182 tiles)
+  if (x.variant & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+__device__ __forceinline__ float xf_sum(const XgmiFuse& x, int64_t idx) {
+  float s = xf_load(x.peers[0], idx);
+  for (int r = 1; r < x.world; ++r) s += xf_load(x.peers[r], idx);
+  return s;
+}
+
+__device__ __forceinline__ void xf_end(const XgmiFuse& x, int tile, uint32_t ep) {
+  if (threadIdx.x == 0) x.epochs[tile] = ep;
+}
+
 // ======================================================================
 // Kernel B: dW1 (MFMA over dZ1 planes x X^T) + fused reg/SGD/plane refresh,
 //           dW2 and bias gradients as extra workgroup roles.
 // ======================================================================
 constexpr int kWMB = 1, kWNB = 2, kWKS = 8, kWT = 64 * kWKS;
 
+// this lane's share of sum(src[0:n]) (combine with wave_sum)
+__device__ __forceinline__ float row_sum(const float* src, int n, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(src);
+  float s = 0.f;
+  for (int j0 = 0; j0 < n; j0 += 64 * 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = j0 + u * 64 + lane;
+      v[u] = buf_load1<float>(rs, j < n ? j * 4 : kOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
+  return s;
+}
+
 struct EpiW2 {
   float* W2;
   float* gW2;
   int H, sgd;
+  int sys;  // gradients into a peer-visible IPC buffer (write-through)
   float reg, lr;
   float pre[kEpiMaxQ];
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
@@ -268,6 +347,7 @@ struct EpiW2 {
     const float w = pre[q];
     const float g = v + reg * w;
     if (sgd) W2[i] = w - lr * g;
+    else if (sys) xf_store(gW2, (int64_t)i, g);
     else gW2[i] = g;
   }
 };
@@ -296,12 +376,14 @@ struct EpiW1 {
   float pre[kEpiMaxQ];
   float* b1;
   float* gb1;
+  int sys;  // gradients into a peer-visible IPC buffer (write-through)
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
     pre[q] = buf_load1<float>(make_rsrc(W1), (ok && col < P) ? (row * P + col) * 4 : kOOB);
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     if (col == P) {  // the all-ones feature: db1[row] (no input scale, no regulariser)
       if (sgd) b1[row] -= lr * v;
+      else if (sys) xf_store(gb1, row, v);
       else gb1[row] = v;
       return;
     }
@@ -313,6 +395,8 @@ struct EpiW1 {
       W1[i] = nw;
       if (npw == 3) split_store<3>(nw, W1p, plane, i);
       else split_store<1>(nw, W1p, plane, i);
+    } else if (sys) {
+      xf_store(gW1, (int64_t)i, g);
     } else {
       gW1[i] = g;
     }
@@ -335,16 +419,44 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   }
   const int bid = blockIdx.x - tc;
   const float reg = (float)a.reg, lr = (float)a.lr;
+  const bool fused = a.xf.world > 0;
+  __shared__ uint32_t s_ep;
   if (bid < t1) {  // ---- dW1 tile
     const int tb = xcd_remap(bid, t1);
     const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
     TileGeom g{r1, a.P + a.bias_col, a.n, a.w1_row0 + (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
-    EpiW1 epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw, reg, lr, a.xscale, {},
-              a.b1, a.gb1};
+    float *gw = a.gW1, *gb = a.gb1;
+    uint32_t ep = 0;
+    if (fused) {  // gradients straight into this step's half of the IPC buffer
+      ep = xf_begin(a.xf, bid, &s_ep);
+      gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(ep & 1u) * a.xf.npad;
+      gb = gw + a.xf.off_b1;
+    }
+    EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.npw, reg, lr,
+              a.xscale, {}, a.b1, gb, fused ? 1 : 0};
     constexpr int U = 4;
     wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
                                                               static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
                                                               red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
+    if (fused) {  // all-reduce this tile with the peers, then SGD + bf16 planes
+      xf_exchange(a.xf, bid, ep);
+      const int64_t half = (int64_t)(ep & 1u) * a.xf.npad;
+      constexpr int TW = 16 * kWNB;
+      for (int e = threadIdx.x; e < 16 * kWMB * TW; e += kWT) {
+        const int row = g.m0 + e / TW, col = g.n0 + e % TW;
+        if (row >= g.M || col >= g.N) continue;
+        if (col < a.P) {
+          const int64_t i = (int64_t)row * a.P + col;
+          const float w = a.W1[i] - lr * xf_sum(a.xf, half + i);
+          a.W1[i] = w;
+          if (a.npw == 3) split_store<3>(w, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
+          else split_store<1>(w, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
+        } else {
+          a.b1[row] -= lr * xf_sum(a.xf, half + a.xf.off_b1 + row);
+        }
+      }
+      xf_end(a.xf, bid, ep);
+    }
     return;
   }
   if (a.gpart) {  // ---- reduce the head's per-block partials of dW2 | db1 | db2, then update
@@ -383,11 +495,41 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     //                        the 8 waves split K = batch; fused reg + SGD (or gradient) epilogue
     const int tb = bid - t1;
     TileGeom g{a.C, a.H, a.n, 0, tb * 16};
-    EpiW2 epi{a.W2, a.gW2, a.H, a.sgd, reg, lr, {}};
+    float* gw = a.gW2;
+    uint32_t ep = 0;
+    if (fused) {
+      ep = xf_begin(a.xf, bid, &s_ep);
+      gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(ep & 1u) * a.xf.npad + a.xf.off_W2;
+    }
+    EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, fused ? 1 : 0, reg, lr, {}};
     if (a.n % 4 == 0)
       wsk_tile<float, 1, 1, kWKS, true, true, 1, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red);
     else
       wsk_tile<float, 1, 1, kWKS, true, true, 0, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red);
+    if (fused) {
+      const int64_t half = (int64_t)(ep & 1u) * a.xf.npad;
+      const bool with_b2 = tb == 0;  // db2 (fused mode has no separate bias role): one wave per class
+      if (with_b2) {
+        for (int c = wv; c < a.C; c += kWKS) {
+          const float sc = wave_sum(row_sum(a.D + (size_t)c * a.ld, a.n, lane));
+          if (lane == 0) xf_store(static_cast<float*>(a.xf.mybuf), half + a.xf.off_b2 + c, sc);
+        }
+      }
+      xf_exchange(a.xf, bid, ep);
+      const int ne = 16 * 16 + (with_b2 ? a.C : 0);
+      for (int e = threadIdx.x; e < ne; e += kWT) {
+        if (e < 256) {
+          const int c = e / 16, h = tb * 16 + e % 16;
+          if (c >= a.C || h >= a.H) continue;
+          const int64_t i = (int64_t)c * a.H + h;
+          a.W2[i] -= lr * xf_sum(a.xf, half + a.xf.off_W2 + i);
+        } else {
+          const int c = e - 256;
+          a.b2[c] -= lr * xf_sum(a.xf, half + a.xf.off_b2 + c);
+        }
+      }
+      xf_end(a.xf, bid, ep);
+    }
     return;
   }
   // ---- bias gradients: one wave per row; rows [0,H) -> db1 from dZ1, [H,H+C) -> db2 from D
@@ -395,20 +537,8 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   if (row >= a.H + a.C) return;
   const bool first = row < a.H;
   const float* src = first ? a.dZ1 + (size_t)row * a.ld : a.D + (size_t)(row - a.H) * a.ld;
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(src);
   const float bpre = buf_load1<float>(make_rsrc(first ? a.b1 : a.b2), (first ? row : row - a.H) * 4);
-  float s = 0.f;
-  for (int j0 = 0; j0 < a.n; j0 += 64 * 16) {
-    float v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int j = j0 + u * 64 + lane;
-      v[u] = buf_load1<float>(rs, j < a.n ? j * 4 : kOOB);
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) s += v[u];
-  }
-  s = wave_sum(s);
+  const float s = wave_sum(row_sum(src, a.n, lane));
   if (lane == 0) {
     float* bp = first ? a.b1 : a.b2;
     const int r = first ? row : row - a.H;
@@ -649,7 +779,13 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   const int w1rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int t1n = cdiv(a.P + a.bias_col, 16 * kWNB), t1 = (big || !do_w1) ? 0 : cdiv(w1rows, 16 * kWMB) * t1n;
   const int t2 = !do_roles ? 0 : (a.gpart ? cdiv(a.C * a.H + a.H + a.C, kWT) : cdiv(a.H, 16));
-  const int tb = (do_roles && !a.gpart) ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
+  const bool fused = a.xf.world > 0;
+  if (fused)
+    CME_REQUIRE(!big && do_w1 && do_roles && a.bias_col && !a.gpart && !a.GTn && a.w1_row0 == 0 && a.w1_rows < 0 &&
+                    a.C <= 16 && a.xf.world <= 8 && t1 + t2 <= mlp_split_fused_tiles(a.P, a.H, 1 << 30),
+                "wgrad: fused all-reduce needs the whole small-layer step with the all-ones XT feature");
+  // fused mode: db2 comes from the first dW2 tile (no separate bias role)
+  const int tb = (do_roles && !a.gpart && !fused) ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
   if (t1 + t2 + tb == 0 && !a.GTn) {
     CME_LAUNCH_CHECK(s);
     return;
@@ -670,6 +806,11 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   if (a.npz == 3) { CME_WG(3) } else { CME_WG(1) }
 #undef CME_WG
   CME_LAUNCH_CHECK(s);
+}
+
+int mlp_split_fused_tiles(int P, int H, int cap) {
+  const int t = cdiv(P + 1, 16 * kWNB) * cdiv(H, 16 * kWMB) + cdiv(H, 16);
+  return t <= cap ? t : -1;
 }
 
 void mlp_split_planes(const float* W, void* planes, int64_t n, int np, hipStream_t s) {

@@ -129,8 +129,32 @@ def xgmi_worker(rank, world, comm, device, out_dir):
         tr = DataParallelTrainer(nn, comm=comm, device=dev, batch_size=800, use_graphs=False, allreduce=mode)
         assert (tr.xgmi is not None) == (mode == "xgmi")
         tr.load(x, y)
+        if mode == "xgmi":
+            # all-reduce fused into the wgrad launch: on whenever every rank's tiles fit on the GPU
+            # (2 ranks sharing one GPU do; 4 do not and must fall back to the separate kernel)
+            res["fused_on"] = float(tr.fused_allreduce)
+            if world == 2:
+                res["ok_fused_enabled"] = float(tr.fused_allreduce)
         tr.train(2, 0.05, 1e-4)
         out[mode] = nn.W[0].copy(), nn.W[1].copy()
+        if mode == "xgmi" and tr.fused_allreduce:  # HIP-graph replay of the fused step == eager steps
+            e = tr.engine
+            snap = tr._snapshot()
+            for _ in range(3):
+                tr.step(800, 800, 0.05, 1e-4)
+            torch.cuda.synchronize()
+            eager = (e.params.clone(), e.W1p.clone())
+            tr._restore(snap)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                tr.step(800, 800, 0.05, 1e-4)
+            for _ in range(3):
+                graph.replay()
+            torch.cuda.synchronize()
+            res["ok_fused_graph"] = float(torch.equal(e.params, eager[0]) and torch.equal(e.W1p, eager[1]))
+            res["ok_fused_err"] = float(tr._xgmi_fused.error() == 0)
+        tr.close()
     res["trainer_w1_diff"] = float(np.abs(out["xgmi"][0] - out["off"][0]).max())
     res["trainer_w2_diff"] = float(np.abs(out["xgmi"][1] - out["off"][1]).max())
     # overlapped bucketed backward (dW1 row chunks all-reduced on a side stream) vs one bucket

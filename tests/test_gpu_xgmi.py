@@ -36,3 +36,12 @@ def test_xgmi_stress_four_ranks():
                        capture_output=True, text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS="2"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "bad_elements=0" in r.stdout, r.stdout[-2000:]
+
+
+def test_xgmi_fused_wgrad_stress_two_ranks():
+    """200 data-parallel steps with the all-reduce fused into the wgrad launch == the same steps through
+    the separate all-reduce kernel, bitwise, on both ranks."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "stress_fused.py"), "2", "200"],
+                       capture_output=True, text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "fused_ranks=2 bad_elements=0" in r.stdout, r.stdout[-2000:]
