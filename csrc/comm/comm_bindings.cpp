@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -41,6 +42,41 @@ void* open_handle(const std::string& b) {
   return p;
 }
 
+// Process-wide pool of exported IPC allocations.  A bucket's buffer is never hipFree'd: closing returns
+// it here and the next bucket of a similar size takes it back (same allocation, same IPC handle).
+// Reason (measured, 4 ranks sharing one GPU): after buffers were freed and re-allocated, a peer's
+// hipIpcOpenMemHandle of a NEW handle returned a mapping of a different rank's buffer -- the runtime's
+// import cache keyed on recycled memory.  Reusing allocations removes the churn; the signature check
+// in open() catches any remaining mix-up loudly instead of summing the wrong gradients.
+struct IpcPool {
+  std::vector<std::pair<void*, size_t>> free_;
+  void* take(size_t bytes, size_t* got) {
+    size_t best = 0;
+    for (size_t i = 1; i < free_.size(); ++i)
+      if (free_[i].second >= bytes && (free_[best].second < bytes || free_[i].second < free_[best].second)) best = i;
+    if (!free_.empty() && free_[best].second >= bytes && free_[best].second <= 2 * bytes + kIpcGranule) {
+      void* p = free_[best].first;
+      *got = free_[best].second;
+      free_.erase(free_.begin() + best);
+      return p;
+    }
+    void* p = nullptr;
+    HIP_CHECK(hipMalloc(&p, bytes));
+    *got = bytes;
+    return p;
+  }
+  void give(void* p, size_t bytes) { free_.emplace_back(p, bytes); }
+};
+IpcPool& ipc_pool() {
+  static IpcPool* p = new IpcPool();  // never destroyed: buffers live until the process exits
+  return *p;
+}
+
+struct Signature {
+  uint64_t magic, rank, nonce, bytes;
+};
+constexpr uint64_t kSigMagic = 0x43'4D'45'58'47'4D'49'31ull;  // "CMEXGMI1"
+
 // Owns this rank's IPC buffers and the peers' mappings.
 class XgmiComm {
  public:
@@ -60,9 +96,12 @@ class XgmiComm {
     // sub-allocated pointers); plain device memory -- hipDeviceMallocUncached pages do not export
     // reliably -- with every flag access a system-scope atomic.
     flags_off_ = (2 * d_.npad * elt_bytes + 4095) / 4096 * 4096;
-    alloc_bytes_ = round_alloc(flags_off_ + flag_bytes());
-    HIP_CHECK(hipMalloc(&d_.mybuf, alloc_bytes_));
+    sig_off_ = flags_off_ + (flag_bytes() + 4095) / 4096 * 4096;
+    d_.mybuf = ipc_pool().take(round_alloc(sig_off_ + sizeof(Signature)), &alloc_bytes_);
     HIP_CHECK(hipMemset(d_.mybuf, 0, alloc_bytes_));
+    std::random_device rd;
+    sig_ = Signature{kSigMagic, (uint64_t)rank, ((uint64_t)rd() << 32) ^ rd(), alloc_bytes_};
+    HIP_CHECK(hipMemcpy(static_cast<char*>(d_.mybuf) + sig_off_, &sig_, sizeof(sig_), hipMemcpyHostToDevice));
     d_.myflags = reinterpret_cast<uint32_t*>(static_cast<char*>(d_.mybuf) + flags_off_);
     HIP_CHECK(hipMalloc(&d_.epochs, nblocks_ * sizeof(uint32_t)));
     HIP_CHECK(hipMemset(d_.epochs, 0, nblocks_ * sizeof(uint32_t)));
@@ -74,15 +113,30 @@ class XgmiComm {
   }
   ~XgmiComm() { close(); }
 
-  py::tuple handles() const { return py::make_tuple(handle_bytes(d_.mybuf, "buffer"), py::bytes("")); }
+  // (IPC handle, signature) -- the signature lets every peer verify what its mapping shows
+  py::tuple handles() const {
+    return py::make_tuple(handle_bytes(d_.mybuf, "buffer"),
+                          py::bytes(reinterpret_cast<const char*>(&sig_), sizeof(sig_)));
+  }
 
   void open(const std::vector<std::pair<std::string, std::string>>& all) {
     CME_REQUIRE((int)all.size() == d_.world, "XgmiComm.open: need one handle pair per rank");
     for (int r = 0; r < d_.world; ++r) {
       if (r == d_.rank) continue;
       d_.peers[r] = open_handle(all[r].first);
-      d_.peerflags[r] = reinterpret_cast<uint32_t*>(static_cast<char*>(d_.peers[r]) + flags_off_);
       opened_.push_back(d_.peers[r]);
+      d_.peerflags[r] = reinterpret_cast<uint32_t*>(static_cast<char*>(d_.peers[r]) + flags_off_);
+      // the mapping must show THAT rank's buffer (its signature, written at its construction)
+      CME_REQUIRE(all[r].second.size() == sizeof(Signature), "XgmiComm.open: bad signature size");
+      Signature want, seen;
+      std::memcpy(&want, all[r].second.data(), sizeof(want));
+      HIP_CHECK(hipMemcpy(&seen, static_cast<char*>(d_.peers[r]) + sig_off_, sizeof(seen), hipMemcpyDeviceToHost));
+      if (std::memcmp(&want, &seen, sizeof(want)) != 0) {
+        char buf[200];
+        std::snprintf(buf, sizeof(buf), "XgmiComm.open: the IPC mapping of rank %d shows another buffer "
+                      "(magic %llx rank %llu)", r, (unsigned long long)seen.magic, (unsigned long long)seen.rank);
+        throw std::runtime_error(buf);
+      }
     }
     ready_ = true;
   }
@@ -117,7 +171,11 @@ class XgmiComm {
 
   void close() {
     close_peers();
-    if (d_.mybuf) (void)hipFree(d_.mybuf);
+    if (d_.mybuf) {  // back to the pool (see IpcPool); its signature is cleared
+      (void)hipDeviceSynchronize();
+      (void)hipMemset(d_.mybuf, 0, alloc_bytes_);
+      ipc_pool().give(d_.mybuf, alloc_bytes_);
+    }
     if (d_.epochs) (void)hipFree(d_.epochs);
     if (d_.err) (void)hipFree(d_.err);
     d_ = XgmiDesc{};
@@ -134,7 +192,8 @@ class XgmiComm {
   size_t flag_bytes() const { return (size_t)nblocks_ * kMaxRanks * sizeof(uint32_t); }
   XgmiDesc d_;
   int64_t nblocks_ = 0;
-  size_t flags_off_ = 0, alloc_bytes_ = 0;
+  size_t flags_off_ = 0, sig_off_ = 0, alloc_bytes_ = 0;
+  Signature sig_{};
   bool ready_ = false;
   std::vector<void*> opened_;
 };
