@@ -171,6 +171,13 @@ class MlpEngine:
         if self.backend == "hip" and self.np and H <= 128 and os.environ.get("CME_HEAD_PARTIALS") == "1":
             self.gpart = torch.zeros(nblk * (C * H + H + C), dtype=torch.float32, device=dev)
         self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
+        # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one monotonic uint32
+        # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
+        # (CME_SEPARATE_HEAD=1: the two-launch form, for A/B measurements)
+        self.fh_counters = None
+        if (self.backend == "hip" and self.np and H <= 128 and C <= 16 and self.gpart is None
+                and os.environ.get("CME_SEPARATE_HEAD") != "1"):
+            self.fh_counters = torch.zeros((ld + 31) // 32, dtype=torch.int32, device=dev)
         self._step = None
 
     def load_dataset(self, x, labels, normalize: bool = False):
@@ -278,6 +285,9 @@ class MlpEngine:
                 s.z2p = self.z2buf.data_ptr()
             if self.gpart is not None:
                 s.gpart = self.gpart.data_ptr()
+            if self.fh_counters is not None:
+                s.fh_counters = self.fh_counters.data_ptr()
+                s.fh_tiles = int(self.fh_counters.numel())
             if self.np and self.XT is not None and self.XT.shape[0] == self.P + 1:
                 s.bias_col = 1
                 if self._a1bufs is not None:

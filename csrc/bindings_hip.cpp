@@ -46,12 +46,17 @@ struct MlpStep {
   // split-bf16 path (mlp_split.h): X/XT are bf16, W1p/dZ1p hold npw/npz bf16 planes
   int split = 0, npw = 3, npz = 3, fused_head = 0;
   uintptr_t stamps = 0;  // diagnostics only
+  uintptr_t hstamps = 0;  // diagnostics only: head-block stamps
   uintptr_t z2p = 0;     // wide-layer head scratch (head_big_scratch_floats), 0: column head
   uintptr_t gpart = 0;   // small-layer gradient partials (split path, H <= 128), 0: recompute in wgrad
   int bias_col = 0;      // XT has an all-ones feature row P: db1 comes out of the dW1 GEMM
   // second stream for the dW2/db2 role kernel (split path, bias_col): it runs concurrently with dW1
   // and the next step's forward GEMM; the next head (which reads W2) waits for it
   uintptr_t stream2 = 0;
+  // split path, H <= 128: uint32 tile counters (>= fh_tiles, zeroed) enable the single-launch forward +
+  // head (mlp_fwd1_head); 0: separate fwd1 + head kernels
+  uintptr_t fh_counters = 0;
+  int fh_tiles = 0;
   hipEvent_t ev_head = nullptr, ev_roles = nullptr;
   bool roles_pending = false;
 
@@ -146,7 +151,6 @@ struct MlpStep {
         if (fused_head) {
           cme::mlp_split_fwdhead(a, S(stream));
         } else {  // tiled forward + the per-column head kernel (fp32 head)
-          if (!(parts & 8)) cme::mlp_split_fwd1(a, S(stream));
           cme::HeadArgs h{};
           h.a1 = a.a1; h.lda = ld; h.W2 = a.W2; h.b2 = a.b2; h.labels = a.labels; h.H = H; h.C = C; h.n = n;
           h.scale = scale; h.D = a.D; h.ldd = ld; h.dZ1 = a.dZ1; h.ldz = ld; h.dZ1_bf16 = nullptr;
@@ -154,8 +158,14 @@ struct MlpStep {
           h.loss_partial = a.loss_partial; h.shift = shift; h.mode = cme::HEAD_TRAIN;
           h.z2part = P_<float>(z2p);
           h.gpart = const_cast<float*>(a.gpart);
+          h.stamps = hstamps ? reinterpret_cast<unsigned long long*>(hstamps) : nullptr;
           join(stream);  // the head reads W2 / b2, updated by the previous step's role kernel
-          if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
+          if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
+            cme::mlp_fwd1_head(a, h, P_<unsigned>(fh_counters), fh_tiles, S(stream));
+          } else {
+            if (!(parts & 8)) cme::mlp_split_fwd1(a, S(stream));
+            if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
+          }
         }
       }
       if (parts & 2) {
@@ -387,11 +397,14 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("dZ1", &MlpStep::dZ1)
       .def_readwrite("dZ1g", &MlpStep::dZ1g)
       .def_readwrite("loss", &MlpStep::loss)
+      .def_readwrite("fh_counters", &MlpStep::fh_counters)
+      .def_readwrite("fh_tiles", &MlpStep::fh_tiles)
       .def_readwrite("shift", &MlpStep::shift)
       .def_readwrite("act", &MlpStep::act)
       .def_readwrite("split", &MlpStep::split)
       .def_readwrite("fused_head", &MlpStep::fused_head)
       .def_readwrite("stamps", &MlpStep::stamps)
+      .def_readwrite("hstamps", &MlpStep::hstamps)
       .def_readwrite("xscale", &MlpStep::xscale)
       .def_readwrite("z2p", &MlpStep::z2p)
       .def_readwrite("gpart", &MlpStep::gpart)

@@ -54,6 +54,8 @@ struct HeadArgs {
   // lookahead step (fp32, H <= 128): a1 holds z1 - b1 (no activation); the head adds b1_pre and applies
   // the sigmoid, writing the activated a1 back
   const float* b1_pre = nullptr;
+  // diagnostics only: s_memrealtime stamps [block][8] (bench/stamps_fh.py)
+  unsigned long long* stamps = nullptr;
 };
 constexpr int kHeadPartialMaxH = 128;
 int64_t head_big_scratch_floats(int H, int n);
@@ -63,6 +65,11 @@ struct SplitStepArgs;
 // step's raw forward GEMM An = W1 . X_next (f: next step's args; with_next = false on the last step)
 void mlp_lookahead_l2(const SplitStepArgs& f, float* Aout, const HeadArgs& h, bool with_next, hipStream_t s);
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t stream);
+// split path, H <= 128: forward GEMM (a1 = sigmoid(W1 X + b1), f) and the train-mode head (h, same a1) in
+// ONE launch -- the last workgroup of every 32-column tile runs the head for it.  counters: >= max_tiles
+// zero-initialised uint32 (one per 32-column tile, monotonic across launches).
+bool mlp_fwd1_head_ok(const SplitStepArgs& f, const HeadArgs& h);
+void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters, int max_tiles, hipStream_t s);
 int mlp_head_num_blocks(int n);
 
 struct WgradArgs {

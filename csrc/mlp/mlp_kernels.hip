@@ -6,6 +6,7 @@
 #include "mma_tile.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace cme {
@@ -77,9 +78,33 @@ __global__ __launch_bounds__(kThreads) void fwd1_kernel(const T* __restrict__ W1
 // weight read in both passes is an LDS broadcast instead of a global load.
 constexpr int kHeadCols = 16;
 constexpr int kCMax = 16;
+constexpr int kSc1 = 16;  // buffer cache-policy bit sc1: write-through stores / L1-bypassing loads
 constexpr int kHeadLdsMax = 64 * 1024;
 
-template <typename P, int NC, bool LDSW, int HPT>
+// Stage W2^T ([h][NC], zero past C) and b2 (NC values, zero past C) into LDS: ws[H*NC] then b2s[NC]
+// (head_lds_elems).  Every load is a range-checked buffer load issued in one burst per thread
+// (a guarded `c < C ? W2[..] : 0` becomes a branch + vmcnt(0) wait per element).  nthr threads.
+__host__ __device__ inline int head_lds_elems(int H, int NC) { return H * NC + NC; }
+
+template <typename P, int NC>
+__device__ __forceinline__ void head_stage(const HeadArgs& a, int t, int nthr, P* ws) {
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.W2), rb = make_rsrc(a.b2);
+  const int H = a.H, C = a.C, tot = H * NC;
+  for (int i0 = t; i0 < tot; i0 += 4 * nthr) {
+    P v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * nthr, h = i / NC, c = i - h * NC;
+      v[u] = buf_load1<P>(rw, (i < tot && c < C) ? (c * H + h) * (int)sizeof(P) : kOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * nthr < tot) ws[i0 + u * nthr] = v[u];
+  }
+  if (t < NC) ws[tot + t] = buf_load1<P>(rb, t < C ? t * (int)sizeof(P) : kOOB);
+}
+
+template <typename P, int NC, bool LDSW, int HPT, bool SC1 = false, bool STAGED = false>
 __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, const int t, char* head_dyn,
                                            P (*zred)[NC][kHeadCols], float* lred,
                                            float (*gs_x)[kHeadCols + 1], float (*gs_d)[kHeadCols + 1]) {
@@ -89,6 +114,8 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
   // HPT > 0: every thread owns at most HPT hidden units (H <= HPT * NPART); their
   // a1 values are loaded ONCE (one burst, before the W2 staging barrier) and
   // reused by both passes.  HPT == 0: generic loop for large H.
+  // SC1: a1 was written earlier in the SAME launch by other workgroups with write-through (sc1)
+  // stores; it is read with sc1 loads (L1 bypass), the hand-off form of fwd1_head_kernel.
   constexpr int COLS = kHeadCols;
   constexpr int NPART = 256 / COLS;
   const P* __restrict__ a1 = static_cast<const P*>(a.a1);
@@ -109,7 +136,13 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
 #pragma unroll
     for (int u = 0; u < HPT; ++u) {
       const int h = part + u * NPART;
-      xa[u] = buf_load1<P>(rs, h < H ? (h * a.lda + b) * (int)sizeof(P) : kOOB);
+      const int off = h < H ? (h * a.lda + b) * (int)sizeof(P) : kOOB;
+      if constexpr (SC1) {
+        static_assert(std::is_same_v<P, float>, "sc1 hand-off: fp32 a1");
+        xa[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, kSc1));
+      } else {
+        xa[u] = buf_load1<P>(rs, off);
+      }
     }
     if (a.b1_pre) {  // lookahead step: a1 holds the pre-activation without bias; finish it here
       const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.b1_pre);
@@ -124,11 +157,19 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
       }
     }
   }
-  if constexpr (LDSW) {
-    for (int i = t; i < H * NC; i += 256) {
-      const int h = i / NC, c = i - h * NC;
-      ws[i] = c < C ? W2[c * H + h] : P(0);
+  // STAGED: the caller ran head_stage into head_dyn and a barrier already
+  static_assert(!STAGED || LDSW, "staged head needs the LDS copy of W2");
+  auto hstamp = [&](int i, bool drain) {  // diagnostics (HeadArgs::stamps): wave 0 lane 0 of the block
+    if (a.stamps) {
+      if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned long long tt = __builtin_amdgcn_s_memrealtime();
+      if (t == 0) a.stamps[(size_t)vb * 8 + i] = tt;
     }
+  };
+  hstamp(0, false);
+  hstamp(1, true);
+  if constexpr (LDSW && !STAGED) {
+    head_stage<P, NC>(a, t, 256, ws);
     __syncthreads();
   }
   auto w2 = [&](int c, int h) -> P {
@@ -176,7 +217,8 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < NC; ++c)
-    z[c] = zred[0][c][col] + zred[1][c][col] + zred[2][c][col] + zred[3][c][col] + (c < C ? b2[c < C ? c : 0] : P(0));
+    z[c] = zred[0][c][col] + zred[1][c][col] + zred[2][c][col] + zred[3][c][col] +
+           (LDSW ? ws[H * NC + c] : (c < C ? b2[c < C ? c : 0] : P(0)));
 
   if (a.mode == HEAD_PREDICT) {
     if (part == 0 && valid) {
@@ -190,6 +232,7 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
     return;
   }
 
+  hstamp(2, false);
   // ---- softmax over the C classes of this column (registers only)
   P m = P(0);
   if (a.shift) {
@@ -273,6 +316,7 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
     }
   }
   // ---- pass 2: dZ1 = (W2^T D) .* a1 .* (1 - a1)
+  hstamp(3, false);
   if (!valid && !gp) return;
   P* dZ1 = static_cast<P*>(a.dZ1);
   __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
@@ -337,6 +381,8 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
       const int h = part + u * NPART;
       if (h < H) emit(h, xa[u]);
     }
+    hstamp(4, false);
+    hstamp(5, true);
   } else {
     for (int h = part; h < H; h += NPART) emit(h, a1[(size_t)h * a.lda + bcol]);
   }
@@ -384,14 +430,268 @@ __global__ __launch_bounds__(512) void lookahead_l2_kernel(SplitStepArgs f, floa
   }
   const int half = threadIdx.x >> 8;
   const int vb = 2 * ((int)blockIdx.x - ntiles) + half;
-  head_block<float, NC, true, 8>(h, vb, threadIdx.x & 255, l2_dyn + half * h.H * NC * (int)sizeof(float),
+  head_block<float, NC, true, 8>(h, vb, threadIdx.x & 255, l2_dyn + half * head_lds_elems(h.H, NC) * (int)sizeof(float),
                                  zred[half], lred[half], gs_x[half], gs_d[half]);
+}
+
+
+// ------------------------------------------------ K2 on MFMA: 32 columns per 512-thread workgroup
+// (fp32 params, train mode, H <= 128, C <= 16).  The VALU head above is latency-bound at these sizes
+// (per thread 80 dependent LDS reads + FMAs per pass: 1.4 us per pass measured with s_memrealtime
+// stamps), so both of its contractions run as v_mfma_f32_16x16x4_f32 tiles instead:
+//   pass 1  z2 (16 x 32) = W2 (16 x H) . a1 (H x 32): wave w -> column half nt = w & 1, hidden quarter
+//           kq = w >> 1 (32 rows, 8 MFMAs); partial tiles summed through LDS by waves 0/1, which then do
+//           softmax / loss / D across the 4 lane groups (classes 4g+i live in lane group g).
+//   pass 2  dA1 (H x 32) = W2^T . D: the K index of step i in lane group g is class 4g+i, which is
+//           EXACTLY where pass 1 left D in the accumulator -> D goes to the other waves as one float4
+//           per lane; each wave then owns (up to) two 16x16 tiles and applies a1 (1 - a1) in place.
+// Lane map of v_mfma_f32_16x16x4f32 (mma_tile.h): lane l gives A[l&15][l>>4], B[l>>4][l&15] and
+// receives C[4(l>>4) + i][l&15].  W2 is staged as [16][kW2S] in LDS (zero past C and past H).
+// SC1: a1 was stored earlier in the same launch with write-through stores (fwd1_head_kernel).
+constexpr int kW2S = 132;      // LDS row stride of the staged W2 (bank spread)
+constexpr int kH32MaxH = 128;  // 8 row tiles = 2 per wave
+constexpr int kH32Cols = 32;
+
+struct Head32Lds {
+  float w2[16 * kW2S];    // W2 [class][hidden], zero past C and past H
+  float b2[16];
+  float zp[3][2][64][4];  // pass-1 partial tiles of hidden quarters 1..3
+  float ds[2][64][4];     // D in accumulator layout, per column half
+};
+
+// Stage W2 / b2 into LDS (512 threads, one burst of range-checked buffer loads).  Measured faster than
+// loading the pass operands straight into registers, in the head kernel and before the fused GEMM.
+__device__ __forceinline__ void head32_stage(const HeadArgs& a, int t, Head32Lds& L) {
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.W2), rb = make_rsrc(a.b2);
+  float v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = t + u * 512, c = i >> 7, h = i & 127;
+    v[u] = buf_load1<float>(rw, (c < a.C && h < a.H) ? (c * a.H + h) * 4 : kOOB);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = t + u * 512;
+    L.w2[(i >> 7) * kW2S + (i & 127)] = v[u];
+  }
+  if (t < 16) L.b2[t] = buf_load1<float>(rb, t < a.C ? t * 4 : kOOB);
+}
+
+// ct: 32-column tile index; 512 threads; W2 / b2 staged in L (head32_stage) and a barrier since
+template <bool SC1>
+__device__ __forceinline__ void head32(const HeadArgs& a, int ct, int t, Head32Lds& L) {
+  const int lane = t & 63, w = t >> 6, c16 = lane & 15, g = lane >> 4;
+  const int nt = w & 1, kq = w >> 1;
+  const int col = ct * kH32Cols + nt * 16 + c16;
+  const bool cval = col < a.n;
+  const int H = a.H, C = a.C, ld = a.lda;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.a1);
+  auto ld_a1 = [&](int h) -> float {
+    const int off = (h < H && cval) ? (h * ld + col) * 4 : kOOB;
+    if constexpr (SC1) return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, off, 0, kSc1));
+    else return buf_load1<float>(ra, off);
+  };
+  // one burst: pass-1 B operands and the pass-2 epilogue activations
+  float bop[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) bop[s] = ld_a1(kq * 32 + 4 * s + g);
+  float xe[2][4];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xe[tt][j] = ld_a1((kq + 4 * tt) * 16 + 4 * g + j);
+  const int lab = (int)__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(a.labels), cval ? col * 4 : kOOB, 0, 0);
+  auto hstamp = [&](int i) {  // diagnostics (HeadArgs::stamps): drained, wave 0 lane 0
+    if (a.stamps) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const unsigned long long tt = __builtin_amdgcn_s_memrealtime();
+      if (t == 0) a.stamps[(size_t)ct * 8 + i] = tt;
+    }
+  };
+  hstamp(0);
+
+  // ---- pass 1: this wave's hidden quarter of z2
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(L.w2[c16 * kW2S + kq * 32 + 4 * s + g], bop[s], acc, 0, 0, 0);
+  if (kq > 0) *reinterpret_cast<f32x4*>(L.zp[kq - 1][nt][lane]) = acc;
+  __syncthreads();
+  if (w < 2) {  // ---- softmax + cross-entropy gradient for the 16 columns of half nt
+#pragma unroll
+    for (int q = 0; q < 3; ++q) acc += *reinterpret_cast<const f32x4*>(L.zp[q][nt][lane]);
+    float z[4];
+    float m = 0.f;
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cls = 4 * g + i;
+      z[i] = acc[i] + L.b2[cls];
+      if (a.shift && cls < C) {
+        m = any ? fmaxf(m, z[i]) : z[i];
+        any = true;
+      }
+    }
+    if (a.shift) {  // class 0 is in lane group 0: every column has a valid entry there
+      float mo = any ? m : -3.402823466e38f;
+      mo = fmaxf(mo, __shfl_xor(mo, 16, 64));
+      mo = fmaxf(mo, __shfl_xor(mo, 32, 64));
+      m = mo;
+    }
+    float e[4], ssum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      e[i] = (4 * g + i) < C ? __expf(z[i] - m) : 0.f;
+      ssum += e[i];
+    }
+    ssum += __shfl_xor(ssum, 16, 64);
+    ssum += __shfl_xor(ssum, 32, 64);
+    const float inv = 1.f / ssum;
+    const float sc = (float)a.scale;
+    float lp = 0.f;
+    f32x4 dv;
+    float* Dg = static_cast<float*>(a.D);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cls = 4 * g + i;
+      const float yh = e[i] * inv;
+      const bool hit = cval && cls == lab;
+      if (hit) lp = -__logf(yh);
+      const float d = (cval && cls < C) ? (yh - (hit ? 1.f : 0.f)) * sc : 0.f;
+      dv[i] = d;
+      if (cval && cls < C) Dg[(size_t)cls * a.ldd + col] = d;
+    }
+    *reinterpret_cast<f32x4*>(L.ds[nt][lane]) = dv;
+    if (a.loss_partial) {
+      const float v = wave_sum(lp);
+      const int vb = 2 * ct + nt;
+      if (lane == 0 && vb * 16 < a.n) a.loss_partial[vb] = v;
+    }
+  }
+  hstamp(1);
+  __syncthreads();
+  hstamp(2);
+  // ---- pass 2: dZ1 = (W2^T D) .* a1 .* (1 - a1) on row tiles kq and kq + 4 of half nt
+  const f32x4 dv = *reinterpret_cast<const f32x4*>(L.ds[nt][lane]);
+  float* dZ1 = static_cast<float*>(a.dZ1);
+  __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
+  __hip_bfloat16* dZp = static_cast<__hip_bfloat16*>(a.dZ1_planes);
+  const size_t pstride = (size_t)H * a.ldz;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt) {
+    const int mt = kq + 4 * tt;
+    if (mt * 16 >= H) break;  // wave-uniform
+    f32x4 r = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      r = __builtin_amdgcn_mfma_f32_16x16x4f32(L.w2[(4 * g + i) * kW2S + mt * 16 + c16], dv[i], r, 0, 0, 0);
+    if (!cval) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int h = mt * 16 + 4 * g + j;
+      if (h >= H) continue;
+      const float x = xe[tt][j];
+      const float dz = r[j] * x * (1.f - x);
+      const size_t zi = (size_t)h * a.ldz + col;
+      dZ1[zi] = dz;
+      if (dZlo) dZlo[zi] = __float2bfloat16(dz);
+      if (dZp) {
+        float rr = dz;
+        for (int p = 0; p < a.npz; ++p) {
+          const __hip_bfloat16 q = __float2bfloat16(rr);
+          dZp[p * pstride + zi] = q;
+          rr -= __bfloat162float(q);
+        }
+      }
+    }
+  }
+  hstamp(3);
+}
+
+__global__ __launch_bounds__(512) void head32_kernel(HeadArgs a) {
+  __shared__ __attribute__((aligned(16))) Head32Lds L;
+  head32_stage(a, threadIdx.x, L);
+  __syncthreads();
+  head32<false>(a, blockIdx.x, threadIdx.x, L);
+}
+
+bool head32_ok(const HeadArgs& a) {
+  return a.mode == HEAD_TRAIN && a.H <= kH32MaxH && a.C <= 16 && !a.gpart && !a.b1_pre;
+}
+
+// ------------------------------------- forward GEMM + head in ONE launch (split path, H <= 128)
+// Workgroups compute 16x32 tiles of a1 = sigmoid(W1 X + b1) exactly as fwd1_split_kernel does, but
+// store them write-through (sc1).  Per 32-column tile, the tm row-tile workgroups each add 1 to a
+// monotonic counter after all their stores drained; the workgroup whose add completes the tile
+// (old + 1 == 0 mod tm) runs the head for those 32 columns (two 256-thread head blocks) with sc1
+// loads of a1.  This is the "last arriver" hand-off of MI355X_MICROARCH.md (sc1 stores, vmcnt(0) in
+// every storing wave, barrier, one agent-scope add per workgroup, sc1 loads; no fences), and it
+// removes the head launch and its kernel boundary from the step (reference: gpuFeedforward +
+// gpuBackprop's first half, fpcode/neural_network.cpp:281-378, were 8 launches with syncs).
+// Placement for speed only: the tm workgroups of a column tile share blockIdx % 8 (one XCD under
+// round-robin dispatch), so the hand-off normally stays inside one L2; correctness does not depend
+// on it.
+struct EpiSigWT {
+  const float* b1;
+  float* a1;
+  int ld;
+  float xscale;
+  float pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int, bool ok) {
+    pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
+  }
+  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
+    const float s = sigmoid_<float>(v * xscale + pre[q]);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), make_rsrc(a1), (row * ld + col) * 4, 0,
+                                          kSc1);
+  }
+};
+
+constexpr int kFHTileCols = 32;  // columns per a1 tile = two head blocks
+
+template <int NPW, int VEC>
+__global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArgs h, unsigned* __restrict__ counters,
+                                                        int tm, int tn) {
+  __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];
+  __shared__ __attribute__((aligned(16))) Head32Lds L;
+  __shared__ int s_last;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int ct = xcd + 8 * (slot / tm), rt = slot % tm;
+  if (ct >= tn) return;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
+  unsigned long long* st = f.stamps ? f.stamps + (size_t)blockIdx.x * 4 : nullptr;  // diagnostics only
+  auto stamp = [&](int i) {
+    if (st && threadIdx.x == 0) st[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  // W2 / b2 for the head, staged by every workgroup before its GEMM (independent of a1; wsk_tile's
+  // internal barrier orders these LDS writes before any head read)
+  head32_stage(h, threadIdx.x, L);
+  TileGeom g{f.H, f.n, f.P, rt * 16, ct * kFHTileCols};
+  EpiSigWT epi{f.b1, f.a1, f.ld, f.xscale, {}};
+  wsk_tile<__hip_bfloat16, 1, 2, 8, true, true, VEC, 4, NPW, uint8_t>(
+      static_cast<const __hip_bfloat16*>(f.W1p), f.P, static_cast<const uint8_t*>(f.X), f.P, g, epi, red,
+      f.H * f.P * (int)sizeof(__hip_bfloat16));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
+  __syncthreads();
+  stamp(1);
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(counters + ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old + 1u) % (unsigned)tm == 0u;
+  }
+  __syncthreads();
+  stamp(2);
+  if (!s_last) return;
+  head32<true>(h, ct, threadIdx.x, L);
+  if (st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(3);
+  }
 }
 
 template <typename P, int NC>
 void launch_head(const HeadArgs& a, hipStream_t s) {
   const dim3 grid((a.n + kHeadCols - 1) / kHeadCols);
-  const size_t lds = (size_t)a.H * NC * sizeof(P);
+  const size_t lds = (size_t)head_lds_elems(a.H, NC) * sizeof(P);
   constexpr int NPART = 256 / kHeadCols;
   if (lds <= (size_t)kHeadLdsMax) {
     if (a.H <= 8 * NPART) head_kernel<P, NC, true, 8><<<grid, 256, lds, s>>>(a);
@@ -850,7 +1150,7 @@ void mlp_lookahead_l2(const SplitStepArgs& f, float* Aout, const HeadArgs& h, bo
   const int tiles_n = cdiv(f.n, 32), ntiles = with_next ? cdiv(f.H, 16) * tiles_n : 0;
   const int nwg = ntiles + cdiv(cdiv(h.n, kHeadCols), 2);
   const int NC = h.C <= 10 ? 10 : 16;
-  const size_t dyn = 2 * (size_t)h.H * NC * sizeof(float);
+  const size_t dyn = 2 * (size_t)head_lds_elems(h.H, NC) * sizeof(float);
 #define CME_L2(nc, np) lookahead_l2_kernel<nc, np><<<nwg, 512, dyn, s>>>(f, Aout, h, ntiles, tiles_n)
   if (NC == 10) {
     if (f.npw == 3) CME_L2(10, 3);
@@ -863,6 +1163,29 @@ void mlp_lookahead_l2(const SplitStepArgs& f, float* Aout, const HeadArgs& h, bo
   CME_LAUNCH_CHECK(s);
 }
 
+bool mlp_fwd1_head_ok(const SplitStepArgs& f, const HeadArgs& h) {
+  return head32_ok(h) && f.H == h.H && f.n == h.n && f.ld % 4 == 0 && h.lda == f.ld &&
+         (int64_t)f.H * f.ld * 4 < (int64_t)kOOB && f.a1 == h.a1;
+}
+
+void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters, int max_tiles, hipStream_t s) {
+  if (f.n <= 0) return;
+  CME_REQUIRE(mlp_fwd1_head_ok(f, h), "fwd1_head: H <= 128, C <= 16, train-mode head over the same a1");
+  CME_REQUIRE((int64_t)f.H * f.P * 2 * f.npw < (int64_t)kOOB && (int64_t)f.n * f.P < (int64_t)kOOB,
+              "fwd1_head: operand too large for 32-bit buffer offsets");
+  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, kFHTileCols);
+  CME_REQUIRE(counters != nullptr && tn <= max_tiles, "fwd1_head: counter array too small");
+  const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 && reinterpret_cast<uintptr_t>(f.W1p) % 16 == 0 &&
+                   f.P % 8 == 0;
+  const int nwg = 8 * tm * cdiv(tn, 8);
+#define CME_FH(np)                                                                    \
+  if (vec) fwd1_head_kernel<np, 1><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);       \
+  else fwd1_head_kernel<np, 0><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);
+  if (f.npw == 3) { CME_FH(3) } else { CME_FH(1) }
+#undef CME_FH
+  CME_LAUNCH_CHECK(s);
+}
+
 int64_t head_big_scratch_floats(int H, int n) { return (int64_t)cdiv(H, kHBRows) * kCMax * hb_cols_pad(n); }
 
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
@@ -872,6 +1195,12 @@ void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
     CME_REQUIRE((int64_t)a.H * a.lda < (int64_t)kOOB / 4, "mlp_head: a1 too large for 32-bit buffer offsets");
     if (a.C == 10) launch_head_big<10>(a, s);
     else launch_head_big<16>(a, s);
+    CME_LAUNCH_CHECK(s);
+    return;
+  }
+  if (dt != DType::F64 && head32_ok(a) && (int64_t)a.H * a.lda < (int64_t)kOOB / 4 &&
+      std::getenv("CME_VALU_HEAD") == nullptr) {  // MFMA head (CME_VALU_HEAD=1: the VALU form, A/B tests)
+    head32_kernel<<<cdiv(a.n, kH32Cols), 512, 0, s>>>(a);
     CME_LAUNCH_CHECK(s);
     return;
   }

@@ -287,3 +287,35 @@ def test_lookahead_graph_equals_eager():
         t.train(2, 0.01, 1e-4)
     for i in range(2):
         np.testing.assert_array_equal(a.nn.W[i], b.nn.W[i])
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("H,n", [(100, 800), (100, 100), (128, 513), (37, 45), (16, 32)])
+def test_fwd1_head_single_launch_matches_two_launches(dtype, H, n):
+    """mlp_fwd1_head (forward GEMM + head in one launch, last-arriver hand-off per 32-column tile)
+    against the separate fwd1 + head kernels: a1, D, dZ1, its bf16 planes, loss partials and the
+    updated params must be BITWISE equal over several SGD steps (same math, same order)."""
+    x, y = synthetic_mnist(2 * n + 7, seed=H)
+    rng = np.random.default_rng(H + n)
+    W1 = rng.standard_normal((H, 784)) * 0.01
+    W2 = rng.standard_normal((10, H)) * 0.01
+    b1 = rng.standard_normal(H) * 0.1
+    b2 = rng.standard_normal(10) * 0.1
+    outs = []
+    for single in (True, False):
+        e = MlpEngine((784, H, 10), dtype, max_cols=n, device="cuda")
+        if not single:
+            e.fh_counters = None
+            e._step = None
+        else:
+            assert e.fh_counters is not None
+        e.load_dataset(x, y, normalize=True)
+        e.set_params(W1, b1, W2, b2)
+        for step, off in enumerate((0, n, 7, 0)):
+            e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True, with_loss=step == 3)
+        torch.cuda.synchronize()
+        outs.append([t.clone().cpu() for t in (e.a1, e.D, e.dZ1, e.dZ1p, e.params)] + [e.loss_sum()])
+    a, b = outs
+    for ta, tb in zip(a[:-1], b[:-1]):
+        assert torch.equal(ta, tb)
+    assert a[-1] == b[-1]
