@@ -57,6 +57,7 @@ struct MlpStep {
   // head (mlp_fwd1_head); 0: separate fwd1 + head kernels
   uintptr_t fh_counters = 0;
   int fh_tiles = 0;
+  int no_gemm_z2 = 0;  // 1: wide-layer head computes z2 itself (A/B tests)
   hipEvent_t ev_head = nullptr, ev_roles = nullptr;
   bool roles_pending = false;
 
@@ -163,7 +164,14 @@ struct MlpStep {
           if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
             cme::mlp_fwd1_head(a, h, P_<unsigned>(fh_counters), fh_tiles, S(stream));
           } else {
-            if (!(parts & 8)) cme::mlp_split_fwd1(a, S(stream));
+            // wide layers: the forward GEMM also leaves the head's z2 partials (unless only the head runs)
+            cme::SplitStepArgs f = a;
+            f.z2part = (z2p && !(parts & 8) && !no_gemm_z2) ? P_<float>(z2p) : nullptr;
+            if (!(parts & 8)) cme::mlp_split_fwd1(f, S(stream));
+            h.z2_chunks = f.z2part ? cme::mlp_split_fwd1_z2_chunks(f) : 0;
+            // with the all-ones XT feature nothing reads dZ1 in fp32 on the wide path (db1 comes out of
+            // the dW1 GEMM over the planes): skip those 4 B/element of HBM writes
+            if (h.z2_chunks > 0 && bias_col && !a.gpart) h.dZ1 = nullptr;
             if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
           }
         }
@@ -399,6 +407,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("loss", &MlpStep::loss)
       .def_readwrite("fh_counters", &MlpStep::fh_counters)
       .def_readwrite("fh_tiles", &MlpStep::fh_tiles)
+      .def_readwrite("no_gemm_z2", &MlpStep::no_gemm_z2)
       .def_readwrite("shift", &MlpStep::shift)
       .def_readwrite("act", &MlpStep::act)
       .def_readwrite("split", &MlpStep::split)

@@ -8,7 +8,7 @@
 //   * C[m][n] = sum_k A[m][k] B[n][k], both operands K-contiguous ("NT");
 //     A = NPA exact bf16 planes (split-fp32, see mlp_split.h), B = uint8 pixels
 //     (exact in bf16, converted at fragment read) or bf16.
-//   * BM x BN workgroup tile, 4 waves as 2x2, each wave (BM/2)x(BN/2) built from
+//   * BM x BN workgroup tile, 4 waves as 2x2 (or 8 as 4x2), each wave's share built from
 //     16x16 blocks of v_mfma_f32_16x16x32_bf16; BK = 64 per stage.
 //   * global -> VGPR -> LDS staging with 16-byte buffer loads (out-of-range
 //     rows / k return zero: no edge branches), two LDS buffers and two register
@@ -20,6 +20,8 @@
 #pragma once
 
 #include "mma_tile.h"
+
+#include <type_traits>
 
 namespace cme {
 
@@ -59,23 +61,35 @@ __device__ __forceinline__ bf16x8_t u8x8_to_bf16(uint2 w) {
   return r;
 }
 
+// Epi::kTileHook present -> lds_gemm_tile calls epi.tile<MB, NB, WRN>(acc, wr, wc, fr, fg, row0, col0, lds)
+// once per workgroup after the element epilogue (row0/col0: this wave's first row / column)
+template <class E, class = void>
+struct HasTileHook : std::false_type {};
+template <class E>
+struct HasTileHook<E, std::void_t<decltype(E::kTileHook)>> : std::true_type {};
+
 }  // namespace lg
 
 // One BM x BN output tile at (m0, n0).  `lds` must hold lg::lds_bytes<...>()
 // bytes (16-byte aligned).  Requirements (checked by the launcher): K % 16 == 0,
 // lda % 8 == 0 (bf16) and ldb % 16 == 0 bytes, 16-byte aligned operand bases.
 // epi(row, col, v) is called for every in-range element of the tile.
-template <int BM, int BN, int NPA, typename TB, class Epi>
+template <int BM, int BN, int NPA, typename TB, class Epi, int NT = lg::kThreads>
 __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__ A, int lda, int plane_bytes,
                                               const TB* __restrict__ B, int ldb, int M, int N, int K, int m0, int n0,
                                               Epi& epi, char* __restrict__ lds) {
   using namespace lg;
-  constexpr int WM = BM / 2, WN = BN / 2, MB = WM / 16, NB = WN / 16;
+  // NT = 256: 4 waves as 2x2; NT = 512: 8 waves as 4x2 (two waves per SIMD hide more of the L2
+  // latency at one workgroup per CU)
+  constexpr int WRN = NT / 64 / 2, WM = BM / WRN, WN = BN / 2, MB = WM / 16, NB = WN / 16;
+  static_assert(MB >= 1 && NB >= 1, "tile too small for the wave layout");
   constexpr int BROW = BTraits<TB>::kRow, BCPR = BTraits<TB>::kChunksPerRow;
   constexpr int A_CHUNKS = BM * (kBK * 2 / 16);  // 16-byte chunks per plane per stage
   constexpr int B_CHUNKS = BN * BCPR;
-  constexpr int AJ = (A_CHUNKS + kThreads - 1) / kThreads, BJ = (B_CHUNKS + kThreads - 1) / kThreads;
-  static_assert(A_CHUNKS % kThreads == 0 && B_CHUNKS % kThreads == 0, "tile/thread mismatch");
+  constexpr int AJ = (A_CHUNKS + NT - 1) / NT, BJ = (B_CHUNKS + NT - 1) / NT;
+  static_assert(A_CHUNKS % NT == 0 && (B_CHUNKS % NT == 0 || B_CHUNKS < NT), "tile/thread mismatch");
+  // B_CHUNKS < NT (narrow uint8 B tiles at 8 waves): only the first B_CHUNKS threads stage B
+  auto b_mine = [&](int j) { return B_CHUNKS % NT == 0 || (int)threadIdx.x + j * NT < B_CHUNKS; };
   constexpr int A_BUF = NPA * BM * kARow, B_BUF = BN * BROW;
 
   const int t = threadIdx.x, lane = t & 63;
@@ -92,14 +106,14 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
   bool a_ok[AJ], b_ok[BJ];
 #pragma unroll
   for (int j = 0; j < AJ; ++j) {
-    const int c = t + j * kThreads, r = c >> 3, kc = c & 7;  // 8 chunks of 8 bf16 per row
+    const int c = t + j * NT, r = c >> 3, kc = c & 7;  // 8 chunks of 8 bf16 per row
     a_ok[j] = m0 + r < M;
     a_off[j] = ((m0 + r) * lda + kc * 8) * 2;
     a_lds[j] = r * kARow + kc * 16;
   }
 #pragma unroll
   for (int j = 0; j < BJ; ++j) {
-    const int c = t + j * kThreads, r = c / BCPR, kc = c % BCPR;
+    const int c = t + j * NT, r = c / BCPR, kc = c % BCPR;
     b_ok[j] = n0 + r < N;
     b_off[j] = (n0 + r) * ldb * (int)sizeof(TB) + kc * 16;
     b_lds[j] = r * BROW + kc * 16;
@@ -112,7 +126,7 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
     const int kb = k0 * 2;  // byte offset of k0 in an A row
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
-      const int kc = (t + j * kThreads) & 7;
+      const int kc = (t + j * NT) & 7;
       const bool ok = a_ok[j] && k0 + kc * 8 < K;
 #pragma unroll
       for (int p = 0; p < NPA; ++p) {
@@ -122,9 +136,10 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
     }
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
-      const int kc = (t + j * kThreads) % BCPR;
+      const int kc = (t + j * NT) % BCPR;
       constexpr int EPC = 16 / (int)sizeof(TB);  // elements per chunk
       const bool ok = b_ok[j] && k0 + kc * EPC < K;
+      if (!b_mine(j)) continue;
       const auto w = __builtin_amdgcn_raw_buffer_load_b128(rb, ok ? b_off[j] + k0 * (int)sizeof(TB) : kOOB, 0, 0);
       __builtin_memcpy(&rB[j], &w, 16);
     }
@@ -136,7 +151,8 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
       for (int j = 0; j < AJ; ++j)
         *reinterpret_cast<uint4*>(ldsA + buf * A_BUF + p * BM * kARow + a_lds[j]) = rA[p][j];
 #pragma unroll
-    for (int j = 0; j < BJ; ++j) *reinterpret_cast<uint4*>(ldsB + buf * B_BUF + b_lds[j]) = rB[j];
+    for (int j = 0; j < BJ; ++j)
+      if (b_mine(j)) *reinterpret_cast<uint4*>(ldsB + buf * B_BUF + b_lds[j]) = rB[j];
   };
 
   f32x4 acc[MB][NB];
@@ -216,6 +232,10 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
         const int col = n0 + wc * WN + nb * 16 + fr;
         if (row < M && col < N) epi(row, col, acc[mb][nb][i]);
       }
+  // optional whole-tile hook on the raw accumulators (e.g. a second tiny MFMA contraction of the tile);
+  // every LDS read of the main loop has passed the last lds_barrier, so `lds` is free for it
+  if constexpr (lg::HasTileHook<Epi>::value)
+    epi.template tile<MB, NB, WRN>(acc, wr, wc, fr, fg, m0 + wr * WM, n0 + wc * WN, lds);
 }
 
 }  // namespace cme

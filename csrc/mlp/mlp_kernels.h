@@ -54,6 +54,9 @@ struct HeadArgs {
   // lookahead step (fp32, H <= 128): a1 holds z1 - b1 (no activation); the head adds b1_pre and applies
   // the sigmoid, writing the activated a1 back
   const float* b1_pre = nullptr;
+  // > 0: z2part already holds z2_chunks row-tile partials [chunk][16][lda] left by the forward GEMM
+  // (SplitStepArgs::z2part); the head then only reduces them and never re-reads a1 for z2
+  int z2_chunks = 0;
   // diagnostics only: s_memrealtime stamps [block][8] (bench/stamps_fh.py)
   unsigned long long* stamps = nullptr;
 };

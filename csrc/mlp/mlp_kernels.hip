@@ -852,6 +852,133 @@ __global__ __launch_bounds__(256) void head_big_dz_kernel(HeadArgs a, int ncb, i
   }
 }
 
+// ----------------------------------- K2 for wide layers when the forward GEMM left z2 partials
+// (HeadArgs::z2_chunks > 0, see EpiSigBig::tile in mlp_split.hip).  One 512-thread workgroup per
+// (128 RT hidden rows x 32 columns): it reduces the partials of its 32 columns (every row block
+// recomputes the same softmax, a 16 x 32 x chunks sum), then each wave forms dZ1 for 16 RT rows x 32
+// columns as 2 RT tiles of v_mfma_f32_16x16x4_f32 (dA1 = W2^T D, K = the 16 classes, class 4g+i in lane
+// group g at step i) and applies a1 (1 - a1).  a1 is read once (the old two-kernel head read it twice).
+constexpr int kHWCols = 32;
+
+// RT row tiles of 16 per wave: 8 * 16 * RT hidden rows per workgroup (launcher picks RT for >= 256 workgroups)
+template <int RT>
+__global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
+  __shared__ float zs[16][kHWCols + 1];
+  __shared__ float Ds[16][kHWCols + 1];
+  __shared__ float ls[kHWCols];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, c16 = lane & 15, g = lane >> 4;
+  const int rb = blockIdx.x % nrb, ct = blockIdx.x / nrb;
+  const int H = a.H, C = a.C, ld = a.lda;
+  const int row0 = (rb * 8 + w) * 16 * RT;
+  // ---- one burst: the z2 partial sums of (class t>>5, column t&31), W2^T operands, a1 of the tiles
+  const int zc = t >> 5, zcol = ct * kHWCols + (t & 31);
+  const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
+  float zsum = 0.f;
+  {
+    int k = 0;
+    for (; k + 8 <= a.z2_chunks; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = buf_load1<float>(rz, zcol < a.n ? (((k + u) * 16 + zc) * ld + zcol) * 4 : kOOB);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) zsum += v[u];
+    }
+    for (; k < a.z2_chunks; ++k) zsum += buf_load1<float>(rz, zcol < a.n ? ((k * 16 + zc) * ld + zcol) * 4 : kOOB);
+  }
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.W2), ra = make_rsrc(a.a1);
+  float wv[RT][4], xv[RT][2][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int hA = row0 + rt * 16 + c16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wv[rt][i] = buf_load1<float>(rw, (4 * g + i < C && hA < H) ? ((4 * g + i) * H + hA) * 4 : kOOB);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int col = ct * kHWCols + cb * 16 + c16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = row0 + rt * 16 + 4 * g + j;
+        xv[rt][cb][j] = buf_load1<float>(ra, (h < H && col < a.n) ? (h * ld + col) * 4 : kOOB);
+      }
+    }
+  }
+  zs[zc][t & 31] = zsum + (zc < C ? static_cast<const float*>(a.b2)[zc < C ? zc : 0] : 0.f);
+  __syncthreads();
+  if (t < kHWCols) {  // ---- softmax / loss / D for column t
+    const int col = ct * kHWCols + t;
+    const bool ok = col < a.n;
+    const int lab = ok ? a.labels[col] : -1;
+    float m = 0.f;
+    if (a.shift) {
+      m = zs[0][t];
+      for (int c = 1; c < C; ++c) m = fmaxf(m, zs[c][t]);
+    }
+    float e[16], sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      e[c] = c < C ? __expf(zs[c][t] - m) : 0.f;
+      sum += e[c];
+    }
+    const float inv = 1.f / sum, sc = (float)a.scale;
+    float lp = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const float y = e[c] * inv;
+      if (c == lab) lp = -__logf(y);
+      const float d = (ok && c < C) ? (y - (c == lab ? 1.f : 0.f)) * sc : 0.f;
+      Ds[c][t] = d;
+      if (rb == 0 && ok && c < C) static_cast<float*>(a.D)[(size_t)c * a.ldd + col] = d;
+    }
+    ls[t] = lp;
+  }
+  __syncthreads();
+  if (rb == 0 && a.loss_partial && t < 2) {  // the column head's layout: one partial per 16 columns
+    const int vb = ct * 2 + t;
+    if (vb * 16 < a.n) {
+      float s = 0.f;
+      for (int k = 0; k < 16; ++k) s += ls[t * 16 + k];
+      a.loss_partial[vb] = s;
+    }
+  }
+  if (row0 >= H) return;  // wave-uniform; no barrier follows
+  float* dZ1 = static_cast<float*>(a.dZ1);
+  __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
+  __hip_bfloat16* dZp = static_cast<__hip_bfloat16*>(a.dZ1_planes);
+  const size_t pstride = (size_t)H * a.ldz;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int col = ct * kHWCols + cb * 16 + c16;
+    float dv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dv[i] = Ds[4 * g + i][cb * 16 + c16];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      f32x4 r = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[rt][i], dv[i], r, 0, 0, 0);
+      if (col >= a.n) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = row0 + rt * 16 + 4 * g + j;
+        if (h >= H) continue;
+        const float x = xv[rt][cb][j];
+        const float dz = r[j] * x * (1.f - x);
+        const size_t zi = (size_t)h * a.ldz + col;
+        if (dZ1) dZ1[zi] = dz;  // nullptr: fp32 dZ1 not needed (planes only)
+        if (dZlo) dZlo[zi] = __float2bfloat16(dz);
+        if (dZp) {
+          float rr = dz;
+          for (int p = 0; p < a.npz; ++p) {
+            const __hip_bfloat16 q = __float2bfloat16(rr);
+            dZp[p * pstride + zi] = q;
+            rr -= __bfloat162float(q);
+          }
+        }
+      }
+    }
+  }
+}
+
 template <int NC>
 void launch_head_big(const HeadArgs& a, hipStream_t s) {
   const int ncb = hb_cdiv(a.n, kHBCols), nch = hb_cdiv(a.H, kHBRows);
@@ -1186,11 +1313,24 @@ void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters
   CME_LAUNCH_CHECK(s);
 }
 
-int64_t head_big_scratch_floats(int H, int n) { return (int64_t)cdiv(H, kHBRows) * kCMax * hb_cols_pad(n); }
+// covers both the two-kernel head's split-H partials and the forward GEMM's row-tile partials
+// (64-row tiles at most, pitch = the activation ld <= hb_cols_pad(n) for ld = n rounded to 16)
+int64_t head_big_scratch_floats(int H, int n) { return (int64_t)cdiv(H, 64) * kCMax * hb_cols_pad(n); }
 
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
   CME_REQUIRE(a.C >= 1 && a.C <= kCMax, "mlp_head: 1 <= C <= 16 required");
+  if (a.z2part && a.z2_chunks > 0 && dt != DType::F64 && a.mode == HEAD_TRAIN && a.C <= 16 && !a.b1_pre &&
+      !a.gpart) {  // partials left by the forward GEMM
+    CME_REQUIRE((int64_t)a.z2_chunks * 16 * a.lda < (int64_t)kOOB / 4 && (int64_t)a.H * a.lda < (int64_t)kOOB / 4,
+                "mlp_head: z2 partials too large for 32-bit buffer offsets");
+    const int nct = cdiv(a.n, kHWCols);
+    if (cdiv(a.H, 512) * nct >= 256) head_wide_kernel<4><<<cdiv(a.H, 512) * nct, 512, 0, s>>>(a, cdiv(a.H, 512));
+    else if (cdiv(a.H, 256) * nct >= 256) head_wide_kernel<2><<<cdiv(a.H, 256) * nct, 512, 0, s>>>(a, cdiv(a.H, 256));
+    else head_wide_kernel<1><<<cdiv(a.H, 128) * nct, 512, 0, s>>>(a, cdiv(a.H, 128));
+    CME_LAUNCH_CHECK(s);
+    return;
+  }
   if (a.z2part && dt != DType::F64 && a.mode == HEAD_TRAIN && a.H >= kHBMinH) {
     CME_REQUIRE((int64_t)a.H * a.lda < (int64_t)kOOB / 4, "mlp_head: a1 too large for 32-bit buffer offsets");
     if (a.C == 10) launch_head_big<10>(a, s);

@@ -85,7 +85,14 @@ struct SplitStepArgs {
   float* z1n = nullptr;
   float c1 = 0.f, c2 = 0.f;
   XgmiFuse xf;
+  // wide layers (LDS GEMM forward): when set, the forward GEMM's tile epilogue also leaves the head's
+  // z2 partial sums, z2part[row tile][16][ld] = W2[:, tile rows] . a1[tile rows, :] (v_mfma_f32_16x16x4
+  // on the activated accumulators), so the head never re-reads a1 for z2 (mlp_split_fwd1_z2_chunks)
+  float* z2part = nullptr;
 };
+
+// number of z2 row-tile partials mlp_split_fwd1 writes for `a` (0: the forward does not produce them)
+int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a);
 
 // flag slots (workgroup tiles) of the fused-all-reduce wgrad launch for a P-H layer with the all-ones
 // feature; -1 when above `cap`

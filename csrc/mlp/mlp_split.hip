@@ -2,6 +2,7 @@
 #include "mlp_split.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "lds_gemm.h"
 #include "mma_tile.h"
@@ -575,8 +576,60 @@ struct EpiSigBig {
   float* a1;
   int ld;
   float xscale;
+  // head z2 partials (nullptr: off): W2 [C][H], z2p [row tile][16][ld]
+  const float* W2;
+  float* z2p;
+  int H, C, N, bm;
+  static constexpr bool kTileHook = true;
   __device__ __forceinline__ void operator()(int row, int col, float v) {
     a1[(size_t)row * ld + col] = sigm(v * xscale + b1[row]);
+  }
+  // z2p[tile] = W2[:, tile rows] . sigmoid(acc): in the 16x16x4 f32 MFMA lane map, step i takes
+  // B[k = fg][n = fr] = a1(row0 + 16 mb + 4 fg + i, col fr) -- exactly accumulator element i -- and
+  // A[m = fr][k = fg] = W2[class fr][that row].  Row waves are summed through LDS.
+  template <int MB, int NB, int WRN>
+  __device__ __forceinline__ void tile(const f32x4 (&acc)[MB][NB], int wr, int wc, int fr, int fg, int row0,
+                                       int col0, char* lds) {
+    if (!z2p) return;
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(W2), rb = make_rsrc(b1);
+    float w[MB][4], bb[MB][4];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int h = row0 + 16 * mb + 4 * fg + i;
+        w[mb][i] = buf_load1<float>(rw, (fr < C && h < H) ? (fr * H + h) * 4 : kOOB);
+        bb[mb][i] = buf_load1<float>(rb, h < H ? h * 4 : kOOB);
+      }
+    f32x4 z[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) z[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mb][i], sigm(acc[mb][nb][i] * xscale + bb[mb][i]), z[nb],
+                                                      0, 0, 0);
+    const int lane = fg * 16 + fr;
+    f32x4* red = reinterpret_cast<f32x4*>(lds);  // [WRN][2][NB][64]
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) red[((wr * 2 + wc) * NB + nb) * 64 + lane] = z[nb];
+    __syncthreads();
+    if (wr != 0) return;
+    const int tile = row0 / bm;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      f32x4 s = red[(wc * NB + nb) * 64 + lane];
+#pragma unroll
+      for (int r = 1; r < WRN; ++r) s += red[((r * 2 + wc) * NB + nb) * 64 + lane];
+      const int col = col0 + 16 * nb + fr;
+      if (col < N) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) z2p[((size_t)tile * 16 + 4 * fg + i) * ld + col] = s[i];
+      }
+    }
   }
 };
 
@@ -609,24 +662,24 @@ struct EpiW1Big {
   }
 };
 
-template <int BM, int BN, int NPW>
-__global__ __launch_bounds__(lg::kThreads) void fwd1_big_kernel(SplitStepArgs a, int tn) {
+template <int BM, int BN, int NPW, int NT>
+__global__ __launch_bounds__(NT) void fwd1_big_kernel(SplitStepArgs a, int tn) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   const int id = xcd_remap(blockIdx.x, gridDim.x);
-  EpiSigBig epi{a.b1, a.a1, a.ld, a.xscale};
-  lds_gemm_tile<BM, BN, NPW, uint8_t>(static_cast<const bf16*>(a.W1p), a.P, a.H * a.P * (int)sizeof(bf16),
+  EpiSigBig epi{a.b1, a.a1, a.ld, a.xscale, a.W2, a.z2part, a.H, a.C, a.n, BM};
+  lds_gemm_tile<BM, BN, NPW, uint8_t, EpiSigBig, NT>(static_cast<const bf16*>(a.W1p), a.P, a.H * a.P * (int)sizeof(bf16),
                                       static_cast<const uint8_t*>(a.X), a.P, a.H, a.n, a.P, (id / tn) * BM,
                                       (id % tn) * BN, epi, lds_dyn);
 }
 
-template <int BM, int BN, int NPZ>
-__global__ __launch_bounds__(lg::kThreads) void wgrad_big_kernel(SplitStepArgs a, int tn) {
+template <int BM, int BN, int NPZ, int NT>
+__global__ __launch_bounds__(NT) void wgrad_big_kernel(SplitStepArgs a, int tn) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   EpiW1Big epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw,
                (float)a.reg, (float)a.lr, a.xscale, a.b1, a.gb1};
   const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
-  lds_gemm_tile<BM, BN, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
+  lds_gemm_tile<BM, BN, NPZ, uint8_t, EpiW1Big, NT>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
                                       static_cast<const uint8_t*>(a.XT), a.ldxt, r1, a.P + a.bias_col, a.n,
                                       a.w1_row0 + (id / tn) * BM, (id % tn) * BN, epi, lds_dyn);
 }
@@ -662,39 +715,60 @@ bool big_wgrad_ok(const SplitStepArgs& a) {
   return a.H >= kBigMinH && a.n % 16 == 0 && a.ld % 8 == 0 && a.ldxt % 16 == 0 && al16(a.dZ1p) && al16(a.XT);
 }
 
+// threads per big-GEMM workgroup: 512 (8 waves, default) or 256 (CME_BIG_THREADS=256, A/B tests)
+int big_threads() {
+  static const int v = [] {
+    const char* e = std::getenv("CME_BIG_THREADS");
+    return (e && std::atoi(e) == 256) ? 256 : 512;
+  }();
+  return v;
+}
+
 // 128x128 tiles when that still gives ~200+ workgroups, else 64x64
-template <int NP>
-void launch_fwd1_big(const SplitStepArgs& a, hipStream_t s) {
+template <int NP, int NT>
+void launch_fwd1_big_nt(const SplitStepArgs& a, hipStream_t s) {
   const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
   if (t128 >= 192) {
     constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
-    set_lds_limit<fwd1_big_kernel<128, 128, NP>>(L);
+    set_lds_limit<fwd1_big_kernel<128, 128, NP, NT>>(L);
     const int tn = cdiv(a.n, 128);
-    fwd1_big_kernel<128, 128, NP><<<t128, lg::kThreads, L, s>>>(a, tn);
+    fwd1_big_kernel<128, 128, NP, NT><<<t128, NT, L, s>>>(a, tn);
   } else {
     constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
-    set_lds_limit<fwd1_big_kernel<64, 64, NP>>(L);
+    set_lds_limit<fwd1_big_kernel<64, 64, NP, NT>>(L);
     const int tn = cdiv(a.n, 64);
-    fwd1_big_kernel<64, 64, NP><<<cdiv(a.H, 64) * tn, lg::kThreads, L, s>>>(a, tn);
+    fwd1_big_kernel<64, 64, NP, NT><<<cdiv(a.H, 64) * tn, NT, L, s>>>(a, tn);
   }
 }
 
 template <int NP>
-void launch_wgrad_big(const SplitStepArgs& a, hipStream_t s) {
+void launch_fwd1_big(const SplitStepArgs& a, hipStream_t s) {
+  if (big_threads() == 512) launch_fwd1_big_nt<NP, 512>(a, s);
+  else launch_fwd1_big_nt<NP, 256>(a, s);
+}
+
+template <int NP, int NT>
+void launch_wgrad_big_nt(const SplitStepArgs& a, hipStream_t s) {
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int NW = a.P + a.bias_col;
   const int t128 = cdiv(rows, 128) * cdiv(NW, 128);
   if (t128 >= 192) {
     constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
-    set_lds_limit<wgrad_big_kernel<128, 128, NP>>(L);
+    set_lds_limit<wgrad_big_kernel<128, 128, NP, NT>>(L);
     const int tn = cdiv(NW, 128);
-    wgrad_big_kernel<128, 128, NP><<<t128, lg::kThreads, L, s>>>(a, tn);
+    wgrad_big_kernel<128, 128, NP, NT><<<t128, NT, L, s>>>(a, tn);
   } else {
     constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
-    set_lds_limit<wgrad_big_kernel<64, 64, NP>>(L);
+    set_lds_limit<wgrad_big_kernel<64, 64, NP, NT>>(L);
     const int tn = cdiv(NW, 64);
-    wgrad_big_kernel<64, 64, NP><<<cdiv(rows, 64) * tn, lg::kThreads, L, s>>>(a, tn);
+    wgrad_big_kernel<64, 64, NP, NT><<<cdiv(rows, 64) * tn, NT, L, s>>>(a, tn);
   }
+}
+
+template <int NP>
+void launch_wgrad_big(const SplitStepArgs& a, hipStream_t s) {
+  if (big_threads() == 512) launch_wgrad_big_nt<NP, 512>(a, s);
+  else launch_wgrad_big_nt<NP, 256>(a, s);
 }
 
 template <int NPW, int NPZ, int NC>
@@ -714,6 +788,12 @@ void launch_fwdhead_nc(const SplitStepArgs& a, hipStream_t s) {
 }  // namespace
 
 int mlp_split_fwdhead_blocks(int n) { return cdiv(n, kFHCols); }
+
+int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a) {
+  if (!a.z2part || a.C > 16 || a.n <= 0 || !big_fwd_ok(a) || big_path_disabled()) return 0;
+  const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
+  return t128 >= 192 ? cdiv(a.H, 128) : cdiv(a.H, 64);  // must match launch_fwd1_big_nt's tile choice
+}
 
 void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
