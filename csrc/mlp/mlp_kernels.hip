@@ -647,12 +647,13 @@ struct EpiSigWT {
   }
 };
 
-constexpr int kFHTileCols = 32;  // columns per a1 tile = two head blocks
-
-template <int NPW, int VEC>
+// NBT 16-column blocks per a1 tile (32 or 64 columns; a 64-column tile halves the W1-plane re-reads
+// through L2 at half the workgroups, but serialises two head passes in the last arriver)
+template <int NPW, int VEC, int NBT>
 __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArgs h, unsigned* __restrict__ counters,
                                                         int tm, int tn) {
-  __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];
+  constexpr int kCols = 16 * NBT;
+  __shared__ __attribute__((aligned(16))) float red[8 * 1 * NBT * 4 * 64];
   __shared__ __attribute__((aligned(16))) Head32Lds L;
   __shared__ int s_last;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -666,9 +667,9 @@ __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArg
   // W2 / b2 for the head, staged by every workgroup before its GEMM (independent of a1; wsk_tile's
   // internal barrier orders these LDS writes before any head read)
   head32_stage(h, threadIdx.x, L);
-  TileGeom g{f.H, f.n, f.P, rt * 16, ct * kFHTileCols};
+  TileGeom g{f.H, f.n, f.P, rt * 16, ct * kCols};
   EpiSigWT epi{f.b1, f.a1, f.ld, f.xscale, {}};
-  wsk_tile<__hip_bfloat16, 1, 2, 8, true, true, VEC, 4, NPW, uint8_t>(
+  wsk_tile<__hip_bfloat16, 1, NBT, 8, true, true, VEC, NBT == 2 ? 4 : 2, NPW, uint8_t>(
       static_cast<const __hip_bfloat16*>(f.W1p), f.P, static_cast<const uint8_t*>(f.X), f.P, g, epi, red,
       f.H * f.P * (int)sizeof(__hip_bfloat16));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
@@ -681,7 +682,8 @@ __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArg
   __syncthreads();
   stamp(2);
   if (!s_last) return;
-  head32<true>(h, ct, threadIdx.x, L);
+#pragma unroll
+  for (int q = 0; q < NBT / 2; ++q) head32<true>(h, ct * (NBT / 2) + q, threadIdx.x, L);
   if (st) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp(3);
@@ -1300,15 +1302,25 @@ void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters
   CME_REQUIRE(mlp_fwd1_head_ok(f, h), "fwd1_head: H <= 128, C <= 16, train-mode head over the same a1");
   CME_REQUIRE((int64_t)f.H * f.P * 2 * f.npw < (int64_t)kOOB && (int64_t)f.n * f.P < (int64_t)kOOB,
               "fwd1_head: operand too large for 32-bit buffer offsets");
-  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, kFHTileCols);
+  // CME_FH_COLS=64: 64-column a1 tiles (A/B tests; measured 15.4 vs 10.3 us at 784-100-10, n=800 -- the
+  // last arriver then runs two head passes back to back)
+  static const int nbt = [] {
+    const char* e = std::getenv("CME_FH_COLS");
+    return (e && std::atoi(e) == 64) ? 4 : 2;
+  }();
+  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 16 * nbt);
   CME_REQUIRE(counters != nullptr && tn <= max_tiles, "fwd1_head: counter array too small");
   const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 && reinterpret_cast<uintptr_t>(f.W1p) % 16 == 0 &&
                    f.P % 8 == 0;
   const int nwg = 8 * tm * cdiv(tn, 8);
-#define CME_FH(np)                                                                    \
-  if (vec) fwd1_head_kernel<np, 1><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);       \
-  else fwd1_head_kernel<np, 0><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);
-  if (f.npw == 3) { CME_FH(3) } else { CME_FH(1) }
+#define CME_FH(np, nb)                                                                    \
+  if (vec) fwd1_head_kernel<np, 1, nb><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);       \
+  else fwd1_head_kernel<np, 0, nb><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);
+  if (nbt == 4) {
+    if (f.npw == 3) { CME_FH(3, 4) } else { CME_FH(1, 4) }
+  } else {
+    if (f.npw == 3) { CME_FH(3, 2) } else { CME_FH(1, 2) }
+  }
 #undef CME_FH
   CME_LAUNCH_CHECK(s);
 }
