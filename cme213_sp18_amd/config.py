@@ -44,6 +44,8 @@ class TrainConfig:
     fault_inject: str = ""      # "rank:step" -- raise on that rank at that step (failure-detection test hook)
     log_json: str = ""          # rank-0 JSON-lines event log
     ckpt_every: int = 0         # epochs between checkpoints (needs --ckpt-dir); 0 = only at the end
+    profile: bool = False       # per-phase event timing + roctx ranges (eager steps), summary at the end
+    overlap_chunks: int = 0     # RCCL path: dW1 all-reduce row chunks overlapped with the backward (0 = auto)
 
     @property
     def H(self):
@@ -73,7 +75,7 @@ NAMED_PRESETS = {
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="python -m cme213_sp18_amd.train",
                                  description="2-layer MLP training on MI355X (CME213 final-project CLI)")
-    ap.add_argument("-n", dest="num_neuron", type=int)
+    ap.add_argument("-n", "--hidden", dest="num_neuron", type=int)
     ap.add_argument("-r", dest="reg", type=float)
     ap.add_argument("-l", dest="learning_rate", type=float)
     ap.add_argument("-e", dest="num_epochs", type=int)
@@ -98,11 +100,16 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-graphs", dest="use_graphs", action="store_false", default=None)
     ap.add_argument("--no-softmax-shift", dest="softmax_shift", action="store_false", default=None)
     ap.add_argument("--ckpt-precision", type=int)
-    ap.add_argument("--allreduce", choices=["auto", "xgmi", "rccl"])
+    ap.add_argument("--allreduce", choices=["auto", "xgmi", "rccl", "host"])
     ap.add_argument("--comm-timeout", type=float)
     ap.add_argument("--fault-inject", help="rank:step")
     ap.add_argument("--log-json")
     ap.add_argument("--ckpt-every", type=int)
+    ap.add_argument("--profile", action="store_true", default=None,
+                    help="time forward+head / weight gradients / all-reduce / SGD per step (eager) and emit roctx "
+                         "ranges for rocprofv3 --marker-trace")
+    ap.add_argument("--overlap-chunks", type=int,
+                    help="RCCL path: number of dW1 row chunks all-reduced while the backward runs (0 = auto)")
     return ap
 
 

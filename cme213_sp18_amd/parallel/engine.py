@@ -324,10 +324,12 @@ class MlpEngine:
         self._xgmi_fuse = (int(bucket.c.desc_address), int(bucket.c.nblocks), int(o[1]), int(o[2]), int(o[3]))
         self._hip_step().set_xgmi(*self._xgmi_fuse)
 
-    def run(self, off: int, n: int, scale: float, reg: float, lr: float, sgd, with_loss: bool = False):
+    def run(self, off: int, n: int, scale: float, reg: float, lr: float, sgd, with_loss: bool = False,
+            parts: int = 3):
         """Forward + backward on samples [off, off+n).  sgd=True: update params in
         place; False: write pre-scaled gradients into ``self.grads``; 2: all-reduce over the attached
-        xGMI bucket and update inside the wgrad launch (attach_xgmi)."""
+        xGMI bucket and update inside the wgrad launch (attach_xgmi).  parts (hip backend): bit0 forward +
+        head, bit1 weight gradients / update -- the per-phase profiler runs the two halves separately."""
         if self.X is None:
             raise RuntimeError("load_dataset() first")
         if n > self.ld:
@@ -342,8 +344,8 @@ class MlpEngine:
                 st.a1 = self.a1.data_ptr()
             st.run(int(off), int(n), float(scale), float(reg), float(lr), 2 if sgd == 2 else int(bool(sgd)),
                    int(bool(with_loss)),
-                   torch.cuda.current_stream(self.device).cuda_stream)
-        else:
+                   torch.cuda.current_stream(self.device).cuda_stream, int(parts))
+        elif parts & 1:  # the torch backend always runs the whole step
             self._torch_step(off, n, scale, reg, lr, sgd, with_loss)
 
     def run_forward_head(self, off: int, n: int, scale: float, with_loss: bool = False):

@@ -61,8 +61,9 @@ class DataParallelTrainer:
     def __init__(self, nn, comm: Communicator | None = None, device=None, dtype: str = "f32",
                  batch_size: int = 800, backend: str = "hip", shift: bool = True, use_graphs: bool = True,
                  normalize: bool = False, path: str = "auto", allreduce: str = "auto", overlap: bool = True,
-                 lookahead: bool = False):
+                 lookahead: bool = False, overlap_chunks: int = 0):
         self.nn = nn
+        self.overlap_chunks = int(overlap_chunks)  # RCCL path: dW1 row chunks (0: ~BUCKET_BYTES each)
         self.comm = comm or NullComm()
         self.R = self.comm.world_size
         self.rank = self.comm.rank
@@ -77,6 +78,10 @@ class DataParallelTrainer:
         self.engine.set_params(*nn.params)
         self._graphs: dict = {}
         self.iter = 0
+        from ..utils.tracing import Roctx
+
+        self.roctx = Roctx()       # CME_ROCTX=1: epoch / phase ranges for rocprofv3 --marker-trace
+        self.profiler = None       # PhaseTimer (enable_profiling / --profile)
         self.xgmi = self._setup_xgmi(allreduce)
         # the same all-reduce fused into the wgrad launch (one kernel less per step, tiles reduced as
         # they finish): own IPC bucket with one flag slot per wgrad tile; enabled by load() once a
@@ -298,6 +303,9 @@ class DataParallelTrainer:
         """Enqueue one global SGD step on the current stream (no host sync)."""
         e = self.engine
         off, n = self.shard(start, length)
+        if self.profiler is not None and n > 0:
+            self._profiled_step(off, n, 1.0 / (n * self.R), reg, lr, with_loss)
+            return
         if n == 0:  # fewer columns than ranks: only the regulariser contributes
             e.reg_only_grads(reg / self.R)
             self._allreduce_sgd(lr)
@@ -313,11 +321,56 @@ class DataParallelTrainer:
             e.run(off, n, scale, reg / self.R, lr, sgd=False, with_loss=with_loss)
             self._allreduce_sgd(lr)
 
+    def _profiled_step(self, off, n, scale, reg, lr, with_loss):
+        """The same step, split into timed phases (PhaseTimer events + roctx ranges; eager only)."""
+        e, P = self.engine, self.profiler
+        single = isinstance(self.comm, NullComm) and self.allreduce_mode != "host"
+        if e.backend != "hip":
+            with P.phase("step"):
+                if single:
+                    e.run(off, n, scale, reg, lr, sgd=True, with_loss=with_loss)
+                else:
+                    e.run(off, n, scale, reg / self.R, lr, sgd=False, with_loss=with_loss)
+                    self._allreduce_sgd(lr)
+            return
+        if single or self.fused_allreduce:
+            sgd, r = (True, reg) if single else (2, reg / self.R)
+            with P.phase("fwd_head"):
+                e.run(off, n, scale, r, lr, sgd=sgd, with_loss=with_loss, parts=1)
+            with P.phase("wgrad_sgd" if single else "wgrad_allreduce_sgd"):
+                e.run(off, n, scale, r, lr, sgd=sgd, with_loss=with_loss, parts=2)
+            return
+        r = reg / self.R
+        with P.phase("fwd_head"):
+            e.run(off, n, scale, r, lr, sgd=False, with_loss=with_loss, parts=1)
+        with P.phase("wgrad"):
+            e.run(off, n, scale, r, lr, sgd=False, with_loss=with_loss, parts=2)
+            e.join()
+        if self.allreduce_mode == "host" or self.xgmi is not None:
+            with P.phase("allreduce_sgd"):
+                self._allreduce_sgd(lr)
+            return
+        with P.phase("allreduce"):
+            self.comm.allreduce_(e.grads)
+        with P.phase("sgd"):
+            e.sgd(lr)
+
+    def enable_profiling(self, roctx: bool = True):
+        """Per-phase timing (and roctx ranges) for the following train() calls: steps run eagerly and
+        split into forward+head / weight-gradient / all-reduce / SGD phases (the graph-replayed
+        production path has no phase boundaries to time).  Returns the PhaseTimer."""
+        from ..utils.tracing import PhaseTimer, Roctx
+
+        self.roctx = Roctx(True) if roctx else self.roctx
+        dev = self.engine.device if self.engine.device.type == "cuda" else None
+        self.profiler = PhaseTimer(dev, self.roctx)
+        return self.profiler
+
     def _buckets(self):
         """dW1 row chunks of ~BUCKET_BYTES (multiples of 128 rows, the blocked-GEMM tile)."""
         e = self.engine
         w1_bytes = e.H * e.P * e.params.element_size()
-        k = max(1, min(8, -(-w1_bytes // BUCKET_BYTES)))
+        k = self.overlap_chunks if self.overlap_chunks > 0 else max(1, min(8, -(-w1_bytes // BUCKET_BYTES)))
         rows = -(-e.H // k)
         rows = -(-rows // 128) * 128
         return [(r0, min(rows, e.H - r0)) for r0 in range(0, e.H, rows)]
@@ -424,7 +477,7 @@ class DataParallelTrainer:
 
             os.makedirs(outdir, exist_ok=True)
             err_file = open(os.path.join(outdir, "CpuGpuDiff.txt"), "w")
-        host_needed = print_every > 0 or debug
+        host_needed = print_every > 0 or debug or self.profiler is not None
         dev = self.engine.device
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
@@ -438,7 +491,8 @@ class DataParallelTrainer:
             for epoch in range(epochs):
                 if not host_needed:
                     maybe_fault(self.iter, len(plan.steps))
-                    self.run_plan(plan, lr, reg)
+                    with self.roctx.range(f"epoch {epoch}"):
+                        self.run_plan(plan, lr, reg)
                     self.iter += len(plan.steps)
                     stats.steps += len(plan.steps)
                     stats.images += sum((ln // self.R) * self.R for _, ln in plan.steps)

@@ -111,8 +111,11 @@ def run(cfg: TrainConfig) -> dict:
         log0(rank, "\nStart Parallel Training")
         tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,
                                  backend=backend, shift=cfg.softmax_shift, use_graphs=cfg.use_graphs,
-                                 normalize=cfg.normalize, path=cfg.path, allreduce=cfg.allreduce)
+                                 normalize=cfg.normalize, path=cfg.path, allreduce=cfg.allreduce,
+                                 overlap_chunks=cfg.overlap_chunks)
         tr.load(ds.x_train, ds.y_train)
+        if cfg.profile:
+            tr.enable_profiling()
         fault = parse_fault(cfg.fault_inject)
         ckpt_meta = lambda done: {"epochs": done + meta.get("epochs", 0), "lr": cfg.learning_rate, "reg": cfg.reg,
                                   "seed": cfg.seed, "dtype": cfg.dtype, "iter": tr.iter}
@@ -138,6 +141,11 @@ def run(cfg: TrainConfig) -> dict:
                 break
         out.update(par_seconds=st.seconds, images_per_sec=st.images_per_sec, engine_path=tr.engine.path,
                    allreduce=tr.allreduce_impl)
+        if tr.profiler is not None:
+            phases = tr.profiler.summary()
+            out["profile"] = phases
+            log0(rank, f"Per-step phases (eager, mean): {tr.profiler.format()}")
+            jlog({"event": "profile", "phases": phases})
         log0(rank, f"Time for Parallel Training: {st.seconds:.6f} seconds ({st.images_per_sec:,.0f} images/s, "
                    f"engine path {tr.engine.path})")
         if rank == 0:

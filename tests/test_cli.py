@@ -49,3 +49,39 @@ def test_cli_end_to_end_cpu(tmp_path):
     pred = (tmp_path / "Outputs" / "Pred_testset.txt").read_text()
     assert len(pred) == 300 and pred.isdigit()
     assert (tmp_path / "ckpt" / "W0.mat").exists() and (tmp_path / "Outputs" / "CpuGpuDiff.txt").exists()
+
+
+def test_long_flags():
+    c = parse_config(["--hidden", "256", "--overlap-chunks", "3", "--profile", "--allreduce", "host"])
+    assert c.num_neuron == 256 and c.overlap_chunks == 3 and c.profile and c.allreduce == "host"
+
+
+def test_cli_profile_cpu(tmp_path):
+    """--profile: per-phase timing summary in the JSON-lines log and in the final record."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    log = tmp_path / "run.jsonl"
+    r = subprocess.run([sys.executable, "-m", "cme213_sp18_amd.train", "--preset", "cpu_plumbing", "-n", "16",
+                        "-e", "1", "--num-train", "1600", "--num-test", "100", "--profile", "--log-json", str(log),
+                        "--outdir", str(tmp_path / "Outputs")],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["profile"]["step"]["count"] == 2  # 1600 / 800 steps, torch backend: one phase per step
+    ev = [json.loads(line) for line in log.read_text().splitlines()]
+    assert any(e.get("event") == "profile" for e in ev)
+
+
+def test_tracing_helpers_cpu():
+    from cme213_sp18_amd.utils.tracing import PhaseTimer, Roctx
+
+    rx = Roctx(enabled=False)
+    assert not rx.enabled
+    with rx.range("noop"):
+        pass
+    t = PhaseTimer(None, rx)
+    for _ in range(3):
+        with t.phase("a"):
+            sum(range(1000))
+    s = t.summary()
+    assert s["a"]["count"] == 3 and s["a"]["total_ms"] >= 0
+    assert "a=" in t.format()

@@ -319,3 +319,22 @@ def test_fwd1_head_single_launch_matches_two_launches(dtype, H, n):
     for ta, tb in zip(a[:-1], b[:-1]):
         assert torch.equal(ta, tb)
     assert a[-1] == b[-1]
+
+
+def test_profiled_steps_match_graph_steps():
+    """enable_profiling(): the same steps split into timed phases (fwd_head, wgrad_sgd) give the same
+    parameters as the graph-replayed production path, and every phase is timed."""
+    x, y = synthetic_mnist(1600, seed=3)
+    outs = []
+    for prof in (False, True):
+        nn = NeuralNetwork([784, 100, 10])
+        tr = DataParallelTrainer(nn, dtype="f32", batch_size=800)
+        tr.load(x, y)
+        if prof:
+            P = tr.enable_profiling(roctx=True)
+        tr.train(2, 0.01, 1e-4)
+        outs.append(tr.engine.params.clone())
+    s = P.summary()
+    assert s["fwd_head"]["count"] == 4 and s["wgrad_sgd"]["count"] == 4
+    assert s["fwd_head"]["mean_ms"] > 0
+    assert torch.equal(outs[0], outs[1])
