@@ -338,3 +338,19 @@ def test_profiled_steps_match_graph_steps():
     assert s["fwd_head"]["count"] == 4 and s["wgrad_sgd"]["count"] == 4
     assert s["fwd_head"]["mean_ms"] > 0
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("dtype,H", [("f32", 100), ("bf16", 100), ("f64", 100), ("f32", 1024)])
+def test_training_is_deterministic(dtype, H):
+    """two runs from the same seed give bitwise-identical parameters (no atomics in any
+    reduction; split-K partials are summed in a fixed order)."""
+    x, y = synthetic_mnist(2400, seed=5)
+    outs = []
+    for _ in range(2):
+        nn = NeuralNetwork([784, H, 10])
+        tr = DataParallelTrainer(nn, dtype=dtype, batch_size=800)
+        tr.load(x, y)
+        tr.train(2, 0.01, 1e-4)
+        torch.cuda.synchronize()
+        outs.append(tr.engine.params.clone())
+    assert torch.equal(outs[0], outs[1])
