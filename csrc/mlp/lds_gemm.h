@@ -35,13 +35,17 @@ template <typename TB>
 struct BTraits;
 template <>
 struct BTraits<uint8_t> {
-  static constexpr int kRow = kBK + 16;       // bytes per B row in LDS
-  static constexpr int kChunksPerRow = kBK / 16;
+  // uint8 pixels are widened to bf16 ONCE, when a stage is written to LDS (16 conversions per thread per
+  // stage), instead of at every fragment read (measured: ~95 VALU conversions per 40 MFMAs per wave)
+  static constexpr int kRow = kBK * 2 + 16;   // bytes per B row in LDS (bf16)
+  static constexpr int kChunksPerRow = kBK / 16;  // 16-byte global chunks (16 pixels) per row
+  static constexpr int kLdsChunk = 32;        // bytes one global chunk occupies in LDS
 };
 template <>
 struct BTraits<__hip_bfloat16> {
   static constexpr int kRow = kBK * 2 + 16;
   static constexpr int kChunksPerRow = kBK * 2 / 16;
+  static constexpr int kLdsChunk = 16;
 };
 
 template <int BM, int BN, int NPA, typename TB>
@@ -74,7 +78,10 @@ struct HasTileHook<E, std::void_t<decltype(E::kTileHook)>> : std::true_type {};
 // bytes (16-byte aligned).  Requirements (checked by the launcher): K % 16 == 0,
 // lda % 8 == 0 (bf16) and ldb % 16 == 0 bytes, 16-byte aligned operand bases.
 // epi(row, col, v) is called for every in-range element of the tile.
-template <int BM, int BN, int NPA, typename TB, class Epi, int NT = lg::kThreads>
+// NKS > 0: the K loop has exactly NKS stages (K in ((NKS-1)*64, NKS*64]) and is fully unrolled -- in a
+// runtime-trip-count loop the compiler's vmcnt tracking merges at the back-edge and drains every load
+// (vmcnt(0)) before the stage-(k+1) LDS stores, i.e. the stage-(k+2) prefetch never stays in flight.
+template <int BM, int BN, int NPA, typename TB, class Epi, int NT = lg::kThreads, int NKS = 0>
 __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__ A, int lda, int plane_bytes,
                                               const TB* __restrict__ B, int ldb, int M, int N, int K, int m0, int n0,
                                               Epi& epi, char* __restrict__ lds) {
@@ -116,7 +123,7 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
     const int c = t + j * NT, r = c / BCPR, kc = c % BCPR;
     b_ok[j] = n0 + r < N;
     b_off[j] = (n0 + r) * ldb * (int)sizeof(TB) + kc * 16;
-    b_lds[j] = r * BROW + kc * 16;
+    b_lds[j] = r * BROW + kc * BTraits<TB>::kLdsChunk;
   }
 
   // two register stages: the loads of K-stage k+2 are issued before stage k is multiplied and are
@@ -152,7 +159,16 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
         *reinterpret_cast<uint4*>(ldsA + buf * A_BUF + p * BM * kARow + a_lds[j]) = rA[p][j];
 #pragma unroll
     for (int j = 0; j < BJ; ++j)
-      if (b_mine(j)) *reinterpret_cast<uint4*>(ldsB + buf * B_BUF + b_lds[j]) = rB[j];
+      if (b_mine(j)) {
+        if constexpr (sizeof(TB) == 1) {  // 16 pixels -> 16 bf16 (32 bytes)
+          const bf16x8_t lo = lg::u8x8_to_bf16(uint2{rB[j].x, rB[j].y});
+          const bf16x8_t hi = lg::u8x8_to_bf16(uint2{rB[j].z, rB[j].w});
+          *reinterpret_cast<bf16x8_t*>(ldsB + buf * B_BUF + b_lds[j]) = lo;
+          *reinterpret_cast<bf16x8_t*>(ldsB + buf * B_BUF + b_lds[j] + 16) = hi;
+        } else {
+          *reinterpret_cast<uint4*>(ldsB + buf * B_BUF + b_lds[j]) = rB[j];
+        }
+      }
   };
 
   f32x4 acc[MB][NB];
@@ -169,12 +185,7 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
       bf16x8_t bf[NB];
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
-        if constexpr (sizeof(TB) == 1) {
-          const uint2 w = *reinterpret_cast<const uint2*>(sB + nb * 16 * BROW + kk * 32 + fg * 8);
-          bf[nb] = lg::u8x8_to_bf16(w);
-        } else {
-          bf[nb] = *reinterpret_cast<const bf16x8_t*>(sB + nb * 16 * BROW + (kk * 32 + fg * 8) * 2);
-        }
+        bf[nb] = *reinterpret_cast<const bf16x8_t*>(sB + nb * 16 * BROW + (kk * 32 + fg * 8) * 2);
       }
       // issue every A fragment read of this k-step before the first MFMA: one LDS round trip per
       // k-step instead of one per fragment (the reads are independent; counted lgkmcnt waits)
@@ -195,7 +206,7 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
     }
   };
 
-  const int nk = (K + kBK - 1) / kBK;
+  const int nk = NKS > 0 ? NKS : (K + kBK - 1) / kBK;
   load_stage(0, ra_reg[0], rb_reg[0]);
   if (nk > 1) load_stage(kBK, ra_reg[1], rb_reg[1]);
   store_stage(0, ra_reg[0], rb_reg[0]);
@@ -212,11 +223,16 @@ __device__ __forceinline__ void lds_gemm_tile(const __hip_bfloat16* __restrict__
   auto step = [&](int kt, uint4 (&rA_cur)[NPA][AJ], uint4 (&rB_cur)[BJ], uint4 (&rA_nxt)[NPA][AJ],
                   uint4 (&rB_nxt)[BJ]) {
     if (kt + 2 < nk) load_stage((kt + 2) * kBK, rA_cur, rB_cur);  // set kt&1 is free again
+    // keep the stage-(k+2) loads ahead of this stage's MFMAs: without the fence the scheduler sinks them
+    // below the stage-(k+1) LDS stores (one register set instead of two), so only one compute phase
+    // covers the load latency (measured in the ISA: loads issued right before the barrier)
+    __builtin_amdgcn_sched_barrier(0);
     compute(kt & 1);
     if (kt + 1 < nk) store_stage((kt + 1) & 1, rA_nxt, rB_nxt);
     lds_barrier();
   };
-  for (int kt = 0; kt < nk; kt += 2) {
+#pragma unroll
+  for (int kt = 0; kt < (NKS > 0 ? NKS : nk); kt += 2) {
     step(kt, ra_reg[0], rb_reg[0], ra_reg[1], rb_reg[1]);
     if (kt + 1 < nk) step(kt + 1, ra_reg[1], rb_reg[1], ra_reg[0], rb_reg[0]);
   }

@@ -662,24 +662,24 @@ struct EpiW1Big {
   }
 };
 
-template <int BM, int BN, int NPW, int NT>
+template <int BM, int BN, int NPW, int NT, int NKS = 0>
 __global__ __launch_bounds__(NT) void fwd1_big_kernel(SplitStepArgs a, int tn) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   EpiSigBig epi{a.b1, a.a1, a.ld, a.xscale, a.W2, a.z2part, a.H, a.C, a.n, BM};
-  lds_gemm_tile<BM, BN, NPW, uint8_t, EpiSigBig, NT>(static_cast<const bf16*>(a.W1p), a.P, a.H * a.P * (int)sizeof(bf16),
+  lds_gemm_tile<BM, BN, NPW, uint8_t, EpiSigBig, NT, NKS>(static_cast<const bf16*>(a.W1p), a.P, a.H * a.P * (int)sizeof(bf16),
                                       static_cast<const uint8_t*>(a.X), a.P, a.H, a.n, a.P, (id / tn) * BM,
                                       (id % tn) * BN, epi, lds_dyn);
 }
 
-template <int BM, int BN, int NPZ, int NT>
+template <int BM, int BN, int NPZ, int NT, int NKS = 0>
 __global__ __launch_bounds__(NT) void wgrad_big_kernel(SplitStepArgs a, int tn) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   EpiW1Big epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw,
                (float)a.reg, (float)a.lr, a.xscale, a.b1, a.gb1};
   const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
-  lds_gemm_tile<BM, BN, NPZ, uint8_t, EpiW1Big, NT>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
+  lds_gemm_tile<BM, BN, NPZ, uint8_t, EpiW1Big, NT, NKS>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
                                       static_cast<const uint8_t*>(a.XT), a.ldxt, r1, a.P + a.bias_col, a.n,
                                       a.w1_row0 + (id / tn) * BM, (id % tn) * BN, epi, lds_dyn);
 }
@@ -725,20 +725,27 @@ int big_threads() {
 }
 
 // 128x128 tiles when that still gives ~200+ workgroups, else 64x64
-template <int NP, int NT>
-void launch_fwd1_big_nt(const SplitStepArgs& a, hipStream_t s) {
+// K-stage count 13 (K = 769..832: P = 784 for the forward, per-rank batch 800 for dW1) gets the
+// fully unrolled K loop; anything else the runtime loop
+template <int NP, int NT, int NKS>
+void launch_fwd1_big_k(const SplitStepArgs& a, hipStream_t s) {
   const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
   if (t128 >= 192) {
     constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
-    set_lds_limit<fwd1_big_kernel<128, 128, NP, NT>>(L);
-    const int tn = cdiv(a.n, 128);
-    fwd1_big_kernel<128, 128, NP, NT><<<t128, NT, L, s>>>(a, tn);
+    set_lds_limit<fwd1_big_kernel<128, 128, NP, NT, NKS>>(L);
+    fwd1_big_kernel<128, 128, NP, NT, NKS><<<t128, NT, L, s>>>(a, cdiv(a.n, 128));
   } else {
     constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
-    set_lds_limit<fwd1_big_kernel<64, 64, NP, NT>>(L);
+    set_lds_limit<fwd1_big_kernel<64, 64, NP, NT, NKS>>(L);
     const int tn = cdiv(a.n, 64);
-    fwd1_big_kernel<64, 64, NP, NT><<<cdiv(a.H, 64) * tn, NT, L, s>>>(a, tn);
+    fwd1_big_kernel<64, 64, NP, NT, NKS><<<cdiv(a.H, 64) * tn, NT, L, s>>>(a, tn);
   }
+}
+
+template <int NP, int NT>
+void launch_fwd1_big_nt(const SplitStepArgs& a, hipStream_t s) {
+  if (cdiv(a.P, lg::kBK) == 13) launch_fwd1_big_k<NP, NT, 13>(a, s);
+  else launch_fwd1_big_k<NP, NT, 0>(a, s);
 }
 
 template <int NP>
@@ -747,22 +754,27 @@ void launch_fwd1_big(const SplitStepArgs& a, hipStream_t s) {
   else launch_fwd1_big_nt<NP, 256>(a, s);
 }
 
-template <int NP, int NT>
-void launch_wgrad_big_nt(const SplitStepArgs& a, hipStream_t s) {
+template <int NP, int NT, int NKS>
+void launch_wgrad_big_k(const SplitStepArgs& a, hipStream_t s) {
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int NW = a.P + a.bias_col;
   const int t128 = cdiv(rows, 128) * cdiv(NW, 128);
   if (t128 >= 192) {
     constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
-    set_lds_limit<wgrad_big_kernel<128, 128, NP, NT>>(L);
-    const int tn = cdiv(NW, 128);
-    wgrad_big_kernel<128, 128, NP, NT><<<t128, NT, L, s>>>(a, tn);
+    set_lds_limit<wgrad_big_kernel<128, 128, NP, NT, NKS>>(L);
+    wgrad_big_kernel<128, 128, NP, NT, NKS><<<t128, NT, L, s>>>(a, cdiv(NW, 128));
   } else {
     constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
-    set_lds_limit<wgrad_big_kernel<64, 64, NP, NT>>(L);
+    set_lds_limit<wgrad_big_kernel<64, 64, NP, NT, NKS>>(L);
     const int tn = cdiv(NW, 64);
-    wgrad_big_kernel<64, 64, NP, NT><<<cdiv(rows, 64) * tn, NT, L, s>>>(a, tn);
+    wgrad_big_kernel<64, 64, NP, NT, NKS><<<cdiv(rows, 64) * tn, NT, L, s>>>(a, tn);
   }
+}
+
+template <int NP, int NT>
+void launch_wgrad_big_nt(const SplitStepArgs& a, hipStream_t s) {
+  if (cdiv(a.n, lg::kBK) == 13) launch_wgrad_big_k<NP, NT, 13>(a, s);
+  else launch_wgrad_big_k<NP, NT, 0>(a, s);
 }
 
 template <int NP>
