@@ -50,6 +50,10 @@ def parse(argv=None):
     ap.add_argument("--mode", default="optimized", choices=["optimized", "reference"],
                     help="reference: the reference's execution model on MI355X -- unfused PyTorch/hipBLAS ops, "
                          "no graphs, host-staged gradient all-reduce (for comparison only)")
+    ap.add_argument("--parallel", default="dp", choices=["dp", "tp"],
+                    help="dp: data parallel (the reference's scheme); tp: hidden-dimension tensor parallel "
+                         "(one z2 all-reduce per step, every rank runs the whole global batch --batch; strong "
+                         "scaling of a fixed model, meant for the wide configs)")
     ap.add_argument("--train-size", type=int, default=54000)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -72,6 +76,8 @@ def main(argv=None) -> int:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE", file=sys.stderr)
     comm, device = init_distributed()
     R, rank = comm.world_size, comm.rank
+    if a.parallel == "tp":
+        return run_tp(a, comm, device)
     global_batch = a.batch * R if a.scaling == "weak" else a.batch
 
     x, y = synthetic_mnist(a.train_size, seed=0)  # identical on every rank, no broadcast
@@ -140,6 +146,68 @@ def main(argv=None) -> int:
                        "hip_graphs": tr.use_graphs, "allreduce": tr.allreduce_impl, "params_finite": ok},
         }
         print(json.dumps(rec), flush=True)
+    shutdown()
+    return 0 if ok else 1
+
+
+def run_tp(a, comm, device) -> int:
+    """Hidden-sharded tensor-parallel step (parallel/tensor_parallel.py): fixed model and global batch
+    (strong scaling), K timed steps bracketed by barrier + synchronize, max over ranks."""
+    import torch
+
+    from cme213_sp18_amd.models.mlp import NeuralNetwork
+    from cme213_sp18_amd.parallel.launcher import shutdown
+    from cme213_sp18_amd.parallel.tensor_parallel import TensorParallelTrainer
+    from cme213_sp18_amd.parallel.trainer import EpochPlan
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    R, rank = comm.world_size, comm.rank
+    B = a.batch
+    x, y = synthetic_mnist(a.train_size, seed=0)
+    nn = NeuralNetwork([784, a.hidden, 10])
+    tr = TensorParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=B, backend=a.backend)
+    tr.load(x, y)
+    full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == B]
+    lr, reg = 1e-3, 1e-4
+
+    def plans_for(k):
+        out, i = [], 0
+        while i < k:
+            m = min(len(full), k - i)
+            out.append(EpochPlan(full[:m]))
+            i += m
+        return out
+
+    warm, timed = plans_for(a.warmup), plans_for(a.steps)
+    graphs = tr.graphs_usable(not a.no_graphs)
+    if graphs:  # every distinct plan captured outside the timed region
+        for p in {tuple(p.steps): p for p in warm + timed}.values():
+            tr.capture(p, lr, reg)
+    for p in warm:
+        tr.run_plan(p, lr, reg, use_graphs=graphs)
+    torch.cuda.synchronize(device)
+    comm.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for p in timed:
+        tr.run_plan(p, lr, reg, use_graphs=graphs)
+    torch.cuda.synchronize(device)
+    comm.barrier()
+    torch.cuda.synchronize(device)
+    dt = comm.allreduce_scalar(time.perf_counter() - t0, op="max")
+    ok = bool(torch.isfinite(tr.engine.params).all().item())
+    value = a.steps * B / dt
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": R, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(1e3 * dt / a.steps, 6), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None,
+            "dtype": {"f32": "fp32", "f64": "fp64", "bf16": "bf16"}[a.dtype],
+            "data": "synthetic (MNIST-shaped 784-dim uint8 images, random-init weights)",
+            "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": B, "seq_len": None,
+                       "parallelism": f"tp{R}", "hidden_per_gpu": a.hidden // R, "backend": a.backend,
+                       "hip_graphs": graphs, "params_finite": ok},
+        }), flush=True)
     shutdown()
     return 0 if ok else 1
 

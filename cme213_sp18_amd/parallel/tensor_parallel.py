@@ -1,0 +1,241 @@
+"""Tensor parallelism over the hidden dimension (an extension; SURVEY §2.6 "optional stretch").
+
+The reference only has data parallelism (fpcode/neural_network.cpp:401-575): every rank holds the whole
+model and the per-batch gradient (784H + 11H + 10 values) is all-reduced.  For the WIDE configs
+(784-4096-10, BASELINE config 4) that is a 13 MB fp32 all-reduce per step.  Sharding the hidden layer
+instead (W1 rows / b1 / W2 columns, "column-then-row" parallel) leaves a single collective per step: the
+SUM of the output pre-activations z2 (C x batch = 32 KB at batch 800), because
+
+    z2   = sum_r W2[:, H_r] . sigmoid(W1[H_r] X + b1[H_r]) + b2     (one all-reduce)
+    D    = (softmax(z2) - y) / B                                     (identical on every rank)
+    dZ1  = (W2[:, H_r]^T D) .* a1_r .* (1 - a1_r)                    (local)
+    dW1[H_r] = dZ1 X^T + reg W1[H_r],  db1[H_r] = dZ1 1,  dW2[:, H_r] = D a1_r^T + reg W2[:, H_r]   (local)
+    db2  = D 1                                                       (identical on every rank)
+
+so there is no gradient all-reduce at all and every rank processes the FULL global batch.  On MI355X the
+z2 partials come for free out of the forward LDS GEMM's tile epilogue (EpiSigBig::tile, H_r >= 512), the
+32 KB all-reduce rides RCCL over xGMI, and the head / weight-gradient kernels are the data-parallel
+engine's (MlpStep.tp_forward / tp_head / run(parts=2)).  f64 and the torch backend run the same
+algorithm in PyTorch ops (CPU-testable with gloo / LoopbackComm).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from .comm import Communicator, NullComm
+from .engine import MlpEngine
+from .trainer import EpochPlan, TrainStats
+
+
+class TensorParallelTrainer:
+    """Hidden-sharded training: rank r owns hidden units [r*H/R, (r+1)*H/R)."""
+
+    def __init__(self, nn, comm: Communicator | None = None, device=None, dtype: str = "f32",
+                 batch_size: int = 800, backend: str = "hip", shift: bool = True, normalize: bool = False,
+                 path: str = "auto"):
+        self.nn = nn
+        self.comm = comm or NullComm()
+        self.R, self.rank = self.comm.world_size, self.comm.rank
+        P, H, C = nn.H
+        if H % self.R:
+            raise ValueError(f"hidden size {H} is not divisible by {self.R} tensor-parallel ranks")
+        self.P, self.H, self.C = P, H, C
+        self.Hs = H // self.R
+        self.rows = slice(self.rank * self.Hs, (self.rank + 1) * self.Hs)
+        self.B = int(batch_size)
+        self.normalize = normalize
+        self.engine = MlpEngine((P, self.Hs, C), dtype=dtype, max_cols=self.B, device=device, backend=backend,
+                                shift=shift, path=path)
+        self._set_shard(*nn.params)
+        e = self.engine
+        # all-reduced pre-activation z2 (without b2), [16][ld] fp32 -- the layout head_wide_kernel reads
+        self.z2 = torch.zeros(16, e.ld, dtype=e.pdt if not e.np else torch.float32, device=e.device)
+        self._z2part = None
+        if e.backend == "hip" and e.np and e.z2buf is not None:
+            self._z2part = e.z2buf
+        self.iter = 0
+        self._graphs: dict = {}
+
+    # ------------------------------------------------------------------ params
+    def _set_shard(self, W1, b1, W2, b2):
+        r = self.rows
+        self.engine.set_params(np.ascontiguousarray(W1[r]), np.ascontiguousarray(b1[r]),
+                               np.ascontiguousarray(W2[:, r]), np.ascontiguousarray(b2))
+
+    def gather_params(self):
+        """Full (W1, b1, W2, b2) as float64 numpy on every rank (zero-padded SUM all-reduce: exact)."""
+        e = self.engine
+        W1s, b1s, W2s, b2 = e.get_params()
+        dev = e.device
+        full = torch.zeros(self.H * self.P + self.H + self.C * self.H, dtype=torch.float64, device=dev)
+        W1 = full[:self.H * self.P].view(self.H, self.P)
+        b1 = full[self.H * self.P:self.H * self.P + self.H]
+        W2 = full[self.H * self.P + self.H:].view(self.C, self.H)
+        W1[self.rows] = torch.as_tensor(W1s, device=dev)
+        b1[self.rows] = torch.as_tensor(b1s, device=dev)
+        W2[:, self.rows] = torch.as_tensor(W2s, device=dev)
+        if self.R > 1:
+            self.comm.allreduce_(full)
+        return (W1.cpu().numpy().copy(), b1.cpu().numpy().copy(), W2.cpu().numpy().copy(), np.array(b2))
+
+    def sync_to(self, nn) -> None:
+        W1, b1, W2, b2 = self.gather_params()
+        nn.W[0][...] = W1
+        nn.b[0][...] = b1
+        nn.W[1][...] = W2
+        nn.b[1][...] = b2
+
+    # -------------------------------------------------------------------- data
+    def load(self, x_train, y_train):
+        self.engine.load_dataset(x_train, y_train, normalize=self.normalize)
+        self.N = self.engine.num_samples
+
+    def epoch_plan(self, N: int | None = None) -> EpochPlan:
+        N = self.N if N is None else N
+        nb = (N + self.B - 1) // self.B
+        return EpochPlan([(b * self.B, min(self.B, N - b * self.B)) for b in range(nb)])
+
+    # -------------------------------------------------------------------- step
+    def step(self, start: int, n: int, lr: float, reg: float, with_loss: bool = False) -> None:
+        """One SGD step on samples [start, start+n) (every rank sees the whole batch)."""
+        e = self.engine
+        if e.backend == "hip" and e.np:
+            self._step_hip(start, n, lr, reg, with_loss)
+        else:
+            self._step_torch(start, n, lr, reg, with_loss)
+
+    def _step_hip(self, off, n, lr, reg, with_loss):
+        e = self.engine
+        st = e._hip_step()
+        stream = torch.cuda.current_stream(e.device).cuda_stream
+        zp = self._z2part
+        chunks = st.tp_forward(int(off), int(n), zp.data_ptr() if zp is not None else 0, stream)
+        C, ld = self.C, e.ld
+        if chunks > 0:
+            self.z2[:, :n] = zp[:chunks * 16 * ld].view(chunks, 16, ld)[:, :, :n].sum(0)
+        else:  # narrow shard (the wave-split-K forward): z2 partial through hipBLAS
+            self.z2[:C, :n] = e.W2 @ e.a1[:, :n]
+        if self.R > 1:
+            self.comm.allreduce_(self.z2)
+        st.tp_head(int(off), int(n), 1.0 / n, int(bool(with_loss)), self.z2.data_ptr(), stream)
+        # local weight gradients + SGD (db1 from the all-ones feature column, dW2 / db2 roles)
+        st.run(int(off), int(n), 1.0 / n, float(reg), float(lr), 1, 0, stream, 2)
+
+    def _step_torch(self, off, n, lr, reg, with_loss):
+        e = self.engine
+        with torch.no_grad():
+            Xb = e.X[off:off + n].to(e.pdt) * e.xscale
+            W1g = e.W1p.to(e.pdt).sum(0) if e.np else e.W1g.to(e.pdt)
+            a1 = torch.sigmoid(Xb @ W1g.t() + e.b1)                 # [n][Hs]
+            z2 = (a1 @ e.W2.t()).t().contiguous()                   # [C][n] partial
+            if self.R > 1:
+                self.comm.allreduce_(z2)
+            z2 = z2.t() + e.b2
+            if e.shift:
+                z2 = z2 - z2.max(dim=1, keepdim=True).values
+            ex = torch.exp(z2)
+            p = ex / ex.sum(dim=1, keepdim=True)
+            lab = e.labels[off:off + n].long()
+            idx = torch.arange(n, device=p.device)
+            if with_loss:
+                e.loss_buf.zero_()
+                e.loss_buf[0] = -torch.log(p[idx, lab]).sum().float()
+            onehot = torch.zeros_like(p)
+            onehot[idx, lab] = 1.0
+            D = (p - onehot) / n
+            dZ1 = (D @ e.W2) * a1 * (1 - a1)
+            e.a1[:, :n] = a1.t()
+            e.D[:, :n] = D.t()
+            e.dZ1[:, :n] = dZ1.t()
+            e.W1.sub_(lr * (dZ1.t() @ Xb + reg * e.W1))
+            e.W2.sub_(lr * (D.t() @ a1 + reg * e.W2))
+            e.b1.sub_(lr * dZ1.sum(0))
+            e.b2.sub_(lr * D.sum(0))
+            e.refresh_shadow()
+
+    def step_loss(self, start: int, n: int, lr: float, reg: float) -> float:
+        """Step + the (pre-update) global loss, reference definition (neural_network.cpp:144-154)."""
+        e = self.engine
+        with torch.no_grad():
+            nrm = float((e.W1.double() ** 2).sum() + (e.W2.double() ** 2).sum())
+        nrm = self.comm.allreduce_scalar(nrm) if self.R > 1 else nrm
+        self.step(start, n, lr, reg, with_loss=True)
+        return e.loss_sum() / n + 0.5 * reg * nrm  # the cross-entropy term is identical on every rank
+
+    # ------------------------------------------------------------------ graphs
+    def graphs_usable(self, use_graphs: bool = True) -> bool:
+        return bool(use_graphs and self.engine.device.type == "cuda" and (self.R == 1 or self.comm.graph_capturable))
+
+    def capture(self, plan: EpochPlan, lr: float, reg: float) -> torch.cuda.CUDAGraph:
+        """Capture every step of ``plan`` into one HIP graph (state-neutral warm-up first); cached."""
+        key = (tuple(plan.steps), float(lr), float(reg))
+        g = self._graphs.get(key)
+        if g is not None:
+            return g
+        e = self.engine
+        snap = e.params.clone(), (e.W1p.clone() if e.W1p is not None else None)
+        side = torch.cuda.Stream(e.device)
+        side.wait_stream(torch.cuda.current_stream(e.device))
+        with torch.cuda.stream(side):  # warm-up (lazy kernel loads, communicator set-up)
+            self.step(*plan.steps[0], lr, reg)
+        torch.cuda.current_stream(e.device).wait_stream(side)
+        torch.cuda.synchronize(e.device)
+        e.params.copy_(snap[0])
+        if snap[1] is not None:
+            e.W1p.copy_(snap[1])
+        torch.cuda.synchronize(e.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for s, ln in plan.steps:
+                self.step(s, ln, lr, reg)
+        torch.cuda.synchronize(e.device)
+        self._graphs[key] = g
+        return g
+
+    def run_plan(self, plan: EpochPlan, lr: float, reg: float, use_graphs: bool = True) -> None:
+        """All steps of ``plan``; replayed from a captured HIP graph when the communicator allows it
+        (RCCL / one rank) -- the z2 all-reduce is then a graph node like the kernels around it."""
+        if self.graphs_usable(use_graphs):
+            self.capture(plan, lr, reg).replay()
+        else:
+            for s, ln in plan.steps:
+                self.step(s, ln, lr, reg)
+
+    # ------------------------------------------------------------------- train
+    def train(self, epochs: int, lr: float, reg: float, print_every: int = 0, log=print) -> TrainStats:
+        stats = TrainStats()
+        plan = self.epoch_plan()
+        dev = self.engine.device
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        self.comm.barrier()
+        t0 = time.perf_counter()
+        for epoch in range(epochs):
+            for s, ln in plan.steps:
+                if print_every > 0 and self.iter % print_every == 0:
+                    l = self.step_loss(s, ln, lr, reg)
+                    stats.losses.append(l)
+                    if self.rank == 0:
+                        log(f"Loss at iteration {self.iter} of epoch {epoch}/{epochs} = {l:.10g}")
+                else:
+                    self.step(s, ln, lr, reg)
+                self.iter += 1
+                stats.steps += 1
+                stats.images += ln
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        self.comm.barrier()
+        stats.seconds = time.perf_counter() - t0
+        self.sync_to(self.nn)
+        return stats
+
+    def predict(self, x) -> np.ndarray:
+        """Argmax labels with the gathered full model (call after train / sync_to)."""
+        e = self.engine
+        full = MlpEngine((self.P, self.H, self.C), dtype=e.dtype, max_cols=min(4096, max(1, len(x))),
+                         device=e.device, backend=e.backend, shift=e.shift)
+        full.set_params(*self.gather_params())
+        return full.predict(x)

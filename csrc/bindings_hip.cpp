@@ -291,6 +291,31 @@ struct MlpStep {
     cme::mlp_split_wgrad(a, S(stream));
   }
 
+  // ---- tensor parallel over the hidden dimension (split paths; parallel/tensor_parallel.py)
+  // forward GEMM of this rank's hidden shard only; with z2p != 0 the LDS GEMM also leaves the z2 row-tile
+  // partials there.  Returns how many it wrote (0: the caller forms W2_s . a1_s itself).
+  int tp_forward(int64_t off, int n, uintptr_t z2p_, uintptr_t stream) {
+    CME_REQUIRE(split && n > 0 && n <= ld, "MlpStep.tp_forward: split path, 0 < n <= ld");
+    cme::SplitStepArgs a = split_args(off, n, 1.0, 0.0, 0.0, 1, 0);
+    a.z2part = z2p_ ? P_<float>(z2p_) : nullptr;
+    cme::mlp_split_fwd1(a, S(stream));
+    return a.z2part ? cme::mlp_split_fwd1_z2_chunks(a) : 0;
+  }
+  // head on the all-reduced pre-activation z2 ([16][ld], without b2): softmax / loss / D for every
+  // column, dZ1 (+ planes) for this rank's hidden rows
+  void tp_head(int64_t off, int n, double scale, int with_loss, uintptr_t z2full, uintptr_t stream) {
+    CME_REQUIRE(split && n > 0 && n <= ld && z2full, "MlpStep.tp_head: split path, 0 < n <= ld, z2 buffer");
+    const cme::SplitStepArgs a = split_args(off, n, scale, 0.0, 0.0, 1, with_loss);
+    cme::HeadArgs h{};
+    h.a1 = a.a1; h.lda = ld; h.W2 = a.W2; h.b2 = a.b2; h.labels = a.labels; h.H = H; h.C = C; h.n = n;
+    h.scale = scale; h.D = a.D; h.ldd = ld; h.dZ1 = a.dZ1; h.ldz = ld; h.dZ1_bf16 = nullptr;
+    h.dZ1_planes = a.dZ1p; h.npz = npz; h.loss_partial = a.loss_partial; h.shift = shift;
+    h.mode = cme::HEAD_TRAIN;
+    h.z2part = P_<float>(z2full);
+    h.z2_chunks = 1;
+    cme::mlp_head(DType::F32, h, S(stream));
+  }
+
   template <typename T>
   static T* P_(uintptr_t p) { return reinterpret_cast<T*>(p); }
 };
@@ -408,6 +433,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("fh_counters", &MlpStep::fh_counters)
       .def_readwrite("fh_tiles", &MlpStep::fh_tiles)
       .def_readwrite("no_gemm_z2", &MlpStep::no_gemm_z2)
+      .def("tp_forward", &MlpStep::tp_forward)
+      .def("tp_head", &MlpStep::tp_head)
       .def_readwrite("shift", &MlpStep::shift)
       .def_readwrite("act", &MlpStep::act)
       .def_readwrite("split", &MlpStep::split)

@@ -179,3 +179,20 @@ def xgmi_spawn_main(out_dir, world):
     from cme213_sp18_amd.parallel.launcher import spawn
 
     spawn(xgmi_worker, world, (out_dir,), backend="gloo")
+
+
+def tp_train_worker(rank, world, comm, device, out_dir, H, N, B, E, lr, reg, dtype):
+    """Hidden-sharded (tensor parallel) training over gloo; saves the gathered full params + losses."""
+    import numpy as np
+
+    from cme213_sp18_amd import NeuralNetwork
+    from cme213_sp18_amd.parallel import TensorParallelTrainer
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    x, y = synthetic_mnist(N, seed=11)
+    nn = NeuralNetwork([784, H, 10])
+    tr = TensorParallelTrainer(nn, comm=comm, device="cpu", dtype=dtype, batch_size=B, backend="torch")
+    tr.load(x, y)
+    st = tr.train(E, lr, reg, print_every=2, log=lambda *_: None)
+    np.savez(os.path.join(out_dir, f"tp{rank}.npz"), W0=nn.W[0], W1=nn.W[1], b0=nn.b[0], b1=nn.b[1],
+             losses=np.array(st.losses), pred=tr.predict(x[:200]))
