@@ -26,7 +26,7 @@ import torch
 from ..utils.common import ulp_distance
 from ._dev import EventTimer, host, kernels, require_cuda, stream_handle
 
-VARIANTS = {"global": 0, "block": 1, "shared": 2}
+VARIANTS = {"global": 0, "block": 1, "shared": 2, "vec": 3}
 MAX_ULPS = 512  # main.cu:229
 
 

@@ -8,6 +8,8 @@
 //                      2b+1-tall column window in registers (1 new load per row)
 //   variant 2 lds    : (64 x 16) tile + b-wide halo staged in LDS, every
 //                      stencil read served from LDS
+//   variant 3 vec    : 4 x-points per lane with 16-byte loads/stores + the
+//                      register column window (fewest instructions per byte)
 #include <algorithm>
 
 #include "../common/hip_common.h"
@@ -90,7 +92,64 @@ __device__ __forceinline__ void stencil_loop_body(float* __restrict__ next, cons
   }
 }
 
+// variant 3 "vec": 4 consecutive x points per lane (16-byte loads / stores), ROWS rows per thread with
+// the (2B+1)-tall float4 column window in registers; the x-neighbours of the centre row come from the
+// two adjacent float4s (B <= 4).  A wave covers 256 consecutive floats of a row (1 KB per instruction).
+// Loads are buffer loads range-checked against the whole grid (4-byte aligned, any B): nothing past
+// the allocation is touched and the interior-only stores are masked per element at the right edge.
+__device__ __forceinline__ f32x4 ld4(__amdgpu_buffer_rsrc_t r, int64_t elem) {
+  const auto w = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(elem * 4), 0, 0);
+  return __builtin_bit_cast(f32x4, w);
+}
+
+template <int ORDER, int ROWS>
+__device__ __forceinline__ void stencil_vec_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
+                                                 int gy, int nx, int ny, float xcfl, float ycfl, int bx, int by) {
+  constexpr int B = Coef<ORDER>::B;
+  constexpr int WIN = 2 * B + 1;
+  const int x0 = (bx * 64 + threadIdx.x) * 4;  // first of this lane's 4 interior x
+  const int y0 = (by * 4 + threadIdx.y) * ROWS;
+  if (x0 >= nx || y0 >= ny) return;
+  const __amdgpu_buffer_rsrc_t rc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(curr), (short)0, (int)((int64_t)gx * gy * 4), 0x00020000);
+  const int64_t col = x0 + B;
+  f32x4 win[WIN];
+#pragma unroll
+  for (int k = 0; k < WIN - 1; ++k) win[k] = ld4(rc, (int64_t)(y0 + k) * gx + col);
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    const int y = y0 + r;
+    if (y >= ny) break;
+    const int64_t rowc = (int64_t)(y + B) * gx + col;
+    win[WIN - 1] = ld4(rc, (int64_t)(y + 2 * B) * gx + col);
+    const f32x4 lf = ld4(rc, rowc - 4), rt = ld4(rc, rowc + 4);
+    float line[12];  // x = x0 + B - 4 .. x0 + B + 7
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      line[j] = lf[j];
+      line[4 + j] = win[B][j];
+      line[8 + j] = rt[j];
+    }
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = apply_stencil<ORDER>(
+          line[4 + j], [&](int k) { return line[4 + j + k]; }, [&](int k) { return win[B + k][j]; }, xcfl, ycfl);
+    float* dst = next + rowc;
+    if (x0 + 4 <= nx && (rowc & 3) == 0) {
+      *reinterpret_cast<f32x4*>(dst) = o;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (x0 + j < nx) dst[j] = o[j];
+    }
+#pragma unroll
+    for (int k = 0; k < WIN - 1; ++k) win[k] = win[k + 1];
+  }
+}
+
 constexpr int kTX = 64, kTY = 16;
+constexpr int kVecRows = 8;
 
 template <int ORDER>
 __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
@@ -161,7 +220,8 @@ __global__ __launch_bounds__(256) void stencil_fused(float* __restrict__ next, c
   const int bx = id % nbx, by = id / nbx;
   if constexpr (VARIANT == 0) stencil_global_body<ORDER>(next, curr, gx, nx, ny, xcfl, ycfl, bx, by);
   else if constexpr (VARIANT == 1) stencil_loop_body<ORDER, 8>(next, curr, gx, nx, ny, xcfl, ycfl, bx, by);
-  else stencil_lds_body<ORDER>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by);
+  else if constexpr (VARIANT == 2) stencil_lds_body<ORDER>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by);
+  else stencil_vec_body<ORDER, kVecRows>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by);
 }
 
 template <int ORDER, int VARIANT>
@@ -169,8 +229,9 @@ void launch_v(float* next, const float* curr, int gx, int gy, float xcfl, float 
               hipStream_t s) {
   constexpr int B = Coef<ORDER>::B;
   const int nx = gx - 2 * B, ny = gy - 2 * B;
-  const int rows_per_block = VARIANT == 0 ? 4 : (VARIANT == 1 ? 4 * 8 : kTY);
-  const int nbx = (nx + 63) / 64, nby = (ny + rows_per_block - 1) / rows_per_block;
+  const int rows_per_block = VARIANT == 0 ? 4 : (VARIANT == 1 ? 4 * 8 : (VARIANT == 2 ? kTY : 4 * kVecRows));
+  const int cols_per_block = VARIANT == 3 ? 256 : 64;
+  const int nbx = (nx + cols_per_block - 1) / cols_per_block, nby = (ny + rows_per_block - 1) / rows_per_block;
   const int nint = nbx * nby;
   const int64_t bc_cells_total = 2 * ((int64_t)gx * B + (int64_t)(gy - 2 * B) * B);
   const int nbc = with_bc ? (int)std::min<int64_t>((bc_cells_total + 255) / 256, 1024) : 0;
@@ -183,7 +244,8 @@ void launch(float* next, const float* curr, int gx, int gy, float xcfl, float yc
             bool with_bc, hipStream_t s) {
   if (variant == 0) launch_v<ORDER, 0>(next, curr, gx, gy, xcfl, ycfl, scale, with_bc, s);
   else if (variant == 1) launch_v<ORDER, 1>(next, curr, gx, gy, xcfl, ycfl, scale, with_bc, s);
-  else launch_v<ORDER, 2>(next, curr, gx, gy, xcfl, ycfl, scale, with_bc, s);
+  else if (variant == 2) launch_v<ORDER, 2>(next, curr, gx, gy, xcfl, ycfl, scale, with_bc, s);
+  else launch_v<ORDER, 3>(next, curr, gx, gy, xcfl, ycfl, scale, with_bc, s);
 }
 
 }  // namespace
@@ -195,7 +257,8 @@ void stencil_step(float* next, const float* curr, int gx, int gy, int order, flo
 
 void stencil_step_bc(float* next, const float* curr, int gx, int gy, int order, float xcfl, float ycfl, int variant,
                      float scale, bool with_bc, hipStream_t s) {
-  CME_REQUIRE(variant >= 0 && variant <= 2, "stencil_step: variant 0 (global), 1 (loop), 2 (lds)");
+  CME_REQUIRE(variant >= 0 && variant <= 3, "stencil_step: variant 0 (global), 1 (loop), 2 (lds), 3 (vec)");
+  CME_REQUIRE((int64_t)gx * gy * 4 < (int64_t)0x7FFFFFF0, "stencil_step: grid too large for 32-bit buffer offsets");
   switch (order) {
     case 2: launch<2>(next, curr, gx, gy, xcfl, ycfl, variant, scale, with_bc, s); break;
     case 4: launch<4>(next, curr, gx, gy, xcfl, ycfl, variant, scale, with_bc, s); break;

@@ -71,9 +71,9 @@ def test_pagerank_gpu(variant, nodes, edges):
 
 
 # ------------------------------------------------------------------ hw3
-@pytest.mark.parametrize("variant", ["global", "block", "shared"])
+@pytest.mark.parametrize("variant", ["global", "block", "shared", "vec"])
 @pytest.mark.parametrize("order", [2, 4, 8])
-@pytest.mark.parametrize("shape", [(64, 64), (257, 131), (1000, 77)])
+@pytest.mark.parametrize("shape", [(64, 64), (257, 131), (1000, 77), (1023, 5)])
 def test_stencil_gpu(variant, order, shape):
     p = hw3.SimParams(shape[0], shape[1], 1.0, 1.0, 20, order)
     g0 = hw3.init_grid(p)
