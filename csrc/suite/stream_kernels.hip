@@ -63,41 +63,63 @@ __global__ void pagerank_kernel(const uint32_t* __restrict__ indptr, const uint3
 }
 
 // ------------------------------------------------------------ even/odd sum
+// Streaming reduction: every thread keeps UNR independent 16-byte loads in flight per iteration
+// (contiguous chunk of the array per workgroup, coalesced across the wave) and accumulates the
+// total and the odd sum (even = total - odd: one masked add per element instead of a branch);
+// wave shuffles + one atomic per workgroup and value.
+constexpr int kSumUnr = 4;
+
 __global__ __launch_bounds__(256) void sum_even_odd_kernel(const uint32_t* __restrict__ v, int64_t n,
                                                            unsigned long long* __restrict__ sums) {
-  unsigned long long e = 0, o = 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long tot = 0, odd = 0;
   const int64_t n4 = n / 4;
   const uint4* v4 = reinterpret_cast<const uint4*>(v);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (kSumUnr - 1) * stride < n4; i += kSumUnr * stride) {
+    uint4 w[kSumUnr];
+#pragma unroll
+    for (int u = 0; u < kSumUnr; ++u) w[u] = v4[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < kSumUnr; ++u) {
+      const uint32_t x[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        tot += x[q];
+        odd += x[q] & (0u - (x[q] & 1u));
+      }
+    }
+  }
+  for (; i < n4; i += stride) {
     const uint4 w = v4[i];
     const uint32_t x[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const unsigned long long val = x[q];
-      if (x[q] & 1u) o += val;
-      else e += val;
+      tot += x[q];
+      odd += x[q] & (0u - (x[q] & 1u));
     }
   }
-  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    if (v[i] & 1u) o += v[i];
-    else e += v[i];
+  for (int64_t j = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+    tot += v[j];
+    odd += v[j] & (0u - (v[j] & 1u));
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
-    e += __shfl_xor(e, off, 64);
-    o += __shfl_xor(o, off, 64);
+    tot += __shfl_xor(tot, off, 64);
+    odd += __shfl_xor(odd, off, 64);
   }
   __shared__ unsigned long long part[2][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
-    part[0][wave] = e;
-    part[1][wave] = o;
+    part[0][wave] = tot;
+    part[1][wave] = odd;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(&sums[0], part[0][0] + part[0][1] + part[0][2] + part[0][3]);
-    atomicAdd(&sums[1], part[1][0] + part[1][1] + part[1][2] + part[1][3]);
+    const unsigned long long t = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+    const unsigned long long o = part[1][0] + part[1][1] + part[1][2] + part[1][3];
+    atomicAdd(&sums[0], t - o);
+    atomicAdd(&sums[1], o);
   }
 }
 
@@ -138,7 +160,8 @@ void sum_even_odd(const uint32_t* v, int64_t n, unsigned long long* sums, hipStr
   HIP_CHECK(hipMemsetAsync(sums, 0, 2 * sizeof(unsigned long long), s));
   if (n <= 0) return;
   CME_REQUIRE((reinterpret_cast<uintptr_t>(v) & 15) == 0, "sum_even_odd: input must be 16-byte aligned");
-  const int grid = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256 + 1);
+  // 4 workgroups per CU, each thread kSumUnr 16-byte loads in flight
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n / 4 + 256 * kSumUnr - 1) / (256 * kSumUnr)));
   sum_even_odd_kernel<<<grid, 256, 0, s>>>(v, n, sums);
   CME_LAUNCH_CHECK(s);
 }
