@@ -90,11 +90,15 @@ def cmd_radix(a):
         srt = hw1.GpuRadixSorter(a.n)
         w = d.clone()
         srt.sort_(w)
-        w.copy_(d)
-        with EventTimer() as t:
-            srt.sort_(w)
-        res.update(gpu_ms=t.ms, gpu_ok=bool(np.array_equal(w.cpu().numpy().view(np.uint32), ref)),
-                   gpu_mkeys_per_s=a.n / (t.ms * 1e-3) / 1e6)
+        reps = 10  # device time per sort, averaged (each rep re-sorts a fresh copy; the copies are timed apart)
+        ms = 0.0
+        for _ in range(reps):
+            w.copy_(d)
+            with EventTimer() as t:
+                srt.sort_(w)
+            ms += t.ms / reps
+        res.update(gpu_ms=ms, gpu_ok=bool(np.array_equal(w.cpu().numpy().view(np.uint32), ref)),
+                   gpu_mkeys_per_s=a.n / (ms * 1e-3) / 1e6)
     except SystemExit:
         pass
     print(json.dumps(res))

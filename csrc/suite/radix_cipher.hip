@@ -25,22 +25,163 @@ constexpr int kRTile = kRT * kRItems;
 
 int64_t radix_tiles(int64_t n) { return (n + kRTile - 1) / kRTile; }
 
+// Pass structure (one 8-bit digit): hist -> scan -> scatter, three launches.
+//   hist    : per 4096-key tile an LDS histogram, written digit-major counts[d][tile]; the per-digit
+//             totals are accumulated with one atomic per (tile, digit) into totals[d]
+//   scan    : one workgroup per digit: base(d) = sum of totals[0..d) (block reduction), then an
+//             exclusive block scan of counts[d][0..tiles) + base -- 256 workgroups in parallel instead
+//             of one workgroup walking 256 x tiles values
+//   scatter : the tile is first sorted by digit IN LDS (stable: 16 rounds of 256 keys, ballot-ranked
+//             within a wave, per-wave digit counts prefix-summed across waves), then written out so
+//             that consecutive threads write consecutive keys of one digit run -- coalesced stores
+//             instead of one scattered 4-byte store per key.
 __global__ __launch_bounds__(kRT) void radix_hist_kernel(const uint32_t* __restrict__ keys, int64_t n, int shift,
-                                                         uint32_t* __restrict__ counts, int64_t tiles) {
+                                                         uint32_t* __restrict__ counts, int64_t tiles,
+                                                         uint32_t* __restrict__ totals) {
   __shared__ uint32_t h[256];
   h[threadIdx.x] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kRTile;
+  uint32_t k[kRItems];
 #pragma unroll
   for (int j = 0; j < kRItems; ++j) {
     const int64_t i = base + j * kRT + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    k[j] = i < n ? keys[i] : 0u;
   }
+#pragma unroll
+  for (int j = 0; j < kRItems; ++j)
+    if (base + j * kRT + threadIdx.x < n) atomicAdd(&h[(k[j] >> shift) & 255u], 1u);
   __syncthreads();
-  counts[(int64_t)threadIdx.x * tiles + blockIdx.x] = h[threadIdx.x];  // digit-major
+  const uint32_t c = h[threadIdx.x];
+  counts[(int64_t)threadIdx.x * tiles + blockIdx.x] = c;  // digit-major
+  if (c) atomicAdd(&totals[threadIdx.x], c);
 }
 
-// exclusive scan of `a` (length L) in place, single workgroup of 1024 threads
+// block-wide exclusive scan of one value per thread (256 threads); returns the exclusive prefix,
+// *total = sum over the block
+__device__ __forceinline__ uint32_t block_exscan256(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (int w = 0; w < wave; ++w) pre += sh[w];
+  *total = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return pre + x - v;
+}
+
+__global__ __launch_bounds__(kRT) void radix_scan_kernel(uint32_t* __restrict__ counts, int64_t tiles,
+                                                         const uint32_t* __restrict__ totals) {
+  __shared__ uint32_t sh[4];
+  const int d = blockIdx.x, t = threadIdx.x;
+  uint32_t tot;
+  const uint32_t pre = block_exscan256(totals[t], sh, &tot);
+  __shared__ uint32_t s_base;
+  if (t == d) s_base = pre;  // exclusive prefix of digit d over the digit totals
+  __syncthreads();
+  uint32_t run = s_base;
+  uint32_t* row = counts + (int64_t)d * tiles;
+  for (int64_t c0 = 0; c0 < tiles; c0 += 4 * kRT) {  // 4 consecutive tiles per thread per round
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t i = c0 + (int64_t)t * 4 + q;
+      v[q] = i < tiles ? row[i] : 0u;
+      s += v[q];
+    }
+    uint32_t rtot;
+    uint32_t ex = block_exscan256(s, sh, &rtot) + run;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t i = c0 + (int64_t)t * 4 + q;
+      if (i < tiles) row[i] = ex;
+      ex += v[q];
+    }
+    run += rtot;
+  }
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  const int lane = threadIdx.x & 63;
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+__global__ __launch_bounds__(kRT) void radix_scatter_kernel(const uint32_t* __restrict__ in,
+                                                            uint32_t* __restrict__ out, int64_t n, int shift,
+                                                            const uint32_t* __restrict__ offsets, int64_t tiles) {
+  __shared__ uint32_t sorted[kRTile];
+  __shared__ uint32_t loc[256];    // tile-local exclusive offset of each digit
+  __shared__ uint32_t glob[256];   // global offset of this tile's first key of each digit
+  __shared__ uint32_t run[256];    // keys of each digit placed so far (tile-local)
+  __shared__ uint32_t wcnt[4][256];
+  __shared__ uint32_t sh[4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kRTile;
+  const int cnt = (int)std::min<int64_t>(kRTile, n - base);
+  uint32_t k[kRItems];
+#pragma unroll
+  for (int j = 0; j < kRItems; ++j) {
+    const int64_t i = base + j * kRT + t;
+    k[j] = i < n ? in[i] : 0u;
+  }
+  // tile-local digit histogram -> exclusive offsets
+  run[t] = 0;
+  glob[t] = offsets[(int64_t)t * tiles + blockIdx.x];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRItems; ++j)
+    if (j * kRT + t < cnt) atomicAdd(&run[(k[j] >> shift) & 255u], 1u);
+  __syncthreads();
+  uint32_t tot;
+  loc[t] = block_exscan256(run[t], sh, &tot);
+  run[t] = 0;
+  __syncthreads();
+  // stable rank of every key inside the tile: rounds of 256 keys in index order
+  for (int j = 0; j < kRItems; ++j) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) wcnt[w][t] = 0;
+    __syncthreads();
+    const bool valid = j * kRT + t < cnt;
+    const uint32_t d = (k[j] >> shift) & 255u;
+    unsigned long long match = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const bool set = (d >> bit) & 1u;
+      const unsigned long long bal = __ballot(set);
+      match &= set ? bal : ~bal;
+    }
+    const int rank = __popcll(match & lanemask_lt());
+    if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(match);  // group leader
+    __syncthreads();
+    if (valid) {
+      uint32_t before = 0;
+      for (int w = 0; w < wave; ++w) before += wcnt[w][d];
+      sorted[loc[d] + run[d] + before + rank] = k[j];
+    }
+    __syncthreads();
+    run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+  }
+  __syncthreads();
+  // write-out in tile order: consecutive threads -> consecutive keys of the same digit run
+#pragma unroll
+  for (int j = 0; j < kRItems; ++j) {
+    const int p = j * kRT + t;
+    if (p < cnt) {
+      const uint32_t key = sorted[p];
+      const uint32_t d = (key >> shift) & 255u;
+      out[glob[d] + (p - loc[d])] = key;
+    }
+  }
+}
+
+// exclusive scan of `a` (length L) in place, single workgroup of 1024 threads (small arrays: the
+// cipher's per-block counts)
 __global__ __launch_bounds__(1024) void scan_exclusive_kernel(uint32_t* __restrict__ a, int64_t L) {
   __shared__ uint32_t part[1024];
   const int t = threadIdx.x;
@@ -61,48 +202,6 @@ __global__ __launch_bounds__(1024) void scan_exclusive_kernel(uint32_t* __restri
     const uint32_t v = a[i];
     a[i] = run;
     run += v;
-  }
-}
-
-__device__ __forceinline__ unsigned long long lanemask_lt() {
-  const int lane = threadIdx.x & 63;
-  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
-}
-
-__global__ __launch_bounds__(kRT) void radix_scatter_kernel(const uint32_t* __restrict__ in,
-                                                            uint32_t* __restrict__ out, int64_t n, int shift,
-                                                            const uint32_t* __restrict__ offsets, int64_t tiles) {
-  __shared__ uint32_t run[256];
-  __shared__ uint32_t wcnt[4][256];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  run[t] = offsets[(int64_t)t * tiles + blockIdx.x];
-  const int64_t base = (int64_t)blockIdx.x * kRTile;
-  for (int j = 0; j < kRItems; ++j) {
-#pragma unroll
-    for (int w = 0; w < 4; ++w) wcnt[w][t] = 0;
-    __syncthreads();
-    const int64_t i = base + j * kRT + t;
-    const bool valid = i < n;
-    const uint32_t key = valid ? in[i] : 0u;
-    const uint32_t d = (key >> shift) & 255u;
-    unsigned long long match = __ballot(valid);
-#pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
-      const bool set = (d >> bit) & 1u;
-      const unsigned long long bal = __ballot(set);
-      match &= set ? bal : ~bal;
-    }
-    const int rank = __popcll(match & lanemask_lt());
-    if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(match);  // group leader
-    __syncthreads();
-    if (valid) {
-      uint32_t before = 0;
-      for (int w = 0; w < wave; ++w) before += wcnt[w][d];
-      out[run[d] + before + rank] = key;
-    }
-    __syncthreads();
-    run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-    __syncthreads();
   }
 }
 
@@ -239,15 +338,18 @@ __global__ __launch_bounds__(256) void residue_hist_kernel(const uint8_t* __rest
 }  // namespace
 
 // ---------------------------------------------------------------- radix API
-int64_t radix_workspace_bytes(int64_t n) { return (int64_t)256 * std::max<int64_t>(1, radix_tiles(n)) * 4; }
+// counts [256][tiles] + totals [256]
+int64_t radix_workspace_bytes(int64_t n) { return ((int64_t)256 * std::max<int64_t>(1, radix_tiles(n)) + 256) * 4; }
 
 void radix_pass_u32(const uint32_t* in, uint32_t* out, int64_t n, int start_bit, void* ws, hipStream_t s) {
   if (n <= 0) return;
   CME_REQUIRE(n < (int64_t)1 << 32, "radix_pass_u32: n must fit in 32 bits");
   const int64_t tiles = radix_tiles(n);
   uint32_t* counts = static_cast<uint32_t*>(ws);
-  radix_hist_kernel<<<(unsigned)tiles, kRT, 0, s>>>(in, n, start_bit, counts, tiles);
-  scan_exclusive_kernel<<<1, 1024, 0, s>>>(counts, 256 * tiles);
+  uint32_t* totals = counts + 256 * tiles;
+  HIP_CHECK(hipMemsetAsync(totals, 0, 256 * sizeof(uint32_t), s));
+  radix_hist_kernel<<<(unsigned)tiles, kRT, 0, s>>>(in, n, start_bit, counts, tiles, totals);
+  radix_scan_kernel<<<256, kRT, 0, s>>>(counts, tiles, totals);
   radix_scatter_kernel<<<(unsigned)tiles, kRT, 0, s>>>(in, out, n, start_bit, counts, tiles);
   CME_LAUNCH_CHECK(s);
 }
