@@ -171,7 +171,7 @@ class MlpEngine:
         if self.backend == "hip" and self.np and H <= 128 and os.environ.get("CME_HEAD_PARTIALS") == "1":
             self.gpart = torch.zeros(nblk * (C * H + H + C), dtype=torch.float32, device=dev)
         self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
-        # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one monotonic uint32
+        # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
         # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
         # (CME_SEPARATE_HEAD=1: the two-launch form, for A/B measurements)
         self.fh_counters = None

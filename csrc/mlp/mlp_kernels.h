@@ -70,7 +70,7 @@ void mlp_lookahead_l2(const SplitStepArgs& f, float* Aout, const HeadArgs& h, bo
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t stream);
 // split path, H <= 128: forward GEMM (a1 = sigmoid(W1 X + b1), f) and the train-mode head (h, same a1) in
 // ONE launch -- the last workgroup of every 32-column tile runs the head for it.  counters: >= max_tiles
-// zero-initialised uint32 (one per 32-column tile, monotonic across launches).
+// zero-initialised uint32 (one per 32-column tile; each launch leaves them at 0 again).
 bool mlp_fwd1_head_ok(const SplitStepArgs& f, const HeadArgs& h);
 void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters, int max_tiles, hipStream_t s);
 int mlp_head_num_blocks(int n);

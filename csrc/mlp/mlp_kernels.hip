@@ -622,8 +622,8 @@ bool head32_ok(const HeadArgs& a) {
 // ------------------------------------- forward GEMM + head in ONE launch (split path, H <= 128)
 // Workgroups compute 16x32 tiles of a1 = sigmoid(W1 X + b1) exactly as fwd1_split_kernel does, but
 // store them write-through (sc1).  Per 32-column tile, the tm row-tile workgroups each add 1 to a
-// monotonic counter after all their stores drained; the workgroup whose add completes the tile
-// (old + 1 == 0 mod tm) runs the head for those 32 columns (two 256-thread head blocks) with sc1
+// counter after all their stores drained; the workgroup whose add completes the tile (old + 1 == tm)
+// re-arms the counter to 0 and runs the head for those 32 columns (two 256-thread head blocks) with sc1
 // loads of a1.  This is the "last arriver" hand-off of MI355X_MICROARCH.md (sc1 stores, vmcnt(0) in
 // every storing wave, barrier, one agent-scope add per workgroup, sc1 loads; no fences), and it
 // removes the head launch and its kernel boundary from the step (reference: gpuFeedforward +
@@ -677,7 +677,10 @@ __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArg
   stamp(1);
   if (threadIdx.x == 0) {
     const unsigned old = __hip_atomic_fetch_add(counters + ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (old + 1u) % (unsigned)tm == 0u;
+    s_last = old + 1u == (unsigned)tm;
+    // the last arriver re-arms the tile's counter for the next launch (every other workgroup of this tile
+    // has already added; the next launch starts after this one ends) -- no wrap-around after 2^32 adds
+    if (s_last) __hip_atomic_store(counters + ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   stamp(2);

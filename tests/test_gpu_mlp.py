@@ -315,6 +315,8 @@ def test_fwd1_head_single_launch_matches_two_launches(dtype, H, n):
             e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True, with_loss=step == 3)
         torch.cuda.synchronize()
         outs.append([t.clone().cpu() for t in (e.a1, e.D, e.dZ1, e.dZ1p, e.params)] + [e.loss_sum()])
+        if single:  # the last arriver of every tile re-arms its counter
+            assert int(e.fh_counters.abs().sum()) == 0
     a, b = outs
     for ta, tb in zip(a[:-1], b[:-1]):
         assert torch.equal(ta, tb)
