@@ -46,6 +46,7 @@ class TrainConfig:
     ckpt_every: int = 0         # epochs between checkpoints (needs --ckpt-dir); 0 = only at the end
     profile: bool = False       # per-phase event timing + roctx ranges (eager steps), summary at the end
     overlap_chunks: int = 0     # RCCL path: dW1 all-reduce row chunks overlapped with the backward (0 = auto)
+    parallel: str = "dp"        # dp (reference scheme) | tp (hidden-dimension tensor parallel, wide layers)
 
     @property
     def H(self):
@@ -108,6 +109,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--profile", action="store_true", default=None,
                     help="time forward+head / weight gradients / all-reduce / SGD per step (eager) and emit roctx "
                          "ranges for rocprofv3 --marker-trace")
+    ap.add_argument("--parallel", choices=["dp", "tp"],
+                    help="dp: data parallel (default); tp: shard the hidden layer over the ranks (one z2 all-reduce "
+                         "per step, every rank runs the whole global batch)")
     ap.add_argument("--overlap-chunks", type=int,
                     help="RCCL path: number of dW1 row chunks all-reduced while the backward runs (0 = auto)")
     return ap

@@ -58,6 +58,9 @@ class TensorParallelTrainer:
             self._z2part = e.z2buf
         self.iter = 0
         self._graphs: dict = {}
+        self.use_graphs = True
+        self.profiler = None
+        self.allreduce_impl = f"z2 all-reduce ({self.comm.name})" if self.R > 1 else "none"
 
     # ------------------------------------------------------------------ params
     def _set_shard(self, W1, b1, W2, b2):
@@ -205,7 +208,13 @@ class TensorParallelTrainer:
                 self.step(s, ln, lr, reg)
 
     # ------------------------------------------------------------------- train
-    def train(self, epochs: int, lr: float, reg: float, print_every: int = 0, log=print) -> TrainStats:
+    def train(self, epochs: int, lr: float, reg: float, print_every: int = 0, debug: bool = False,
+              outdir: str = "Outputs", log=print, on_event=None, fault=None) -> TrainStats:
+        """Training loop with the data-parallel trainer's interface (loss every ``print_every`` steps,
+        JSON-lines epoch events, ``fault=(rank, step)`` injection); graph-replayed epochs when no loss is
+        printed.  ``debug`` (the reference's per-iteration CPU diff) is data-parallel only."""
+        from .trainer import FaultInjected
+
         stats = TrainStats()
         plan = self.epoch_plan()
         dev = self.engine.device
@@ -214,17 +223,36 @@ class TensorParallelTrainer:
         self.comm.barrier()
         t0 = time.perf_counter()
         for epoch in range(epochs):
-            for s, ln in plan.steps:
-                if print_every > 0 and self.iter % print_every == 0:
-                    l = self.step_loss(s, ln, lr, reg)
-                    stats.losses.append(l)
-                    if self.rank == 0:
-                        log(f"Loss at iteration {self.iter} of epoch {epoch}/{epochs} = {l:.10g}")
-                else:
-                    self.step(s, ln, lr, reg)
-                self.iter += 1
-                stats.steps += 1
-                stats.images += ln
+            if fault is not None and fault[0] == self.rank and self.iter <= fault[1] < self.iter + len(plan.steps):
+                raise FaultInjected(f"injected fault on rank {self.rank} at step {fault[1]}")
+            if print_every <= 0 and self.profiler is None:
+                self.run_plan(plan, lr, reg, use_graphs=self.use_graphs)
+                self.iter += len(plan.steps)
+                stats.steps += len(plan.steps)
+                stats.images += sum(ln for _, ln in plan.steps)
+            else:
+                for s, ln in plan.steps:
+                    if print_every > 0 and self.iter % print_every == 0:
+                        l = self.step_loss(s, ln, lr, reg)
+                        stats.losses.append(l)
+                        if self.rank == 0:
+                            log(f"Loss at iteration {self.iter} of epoch {epoch}/{epochs} = {l:.10g}")
+                        if on_event is not None:
+                            on_event({"event": "loss", "iter": self.iter, "epoch": epoch, "loss": l})
+                    elif self.profiler is not None:
+                        with self.profiler.phase("step"):
+                            self.step(s, ln, lr, reg)
+                    else:
+                        self.step(s, ln, lr, reg)
+                    self.iter += 1
+                    stats.steps += 1
+                    stats.images += ln
+            if on_event is not None:
+                if dev.type == "cuda":
+                    torch.cuda.synchronize(dev)
+                el = time.perf_counter() - t0
+                on_event({"event": "epoch", "epoch": epoch, "iter": self.iter, "seconds": el,
+                          "images_per_s": stats.images / el if el > 0 else None})
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         self.comm.barrier()
@@ -232,10 +260,19 @@ class TensorParallelTrainer:
         self.sync_to(self.nn)
         return stats
 
+    def enable_profiling(self, roctx: bool = True):
+        """Per-step timing (eager steps) + roctx ranges; returns the PhaseTimer."""
+        from ..utils.tracing import PhaseTimer, Roctx
+
+        dev = self.engine.device if self.engine.device.type == "cuda" else None
+        self.profiler = PhaseTimer(dev, Roctx(True) if roctx else None)
+        return self.profiler
+
     def predict(self, x) -> np.ndarray:
-        """Argmax labels with the gathered full model (call after train / sync_to)."""
+        """Argmax labels with the full model in ``self.nn`` (gathered by train() / sync_to() on every rank,
+        so this needs no collective and may run on one rank only)."""
         e = self.engine
         full = MlpEngine((self.P, self.H, self.C), dtype=e.dtype, max_cols=min(4096, max(1, len(x))),
                          device=e.device, backend=e.backend, shift=e.shift)
-        full.set_params(*self.gather_params())
+        full.set_params(*self.nn.params)
         return full.predict(x)

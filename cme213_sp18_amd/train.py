@@ -109,10 +109,21 @@ def run(cfg: TrainConfig) -> dict:
             log0(rank, f"Precision on validation set for sequential training = {out['seq_dev_precision']}")
         comm.barrier()  # the parallel run's debug diff reads the CPU snapshots
         log0(rank, "\nStart Parallel Training")
-        tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,
-                                 backend=backend, shift=cfg.softmax_shift, use_graphs=cfg.use_graphs,
-                                 normalize=cfg.normalize, path=cfg.path, allreduce=cfg.allreduce,
-                                 overlap_chunks=cfg.overlap_chunks)
+        if cfg.parallel == "tp":
+            from .parallel.tensor_parallel import TensorParallelTrainer
+
+            if cfg.debug:
+                log0(rank, "note: -d (per-iteration CPU diff) is data-parallel only; ignored with --parallel tp")
+                cfg.debug = False
+            tr = TensorParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,
+                                       backend=backend, shift=cfg.softmax_shift, normalize=cfg.normalize,
+                                       path=cfg.path)
+            tr.use_graphs = cfg.use_graphs
+        else:
+            tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,
+                                     backend=backend, shift=cfg.softmax_shift, use_graphs=cfg.use_graphs,
+                                     normalize=cfg.normalize, path=cfg.path, allreduce=cfg.allreduce,
+                                     overlap_chunks=cfg.overlap_chunks)
         tr.load(ds.x_train, ds.y_train)
         if cfg.profile:
             tr.enable_profiling()

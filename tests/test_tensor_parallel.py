@@ -70,3 +70,25 @@ def test_loopback_tp_world4_and_divisibility():
     with pytest.raises(ValueError):
         TensorParallelTrainer(NeuralNetwork([784, 30, 10]), comm=LoopbackComm.create(4)[0], device="cpu",
                               dtype="f64", backend="torch")
+
+
+def test_cli_tensor_parallel_gloo(tmp_path):
+    """python -m torch.distributed.run ... cme213_sp18_amd.train --parallel tp on 2 CPU ranks (gloo):
+    trains, prints the loss, predicts on rank 0 only (no collective) and exits cleanly."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    port = 29000 + (os.getpid() * 7) % 2000
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "cme213_sp18_amd.train",
+                        "--parallel", "tp", "--preset", "cpu_plumbing", "-n", "16", "-e", "1", "-p", "1",
+                        "--num-train", "1700", "--num-test", "100", "--outdir", str(tmp_path / "Outputs")],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "Loss at iteration 0" in r.stdout
+    out = json.loads([line for line in r.stdout.splitlines() if line.startswith("{")][-1])
+    assert out["allreduce"].startswith("z2 all-reduce") and 0.0 <= out["par_dev_precision"] <= 1.0
