@@ -107,6 +107,10 @@ def main(argv=None) -> int:
             print(f"warning: HIP graph capture failed ({ex!r}); running eager steps", file=sys.stderr)
             tr.use_graphs = False
             tr._graphs.clear()
+    # every rank done capturing before the first warm-up step: with the xGMI all-reduce a step waits
+    # (bounded) for its peers' same step, so a rank still capturing would count against that bound
+    torch.cuda.synchronize(device)
+    comm.barrier()
     for p in warm_plans:
         tr.run_plan(p, lr, reg)
     torch.cuda.synchronize(device)
