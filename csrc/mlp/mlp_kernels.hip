@@ -880,15 +880,18 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
   const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
   float zsum = 0.f;
   {
-    int k = 0;
-    for (; k + 8 <= a.z2_chunks; k += 8) {
-      float v[8];
+    // every partial of this (class, column) in ONE burst of kZ2Burst loads (chunks past z2_chunks read the
+    // range-checked zero) instead of z2_chunks / 8 dependent round trips: 32 chunks at H = 4096 (128-row
+    // forward tiles), 16 at H = 1024.  Summed in chunk order as before (adding the zeros changes no bit).
+    constexpr int kZ2Burst = 32;
+    float v[kZ2Burst];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = buf_load1<float>(rz, zcol < a.n ? (((k + u) * 16 + zc) * ld + zcol) * 4 : kOOB);
+    for (int u = 0; u < kZ2Burst; ++u)
+      v[u] = buf_load1<float>(rz, (zcol < a.n && u < a.z2_chunks) ? ((u * 16 + zc) * ld + zcol) * 4 : kOOB);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) zsum += v[u];
-    }
-    for (; k < a.z2_chunks; ++k) zsum += buf_load1<float>(rz, zcol < a.n ? ((k * 16 + zc) * ld + zcol) * 4 : kOOB);
+    for (int u = 0; u < kZ2Burst; ++u) zsum += v[u];
+    for (int k = kZ2Burst; k < a.z2_chunks; ++k)
+      zsum += buf_load1<float>(rz, zcol < a.n ? ((k * 16 + zc) * ld + zcol) * 4 : kOOB);
   }
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.W2), ra = make_rsrc(a.a1);
   float wv[RT][4], xv[RT][2][4];

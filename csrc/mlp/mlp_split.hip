@@ -404,6 +404,9 @@ struct EpiW1 {
   }
 };
 
+__device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
+                                            uint32_t* s_ep);
+
 template <int NPZ, int VEC>
 __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2, int tc,
                                                           int tcn) {
@@ -460,6 +463,16 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     }
     return;
   }
+  wgrad_roles(a, bid, t1, t2, red, &s_ep);
+}
+
+// The weight-gradient launch's workgroups past its t1 dW1 tiles: the head-partials reduction (gpart), or
+// t2 dW2 tiles (+ the fused xGMI exchange) followed by the bias-row workgroups.  `red`: kWKS * 4 * 64
+// floats of LDS.  Shared by wgrad_split_kernel and wgrad_big_kernel (the wide path's extra workgroups).
+__device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
+                                            uint32_t* s_ep) {
+  const float reg = (float)a.reg, lr = (float)a.lr;
+  const bool fused = a.xf.world > 0;
   if (a.gpart) {  // ---- reduce the head's per-block partials of dW2 | db1 | db2, then update
     const int tot = a.C * a.H + a.H + a.C;
     const int e = (bid - t1) * kWT + threadIdx.x;
@@ -499,7 +512,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     float* gw = a.gW2;
     uint32_t ep = 0;
     if (fused) {
-      ep = xf_begin(a.xf, bid, &s_ep);
+      ep = xf_begin(a.xf, bid, s_ep);
       gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(ep & 1u) * a.xf.npad + a.xf.off_W2;
     }
     EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, fused ? 1 : 0, reg, lr, {}};
@@ -673,9 +686,15 @@ __global__ __launch_bounds__(NT) void fwd1_big_kernel(SplitStepArgs a, int tn) {
 }
 
 template <int BM, int BN, int NPZ, int NT, int NKS = 0>
-__global__ __launch_bounds__(NT) void wgrad_big_kernel(SplitStepArgs a, int tn) {
+__global__ __launch_bounds__(NT) void wgrad_big_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  if ((int)blockIdx.x >= tbig) {  // the dW2 / db2 roles riding in this launch (launched with NT == kWT only)
+    if constexpr (NT == kWT)
+      wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
+                  reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)));
+    return;
+  }
+  const int id = xcd_remap(blockIdx.x, tbig);
   EpiW1Big epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw,
                (float)a.reg, (float)a.lr, a.xscale, a.b1, a.gb1};
   const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
@@ -754,33 +773,35 @@ void launch_fwd1_big(const SplitStepArgs& a, hipStream_t s) {
   else launch_fwd1_big_nt<NP, 256>(a, s);
 }
 
+// t2 / tb > 0: that many dW2-tile / bias-row role workgroups ride in the same launch after the dW1 tiles
 template <int NP, int NT, int NKS>
-void launch_wgrad_big_k(const SplitStepArgs& a, hipStream_t s) {
+void launch_wgrad_big_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int NW = a.P + a.bias_col;
   const int t128 = cdiv(rows, 128) * cdiv(NW, 128);
   if (t128 >= 192) {
     constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
     set_lds_limit<wgrad_big_kernel<128, 128, NP, NT, NKS>>(L);
-    wgrad_big_kernel<128, 128, NP, NT, NKS><<<t128, NT, L, s>>>(a, cdiv(NW, 128));
+    wgrad_big_kernel<128, 128, NP, NT, NKS><<<t128 + t2 + tb, NT, L, s>>>(a, cdiv(NW, 128), t128, t2);
   } else {
     constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
     set_lds_limit<wgrad_big_kernel<64, 64, NP, NT, NKS>>(L);
     const int tn = cdiv(NW, 64);
-    wgrad_big_kernel<64, 64, NP, NT, NKS><<<cdiv(rows, 64) * tn, NT, L, s>>>(a, tn);
+    const int t64 = cdiv(rows, 64) * tn;
+    wgrad_big_kernel<64, 64, NP, NT, NKS><<<t64 + t2 + tb, NT, L, s>>>(a, tn, t64, t2);
   }
 }
 
 template <int NP, int NT>
-void launch_wgrad_big_nt(const SplitStepArgs& a, hipStream_t s) {
-  if (cdiv(a.n, lg::kBK) == 13) launch_wgrad_big_k<NP, NT, 13>(a, s);
-  else launch_wgrad_big_k<NP, NT, 0>(a, s);
+void launch_wgrad_big_nt(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
+  if (cdiv(a.n, lg::kBK) == 13) launch_wgrad_big_k<NP, NT, 13>(a, t2, tb, s);
+  else launch_wgrad_big_k<NP, NT, 0>(a, t2, tb, s);
 }
 
 template <int NP>
-void launch_wgrad_big(const SplitStepArgs& a, hipStream_t s) {
-  if (big_threads() == 512) launch_wgrad_big_nt<NP, 512>(a, s);
-  else launch_wgrad_big_nt<NP, 256>(a, s);
+void launch_wgrad_big(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
+  if (big_threads() == 512) launch_wgrad_big_nt<NP, 512>(a, t2, tb, s);
+  else launch_wgrad_big_nt<NP, 256>(a, 0, 0, s);  // role workgroups need kWT threads
 }
 
 template <int NPW, int NPZ, int NC>
@@ -864,9 +885,20 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   CME_REQUIRE(a.w1_row0 >= 0 && (a.w1_rows < 0 || a.w1_row0 + a.w1_rows <= a.H), "wgrad: bad dW1 row range");
   const bool big = big_wgrad_ok(a) && !big_path_disabled();
   const bool do_w1 = (a.wg_parts & 1) && a.w1_rows != 0, do_roles = (a.wg_parts & 2) != 0;
-  if (big && do_w1) {  // dW1 as a blocked GEMM; dW2 + bias roles stay in the split kernel below (t1 = 0)
-    if (a.npz == 3) launch_wgrad_big<3>(a, s);
-    else launch_wgrad_big<1>(a, s);
+  if (big && do_w1) {  // dW1 as a blocked GEMM
+    // the dW2 / db2 roles ride in the same launch as extra workgroups: one launch and its boundary fewer,
+    // and they run on the CUs the dW1 tiles leave idle (else they follow in the split kernel below, t1 = 0;
+    // CME_NO_ROLE_FOLD=1 for A/B tests)
+    static const bool no_fold = std::getenv("CME_NO_ROLE_FOLD") != nullptr;
+    const bool fold = do_roles && !a.gpart && a.xf.world == 0 && big_threads() == kWT && !no_fold;
+    const int t2f = fold ? cdiv(a.H, 16) : 0;
+    const int tbf = fold ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
+    if (a.npz == 3) launch_wgrad_big<3>(a, t2f, tbf, s);
+    else launch_wgrad_big<1>(a, t2f, tbf, s);
+    if (fold) {
+      CME_LAUNCH_CHECK(s);
+      return;
+    }
   }
   const int w1rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int t1n = cdiv(a.P + a.bias_col, 16 * kWNB), t1 = (big || !do_w1) ? 0 : cdiv(w1rows, 16 * kWMB) * t1n;
