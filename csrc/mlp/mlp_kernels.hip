@@ -871,6 +871,7 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
   __shared__ float zs[16][kHWCols + 1];
   __shared__ float Ds[16][kHWCols + 1];
   __shared__ float ls[kHWCols];
+  __shared__ float ts[8][16][kHWCols + 1];  // per wave: one 16 x 32 dZ1 tile, re-read as 8-column rows
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, c16 = lane & 15, g = lane >> 4;
   const int rb = blockIdx.x % nrb, ct = blockIdx.x / nrb;
   const int H = a.H, C = a.C, ld = a.lda;
@@ -953,37 +954,87 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
   __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
   __hip_bfloat16* dZp = static_cast<__hip_bfloat16*>(a.dZ1_planes);
   const size_t pstride = (size_t)H * a.ldz;
+  float dv[2][4];
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    const int col = ct * kHWCols + cb * 16 + c16;
-    float dv[4];
+  for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dv[i] = Ds[4 * g + i][cb * 16 + c16];
+    for (int i = 0; i < 4; ++i) dv[cb][i] = Ds[4 * g + i][cb * 16 + c16];
+  // The MFMA leaves each lane 4 ROWS of one column; stored straight from there every plane store is a
+  // 2-byte scatter (32-byte row pieces).  The tile goes through this wave's LDS tile instead and comes
+  // back as 8 consecutive columns per lane: one 16-byte store per plane (64-byte row pieces).
+  const int sr = lane >> 2, sc = (lane & 3) * 8;
+  const int scol = ct * kHWCols + sc;
+  const bool vec = a.ldz % 8 == 0;  // 16-byte aligned rows (ld is padded to 16)
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
+  for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
       f32x4 r = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) r = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[rt][i], dv[i], r, 0, 0, 0);
-      if (col >= a.n) continue;
+      for (int i = 0; i < 4; ++i) r = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[rt][i], dv[cb][i], r, 0, 0, 0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int h = row0 + rt * 16 + 4 * g + j;
-        if (h >= H) continue;
         const float x = xv[rt][cb][j];
-        const float dz = r[j] * x * (1.f - x);
-        const size_t zi = (size_t)h * a.ldz + col;
-        if (dZ1) dZ1[zi] = dz;  // nullptr: fp32 dZ1 not needed (planes only)
-        if (dZlo) dZlo[zi] = __float2bfloat16(dz);
+        ts[w][4 * g + j][cb * 16 + c16] = r[j] * x * (1.f - x);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int h = row0 + rt * 16 + sr;
+    if (h < H) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ts[w][sr][sc + u];
+      const size_t zi = (size_t)h * a.ldz + scol;
+      if (vec && scol + 8 <= a.n) {
+        if (dZ1) {  // nullptr: fp32 dZ1 not needed (planes only)
+          *reinterpret_cast<f32x4*>(dZ1 + zi) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(dZ1 + zi + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        }
+        if (dZlo) {
+          __hip_bfloat16 q[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) q[u] = __float2bfloat16(v[u]);
+          uint4 qw;
+          __builtin_memcpy(&qw, q, 16);
+          *reinterpret_cast<uint4*>(dZlo + zi) = qw;
+        }
         if (dZp) {
-          float rr = dz;
           for (int p = 0; p < a.npz; ++p) {
-            const __hip_bfloat16 q = __float2bfloat16(rr);
-            dZp[p * pstride + zi] = q;
-            rr -= __bfloat162float(q);
+            __hip_bfloat16 q[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              q[u] = __float2bfloat16(v[u]);
+              v[u] -= __bfloat162float(q[u]);
+            }
+            uint4 qw;
+            __builtin_memcpy(&qw, q, 16);
+            *reinterpret_cast<uint4*>(dZp + p * pstride + zi) = qw;
+          }
+        }
+      } else {  // ragged last columns / unpadded rows
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (scol + u >= a.n) break;
+          const float dz = v[u];
+          if (dZ1) dZ1[zi + u] = dz;
+          if (dZlo) dZlo[zi + u] = __float2bfloat16(dz);
+          if (dZp) {
+            float rr = dz;
+            for (int p = 0; p < a.npz; ++p) {
+              const __hip_bfloat16 q = __float2bfloat16(rr);
+              dZp[p * pstride + zi + u] = q;
+              rr -= __bfloat162float(q);
+            }
           }
         }
       }
     }
+    // every lane's reads of this tile are done before the next row tile overwrites it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
