@@ -45,3 +45,19 @@ def test_xgmi_fused_wgrad_stress_two_ranks():
                        capture_output=True, text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS="2"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "fused_ranks=2 bad_elements=0" in r.stdout, r.stdout[-2000:]
+
+
+def test_allreduce_bench_two_ranks_shared_gpu(tmp_path):
+    """bench/allreduce_bench.py end to end (xGMI kernel path, 2 ranks sharing the GPU): every size correct."""
+    import json
+
+    out = tmp_path / "ar.json"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29661",
+                        os.path.join(ROOT, "bench", "allreduce_bench.py"), "--paths", "xgmi", "--max-bytes",
+                        str(1 << 20), "--iters", "5", "--json", str(out)],
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, CME_SHARED_GPU="1", OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    recs = json.loads(out.read_text())
+    assert len(recs) >= 5 and all(x["correct"] and x["peer_wait_timeouts"] == 0 for x in recs), recs
