@@ -104,8 +104,12 @@ class DataParallelTrainer:
                     print(f"[rank {self.rank}] fused xgmi bucket unavailable ({ex})", flush=True)
         if self.xgmi is not None and bool(use_graphs) and backend == "hip":
             self.use_graphs = True  # the xGMI steps are pure device work: capturable whatever the group
+        # the overlapped backward only pays with >= 2 dW1 chunks; a gradient that fits ONE bucket (H=100:
+        # 318 KB, H=1024: 3.3 MB) goes as ONE all-reduce on the compute stream after the whole wgrad launch
+        # (two latency-bound collectives and a second graph stream would cost more than they hide)
         self._bucketed = (self.R > 1 and self.xgmi is None and allreduce != "host" and overlap
-                          and self.engine.supports_bucketed_wgrad and self.engine.device.type == "cuda")
+                          and self.engine.supports_bucketed_wgrad and self.engine.device.type == "cuda"
+                          and len(self._buckets()) > 1)
         self._comm_stream = torch.cuda.Stream(self.engine.device) if self._bucketed else None
         # single process, opt-in: two-launch lookahead schedule (parallel/lookahead.py).  Measured on
         # MI355X at H=100: 21.0 us/step vs 18.3 for the plain three launches -- the fused launches
