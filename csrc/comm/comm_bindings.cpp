@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -61,9 +62,22 @@ struct IpcPool {
       return p;
     }
     void* p = nullptr;
-    HIP_CHECK(hipMalloc(&p, bytes));
+    if (fine_grained()) HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained));
+    else HIP_CHECK(hipMalloc(&p, bytes));
     *got = bytes;
     return p;
+  }
+  // Fine-grained device memory for the exported buffers (default; CME_XGMI_MEM=plain: hipMalloc).  Peers
+  // store flags into this buffer and read gradients from it across xGMI; in fine-grained memory the
+  // owner's polls are coherent with those remote stores by construction, instead of depending on how the
+  // owner's L2 treats a coarse-grained line that another GPU wrote.  Measured with ranks sharing one
+  // GPU: same step time and all-reduce latency as plain memory (profiles/xgmi_fused_notes.md).
+  static bool fine_grained() {
+    static const bool v = [] {
+      const char* e = std::getenv("CME_XGMI_MEM");
+      return !(e && std::string(e) == "plain");
+    }();
+    return v;
   }
   void give(void* p, size_t bytes) { free_.emplace_back(p, bytes); }
 };
@@ -93,8 +107,8 @@ class XgmiComm {
     nblocks_ = std::max<int64_t>({1, xgmi_num_blocks(n), flag_slots});
     // ONE dedicated allocation per rank, [data: 2 x npad | flags: nblocks x 8 words], exported with one
     // IPC handle.  Rounded to 2 MiB so the runtime never sub-allocates it (hipIpcGetMemHandle rejects
-    // sub-allocated pointers); plain device memory -- hipDeviceMallocUncached pages do not export
-    // reliably -- with every flag access a system-scope atomic.
+    // sub-allocated pointers); fine-grained device memory (IpcPool::fine_grained; hipDeviceMallocUncached
+    // pages did not export reliably), with every flag access a system-scope atomic.
     flags_off_ = (2 * d_.npad * elt_bytes + 4095) / 4096 * 4096;
     sig_off_ = flags_off_ + (flag_bytes() + 4095) / 4096 * 4096;
     d_.mybuf = ipc_pool().take(round_alloc(sig_off_ + sizeof(Signature)), &alloc_bytes_);
