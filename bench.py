@@ -82,37 +82,58 @@ def main(argv=None) -> int:
 
     x, y = synthetic_mnist(a.train_size, seed=0)  # identical on every rank, no broadcast
     nn = NeuralNetwork([784, a.hidden, 10])
-    tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=global_batch,
-                             backend=a.backend, use_graphs=not a.no_graphs, allreduce=a.allreduce)
-    tr.load(x, y)
-    full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == global_batch]
-    if not full:
-        raise SystemExit("training split smaller than one global batch")
     lr, reg = 1e-3, 1e-4  # reference defaults (fpcode/main.cpp:58-60)
 
-    def plans_for(k: int):
-        out, i = [], 0
-        while i < k:
-            m = min(len(full), k - i)
-            out.append(EpochPlan(full[:m]))
-            i += m
-        return out
+    def prepare(allreduce: str):
+        """Trainer + captured graphs + W warm-up steps.  Returns (trainer, timed plans)."""
+        tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=global_batch,
+                                 backend=a.backend, use_graphs=not a.no_graphs, allreduce=allreduce)
+        tr.load(x, y)
+        full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == global_batch]
+        if not full:
+            raise SystemExit("training split smaller than one global batch")
 
-    warm_plans, timed_plans = plans_for(a.warmup), plans_for(a.steps)
-    if tr.use_graphs:  # capture outside the timed region (graphs are cached by plan)
-        try:
-            for p in {tuple(p.steps): p for p in warm_plans + timed_plans}.values():
-                tr.capture(p, lr, reg)
-        except Exception as ex:  # pragma: no cover - depends on the collective backend
-            print(f"warning: HIP graph capture failed ({ex!r}); running eager steps", file=sys.stderr)
-            tr.use_graphs = False
-            tr._graphs.clear()
-    # every rank done capturing before the first warm-up step: with the xGMI all-reduce a step waits
-    # (bounded) for its peers' same step, so a rank still capturing would count against that bound
+        def plans_for(k: int):
+            out, i = [], 0
+            while i < k:
+                m = min(len(full), k - i)
+                out.append(EpochPlan(full[:m]))
+                i += m
+            return out
+
+        warm_plans, timed_plans = plans_for(a.warmup), plans_for(a.steps)
+        if tr.use_graphs:  # capture outside the timed region (graphs are cached by plan)
+            try:
+                for p in {tuple(p.steps): p for p in warm_plans + timed_plans}.values():
+                    tr.capture(p, lr, reg)
+            except Exception as ex:  # pragma: no cover - depends on the collective backend
+                print(f"warning: HIP graph capture failed ({ex!r}); running eager steps", file=sys.stderr)
+                tr.use_graphs = False
+                tr._graphs.clear()
+        # every rank done capturing before the first warm-up step: with the xGMI all-reduce a step waits
+        # (bounded) for its peers' same step, so a rank still capturing would count against that bound
+        torch.cuda.synchronize(device)
+        comm.barrier()
+        for p in warm_plans:
+            tr.run_plan(p, lr, reg)
+        return tr, timed_plans
+
+    tr, timed_plans = prepare(a.allreduce)
     torch.cuda.synchronize(device)
     comm.barrier()
-    for p in warm_plans:
-        tr.run_plan(p, lr, reg)
+    if tr.allreduce_impl.startswith("xgmi") and a.allreduce == "auto":
+        # a bounded peer wait that timed out during the warm-up (the xGMI protocol misbehaving on this
+        # node) -> every rank drops to RCCL together, from the initial weights, before anything is timed
+        try:
+            tr.check_comm()
+            bad = float(os.environ.get("CME_BENCH_TEST_FALLBACK") == "1")  # test hook: take the fallback
+        except RuntimeError:
+            bad = 1.0
+        if comm.allreduce_scalar(bad, op="max") > 0:
+            if rank == 0:
+                print("warning: xGMI all-reduce peer wait timed out in warm-up; re-running on RCCL", file=sys.stderr)
+            tr.close()
+            tr, timed_plans = prepare("rccl")
     torch.cuda.synchronize(device)
     comm.barrier()
     torch.cuda.synchronize(device)
