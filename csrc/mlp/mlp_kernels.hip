@@ -1394,8 +1394,15 @@ void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
     CME_REQUIRE((int64_t)a.z2_chunks * 16 * a.lda < (int64_t)kOOB / 4 && (int64_t)a.H * a.lda < (int64_t)kOOB / 4,
                 "mlp_head: z2 partials too large for 32-bit buffer offsets");
     const int nct = cdiv(a.n, kHWCols);
-    if (cdiv(a.H, 512) * nct >= 256) head_wide_kernel<4><<<cdiv(a.H, 512) * nct, 512, 0, s>>>(a, cdiv(a.H, 512));
-    else if (cdiv(a.H, 256) * nct >= 256) head_wide_kernel<2><<<cdiv(a.H, 256) * nct, 512, 0, s>>>(a, cdiv(a.H, 256));
+    // row tiles per wave: the largest RT that still gives >= 256 workgroups (CME_HW_RT=1|2|4 forces one)
+    static const int force_rt = [] {
+      const char* e = std::getenv("CME_HW_RT");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int rt = force_rt ? force_rt
+                            : (cdiv(a.H, 512) * nct >= 256 ? 4 : (cdiv(a.H, 256) * nct >= 256 ? 2 : 1));
+    if (rt == 4) head_wide_kernel<4><<<cdiv(a.H, 512) * nct, 512, 0, s>>>(a, cdiv(a.H, 512));
+    else if (rt == 2) head_wide_kernel<2><<<cdiv(a.H, 256) * nct, 512, 0, s>>>(a, cdiv(a.H, 256));
     else head_wide_kernel<1><<<cdiv(a.H, 128) * nct, 512, 0, s>>>(a, cdiv(a.H, 128));
     CME_LAUNCH_CHECK(s);
     return;
