@@ -124,12 +124,8 @@ def main(argv=None) -> int:
     if tr.allreduce_impl.startswith("xgmi") and a.allreduce == "auto":
         # a bounded peer wait that timed out during the warm-up (the xGMI protocol misbehaving on this
         # node) -> every rank drops to RCCL together, from the initial weights, before anything is timed
-        try:
-            tr.check_comm()
-            bad = float(os.environ.get("CME_BENCH_TEST_FALLBACK") == "1")  # test hook: take the fallback
-        except RuntimeError:
-            bad = 1.0
-        if comm.allreduce_scalar(bad, op="max") > 0:
+        forced = os.environ.get("CME_BENCH_TEST_FALLBACK") == "1"  # test hook: take the fallback
+        if tr.comm_failed() or comm.allreduce_scalar(float(forced), op="max") > 0:
             if rank == 0:
                 print("warning: xGMI all-reduce peer wait timed out in warm-up; re-running on RCCL", file=sys.stderr)
             tr.close()
@@ -146,10 +142,14 @@ def main(argv=None) -> int:
     dt = time.perf_counter() - t0
     dt = comm.allreduce_scalar(dt, op="max")
 
-    # sanity: parameters finite after training, peer waits never timed out
-    ok = bool(torch.isfinite(tr.engine.params).all().item())
-    tr.check_comm()
-    images = a.steps * global_batch
+    # sanity, agreed by every rank: parameters finite everywhere and no xGMI peer wait timed out anywhere;
+    # otherwise the record is marked invalid and every rank exits non-zero
+    finite = bool(torch.isfinite(tr.engine.params).all().item())
+    bad = comm.allreduce_scalar(0.0 if finite else 1.0, op="max") > 0
+    comm_failed = tr.comm_failed()
+    ok = not bad and not comm_failed
+    # strong scaling drops the remainder columns when R does not divide the batch (trainer.shard)
+    images = a.steps * (global_batch // R) * R
     value = images / dt
     if rank == 0:
         rec = {
@@ -168,8 +168,11 @@ def main(argv=None) -> int:
             "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": global_batch, "seq_len": None,
                        "parallelism": f"dp{R}", "per_gpu_batch": global_batch // R, "backend": a.backend,
                        "mode": a.mode,
-                       "hip_graphs": tr.use_graphs, "allreduce": tr.allreduce_impl, "params_finite": ok},
+                       "hip_graphs": tr.use_graphs, "allreduce": tr.allreduce_impl, "params_finite": not bad,
+                       "comm_ok": not comm_failed},
         }
+        if not ok:
+            rec["invalid"] = "non-finite parameters" if bad else "an xGMI peer wait timed out"
         print(json.dumps(rec), flush=True)
     shutdown()
     return 0 if ok else 1
@@ -220,7 +223,7 @@ def run_tp(a, comm, device) -> int:
     comm.barrier()
     torch.cuda.synchronize(device)
     dt = comm.allreduce_scalar(time.perf_counter() - t0, op="max")
-    ok = bool(torch.isfinite(tr.engine.params).all().item())
+    ok = comm.allreduce_scalar(0.0 if bool(torch.isfinite(tr.engine.params).all().item()) else 1.0, op="max") == 0
     value = a.steps * B / dt
     if rank == 0:
         print(json.dumps({

@@ -86,8 +86,7 @@ def resolve_path(dtype: str, path: str = "auto") -> str:
 
 class MlpEngine:
     def __init__(self, H=(784, 100, 10), dtype: str = "f32", max_cols: int = 800, device=None,
-                 backend: str = "hip", shift: bool = True, feature_major_copy: bool = True, path: str = "auto",
-                 overlap_roles: bool = False):
+                 backend: str = "hip", shift: bool = True, feature_major_copy: bool = True, path: str = "auto"):
         if dtype not in DTYPE_CODES:
             raise ValueError(f"dtype must be one of {list(DTYPE_CODES)}")
         self.P, self.H, self.C = (int(h) for h in H)
@@ -116,15 +115,6 @@ class MlpEngine:
         # is nothing next to 288 GB of HBM.
         self.feature_major_copy = bool(feature_major_copy) or self.path.startswith("split")
         self._configure_path()
-        # split paths: the dW2/db2 role kernel runs on a side stream, concurrently with dW1 and the
-        # next step's forward GEMM (a1 is double-buffered so that forward cannot overwrite it early)
-        import os
-
-        # measured: a second stream inside the HIP graph costs more than it hides at these kernel
-        # sizes (20 -> 34 us/step), so it is off unless asked for (CME_ROLE_OVERLAP=1)
-        self.overlap_roles = ((bool(overlap_roles) or os.environ.get("CME_ROLE_OVERLAP") == "1")
-                              and backend == "hip" and self.device.type == "cuda")
-        self._aux_stream = None
         self._alloc_acts(max_cols)
         self._step = None
         self._xgmi_fuse = None
@@ -147,8 +137,6 @@ class MlpEngine:
         self.ld = _round_up(max(int(max_cols), 1), 16)
         dev, H, C, ld = self.device, self.H, self.C, self.ld
         self.a1 = torch.zeros(H, ld, dtype=self.pdt, device=dev)
-        self._a1bufs = [self.a1, torch.zeros_like(self.a1)] if (self.overlap_roles and self.np) else None
-        self._a1k = 0
         self.dZ1 = torch.zeros(H, ld, dtype=self.pdt, device=dev)
         self.D = torch.zeros(C, ld, dtype=self.pdt, device=dev)
         if self.np:
@@ -162,21 +150,11 @@ class MlpEngine:
         if self.backend == "hip" and H >= 512 and self.pdt == torch.float32:
             self.z2buf = torch.zeros(int(hip().head_big_scratch_floats(H, ld)), dtype=torch.float32, device=dev)
         nblk = (ld + 15) // 16
-        # optional (CME_HEAD_PARTIALS=1, needs CME_NO_BIAS_COL=1): the head leaves per-16-column partials
-        # of dW2|db1|db2 for the weight-gradient launch to reduce; the default instead overlaps the
-        # dW2/db2 role kernel with dW1 on a side stream and takes db1 from the dW1 GEMM
-        import os
-
-        self.gpart = None
-        if self.backend == "hip" and self.np and H <= 128 and os.environ.get("CME_HEAD_PARTIALS") == "1":
-            self.gpart = torch.zeros(nblk * (C * H + H + C), dtype=torch.float32, device=dev)
         self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
         # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
         # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
-        # (CME_SEPARATE_HEAD=1: the two-launch form, for A/B measurements)
         self.fh_counters = None
-        if (self.backend == "hip" and self.np and H <= 128 and C <= 16 and self.gpart is None
-                and os.environ.get("CME_SEPARATE_HEAD") != "1"):
+        if self.backend == "hip" and self.np and H <= 128 and C <= 16:
             self.fh_counters = torch.zeros((ld + 31) // 32, dtype=torch.int32, device=dev)
         self._step = None
 
@@ -209,9 +187,7 @@ class MlpEngine:
             if normalize:
                 xd = xd / 255.0
             self.X = xd.to(self.gdt).contiguous()
-        import os
-
-        if self.feature_major_copy and self.np and os.environ.get("CME_NO_BIAS_COL") != "1":
+        if self.feature_major_copy and self.np:
             # + an all-ones feature row: the dW1 GEMM's extra column is db1 (no separate bias reduction)
             self.XT = torch.cat([self.X.t(), torch.ones(1, self.X.shape[0], dtype=self.X.dtype, device=self.device)])
             self.XT = self.XT.contiguous()
@@ -246,9 +222,7 @@ class MlpEngine:
                 self.W1g.copy_(self.W1.to(torch.bfloat16))
 
     def join(self):
-        """Make the current stream wait for an outstanding side-stream role kernel (W2/b2 update)."""
-        if self._step is not None and self.backend == "hip":
-            self._step.join(torch.cuda.current_stream(self.device).cuda_stream)
+        """Kept for API stability: every kernel of a step runs on the caller's stream, nothing to join."""
 
     def get_params(self):
         """Host float64 copies (W1, b1, W2, b2)."""
@@ -283,17 +257,11 @@ class MlpEngine:
                 s.dZ1p = self.dZ1p.data_ptr()
             if self.z2buf is not None:
                 s.z2p = self.z2buf.data_ptr()
-            if self.gpart is not None:
-                s.gpart = self.gpart.data_ptr()
             if self.fh_counters is not None:
                 s.fh_counters = self.fh_counters.data_ptr()
                 s.fh_tiles = int(self.fh_counters.numel())
             if self.np and self.XT is not None and self.XT.shape[0] == self.P + 1:
                 s.bias_col = 1
-                if self._a1bufs is not None:
-                    if self._aux_stream is None:
-                        self._aux_stream = torch.cuda.Stream(self.device)
-                    s.stream2 = self._aux_stream.cuda_stream
             if self._xgmi_fuse is not None and s.bias_col:
                 s.set_xgmi(*self._xgmi_fuse)
             self._step = s
@@ -303,12 +271,10 @@ class MlpEngine:
     def fused_allreduce_slots(self) -> int:
         """Flag slots (one per wgrad workgroup tile) the fused data-parallel step needs; 0 when this
         engine cannot run it (split path, H <= 128, all-ones XT feature, no head partials)."""
-        import os
-
         bias_feature = (self.XT.shape[0] == self.P + 1 if self.XT is not None   # loaded, or will be
-                        else self.feature_major_copy and os.environ.get("CME_NO_BIAS_COL") != "1")
+                        else self.feature_major_copy)
         if not (self.backend == "hip" and self.np and self.H <= 128 and self.device.type == "cuda"
-                and self.gpart is None and bias_feature):
+                and bias_feature):
             return 0
         return max(0, int(hip().mlp_split_fused_tiles(self.P, self.H, 1 << 30)))
 
@@ -338,10 +304,6 @@ class MlpEngine:
             raise IndexError("batch slice outside the resident dataset")
         if self.backend == "hip":
             st = self._hip_step()
-            if self._a1bufs is not None and st.stream2:  # alternate a1 buffers (roles may still read the last)
-                self._a1k ^= 1
-                self.a1 = self._a1bufs[self._a1k]
-                st.a1 = self.a1.data_ptr()
             st.run(int(off), int(n), float(scale), float(reg), float(lr), 2 if sgd == 2 else int(bool(sgd)),
                    int(bool(with_loss)),
                    torch.cuda.current_stream(self.device).cuda_stream, int(parts))

@@ -179,7 +179,10 @@ class TensorParallelTrainer:
         if g is not None:
             return g
         e = self.engine
-        snap = e.params.clone(), (e.W1p.clone() if e.W1p is not None else None)
+        # every derived copy of W1 too: the bf16 shadow W1g (bf16 + mfma path) is refreshed after the
+        # update, so the warm-up step leaves it one step ahead of the restored master
+        snap = (e.params.clone(), (e.W1p.clone() if e.W1p is not None else None),
+                (e.W1g.clone() if e.W1g is not e.W1 else None))
         side = torch.cuda.Stream(e.device)
         side.wait_stream(torch.cuda.current_stream(e.device))
         with torch.cuda.stream(side):  # warm-up (lazy kernel loads, communicator set-up)
@@ -189,6 +192,8 @@ class TensorParallelTrainer:
         e.params.copy_(snap[0])
         if snap[1] is not None:
             e.W1p.copy_(snap[1])
+        if snap[2] is not None:
+            e.W1g.copy_(snap[2])
         torch.cuda.synchronize(e.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):

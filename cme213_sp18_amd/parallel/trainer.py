@@ -40,6 +40,10 @@ class FaultInjected(RuntimeError):
     """Raised by ``train(fault=(rank, step))`` -- the failure-detection test hook."""
 
 
+class CommFailure(RuntimeError):
+    """Raised on every rank together when a peer-to-peer all-reduce wait timed out on any rank."""
+
+
 @dataclass
 class EpochPlan:
     steps: list  # [(start, length)]
@@ -61,9 +65,12 @@ class DataParallelTrainer:
     def __init__(self, nn, comm: Communicator | None = None, device=None, dtype: str = "f32",
                  batch_size: int = 800, backend: str = "hip", shift: bool = True, use_graphs: bool = True,
                  normalize: bool = False, path: str = "auto", allreduce: str = "auto", overlap: bool = True,
-                 lookahead: bool = False, overlap_chunks: int = 0):
+                 overlap_chunks: int = 0, fuse_allreduce: bool = True):
         self.nn = nn
-        self.overlap_chunks = int(overlap_chunks)  # RCCL path: dW1 row chunks (0: ~BUCKET_BYTES each)
+        # RCCL path: dW1 row chunks all-reduced while the next chunk is computed (0: ~BUCKET_BYTES each).
+        # Setting it also forces the overlapped path with ONE rank of a real process group (nccl world 1),
+        # so a one-GPU box exercises the side-stream + graph-captured backward.
+        self.overlap_chunks = int(overlap_chunks)
         self.comm = comm or NullComm()
         self.R = self.comm.world_size
         self.rank = self.comm.rank
@@ -88,7 +95,7 @@ class DataParallelTrainer:
         # bitwise comparison with the separate-kernel step has passed on every rank
         self._xgmi_fused = None
         self.fused_allreduce = False
-        if self.xgmi is not None and os.environ.get("CME_XGMI_FUSED", "1") != "0":
+        if self.xgmi is not None and fuse_allreduce:
             slots = self.engine.fused_allreduce_slots()
             if slots and self.engine.params.dtype == torch.float32 and self._fused_fits(slots):
                 from .xgmi import XgmiBucket
@@ -107,16 +114,11 @@ class DataParallelTrainer:
         # the overlapped backward only pays with >= 2 dW1 chunks; a gradient that fits ONE bucket (H=100:
         # 318 KB, H=1024: 3.3 MB) goes as ONE all-reduce on the compute stream after the whole wgrad launch
         # (two latency-bound collectives and a second graph stream would cost more than they hide)
-        self._bucketed = (self.R > 1 and self.xgmi is None and allreduce != "host" and overlap
+        multi = self.R > 1 or (self.overlap_chunks > 0 and not isinstance(self.comm, NullComm))
+        self._bucketed = (multi and self.xgmi is None and allreduce != "host" and overlap
                           and self.engine.supports_bucketed_wgrad and self.engine.device.type == "cuda"
                           and len(self._buckets()) > 1)
         self._comm_stream = torch.cuda.Stream(self.engine.device) if self._bucketed else None
-        # single process, opt-in: two-launch lookahead schedule (parallel/lookahead.py).  Measured on
-        # MI355X at H=100: 21.0 us/step vs 18.3 for the plain three launches -- the fused launches
-        # double the workgroups per CU and each kernel is already L2->CU bandwidth bound, so the
-        # shorter dependency chain does not pay; kept for larger-batch / latency-bound regimes.
-        self.lookahead = bool(lookahead) and isinstance(self.comm, NullComm)
-        self._la = None
         self.allreduce_impl = "none" if self.R == 1 else (
             "xgmi" if self.xgmi is not None else "host-gloo" if allreduce == "host" else self.comm.name)
 
@@ -188,10 +190,25 @@ class DataParallelTrainer:
         return all(out)
 
     def check_comm(self) -> None:
-        """Raise if a peer wait of an xGMI all-reduce timed out (a rank stalled or died)."""
+        """Raise if a peer wait of an xGMI all-reduce timed out on THIS rank (local check, no collective)."""
         for b in (self.xgmi, self._xgmi_fused):
             if b is not None:
                 b.check()
+
+    def comm_failed(self) -> bool:
+        """Collective: True on EVERY rank when any rank's xGMI peer wait timed out.  A block whose wait
+        timed out applied nothing (csrc/comm/xgmi_allreduce.hip), but other ranks may have applied that
+        step, so the replicas can no longer be trusted to agree -- callers stop (or restart) as one."""
+        local = any(b is not None and b.error() for b in (self.xgmi, self._xgmi_fused))
+        if self.R == 1:
+            return local
+        return self.comm.allreduce_scalar(1.0 if local else 0.0, op="max") > 0
+
+    def assert_comm_ok(self) -> None:
+        """Collective: raise CommFailure on every rank together if any rank's peer wait timed out."""
+        if (self.xgmi is not None or self._xgmi_fused is not None) and self.comm_failed():
+            raise CommFailure(f"rank {self.rank}: an xGMI all-reduce peer wait timed out on some rank "
+                              "(a rank stalled or died); no rank applied the affected update")
 
     def close(self) -> None:
         """Collective: release the xGMI IPC buckets (every rank must call it)."""
@@ -231,15 +248,9 @@ class DataParallelTrainer:
         self.engine.load_dataset(x_train, y_train, normalize=self.normalize)
         self.N = self.engine.num_samples
         self._graphs.clear()
-        self._la = None
         if self._xgmi_fused is not None:
             self.fused_allreduce = self._check_fused()
             self.allreduce_impl = "xgmi-fused" if self.fused_allreduce else "xgmi"
-        if self.lookahead:
-            from .lookahead import LookaheadRunner
-
-            if LookaheadRunner.supported(self.engine):
-                self._la = LookaheadRunner(self.engine)
 
     def _check_fused(self) -> bool:
         """One step from the same state through both all-reduce paths (separate xGMI kernel, and
@@ -280,18 +291,9 @@ class DataParallelTrainer:
                 print("[xgmi] fused all-reduce self-check failed; using the separate kernel", flush=True)
         return ok
 
-    def _uses_lookahead(self, plan: EpochPlan) -> bool:
-        from .lookahead import LookaheadRunner
-
-        return self._la is not None and LookaheadRunner.plan_ok(plan.steps)
-
     def _enqueue_plan(self, plan: EpochPlan, lr: float, reg: float) -> None:
-        if self._uses_lookahead(plan):
-            self._la.run(plan.steps, lr, reg)
-        else:
-            for s, ln in plan.steps:
-                self.step(s, ln, lr, reg)
-        self.engine.join()
+        for s, ln in plan.steps:
+            self.step(s, ln, lr, reg)
 
     def epoch_plan(self, N: int | None = None) -> EpochPlan:
         N = self.N if N is None else N
@@ -437,20 +439,17 @@ class DataParallelTrainer:
         if g is not None:
             return g
         snap = self._snapshot()
-        if self._uses_lookahead(plan):
-            self._la.gram(plan.steps)  # data-only Gram matrices: computed once, outside the graph
         side = torch.cuda.Stream(self.engine.device)
         side.wait_stream(torch.cuda.current_stream(self.engine.device))
         with torch.cuda.stream(side):  # warm-up: lazy kernel loads, communicator init
-            self._enqueue_plan(EpochPlan(plan.steps[:2]) if self._uses_lookahead(plan) else EpochPlan(plan.steps[:1]),
-                               lr, reg)
+            self._enqueue_plan(EpochPlan(plan.steps[:1]), lr, reg)
         torch.cuda.current_stream(self.engine.device).wait_stream(side)
         torch.cuda.synchronize(self.engine.device)
         self._restore(snap)
         torch.cuda.synchronize(self.engine.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._enqueue_plan(plan, lr, reg)  # (joins any side-stream role kernel before the capture ends)
+            self._enqueue_plan(plan, lr, reg)
         torch.cuda.synchronize(self.engine.device)
         self._graphs[key] = g
         return g
@@ -463,24 +462,32 @@ class DataParallelTrainer:
 
     # ---------------------------------------------------------------- train
     def train(self, epochs: int, lr: float, reg: float, print_every: int = 0, debug: bool = False,
-              outdir: str = "Outputs", log=print, on_event=None, fault: tuple[int, int] | None = None) -> TrainStats:
+              outdir: str = "Outputs", log=print, on_event=None, fault: tuple[int, int] | None = None,
+              diff_file=None) -> TrainStats:
         """Full training loop (neural_network.cpp:446-555).  Eager steps where the
         host must look at a step (loss printing / debug diffs), graphs elsewhere.
 
         on_event(dict): structured progress records (loss, epoch) for JSON-lines logs.
         fault=(rank, step): raise FaultInjected on that rank when the global step
         counter reaches ``step`` (before it runs) -- tests that a failing rank
-        takes the job down instead of leaving its peers hung."""
+        takes the job down instead of leaving its peers hung.
+
+        diff_file: an open text file for the -d CPU-vs-GPU diff rows (the caller owns it across
+        several train() segments); None: this call opens Outputs/CpuGpuDiff.txt itself -- truncated
+        on a fresh run (iter 0), appended to when training resumes mid-run.
+
+        With the xGMI all-reduce, every epoch ends with a collective check of the peer-wait error flag
+        (assert_comm_ok): a timed-out wait raises CommFailure on every rank before another epoch runs."""
         from ..utils.checkpoint import write_diff_gpu_cpu
 
         stats = TrainStats()
         plan = self.epoch_plan()
-        err_file = None
-        if debug and self.rank == 0:  # only rank 0 owns the diff file (reference truncates it on every rank)
-            import os
-
+        err_file, own_file = diff_file, False
+        if debug and self.rank == 0 and err_file is None:  # only rank 0 owns the diff file
             os.makedirs(outdir, exist_ok=True)
-            err_file = open(os.path.join(outdir, "CpuGpuDiff.txt"), "w")
+            err_file = open(os.path.join(outdir, "CpuGpuDiff.txt"), "w" if self.iter == 0 else "a")
+            own_file = True
+        xgmi_live = self.xgmi is not None or self._xgmi_fused is not None
         host_needed = print_every > 0 or debug or self.profiler is not None
         dev = self.engine.device
         if dev.type == "cuda":
@@ -497,6 +504,8 @@ class DataParallelTrainer:
                     maybe_fault(self.iter, len(plan.steps))
                     with self.roctx.range(f"epoch {epoch}"):
                         self.run_plan(plan, lr, reg)
+                    if xgmi_live:
+                        self.assert_comm_ok()  # syncs; every rank raises together
                     self.iter += len(plan.steps)
                     stats.steps += len(plan.steps)
                     stats.images += sum((ln // self.R) * self.R for _, ln in plan.steps)
@@ -526,12 +535,13 @@ class DataParallelTrainer:
                     self.iter += 1
                     stats.steps += 1
                     stats.images += (ln // self.R) * self.R
+                if xgmi_live:
+                    self.assert_comm_ok()
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
-            self.check_comm()
             self.comm.barrier()
         finally:
-            if err_file is not None:
+            if own_file:
                 err_file.close()
         stats.seconds = time.perf_counter() - t0
         self.sync_to(self.nn)

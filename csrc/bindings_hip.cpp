@@ -8,7 +8,6 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
-#include <cstdlib>
 
 #include "comm/xgmi_allreduce.h"
 #include "common/hip_common.h"
@@ -48,29 +47,11 @@ struct MlpStep {
   uintptr_t stamps = 0;  // diagnostics only
   uintptr_t hstamps = 0;  // diagnostics only: head-block stamps
   uintptr_t z2p = 0;     // wide-layer head scratch (head_big_scratch_floats), 0: column head
-  uintptr_t gpart = 0;   // small-layer gradient partials (split path, H <= 128), 0: recompute in wgrad
   int bias_col = 0;      // XT has an all-ones feature row P: db1 comes out of the dW1 GEMM
-  // second stream for the dW2/db2 role kernel (split path, bias_col): it runs concurrently with dW1
-  // and the next step's forward GEMM; the next head (which reads W2) waits for it
-  uintptr_t stream2 = 0;
   // split path, H <= 128: uint32 tile counters (>= fh_tiles, zeroed) enable the single-launch forward +
   // head (mlp_fwd1_head); 0: separate fwd1 + head kernels
   uintptr_t fh_counters = 0;
   int fh_tiles = 0;
-  int no_gemm_z2 = 0;  // 1: wide-layer head computes z2 itself (A/B tests)
-  hipEvent_t ev_head = nullptr, ev_roles = nullptr;
-  bool roles_pending = false;
-
-  ~MlpStep() {
-    if (ev_head) (void)hipEventDestroy(ev_head);
-    if (ev_roles) (void)hipEventDestroy(ev_roles);
-  }
-  void join(uintptr_t stream) {  // make `stream` wait for an outstanding role kernel on stream2
-    if (roles_pending) {
-      HIP_CHECK(hipStreamWaitEvent(S(stream), ev_roles, 0));
-      roles_pending = false;
-    }
-  }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
   void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2) {
@@ -100,8 +81,6 @@ struct MlpStep {
     f.off_b1 = off_b1;
     f.off_W2 = off_W2;
     f.off_b2 = off_b2;
-    const char* v = std::getenv("CME_XF_VARIANT");
-    f.variant = v ? std::atoi(v) : 0;
     xf = f;
   }
   float xscale = 1.f;    // split path: inputs are uint8 * xscale
@@ -125,10 +104,6 @@ struct MlpStep {
     a.scale = scale; a.reg = reg; a.lr = lr; a.sgd = sgd; a.shift = shift; a.mode = 0;
     a.stamps = reinterpret_cast<unsigned long long*>(stamps);
     a.bias_col = bias_col;
-    if (gpart && !bias_col && !fused_head && H <= cme::kHeadPartialMaxH) {  // db1 would be computed twice
-      a.gpart = P_<float>(gpart);
-      a.gblocks = cme::mlp_head_num_blocks(n);
-    }
     return a;
   }
 
@@ -158,46 +133,23 @@ struct MlpStep {
           h.dZ1_planes = a.dZ1p; h.npz = npz;
           h.loss_partial = a.loss_partial; h.shift = shift; h.mode = cme::HEAD_TRAIN;
           h.z2part = P_<float>(z2p);
-          h.gpart = const_cast<float*>(a.gpart);
           h.stamps = hstamps ? reinterpret_cast<unsigned long long*>(hstamps) : nullptr;
-          join(stream);  // the head reads W2 / b2, updated by the previous step's role kernel
           if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
             cme::mlp_fwd1_head(a, h, P_<unsigned>(fh_counters), fh_tiles, S(stream));
           } else {
             // wide layers: the forward GEMM also leaves the head's z2 partials (unless only the head runs)
             cme::SplitStepArgs f = a;
-            f.z2part = (z2p && !(parts & 8) && !no_gemm_z2) ? P_<float>(z2p) : nullptr;
+            f.z2part = (z2p && !(parts & 8)) ? P_<float>(z2p) : nullptr;
             if (!(parts & 8)) cme::mlp_split_fwd1(f, S(stream));
             h.z2_chunks = f.z2part ? cme::mlp_split_fwd1_z2_chunks(f) : 0;
             // with the all-ones XT feature nothing reads dZ1 in fp32 on the wide path (db1 comes out of
             // the dW1 GEMM over the planes): skip those 4 B/element of HBM writes
-            if (h.z2_chunks > 0 && bias_col && !a.gpart) h.dZ1 = nullptr;
+            if (h.z2_chunks > 0 && bias_col) h.dZ1 = nullptr;
             if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
           }
         }
       }
-      if (parts & 2) {
-        if (stream2 && bias_col && !a.gpart && sgd != 2) {
-          if (!ev_head) {
-            HIP_CHECK(hipEventCreateWithFlags(&ev_head, hipEventDisableTiming));
-            HIP_CHECK(hipEventCreateWithFlags(&ev_roles, hipEventDisableTiming));
-          }
-          join(stream);
-          HIP_CHECK(hipEventRecord(ev_head, S(stream)));
-          HIP_CHECK(hipStreamWaitEvent(S(stream2), ev_head, 0));
-          cme::SplitStepArgs r = a;
-          r.wg_parts = 2;  // dW2 + db2 on the side stream
-          cme::mlp_split_wgrad(r, S(stream2));
-          HIP_CHECK(hipEventRecord(ev_roles, S(stream2)));
-          roles_pending = true;
-          cme::SplitStepArgs w = a;
-          w.wg_parts = 1;  // dW1 + db1 (+ SGD, planes) on the main stream
-          cme::mlp_split_wgrad(w, S(stream));
-          if (!sgd) join(stream);  // gradient bucket complete before the all-reduce
-        } else {
-          cme::mlp_split_wgrad(a, S(stream));
-        }
-      }
+      if (parts & 2) cme::mlp_split_wgrad(a, S(stream));
       return;
     }
     CME_REQUIRE(sgd != 2, "MlpStep.run(sgd=2): split paths only");
@@ -235,46 +187,6 @@ struct MlpStep {
     w.gW2 = reinterpret_cast<void*>(gW2); w.gb2 = reinterpret_cast<void*>(gb2);
     w.W1_bf16 = d == DType::BF16 ? reinterpret_cast<void*>(W1g) : nullptr;
     if (parts & 2) cme::mlp_wgrad(d, w, S(stream));
-  }
-
-  // ---- lookahead steps (single process; see cme213_sp18_amd/parallel/lookahead.py)
-  // prologue: zbuf = xscale * (W1 . X[off:off+n])  (pre-activation without bias)
-  void la_prologue(int64_t off, int n, uintptr_t zbuf, uintptr_t stream) {
-    CME_REQUIRE(split && bias_col, "lookahead: split path with the all-ones XT feature");
-    cme::SplitStepArgs a = split_args(off, n, 1.0, 0.0, 0.0, 1, 0);
-    cme::mlp_split_fwd_raw(a, P_<float>(zbuf), a.xscale, S(stream));
-  }
-  // launch L2 of step (off, n): head on zcur (pre-activation + b1 -> sigmoid, written back) and, when
-  // n_next > 0, the raw forward An = W1 . X[off_next:off_next+n_next] into abuf
-  void la_l2(int64_t off, int n, double scale, int with_loss, uintptr_t zcur, int64_t off_next, int n_next,
-             uintptr_t abuf, uintptr_t stream) {
-    CME_REQUIRE(split && bias_col, "lookahead: split path with the all-ones XT feature");
-    const cme::SplitStepArgs a = split_args(off, n, scale, 0.0, 0.0, 1, with_loss);
-    cme::HeadArgs h{};
-    h.a1 = reinterpret_cast<void*>(zcur); h.lda = ld; h.W2 = a.W2; h.b2 = a.b2; h.labels = a.labels; h.H = H;
-    h.C = C; h.n = n; h.scale = scale; h.D = a.D; h.ldd = ld; h.dZ1 = a.dZ1; h.ldz = ld; h.dZ1_bf16 = nullptr;
-    h.dZ1_planes = a.dZ1p; h.npz = npz; h.loss_partial = a.loss_partial; h.shift = shift;
-    h.mode = cme::HEAD_TRAIN; h.b1_pre = a.b1;
-    cme::SplitStepArgs f = split_args(n_next > 0 ? off_next : off, n_next > 0 ? n_next : n, 1.0, 0.0, 0.0, 1, 0);
-    cme::mlp_lookahead_l2(f, P_<float>(abuf), h, n_next > 0, S(stream));
-  }
-  // launch L1 of step (off, n): dW1/db1/dW2/db2 with the fused SGD and, when n_next > 0, the next
-  // step's pre-activation z_next = c1 * abuf - c2 * dZ1 . GT^T  (GT [n_next][ldg] fp32 Gram matrix)
-  void la_l1(int64_t off, int n, double scale, double reg, double lr, uintptr_t zcur, int n_next, uintptr_t GT,
-             int ldg, uintptr_t abuf, uintptr_t znext, double c1, double c2, uintptr_t stream) {
-    CME_REQUIRE(split && bias_col, "lookahead: split path with the all-ones XT feature");
-    cme::SplitStepArgs a = split_args(off, n, scale, reg, lr, 1, 0);
-    a.a1 = P_<float>(zcur);  // the head wrote the activated a1 back there (dW2 reads it)
-    if (n_next > 0) {
-      a.GTn = P_<float>(GT);
-      a.ldg = ldg;
-      a.n_next = n_next;
-      a.An = P_<float>(abuf);
-      a.z1n = P_<float>(znext);
-      a.c1 = (float)c1;
-      a.c2 = (float)c2;
-    }
-    cme::mlp_split_wgrad(a, S(stream));
   }
 
   // Weight-gradient pieces of a step whose forward + head already ran (parts=1): used by the
@@ -432,7 +344,6 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("loss", &MlpStep::loss)
       .def_readwrite("fh_counters", &MlpStep::fh_counters)
       .def_readwrite("fh_tiles", &MlpStep::fh_tiles)
-      .def_readwrite("no_gemm_z2", &MlpStep::no_gemm_z2)
       .def("tp_forward", &MlpStep::tp_forward)
       .def("tp_head", &MlpStep::tp_head)
       .def_readwrite("shift", &MlpStep::shift)
@@ -443,16 +354,9 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("hstamps", &MlpStep::hstamps)
       .def_readwrite("xscale", &MlpStep::xscale)
       .def_readwrite("z2p", &MlpStep::z2p)
-      .def_readwrite("gpart", &MlpStep::gpart)
       .def_readwrite("bias_col", &MlpStep::bias_col)
-      .def_readwrite("stream2", &MlpStep::stream2)
-      .def("join", &MlpStep::join, py::arg("stream"))
       .def("set_xgmi", &MlpStep::set_xgmi, py::arg("desc"), py::arg("slots"), py::arg("off_b1"), py::arg("off_W2"),
            py::arg("off_b2"))
-      .def_property_readonly("roles_pending", [](const MlpStep& s) { return s.roles_pending; })
-      .def("la_prologue", &MlpStep::la_prologue)
-      .def("la_l2", &MlpStep::la_l2)
-      .def("la_l1", &MlpStep::la_l1)
       .def("run_wgrad", &MlpStep::run_wgrad, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"),
            py::arg("lr"), py::arg("sgd"), py::arg("parts"), py::arg("row0"), py::arg("rows"), py::arg("stream"))
       .def_readwrite("npw", &MlpStep::npw)

@@ -62,23 +62,15 @@ struct IpcPool {
       return p;
     }
     void* p = nullptr;
-    if (fine_grained()) HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained));
-    else HIP_CHECK(hipMalloc(&p, bytes));
+    HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained));
     *got = bytes;
     return p;
   }
-  // Fine-grained device memory for the exported buffers (default; CME_XGMI_MEM=plain: hipMalloc).  Peers
-  // store flags into this buffer and read gradients from it across xGMI; in fine-grained memory the
-  // owner's polls are coherent with those remote stores by construction, instead of depending on how the
-  // owner's L2 treats a coarse-grained line that another GPU wrote.  Measured with ranks sharing one
-  // GPU: same step time and all-reduce latency as plain memory (profiles/xgmi_fused_notes.md).
-  static bool fine_grained() {
-    static const bool v = [] {
-      const char* e = std::getenv("CME_XGMI_MEM");
-      return !(e && std::string(e) == "plain");
-    }();
-    return v;
-  }
+  // Fine-grained device memory for the exported buffers.  Peers store flags into this buffer and read
+  // gradients from it across xGMI; in fine-grained memory the owner's polls are coherent with those
+  // remote stores by construction, instead of depending on how the owner's L2 treats a coarse-grained
+  // line that another GPU wrote.  Measured with ranks sharing one GPU: same step time and all-reduce
+  // latency as plain hipMalloc memory (profiles/xgmi_fused_notes.md).
   void give(void* p, size_t bytes) { free_.emplace_back(p, bytes); }
 };
 IpcPool& ipc_pool() {

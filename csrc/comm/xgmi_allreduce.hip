@@ -8,7 +8,11 @@
 //   1. copies the local gradient chunk into this step's half of a
 //      double-buffered IPC buffer and releases it at system scope,
 //   2. signals every peer (per-block flag in the peer's uncached flag page),
-//   3. waits for every peer's flag (bounded spin -> error flag, never a hang),
+//   3. waits for every peer's flag (bounded spin -> error flag, never a hang;
+//      a block whose wait timed out -- or that starts after ANY block of this
+//      rank has flagged an error -- applies NOTHING: params and planes stay as
+//      they were, so a stalled peer can never make this rank step on stale or
+//      half-written gradients; the trainer all-reduces the flag and stops),
 //   4. reads all R gradients of its chunk straight from the peers' HBM over
 //      xGMI, sums them in rank order (bit-identical on every rank), and
 //   5. applies params -= lr * sum, refreshing the bf16 W1 planes / shadow.
@@ -18,7 +22,6 @@
 #include <hip/hip_bf16.h>
 
 #include <algorithm>
-#include <cstdlib>
 
 #include "../common/hip_common.h"
 #include "xgmi_allreduce.h"
@@ -48,7 +51,6 @@ struct Args {
   __hip_bfloat16* planes;
   int np;
   int rank, world, mode;
-  int variant;  // diagnostics (CME_XGMI_VARIANT): bit1 extra acquire fence (L2 invalidate)
 };
 
 constexpr int kSysCoherent = 1 | 16;  // buffer-load cache policy sc0 | sc1 (system coherent)
@@ -102,12 +104,18 @@ __device__ __forceinline__ void update_one(const Args<T>& a, int64_t i, T sum) {
 }
 
 // One chunk (kChunk elements) through copy -> release -> signal -> wait -> reduce -> update.
+// s_sync[0]: this chunk's epoch, s_sync[1]: 1 when the chunk must not be applied (block-uniform via LDS)
 template <typename T>
-__device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* s_epoch) {
+__device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* s_sync) {
   const int t = threadIdx.x;
-  if (t == 0) *s_epoch = a.epochs[c] + 1;
+  if (t == 0) {
+    s_sync[0] = a.epochs[c] + 1;
+    // an earlier wait of this rank timed out: the replicas may already disagree -> apply nothing more
+    s_sync[1] = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  }
   __syncthreads();
-  const uint32_t epoch = *s_epoch;
+  if (s_sync[1]) return;
+  const uint32_t epoch = s_sync[0];
   const int64_t half = (int64_t)(epoch & 1u) * a.npad;
   const int64_t i0 = c * kChunk + (int64_t)t * kVec;
 
@@ -156,13 +164,14 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
     while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       if (++spins > kSpinLimit) {
         atomicExch(a.err, 1);
+        s_sync[1] = 1;  // (benign race between the waiting lanes: they all store 1)
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
   }
   __syncthreads();
-  if (a.variant & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // diagnostics: full L2 invalidate
+  if (s_sync[1]) return;  // a peer never arrived: leave params, planes and this chunk's epoch untouched
 
   // 4. sum the R gradients of my elements in rank order, 5. update.
   //    Peer data is read with system-coherent loads (sc0 sc1), i.e. as relaxed system-scope atomics,
@@ -194,22 +203,14 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
 // same chunk of its peers, and the capped grid is always fully resident.
 template <typename T>
 __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(Args<T> a, int64_t nchunks) {
-  __shared__ uint32_t s_epoch;
+  __shared__ uint32_t s_sync[2];
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    do_chunk(a, c, &s_epoch);
+    do_chunk(a, c, s_sync);
     __syncthreads();
   }
 }
 
 }  // namespace
-
-int variant_from_env() {
-  static const int v = [] {
-    const char* e = std::getenv("CME_XGMI_VARIANT");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
 
 int64_t xgmi_padded_count(int64_t n) { return (n + kChunk - 1) / kChunk * kChunk; }
 int64_t xgmi_num_blocks(int64_t n) { return (n + kChunk - 1) / kChunk; }
@@ -246,7 +247,6 @@ void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* param
     a.rank = d.rank;
     a.world = d.world;
     a.mode = mode;
-    a.variant = variant_from_env();
     xgmi_allreduce_kernel<T><<<grid, kThreads, 0, s>>>(a, nchunks);
   };
   if (dtype == 1) fill((double*)nullptr);

@@ -47,26 +47,15 @@ struct HeadArgs {
   // the split-H z2 partial sums; when set, the head runs as two grid-wide kernels instead of one
   // column-parallel kernel whose per-thread loop over H is serial
   float* z2part = nullptr;
-  // small layers (H <= 128, fp32, train): per-block partial sums of the OTHER gradients, so the
-  // weight-gradient launch only reduces them: gpart[blk][C*H + H + C] = (dW2 [C][H] | db1 [H] | db2 [C])
-  // over this block's 16 columns (mlp_head_num_blocks(n) blocks)
-  float* gpart = nullptr;
-  // lookahead step (fp32, H <= 128): a1 holds z1 - b1 (no activation); the head adds b1_pre and applies
-  // the sigmoid, writing the activated a1 back
-  const float* b1_pre = nullptr;
   // > 0: z2part already holds z2_chunks row-tile partials [chunk][16][lda] left by the forward GEMM
   // (SplitStepArgs::z2part); the head then only reduces them and never re-reads a1 for z2
   int z2_chunks = 0;
   // diagnostics only: s_memrealtime stamps [block][8] (bench/stamps_fh.py)
   unsigned long long* stamps = nullptr;
 };
-constexpr int kHeadPartialMaxH = 128;
 int64_t head_big_scratch_floats(int H, int n);
 
 struct SplitStepArgs;
-// lookahead step launch "L2": this step's head (a1 given as pre-activation, h.b1_pre) + the next
-// step's raw forward GEMM An = W1 . X_next (f: next step's args; with_next = false on the last step)
-void mlp_lookahead_l2(const SplitStepArgs& f, float* Aout, const HeadArgs& h, bool with_next, hipStream_t s);
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t stream);
 // split path, H <= 128: forward GEMM (a1 = sigmoid(W1 X + b1), f) and the train-mode head (h, same a1) in
 // ONE launch -- the last workgroup of every 32-column tile runs the head for it.  counters: >= max_tiles

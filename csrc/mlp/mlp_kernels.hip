@@ -106,11 +106,9 @@ __device__ __forceinline__ void head_stage(const HeadArgs& a, int t, int nthr, P
 
 template <typename P, int NC, bool LDSW, int HPT, bool SC1 = false, bool STAGED = false>
 __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, const int t, char* head_dyn,
-                                           P (*zred)[NC][kHeadCols], float* lred,
-                                           float (*gs_x)[kHeadCols + 1], float (*gs_d)[kHeadCols + 1]) {
-  // One head block (kHeadCols columns, 256 threads) -- vb: the block index, t: thread in [0, 256).
-  // Called by head_kernel (one block per workgroup) and by the lookahead step kernel (two per
-  // 512-thread workgroup); every barrier below is reached by all threads of the workgroup.
+                                           P (*zred)[NC][kHeadCols], float* lred) {
+  // One head block (kHeadCols columns, 256 threads) -- vb: the block index, t: thread in [0, 256);
+  // every barrier below is reached by all threads of the workgroup.
   // HPT > 0: every thread owns at most HPT hidden units (H <= HPT * NPART); their
   // a1 values are loaded ONCE (one burst, before the W2 staging barrier) and
   // reused by both passes.  HPT == 0: generic loop for large H.
@@ -142,18 +140,6 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
         xa[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, kSc1));
       } else {
         xa[u] = buf_load1<P>(rs, off);
-      }
-    }
-    if (a.b1_pre) {  // lookahead step: a1 holds the pre-activation without bias; finish it here
-      const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.b1_pre);
-      P* a1w = const_cast<P*>(a1);
-#pragma unroll
-      for (int u = 0; u < HPT; ++u) {
-        const int h = part + u * NPART;
-        const P bb = (P)buf_load1<float>(rb, h < H ? h * 4 : kOOB);
-        const P v = P(1) / (P(1) + dev_exp<P>(-(xa[u] + bb)));
-        xa[u] = h < H ? v : P(0);
-        if (valid && h < H) a1w[(size_t)h * a.lda + bcol] = v;
       }
     }
   }
@@ -283,58 +269,13 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
     __syncthreads();
     if (t == 0 && vb * COLS < a.n) a.loss_partial[vb] = lred[0] + lred[1] + lred[2] + lred[3];
   }
-  // ---- partial dW2 / db2 over this block's 16 columns (reduced by the weight-gradient launch):
-  //      stage a1 and D of the block in LDS, then every thread does whole 16-term dot products
-  //      (cross-lane shuffles of 80 values per thread cost ~13 us here; LDS staging ~0.3 us)
-  const bool gp = HPT > 0 && a.gpart != nullptr;
-  const int gstride = C * H + H + C;
-  float* gpb = gp ? a.gpart + (size_t)vb * gstride : nullptr;
-  if constexpr (HPT > 0) {
-    if (gp) {
-#pragma unroll
-      for (int u = 0; u < HPT; ++u) gs_x[part + u * NPART][col] = valid ? (float)xa[u] : 0.f;
-      if (part == 0) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) gs_d[c][col] = valid ? (float)z[c] : 0.f;
-      }
-      __syncthreads();
-      for (int e = t; e < C * H + C; e += 256) {
-        float acc = 0.f;
-        if (e < C * H) {
-          const int c = e / H, h = e - c * H;
-#pragma unroll
-          for (int k = 0; k < COLS; ++k) acc += gs_d[c][k] * gs_x[h][k];
-          gpb[e] = acc;
-        } else {
-          const int c = e - C * H;
-#pragma unroll
-          for (int k = 0; k < COLS; ++k) acc += gs_d[c][k];
-          gpb[C * H + H + c] = acc;
-        }
-      }
-      __syncthreads();  // gs_x is reused for dZ1 below
-    }
-  }
   // ---- pass 2: dZ1 = (W2^T D) .* a1 .* (1 - a1)
   hstamp(3, false);
-  if (!valid && !gp) return;
+  if (!valid) return;
   P* dZ1 = static_cast<P*>(a.dZ1);
   __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
   __hip_bfloat16* dZp = static_cast<__hip_bfloat16*>(a.dZ1_planes);
   const size_t pstride = (size_t)a.H * a.ldz;
-  auto emit_store = [&](int h, P dz) {
-    const size_t zi = (size_t)h * a.ldz + bcol;
-    dZ1[zi] = dz;
-    if (dZlo) dZlo[zi] = __float2bfloat16((float)dz);
-    if (dZp) {  // exact split into npz bf16 planes (mlp_split.h)
-      float r = (float)dz;
-      for (int p = 0; p < a.npz; ++p) {
-        const __hip_bfloat16 q = __float2bfloat16(r);
-        dZp[p * pstride + zi] = q;
-        r -= __bfloat162float(q);
-      }
-    }
-  };
   auto emit = [&](int h, P x) {
     P da = P(0);
 #pragma unroll
@@ -353,29 +294,6 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
     }
   };
   if constexpr (HPT > 0) {
-    if (gp) {  // dZ1 as usual, plus its 16-column partial row sums (db1) through LDS
-#pragma unroll
-      for (int u = 0; u < HPT; ++u) {
-        const int h = part + u * NPART;
-        P dz = P(0);
-        if (valid && h < H) {
-          P da = P(0);
-#pragma unroll
-          for (int c = 0; c < NC; ++c) da += w2(c, h) * z[c];
-          dz = da * xa[u] * (P(1) - xa[u]);
-          emit_store(h, dz);
-        }
-        gs_x[h][col] = (float)dz;
-      }
-      __syncthreads();
-      if (t < H) {
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < COLS; ++k) acc += gs_x[t][k];
-        gpb[C * H + t] = acc;
-      }
-      return;
-    }
 #pragma unroll
     for (int u = 0; u < HPT; ++u) {
       const int h = part + u * NPART;
@@ -393,47 +311,8 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) char head_dyn[];
   __shared__ P zred[4][NC][kHeadCols];
   __shared__ float lred[4];
-  __shared__ float gs_x[HPT > 0 ? HPT * (256 / kHeadCols) : 1][kHeadCols + 1];
-  __shared__ float gs_d[NC][kHeadCols + 1];
-  head_block<P, NC, LDSW, HPT>(a, blockIdx.x, threadIdx.x, head_dyn, zred, lred, gs_x, gs_d);
+  head_block<P, NC, LDSW, HPT>(a, blockIdx.x, threadIdx.x, head_dyn, zred, lred);
 }
-
-// ------------------------------------------- lookahead step, launch "L2" (see parallel/lookahead.py)
-// Workgroups [0, ntiles): raw forward tiles An = W1 . X_next for the NEXT step (W1 already updated by
-// the previous launch).  The rest: two head blocks each (512 threads = 2 x 256) for THIS step, whose
-// a1 arrives as a pre-activation (HeadArgs::b1_pre).  Both halves are independent; the critical path
-// (head) and the off-path GEMM share one launch.
-struct EpiScaleStoreK {
-  float* out;
-  int ld;
-  __device__ __forceinline__ void prefetch(int, int, int, bool) {}
-  __device__ __forceinline__ void operator()(int, int row, int col, float v) { out[(size_t)row * ld + col] = v; }
-};
-
-template <int NC, int NPW>
-__global__ __launch_bounds__(512) void lookahead_l2_kernel(SplitStepArgs f, float* Aout, HeadArgs h, int ntiles,
-                                                          int tiles_n) {
-  __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];
-  extern __shared__ __attribute__((aligned(16))) char l2_dyn[];
-  __shared__ float zred[2][4][NC][kHeadCols];
-  __shared__ float lred[2][4];
-  __shared__ float gs_x[2][8 * (256 / kHeadCols)][kHeadCols + 1];
-  __shared__ float gs_d[2][NC][kHeadCols + 1];
-  if ((int)blockIdx.x < ntiles) {
-    const int bid = xcd_remap(blockIdx.x, ntiles);
-    TileGeom g{f.H, f.n, f.P, (bid / tiles_n) * 16, (bid % tiles_n) * 32};
-    EpiScaleStoreK epi{Aout, f.ld};
-    wsk_tile<__hip_bfloat16, 1, 2, 8, true, true, 1, 4, NPW, uint8_t>(
-        static_cast<const __hip_bfloat16*>(f.W1p), f.P, static_cast<const uint8_t*>(f.X), f.P, g, epi, red,
-        f.H * f.P * (int)sizeof(__hip_bfloat16));
-    return;
-  }
-  const int half = threadIdx.x >> 8;
-  const int vb = 2 * ((int)blockIdx.x - ntiles) + half;
-  head_block<float, NC, true, 8>(h, vb, threadIdx.x & 255, l2_dyn + half * head_lds_elems(h.H, NC) * (int)sizeof(float),
-                                 zred[half], lred[half], gs_x[half], gs_d[half]);
-}
-
 
 // ------------------------------------------------ K2 on MFMA: 32 columns per 512-thread workgroup
 // (fp32 params, train mode, H <= 128, C <= 16).  The VALU head above is latency-bound at these sizes
@@ -616,7 +495,7 @@ __global__ __launch_bounds__(512) void head32_kernel(HeadArgs a) {
 }
 
 bool head32_ok(const HeadArgs& a) {
-  return a.mode == HEAD_TRAIN && a.H <= kH32MaxH && a.C <= 16 && !a.gpart && !a.b1_pre;
+  return a.mode == HEAD_TRAIN && a.H <= kH32MaxH && a.C <= 16;
 }
 
 // ------------------------------------- forward GEMM + head in ONE launch (split path, H <= 128)
@@ -1327,28 +1206,6 @@ void mlp_forward1(DType dt, const void* W1g, const void* b1, const void* X, int 
 
 int mlp_head_num_blocks(int n) { return cdiv(n, kHeadCols); }
 
-void mlp_lookahead_l2(const SplitStepArgs& f, float* Aout, const HeadArgs& h, bool with_next, hipStream_t s) {
-  CME_REQUIRE(h.H <= 8 * (256 / kHeadCols) && h.C <= kCMax && h.b1_pre && h.mode == HEAD_TRAIN,
-              "lookahead: H <= 128, train-mode head with b1_pre");
-  CME_REQUIRE(reinterpret_cast<uintptr_t>(f.X) % 4 == 0 && reinterpret_cast<uintptr_t>(f.W1p) % 16 == 0 &&
-                  f.P % 8 == 0,
-              "lookahead: aligned operands");
-  const int tiles_n = cdiv(f.n, 32), ntiles = with_next ? cdiv(f.H, 16) * tiles_n : 0;
-  const int nwg = ntiles + cdiv(cdiv(h.n, kHeadCols), 2);
-  const int NC = h.C <= 10 ? 10 : 16;
-  const size_t dyn = 2 * (size_t)head_lds_elems(h.H, NC) * sizeof(float);
-#define CME_L2(nc, np) lookahead_l2_kernel<nc, np><<<nwg, 512, dyn, s>>>(f, Aout, h, ntiles, tiles_n)
-  if (NC == 10) {
-    if (f.npw == 3) CME_L2(10, 3);
-    else CME_L2(10, 1);
-  } else {
-    if (f.npw == 3) CME_L2(16, 3);
-    else CME_L2(16, 1);
-  }
-#undef CME_L2
-  CME_LAUNCH_CHECK(s);
-}
-
 bool mlp_fwd1_head_ok(const SplitStepArgs& f, const HeadArgs& h) {
   return head32_ok(h) && f.H == h.H && f.n == h.n && f.ld % 4 == 0 && h.lda == f.ld &&
          (int64_t)f.H * f.ld * 4 < (int64_t)kOOB && f.a1 == h.a1;
@@ -1359,25 +1216,18 @@ void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters
   CME_REQUIRE(mlp_fwd1_head_ok(f, h), "fwd1_head: H <= 128, C <= 16, train-mode head over the same a1");
   CME_REQUIRE((int64_t)f.H * f.P * 2 * f.npw < (int64_t)kOOB && (int64_t)f.n * f.P < (int64_t)kOOB,
               "fwd1_head: operand too large for 32-bit buffer offsets");
-  // CME_FH_COLS=64: 64-column a1 tiles (A/B tests; measured 15.4 vs 10.3 us at 784-100-10, n=800 -- the
-  // last arriver then runs two head passes back to back)
-  static const int nbt = [] {
-    const char* e = std::getenv("CME_FH_COLS");
-    return (e && std::atoi(e) == 64) ? 4 : 2;
-  }();
+  // 32-column a1 tiles (64-column tiles measured 15.4 vs 10.3 us at 784-100-10, n=800: the last arriver
+  // then runs two head passes back to back)
+  constexpr int nbt = 2;
   const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 16 * nbt);
   CME_REQUIRE(counters != nullptr && tn <= max_tiles, "fwd1_head: counter array too small");
   const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 && reinterpret_cast<uintptr_t>(f.W1p) % 16 == 0 &&
                    f.P % 8 == 0;
   const int nwg = 8 * tm * cdiv(tn, 8);
-#define CME_FH(np, nb)                                                                    \
-  if (vec) fwd1_head_kernel<np, 1, nb><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);       \
-  else fwd1_head_kernel<np, 0, nb><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);
-  if (nbt == 4) {
-    if (f.npw == 3) { CME_FH(3, 4) } else { CME_FH(1, 4) }
-  } else {
-    if (f.npw == 3) { CME_FH(3, 2) } else { CME_FH(1, 2) }
-  }
+#define CME_FH(np)                                                                         \
+  if (vec) fwd1_head_kernel<np, 1, nbt><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);       \
+  else fwd1_head_kernel<np, 0, nbt><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);
+  if (f.npw == 3) { CME_FH(3) } else { CME_FH(1) }
 #undef CME_FH
   CME_LAUNCH_CHECK(s);
 }
@@ -1389,18 +1239,14 @@ int64_t head_big_scratch_floats(int H, int n) { return (int64_t)cdiv(H, 64) * kC
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
   CME_REQUIRE(a.C >= 1 && a.C <= kCMax, "mlp_head: 1 <= C <= 16 required");
-  if (a.z2part && a.z2_chunks > 0 && dt != DType::F64 && a.mode == HEAD_TRAIN && a.C <= 16 && !a.b1_pre &&
-      !a.gpart) {  // partials left by the forward GEMM
+  if (a.z2part && a.z2_chunks > 0 && dt != DType::F64 && a.mode == HEAD_TRAIN && a.C <= 16) {
+    // partials left by the forward GEMM
     CME_REQUIRE((int64_t)a.z2_chunks * 16 * a.lda < (int64_t)kOOB / 4 && (int64_t)a.H * a.lda < (int64_t)kOOB / 4,
                 "mlp_head: z2 partials too large for 32-bit buffer offsets");
     const int nct = cdiv(a.n, kHWCols);
-    // row tiles per wave: the largest RT that still gives >= 256 workgroups (CME_HW_RT=1|2|4 forces one)
-    static const int force_rt = [] {
-      const char* e = std::getenv("CME_HW_RT");
-      return e ? std::atoi(e) : 0;
-    }();
-    const int rt = force_rt ? force_rt
-                            : (cdiv(a.H, 512) * nct >= 256 ? 4 : (cdiv(a.H, 256) * nct >= 256 ? 2 : 1));
+    // row tiles per wave: the largest RT that still gives >= 256 workgroups (RT 1/2/4 measured at H=1024
+    // and 4096: this choice is the best or tied)
+    const int rt = cdiv(a.H, 512) * nct >= 256 ? 4 : (cdiv(a.H, 256) * nct >= 256 ? 2 : 1);
     if (rt == 4) head_wide_kernel<4><<<cdiv(a.H, 512) * nct, 512, 0, s>>>(a, cdiv(a.H, 512));
     else if (rt == 2) head_wide_kernel<2><<<cdiv(a.H, 256) * nct, 512, 0, s>>>(a, cdiv(a.H, 256));
     else head_wide_kernel<1><<<cdiv(a.H, 128) * nct, 512, 0, s>>>(a, cdiv(a.H, 128));
@@ -1414,8 +1260,7 @@ void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
     CME_LAUNCH_CHECK(s);
     return;
   }
-  if (dt != DType::F64 && head32_ok(a) && (int64_t)a.H * a.lda < (int64_t)kOOB / 4 &&
-      std::getenv("CME_VALU_HEAD") == nullptr) {  // MFMA head (CME_VALU_HEAD=1: the VALU form, A/B tests)
+  if (dt != DType::F64 && head32_ok(a) && (int64_t)a.H * a.lda < (int64_t)kOOB / 4) {  // MFMA head
     head32_kernel<<<cdiv(a.n, kH32Cols), 512, 0, s>>>(a);
     CME_LAUNCH_CHECK(s);
     return;

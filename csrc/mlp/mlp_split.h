@@ -40,7 +40,6 @@ struct XgmiFuse {
   int rank = 0, world = 0;
   int64_t npad = 0;
   int64_t off_b1 = 0, off_W2 = 0, off_b2 = 0;  // flat-arena offsets ([W1|b1|W2|b2], 64-aligned)
-  int variant = 0;  // diagnostics (CME_XF_VARIANT): bit0 relaxed flag store, bit1 extra acquire fence
 };
 
 struct SplitStepArgs {
@@ -67,23 +66,9 @@ struct SplitStepArgs {
   // weight-gradient launch selection (bucketed all-reduce overlap): wg_parts bit0 = dW1 rows
   // [w1_row0, w1_row0 + w1_rows) (w1_rows < 0: all), bit1 = dW2 + bias gradients
   int wg_parts = 3, w1_row0 = 0, w1_rows = -1;
-  // when the head produced per-block partial sums of dW2 / db1 / db2 (HeadArgs::gpart), the
-  // weight-gradient launch reduces those instead of recomputing them from D and a1
-  const float* gpart = nullptr;
-  int gblocks = 0;
   // XT carries an extra all-ones feature row P: the dW1 GEMM's column P is then sum_b dZ1[h][b] = db1[h]
   // (exact, same planes), so db1 / b1 come out of the dW1 launch and the role kernel only does dW2 / db2
   int bias_col = 0;
-  // role selection inside the weight-gradient launch (bit0 dW2, bit1 db1, bit2 db2); 7 = all
-  int role_mask = 7;
-  // lookahead (single process, see parallel/lookahead.py): the same launch also computes the NEXT
-  // step's pre-activation  z1n = c1 * An - c2 * (dZ1 . GTn^T)  on extra tiles, where An = W1 X_next
-  // (raw), GTn[j][k] = x_next_j . x_k (exact integer Gram of the two batches, fp32); zero tiles: off
-  const float* GTn = nullptr;
-  int ldg = 0, n_next = 0;
-  const float* An = nullptr;
-  float* z1n = nullptr;
-  float c1 = 0.f, c2 = 0.f;
   XgmiFuse xf;
   // wide layers (LDS GEMM forward): when set, the forward GEMM's tile epilogue also leaves the head's
   // z2 partial sums, z2part[row tile][16][ld] = W2[:, tile rows] . a1[tile rows, :] (v_mfma_f32_16x16x4
@@ -102,8 +87,6 @@ void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);
 // tiled forward only: a1 = sigmoid(W1 X + b1) (pair with mlp_head for the 3-kernel step)
 void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s);
 void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s);
-// raw forward tiles An = W1 . X (no bias / activation) into `out` [H][ld], times `scale`
-void mlp_split_fwd_raw(const SplitStepArgs& a, float* out, float scale, hipStream_t s);
 int mlp_split_fwdhead_blocks(int n);
 
 // planes[p][i] for i < n: exact np-way bf16 split of W[i] (np = 1: plain rounding).

@@ -2,7 +2,6 @@
 #include "mlp_split.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 #include "lds_gemm.h"
 #include "mma_tile.h"
@@ -218,25 +217,6 @@ struct EpiSig {
   }
 };
 
-struct EpiScaleStore {
-  float* out;
-  int ld;
-  float s;
-  __device__ __forceinline__ void prefetch(int, int, int, bool) {}
-  __device__ __forceinline__ void operator()(int, int row, int col, float v) { out[(size_t)row * ld + col] = v * s; }
-};
-
-template <int NPW, int VEC>
-__global__ __launch_bounds__(64 * kF1KS) void fwd_raw_kernel(SplitStepArgs a, int tiles_n, float* out, float scale) {
-  __shared__ __attribute__((aligned(16))) float red[kF1KS * kF1MB * kF1NB * 4 * 64];
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  TileGeom g{a.H, a.n, a.P, (bid / tiles_n) * 16 * kF1MB, (bid % tiles_n) * 16 * kF1NB};
-  EpiScaleStore epi{out, a.ld, scale};
-  wsk_tile<bf16, kF1MB, kF1NB, kF1KS, true, true, VEC, 4, NPW, uint8_t>(static_cast<const bf16*>(a.W1p), a.P,
-                                                               static_cast<const uint8_t*>(a.X), a.P, g, epi, red,
-                                                               a.H * a.P * (int)sizeof(bf16));
-}
-
 template <int NPW, int VEC>
 __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a, int tiles_n) {
   __shared__ __attribute__((aligned(16))) float red[kF1KS * kF1MB * kF1NB * 4 * 64];
@@ -268,27 +248,34 @@ __device__ __forceinline__ float xf_load(const void* base, int64_t idx) {
   return __builtin_bit_cast(float, w);
 }
 
-__device__ __forceinline__ uint32_t xf_begin(const XgmiFuse& x, int tile, uint32_t* s_ep) {
-  if (threadIdx.x == 0) *s_ep = x.epochs[tile] + 1;
+// s_xf[0]: the tile's epoch; s_xf[1]: 1 = the tile is NOT exchanged or applied (block-uniform via LDS).
+// A rank whose earlier wait timed out stops taking part altogether: it neither writes its IPC buffer (a
+// peer may still be reading the other epoch's half there) nor publishes flags nor applies updates, so
+// its peers time out too and every rank reports the error instead of stepping on stale data.
+__device__ __forceinline__ bool xf_begin(const XgmiFuse& x, int tile, uint32_t* s_xf) {
+  if (threadIdx.x == 0) {
+    s_xf[0] = x.epochs[tile] + 1;
+    s_xf[1] = __hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  }
   __syncthreads();
-  return *s_ep;
+  return s_xf[1] == 0;
 }
 
-// every thread's gradient stores of this tile are complete -> publish, wait for the peers
-__device__ __forceinline__ void xf_exchange(const XgmiFuse& x, int tile, uint32_t ep) {
+// every thread's gradient stores of this tile are complete -> publish, wait for the peers.  Returns false
+// (block-uniform) when a peer's flag never arrived: the caller then applies nothing for this tile.
+__device__ __forceinline__ bool xf_exchange(const XgmiFuse& x, int tile, uint32_t* s_xf) {
+  const uint32_t ep = s_xf[0];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int t = threadIdx.x;
   if (t < x.world) {
-    if (x.variant & 1)
-      __hip_atomic_store(x.peerflags[t] + tile * 8 + x.rank, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else
-      __hip_atomic_store(x.peerflags[t] + tile * 8 + x.rank, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(x.peerflags[t] + tile * 8 + x.rank, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t spins = 0;
     const uint32_t* f = x.myflags + tile * 8 + t;
     while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) < 0) {
       if (++spins > kXfSpinLimit) {
         atomicExch(x.err, 1);
+        s_xf[1] = 1;  // (the waiting lanes may race here: they all store 1)
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -297,7 +284,7 @@ __device__ __forceinline__ void xf_exchange(const XgmiFuse& x, int tile, uint32_
   __syncthreads();
   // no acquire fence: every peer datum is read with system-coherent loads (xf_load) issued after the
   // flag was observed; a full L2 invalidation per tile measured +9 us per step (182 tiles)
-  if (x.variant & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  return s_xf[1] == 0;
 }
 
 __device__ __forceinline__ float xf_sum(const XgmiFuse& x, int64_t idx) {
@@ -306,8 +293,8 @@ __device__ __forceinline__ float xf_sum(const XgmiFuse& x, int64_t idx) {
   return s;
 }
 
-__device__ __forceinline__ void xf_end(const XgmiFuse& x, int tile, uint32_t ep) {
-  if (threadIdx.x == 0) x.epochs[tile] = ep;
+__device__ __forceinline__ void xf_end(const XgmiFuse& x, int tile, const uint32_t* s_xf) {
+  if (threadIdx.x == 0) x.epochs[tile] = s_xf[0];
 }
 
 // ======================================================================
@@ -353,20 +340,6 @@ struct EpiW2 {
   }
 };
 
-struct EpiCombine {
-  const float* An;
-  float* z1n;
-  int ld;
-  float c1, c2;
-  float pre[kEpiMaxQ];
-  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
-    pre[q] = buf_load1<float>(make_rsrc(An), ok ? (row * ld + col) * 4 : kOOB);
-  }
-  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
-    z1n[(size_t)row * ld + col] = c1 * pre[q] - c2 * v;
-  }
-};
-
 struct EpiW1 {
   float* W1;
   float* gW1;
@@ -405,46 +378,34 @@ struct EpiW1 {
 };
 
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
-                                            uint32_t* s_ep);
+                                            uint32_t* s_xf);
 
 template <int NPZ, int VEC>
-__global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2, int tc,
-                                                          int tcn) {
+__global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
-  if ((int)blockIdx.x < tc) {  // ---- lookahead: next step's pre-activation (critical path: first ids)
-    const int tb = blockIdx.x;
-    TileGeom g{a.H, a.n_next, a.n, (tb / tcn) * 16 * kWMB, (tb % tcn) * 16 * kWNB};
-    EpiCombine epi{a.An, a.z1n, a.ld, a.c1, a.c2, {}};
-    if (VEC == 1)
-      wsk_tile<float, kWMB, kWNB, kWKS, true, true, 1, 8>(a.dZ1, a.ld, a.GTn, a.ldg, g, epi, red);
-    else
-      wsk_tile<float, kWMB, kWNB, kWKS, true, true, 0, 8>(a.dZ1, a.ld, a.GTn, a.ldg, g, epi, red);
-    return;
-  }
-  const int bid = blockIdx.x - tc;
+  __shared__ uint32_t s_xf[2];
+  const int bid = blockIdx.x;
   const float reg = (float)a.reg, lr = (float)a.lr;
   const bool fused = a.xf.world > 0;
-  __shared__ uint32_t s_ep;
   if (bid < t1) {  // ---- dW1 tile
     const int tb = xcd_remap(bid, t1);
     const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
     TileGeom g{r1, a.P + a.bias_col, a.n, a.w1_row0 + (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
     float *gw = a.gW1, *gb = a.gb1;
-    uint32_t ep = 0;
-    if (fused) {  // gradients straight into this step's half of the IPC buffer
-      ep = xf_begin(a.xf, bid, &s_ep);
-      gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(ep & 1u) * a.xf.npad;
+    // fused: gradients straight into this step's half of the IPC buffer (unless this rank is in error)
+    const bool live = fused && xf_begin(a.xf, bid, s_xf);
+    if (live) {
+      gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(s_xf[0] & 1u) * a.xf.npad;
       gb = gw + a.xf.off_b1;
     }
     EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.npw, reg, lr,
-              a.xscale, {}, a.b1, gb, fused ? 1 : 0};
+              a.xscale, {}, a.b1, gb, live ? 1 : 0};
     constexpr int U = 4;
     wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
                                                               static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
                                                               red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
-    if (fused) {  // all-reduce this tile with the peers, then SGD + bf16 planes
-      xf_exchange(a.xf, bid, ep);
-      const int64_t half = (int64_t)(ep & 1u) * a.xf.npad;
+    if (live && xf_exchange(a.xf, bid, s_xf)) {  // all-reduced with the peers: SGD + bf16 planes
+      const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf.npad;
       constexpr int TW = 16 * kWNB;
       for (int e = threadIdx.x; e < 16 * kWMB * TW; e += kWT) {
         const int row = g.m0 + e / TW, col = g.n0 + e % TW;
@@ -459,50 +420,20 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
           a.b1[row] -= lr * xf_sum(a.xf, half + a.xf.off_b1 + row);
         }
       }
-      xf_end(a.xf, bid, ep);
+      xf_end(a.xf, bid, s_xf);
     }
     return;
   }
-  wgrad_roles(a, bid, t1, t2, red, &s_ep);
+  wgrad_roles(a, bid, t1, t2, red, s_xf);
 }
 
-// The weight-gradient launch's workgroups past its t1 dW1 tiles: the head-partials reduction (gpart), or
-// t2 dW2 tiles (+ the fused xGMI exchange) followed by the bias-row workgroups.  `red`: kWKS * 4 * 64
-// floats of LDS.  Shared by wgrad_split_kernel and wgrad_big_kernel (the wide path's extra workgroups).
+// The weight-gradient launch's workgroups past its t1 dW1 tiles: t2 dW2 tiles (+ the fused xGMI exchange)
+// followed by the bias-row workgroups.  `red`: kWKS * 4 * 64 floats of LDS, `s_xf`: 2 words of LDS.
+// Shared by wgrad_split_kernel and wgrad_big_kernel (the wide path's extra workgroups).
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
-                                            uint32_t* s_ep) {
+                                            uint32_t* s_xf) {
   const float reg = (float)a.reg, lr = (float)a.lr;
   const bool fused = a.xf.world > 0;
-  if (a.gpart) {  // ---- reduce the head's per-block partials of dW2 | db1 | db2, then update
-    const int tot = a.C * a.H + a.H + a.C;
-    const int e = (bid - t1) * kWT + threadIdx.x;
-    if (e >= tot) return;
-    float s = 0.f;
-    int b = 0;
-    for (; b + 8 <= a.gblocks; b += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = a.gpart[(size_t)(b + u) * tot + e];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; b < a.gblocks; ++b) s += a.gpart[(size_t)b * tot + e];
-    if (e < a.C * a.H) {
-      const float w = a.W2[e];
-      const float g = s + reg * w;
-      if (a.sgd) a.W2[e] = w - lr * g;
-      else a.gW2[e] = g;
-    } else if (e < a.C * a.H + a.H) {
-      const int h = e - a.C * a.H;
-      if (a.sgd) a.b1[h] -= lr * s;
-      else a.gb1[h] = s;
-    } else {
-      const int c = e - a.C * a.H - a.H;
-      if (a.sgd) a.b2[c] -= lr * s;
-      else a.gb2[c] = s;
-    }
-    return;
-  }
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (bid < t1 + t2) {  // ---- dW2 = D a1^T on MFMA (exact f32 16x16x4): one 16x16 tile per workgroup,
@@ -510,40 +441,36 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     const int tb = bid - t1;
     TileGeom g{a.C, a.H, a.n, 0, tb * 16};
     float* gw = a.gW2;
-    uint32_t ep = 0;
-    if (fused) {
-      ep = xf_begin(a.xf, bid, s_ep);
-      gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(ep & 1u) * a.xf.npad + a.xf.off_W2;
-    }
-    EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, fused ? 1 : 0, reg, lr, {}};
+    const bool live = fused && xf_begin(a.xf, bid, s_xf);
+    const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf.npad;
+    if (live) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
+    EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, live ? 1 : 0, reg, lr, {}};
     if (a.n % 4 == 0)
       wsk_tile<float, 1, 1, kWKS, true, true, 1, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red);
     else
       wsk_tile<float, 1, 1, kWKS, true, true, 0, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red);
-    if (fused) {
-      const int64_t half = (int64_t)(ep & 1u) * a.xf.npad;
-      const bool with_b2 = tb == 0;  // db2 (fused mode has no separate bias role): one wave per class
-      if (with_b2) {
-        for (int c = wv; c < a.C; c += kWKS) {
-          const float sc = wave_sum(row_sum(a.D + (size_t)c * a.ld, a.n, lane));
-          if (lane == 0) xf_store(static_cast<float*>(a.xf.mybuf), half + a.xf.off_b2 + c, sc);
-        }
+    if (!live) return;
+    const bool with_b2 = tb == 0;  // db2 (fused mode has no separate bias role): one wave per class
+    if (with_b2) {
+      for (int c = wv; c < a.C; c += kWKS) {
+        const float sc = wave_sum(row_sum(a.D + (size_t)c * a.ld, a.n, lane));
+        if (lane == 0) xf_store(static_cast<float*>(a.xf.mybuf), half + a.xf.off_b2 + c, sc);
       }
-      xf_exchange(a.xf, bid, ep);
-      const int ne = 16 * 16 + (with_b2 ? a.C : 0);
-      for (int e = threadIdx.x; e < ne; e += kWT) {
-        if (e < 256) {
-          const int c = e / 16, h = tb * 16 + e % 16;
-          if (c >= a.C || h >= a.H) continue;
-          const int64_t i = (int64_t)c * a.H + h;
-          a.W2[i] -= lr * xf_sum(a.xf, half + a.xf.off_W2 + i);
-        } else {
-          const int c = e - 256;
-          a.b2[c] -= lr * xf_sum(a.xf, half + a.xf.off_b2 + c);
-        }
-      }
-      xf_end(a.xf, bid, ep);
     }
+    if (!xf_exchange(a.xf, bid, s_xf)) return;
+    const int ne = 16 * 16 + (with_b2 ? a.C : 0);
+    for (int e = threadIdx.x; e < ne; e += kWT) {
+      if (e < 256) {
+        const int c = e / 16, h = tb * 16 + e % 16;
+        if (c >= a.C || h >= a.H) continue;
+        const int64_t i = (int64_t)c * a.H + h;
+        a.W2[i] -= lr * xf_sum(a.xf, half + a.xf.off_W2 + i);
+      } else {
+        const int c = e - 256;
+        a.b2[c] -= lr * xf_sum(a.xf, half + a.xf.off_b2 + c);
+      }
+    }
+    xf_end(a.xf, bid, s_xf);
     return;
   }
   // ---- bias gradients: one wave per row; rows [0,H) -> db1 from dZ1, [H,H+C) -> db2 from D
@@ -717,14 +644,8 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 inline bool al4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
 
-constexpr int kBigMinH = 512;
-bool big_path_disabled() {  // CME_NO_BIG_GEMM=1: force the wave-split-K kernels (A/B tests)
-  static const bool v = [] {
-    const char* e = std::getenv("CME_NO_BIG_GEMM");
-    return e && e[0] == '1';
-  }();
-  return v;
-}  // below this the wave-split-K kernels win (too few tiles to fill the chip)
+constexpr int kBigMinH = 512;  // below this the wave-split-K kernels win (too few tiles to fill the chip)
+constexpr int kBigThreads = 512;
 
 // true when the LDS-staged GEMM path applies: wide hidden layer and 16-byte aligned K-contiguous rows
 bool big_fwd_ok(const SplitStepArgs& a) {
@@ -732,15 +653,6 @@ bool big_fwd_ok(const SplitStepArgs& a) {
 }
 bool big_wgrad_ok(const SplitStepArgs& a) {
   return a.H >= kBigMinH && a.n % 16 == 0 && a.ld % 8 == 0 && a.ldxt % 16 == 0 && al16(a.dZ1p) && al16(a.XT);
-}
-
-// threads per big-GEMM workgroup: 512 (8 waves, default) or 256 (CME_BIG_THREADS=256, A/B tests)
-int big_threads() {
-  static const int v = [] {
-    const char* e = std::getenv("CME_BIG_THREADS");
-    return (e && std::atoi(e) == 256) ? 256 : 512;
-  }();
-  return v;
 }
 
 // 128x128 tiles when that still gives ~200+ workgroups, else 64x64
@@ -769,8 +681,7 @@ void launch_fwd1_big_nt(const SplitStepArgs& a, hipStream_t s) {
 
 template <int NP>
 void launch_fwd1_big(const SplitStepArgs& a, hipStream_t s) {
-  if (big_threads() == 512) launch_fwd1_big_nt<NP, 512>(a, s);
-  else launch_fwd1_big_nt<NP, 256>(a, s);
+  launch_fwd1_big_nt<NP, kBigThreads>(a, s);
 }
 
 // t2 / tb > 0: that many dW2-tile / bias-row role workgroups ride in the same launch after the dW1 tiles
@@ -800,8 +711,8 @@ void launch_wgrad_big_nt(const SplitStepArgs& a, int t2, int tb, hipStream_t s) 
 
 template <int NP>
 void launch_wgrad_big(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
-  if (big_threads() == 512) launch_wgrad_big_nt<NP, 512>(a, t2, tb, s);
-  else launch_wgrad_big_nt<NP, 256>(a, 0, 0, s);  // role workgroups need kWT threads
+  static_assert(kBigThreads == kWT, "the role workgroups riding in the dW1 launch need kWT threads");
+  launch_wgrad_big_nt<NP, kBigThreads>(a, t2, tb, s);
 }
 
 template <int NPW, int NPZ, int NC>
@@ -823,7 +734,7 @@ void launch_fwdhead_nc(const SplitStepArgs& a, hipStream_t s) {
 int mlp_split_fwdhead_blocks(int n) { return cdiv(n, kFHCols); }
 
 int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a) {
-  if (!a.z2part || a.C > 16 || a.n <= 0 || !big_fwd_ok(a) || big_path_disabled()) return 0;
+  if (!a.z2part || a.C > 16 || a.n <= 0 || !big_fwd_ok(a)) return 0;
   const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
   return t128 >= 192 ? cdiv(a.H, 128) : cdiv(a.H, 64);  // must match launch_fwd1_big_nt's tile choice
 }
@@ -833,7 +744,7 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
   CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
               "split path: operand too large for 32-bit buffer offsets");
   CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
-  if (big_fwd_ok(a) && !big_path_disabled()) {
+  if (big_fwd_ok(a)) {
     if (a.npw == 3) launch_fwd1_big<3>(a, s);
     else launch_fwd1_big<1>(a, s);
     CME_LAUNCH_CHECK(s);
@@ -847,21 +758,6 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
   else fwd1_split_kernel<np, 0><<<grid, 64 * kF1KS, 0, s>>>(a, tn);
   if (a.npw == 3) { CME_F1(3) } else { CME_F1(1) }
 #undef CME_F1
-  CME_LAUNCH_CHECK(s);
-}
-
-void mlp_split_fwd_raw(const SplitStepArgs& a, float* out, float scale, hipStream_t s) {
-  if (a.n <= 0) return;
-  CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
-  const int tn = cdiv(a.n, 16 * kF1NB), tm = cdiv(a.H, 16 * kF1MB);
-  const bool vec = al4(a.X) && al16(a.W1p) && a.P % 8 == 0;
-  if (a.npw == 3) {
-    if (vec) fwd_raw_kernel<3, 1><<<tm * tn, 64 * kF1KS, 0, s>>>(a, tn, out, scale);
-    else fwd_raw_kernel<3, 0><<<tm * tn, 64 * kF1KS, 0, s>>>(a, tn, out, scale);
-  } else {
-    if (vec) fwd_raw_kernel<1, 1><<<tm * tn, 64 * kF1KS, 0, s>>>(a, tn, out, scale);
-    else fwd_raw_kernel<1, 0><<<tm * tn, 64 * kF1KS, 0, s>>>(a, tn, out, scale);
-  }
   CME_LAUNCH_CHECK(s);
 }
 
@@ -883,50 +779,39 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   CME_REQUIRE((int64_t)a.H * a.ld * 2 * a.npz < (int64_t)kOOB && (int64_t)a.P * a.ldxt < (int64_t)kOOB,
               "split path: operand too large for 32-bit buffer offsets");
   CME_REQUIRE(a.w1_row0 >= 0 && (a.w1_rows < 0 || a.w1_row0 + a.w1_rows <= a.H), "wgrad: bad dW1 row range");
-  const bool big = big_wgrad_ok(a) && !big_path_disabled();
+  const bool fused = a.xf.world > 0;
+  const bool big = big_wgrad_ok(a) && !fused;
   const bool do_w1 = (a.wg_parts & 1) && a.w1_rows != 0, do_roles = (a.wg_parts & 2) != 0;
-  if (big && do_w1) {  // dW1 as a blocked GEMM
-    // the dW2 / db2 roles ride in the same launch as extra workgroups: one launch and its boundary fewer,
-    // and they run on the CUs the dW1 tiles leave idle (else they follow in the split kernel below, t1 = 0;
-    // CME_NO_ROLE_FOLD=1 for A/B tests)
-    static const bool no_fold = std::getenv("CME_NO_ROLE_FOLD") != nullptr;
-    const bool fold = do_roles && !a.gpart && a.xf.world == 0 && big_threads() == kWT && !no_fold;
-    const int t2f = fold ? cdiv(a.H, 16) : 0;
-    const int tbf = fold ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
+  if (big && do_w1) {  // dW1 as a blocked GEMM; the dW2 / db2 roles ride in the same launch as extra
+    // workgroups: one launch and its boundary fewer, and they run on the CUs the dW1 tiles leave idle
+    const int t2f = do_roles ? cdiv(a.H, 16) : 0;
+    const int tbf = do_roles ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
     if (a.npz == 3) launch_wgrad_big<3>(a, t2f, tbf, s);
     else launch_wgrad_big<1>(a, t2f, tbf, s);
-    if (fold) {
-      CME_LAUNCH_CHECK(s);
-      return;
-    }
+    CME_LAUNCH_CHECK(s);
+    return;
   }
   const int w1rows = a.w1_rows < 0 ? a.H : a.w1_rows;
-  const int t1n = cdiv(a.P + a.bias_col, 16 * kWNB), t1 = (big || !do_w1) ? 0 : cdiv(w1rows, 16 * kWMB) * t1n;
-  const int t2 = !do_roles ? 0 : (a.gpart ? cdiv(a.C * a.H + a.H + a.C, kWT) : cdiv(a.H, 16));
-  const bool fused = a.xf.world > 0;
+  const int t1n = cdiv(a.P + a.bias_col, 16 * kWNB), t1 = do_w1 ? cdiv(w1rows, 16 * kWMB) * t1n : 0;
+  const int t2 = do_roles ? cdiv(a.H, 16) : 0;
   if (fused)
-    CME_REQUIRE(!big && do_w1 && do_roles && a.bias_col && !a.gpart && !a.GTn && a.w1_row0 == 0 && a.w1_rows < 0 &&
-                    a.C <= 16 && a.xf.world <= 8 && t1 + t2 <= mlp_split_fused_tiles(a.P, a.H, 1 << 30),
+    CME_REQUIRE(do_w1 && do_roles && a.bias_col && a.w1_row0 == 0 && a.w1_rows < 0 && a.C <= 16 &&
+                    a.xf.world <= 8 && t1 + t2 <= mlp_split_fused_tiles(a.P, a.H, 1 << 30),
                 "wgrad: fused all-reduce needs the whole small-layer step with the all-ones XT feature");
   // fused mode: db2 comes from the first dW2 tile (no separate bias role)
-  const int tb = (do_roles && !a.gpart && !fused) ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
-  if (t1 + t2 + tb == 0 && !a.GTn) {
+  const int tb = (do_roles && !fused) ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
+  if (t1 + t2 + tb == 0) {
     CME_LAUNCH_CHECK(s);
     return;
   }
   // dZ1 planes: 16-byte vectors when n % 8 == 0, 8-byte halves when n % 4 == 0; XT bytes need 4-byte rows
   const bool base_ok = al16(a.dZ1p) && al4(a.XT) && a.ld % 8 == 0 && a.ldxt % 4 == 0;
   const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? 1 : (a.n % 4 == 0 ? 2 : 0));
-  const int tcn = a.GTn ? cdiv(a.n_next, 16 * kWNB) : 0;
-  const int tc = a.GTn ? cdiv(a.H, 16 * kWMB) * tcn : 0;
-  if (a.GTn)
-    CME_REQUIRE(a.n % 4 == 0 && a.ldg % 4 == 0 && a.ld % 4 == 0 && al16(a.GTn) && al16(a.dZ1) && vec == 1,
-                "lookahead: 16-byte aligned fp32 operands with n % 4 == 0");
-  const dim3 grid(tc + t1 + t2 + tb);
-#define CME_WG(npz)                                                                               \
-  if (vec == 1) wgrad_split_kernel<npz, 1><<<grid, kWT, 0, s>>>(a, t1, t1n, t2, tc, tcn);         \
-  else if (vec == 2) wgrad_split_kernel<npz, 2><<<grid, kWT, 0, s>>>(a, t1, t1n, t2, tc, tcn);    \
-  else wgrad_split_kernel<npz, 0><<<grid, kWT, 0, s>>>(a, t1, t1n, t2, tc, tcn);
+  const dim3 grid(t1 + t2 + tb);
+#define CME_WG(npz)                                                                   \
+  if (vec == 1) wgrad_split_kernel<npz, 1><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);      \
+  else if (vec == 2) wgrad_split_kernel<npz, 2><<<grid, kWT, 0, s>>>(a, t1, t1n, t2); \
+  else wgrad_split_kernel<npz, 0><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);
   if (a.npz == 3) { CME_WG(3) } else { CME_WG(1) }
 #undef CME_WG
   CME_LAUNCH_CHECK(s);

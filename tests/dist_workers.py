@@ -1,4 +1,5 @@
 """Worker entry points for the multi-process tests (must be importable by spawn)."""
+import hashlib
 import os
 
 import numpy as np
@@ -56,7 +57,23 @@ def nccl_graph_worker(out_dir):
         t2 = DataParallelTrainer(ref, use_graphs=True)  # NullComm: fused SGD
         t2.load(x, y)
         t2.train(2, 0.01, 1e-4)
-        np.savez(os.path.join(out_dir, "nccl.npz"), a=nn.W[0], b=ref.W[0], a1=nn.b[0], b1=ref.b[0])
+        # the overlapped RCCL backward (dW1 row chunks all-reduced on a side stream while the next chunk
+        # is computed), forced at world 1 and captured in the HIP graph, against the fused single-process step
+        outs = {}
+        for H in (1024, 4096):
+            nb = NeuralNetwork([784, H, 10])
+            rb = nb.copy()
+            tb = DataParallelTrainer(nb, comm=TorchDistComm(), use_graphs=True, overlap_chunks=4)
+            assert tb._bucketed and tb.use_graphs and len(tb._buckets()) == 4
+            tb.load(x, y)
+            tb.train(1, 0.01, 1e-4)
+            tr1 = DataParallelTrainer(rb, use_graphs=True)
+            tr1.load(x, y)
+            tr1.train(1, 0.01, 1e-4)
+            a = np.concatenate([nb.W[0].ravel(), nb.W[1].ravel(), nb.b[0].ravel(), nb.b[1].ravel()])
+            b = np.concatenate([rb.W[0].ravel(), rb.W[1].ravel(), rb.b[0].ravel(), rb.b[1].ravel()])
+            outs[f"bucketed_rel_{H}"] = np.abs(a - b).max() / np.abs(b).max()
+        np.savez(os.path.join(out_dir, "nccl.npz"), a=nn.W[0], b=ref.W[0], a1=nn.b[0], b1=ref.b[0], **outs)
     finally:
         dist.destroy_process_group()
 
@@ -196,3 +213,141 @@ def tp_train_worker(rank, world, comm, device, out_dir, H, N, B, E, lr, reg, dty
     st = tr.train(E, lr, reg, print_every=2, log=lambda *_: None)
     np.savez(os.path.join(out_dir, f"tp{rank}.npz"), W0=nn.W[0], W1=nn.W[1], b0=nn.b[0], b1=nn.b[1],
              losses=np.array(st.losses), pred=tr.predict(x[:200]))
+
+
+def xgmi_stall_worker(rank, world, comm, device, out_dir):
+    """A stalled peer (rank 1 skips a step) must make rank 0's xGMI all-reduce time out WITHOUT touching
+    params or bf16 planes, keep every later step a no-op on that rank, and surface as an error on EVERY
+    rank through the collective check (csrc/comm/xgmi_allreduce.hip, mlp_split.hip xf_exchange)."""
+    import time
+
+    from cme213_sp18_amd import NeuralNetwork
+    from cme213_sp18_amd.parallel import DataParallelTrainer
+    from cme213_sp18_amd.parallel.trainer import CommFailure
+    from cme213_sp18_amd.parallel.xgmi import XgmiBucket
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    res = {}
+    # ---- A: the separate all-reduce + SGD kernel
+    n, w1n = 5000, 3136
+    xb = XgmiBucket(comm.group, rank, world, n, torch.float32, dev)
+    params = torch.randn(n, generator=torch.Generator().manual_seed(1)).to(dev)
+    planes = torch.zeros(3, w1n, dtype=torch.bfloat16, device=dev)
+    grads = torch.full((n,), float(rank + 1), device=dev)
+    xb.sgd_(grads, params, 0.01, planes, 3, w1n)  # one good step on both ranks
+    torch.cuda.synchronize()
+    res["A_first_ok"] = float(xb.error() == 0)
+    comm.barrier()
+    if rank == 0:  # rank 1 stalls: it never joins this step
+        before = (params.clone(), planes.clone())
+        t0 = time.perf_counter()
+        xb.sgd_(grads, params, 0.01, planes, 3, w1n)
+        torch.cuda.synchronize()
+        res["A_timeout_s"] = time.perf_counter() - t0
+        res["A_err"] = float(xb.error())
+        res["A_untouched"] = float(torch.equal(params, before[0]) and torch.equal(planes, before[1]))
+        t0 = time.perf_counter()  # a rank in error applies nothing more and does not wait again
+        xb.sgd_(grads, params, 0.01, planes, 3, w1n)
+        torch.cuda.synchronize()
+        res["A_after_s"] = time.perf_counter() - t0
+        res["A_after_untouched"] = float(torch.equal(params, before[0]))
+    flag = comm.allreduce_scalar(float(xb.error()), op="max")
+    res["A_collective_err"] = float(flag > 0)
+    xb.close()
+    # ---- B: the all-reduce fused into the weight-gradient launch, through the trainer
+    x, y = synthetic_mnist(3200, seed=3)
+    nn = NeuralNetwork([784, 100, 10])
+    tr = DataParallelTrainer(nn, comm=comm, device=dev, batch_size=800, use_graphs=False, allreduce="xgmi")
+    tr.load(x, y)
+    res["B_fused"] = float(tr.fused_allreduce)
+    e = tr.engine
+    tr.step(0, 800, 0.05, 1e-4)
+    torch.cuda.synchronize()
+    comm.barrier()
+    if rank == 0:
+        before = (e.params.clone(), e.W1p.clone())
+        tr.step(800, 800, 0.05, 1e-4)  # rank 1 stalls
+        torch.cuda.synchronize()
+        res["B_untouched"] = float(torch.equal(e.params, before[0]) and torch.equal(e.W1p, before[1]))
+    res["B_comm_failed"] = float(tr.comm_failed())
+    # a whole epoch after the failure: rank 0 (in error) publishes nothing, so rank 1 times out once and
+    # applies nothing either; the epoch-end check raises on BOTH ranks
+    before = e.params.clone()
+    try:
+        tr.train(1, 0.05, 1e-4)
+        res["B_raised"] = 0.0
+    except CommFailure:
+        res["B_raised"] = 1.0
+    torch.cuda.synchronize()
+    res["B_epoch_untouched"] = float(torch.equal(e.params, before))
+    tr.close()
+    np.savez(os.path.join(out_dir, f"stall{rank}.npz"), **{k: np.array(v) for k, v in res.items()})
+
+
+def xgmi_stall_main(out_dir):
+    from cme213_sp18_amd.parallel.launcher import spawn
+
+    spawn(xgmi_stall_worker, 2, (out_dir,), backend="gloo")
+
+
+# ------------------------------------------------------------------ one rank per GPU (needs >= N GPUs)
+DP_MODES = (  # (name, H, trainer kwargs)
+    ("xgmi-fused", 100, dict(allreduce="xgmi")),
+    ("xgmi", 100, dict(allreduce="xgmi", fuse_allreduce=False)),
+    ("rccl", 100, dict(allreduce="rccl")),
+    ("rccl-bucketed", 4096, dict(allreduce="rccl", overlap_chunks=4)),
+    ("host", 100, dict(allreduce="host")),
+)
+
+
+def multigpu_dp_worker(rank, world, comm, device, out_dir, modes, scalings, steps):
+    """Every DP all-reduce path on `world` ranks, one per GPU (or sharing GPU 0 under CME_SHARED_GPU=1),
+    against a single-process run of the same global batch on this rank's GPU: all replicas must be
+    BITWISE identical, and the data-parallel result within fp32 reassociation of the single-process one.
+    weak: global batch 800*R (800 per rank); strong: 800 split over the ranks (800/R each,
+    fpcode/neural_network.cpp:458)."""
+    import json
+
+    from cme213_sp18_amd import NeuralNetwork
+    from cme213_sp18_amd.parallel import DataParallelTrainer
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    import torch.distributed as dist
+
+    res = {}
+    for name, H, kw in DP_MODES:
+        if name not in modes:
+            continue
+        for scaling in scalings:
+            B = 800 * world if scaling == "weak" else 800
+            x, y = synthetic_mnist(B * steps, seed=5)
+            nn = NeuralNetwork([784, H, 10])
+            ref = nn.copy()
+            tr = DataParallelTrainer(nn, comm=comm, device=device, batch_size=B, use_graphs=True, **kw)
+            tr.load(x, y)
+            impl = tr.allreduce_impl
+            p0 = tr.engine.params.detach().double().cpu()
+            tr.train(1, 0.05, 1e-4)
+            got = tr.engine.params.detach().double().cpu()
+            tr.close()
+            single = DataParallelTrainer(ref, device=device, batch_size=B, use_graphs=True)  # one process
+            single.load(x, y)
+            single.train(1, 0.05, 1e-4)
+            want = single.engine.params.detach().double().cpu()
+            digests = [None] * world
+            dist.all_gather_object(digests, hashlib.sha1(got.numpy().tobytes()).hexdigest(), group=comm.group)
+            key = f"{name}/{scaling}"
+            res[key] = {"impl": impl, "replicas_equal": len(set(digests)) == 1,
+                        "rel_vs_single": float((got - want).abs().max() / want.abs().max()),
+                        "moved": float((got - p0).abs().max())}
+    if rank == 0:
+        with open(os.path.join(out_dir, "multigpu.json"), "w") as f:
+            json.dump(res, f)
+
+
+def multigpu_dp_main(out_dir, world, modes, scalings, steps, backend):
+    from cme213_sp18_amd.parallel.launcher import spawn
+
+    spawn(multigpu_dp_worker, world, (out_dir, modes, scalings, steps), backend=backend)

@@ -1,4 +1,5 @@
-"""RCCL path on the real GPU: the DP step with its all-reduce captured in a HIP graph."""
+"""RCCL path on the real GPU (world 1): the DP step with its all-reduce captured in a HIP graph, and the
+overlapped bucketed backward (side stream, forced with overlap_chunks) captured the same way."""
 import os
 import subprocess
 import sys
@@ -18,3 +19,5 @@ def test_nccl_dp_step_in_graph_matches_fused(tmp_path):
     z = np.load(tmp_path / "nccl.npz")
     np.testing.assert_array_equal(z["a"], z["b"])
     np.testing.assert_array_equal(z["a1"], z["b1"])
+    for H in (1024, 4096):  # bucketed + side-stream RCCL backward in the graph == the fused step
+        assert float(z[f"bucketed_rel_{H}"]) <= 1e-6, (H, float(z[f"bucketed_rel_{H}"]))

@@ -259,36 +259,6 @@ def test_wide_step_matches_torch(dt, path, H, n):
         assert torch.equal(hipe.W1p.float().sum(0), hipe.W1)
 
 
-@pytest.mark.parametrize("normalize", [False, True])
-def test_lookahead_schedule_matches_plain_steps(normalize):
-    """Two-launch lookahead schedule (parallel/lookahead.py) == the plain three-launch step, fp32-class."""
-    x, y = synthetic_mnist(6400, seed=9)
-    nn = NeuralNetwork([784, 100, 10])
-    out = {}
-    for la in (True, False):
-        t = DataParallelTrainer(nn.copy(), dtype="f32", use_graphs=True, lookahead=la, normalize=normalize)
-        t.load(x, y)
-        assert (t._la is not None) == la
-        t.train(3, 0.05 if normalize else 1e-3, 1e-4)
-        out[la] = t.nn
-    for i in range(2):
-        np.testing.assert_allclose(out[True].W[i], out[False].W[i], rtol=2e-4, atol=2e-6)
-        np.testing.assert_allclose(out[True].b[i], out[False].b[i], rtol=2e-4, atol=2e-6)
-
-
-def test_lookahead_graph_equals_eager():
-    x, y = synthetic_mnist(4000, seed=2)
-    nn = NeuralNetwork([784, 100, 10])
-    a = DataParallelTrainer(nn.copy(), dtype="f32", use_graphs=True, lookahead=True)
-    b = DataParallelTrainer(nn.copy(), dtype="f32", use_graphs=False, lookahead=True)
-    for t in (a, b):
-        t.load(x, y)
-        assert t._la is not None
-        t.train(2, 0.01, 1e-4)
-    for i in range(2):
-        np.testing.assert_array_equal(a.nn.W[i], b.nn.W[i])
-
-
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("H,n", [(100, 800), (100, 100), (128, 513), (37, 45), (16, 32)])
 def test_fwd1_head_single_launch_matches_two_launches(dtype, H, n):
