@@ -106,6 +106,7 @@ class MlpEngine:
         self.W1, self.b1, self.W2, self.b2 = self.layout.views(self.params)
         self.gW1, self.gb1, self.gW2, self.gb2 = self.layout.views(self.grads)
         self.X = None
+        self.Xw = self.XTw = None  # wide-layer bf16 copies (load_dataset)
         self.XT = None
         self.labels = None
         self._normalize = False
@@ -193,6 +194,13 @@ class MlpEngine:
             self.XT = self.XT.contiguous()
         else:
             self.XT = self.X.t().contiguous() if self.feature_major_copy else None
+        # wide layers on the hip backend: bf16 copies of both layouts for the direct-to-LDS GEMM engine
+        # (csrc/mlp/glds_gemm.h streams operands global -> LDS unconverted; 2 B/pixel, ~170 MB for the
+        # 54k-image training split -- nothing next to 288 GB of HBM)
+        self.Xw = self.XTw = None
+        if self.np and self.backend == "hip" and self.H >= 512 and self.XT is not None:
+            self.Xw = self.X.to(torch.bfloat16).contiguous()
+            self.XTw = self.XT.to(torch.bfloat16).contiguous()
         self.labels = torch.as_tensor(np.asarray(labels, dtype=np.int32)).to(self.device).contiguous()
         self.num_samples = int(self.X.shape[0])
         self._step = None
@@ -241,6 +249,8 @@ class MlpEngine:
             s.X = self.X.data_ptr() if loaded else 0
             s.labels = self.labels.data_ptr() if loaded else 0
             s.XT = self.XT.data_ptr() if loaded and self.XT is not None else 0
+            s.Xw = self.Xw.data_ptr() if loaded and self.Xw is not None else 0
+            s.XTw = self.XTw.data_ptr() if loaded and self.XTw is not None else 0
             s.N = self.num_samples if loaded else 0
             s.W1, s.b1, s.W2, s.b2 = (t.data_ptr() for t in (self.W1, self.b1, self.W2, self.b2))
             s.W1g = self.W1g.data_ptr()

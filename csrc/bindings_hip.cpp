@@ -36,6 +36,7 @@ struct MlpStep {
   int P = 784, H = 100, C = 10, ld = 0;
   uintptr_t X = 0, labels = 0;            // device-resident dataset (gemm dtype) + int32 labels
   uintptr_t XT = 0;                       // optional feature-major copy [P][N]
+  uintptr_t Xw = 0, XTw = 0;              // wide layers: bf16 copies of X [N][P] / XT [P+1][N] (0: none)
   int64_t N = 0;                          // samples in the resident dataset (ld of XT)
   uintptr_t W1 = 0, b1 = 0, W2 = 0, b2 = 0, W1g = 0;  // params (+ bf16 shadow of W1)
   uintptr_t gW1 = 0, gb1 = 0, gW2 = 0, gb2 = 0;       // gradient bucket views
@@ -94,6 +95,8 @@ struct MlpStep {
     a.XT = reinterpret_cast<const char*>(XT) + (size_t)off;
     a.xscale = xscale;
     a.ldxt = (int)N;
+    if (Xw) a.Xw = reinterpret_cast<const char*>(Xw) + (size_t)off * P * 2;
+    if (XTw) a.XTw = reinterpret_cast<const char*>(XTw) + (size_t)off * 2;
     a.labels = P_<int>(labels) + off;
     a.W1 = P_<float>(W1); a.b1 = P_<float>(b1); a.W2 = P_<float>(W2); a.b2 = P_<float>(b2);
     a.W1p = reinterpret_cast<void*>(W1p);
@@ -145,6 +148,11 @@ struct MlpStep {
             // with the all-ones XT feature nothing reads dZ1 in fp32 on the wide path (db1 comes out of
             // the dW1 GEMM over the planes): skip those 4 B/element of HBM writes
             if (h.z2_chunks > 0 && bias_col) h.dZ1 = nullptr;
+            // ... unless the dW1 GEMM splits fp32 dZ1 in registers: then fp32 dZ1 and no planes
+            if (cme::mlp_split_wgrad_fp32_dz(a)) {
+              h.dZ1 = a.dZ1;
+              h.dZ1_planes = nullptr;
+            }
             if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
           }
         }
@@ -327,6 +335,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("X", &MlpStep::X)
       .def_readwrite("labels", &MlpStep::labels)
       .def_readwrite("XT", &MlpStep::XT)
+      .def_readwrite("Xw", &MlpStep::Xw)
+      .def_readwrite("XTw", &MlpStep::XTw)
       .def_readwrite("N", &MlpStep::N)
       .def_readwrite("W1", &MlpStep::W1)
       .def_readwrite("b1", &MlpStep::b1)

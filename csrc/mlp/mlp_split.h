@@ -74,10 +74,17 @@ struct SplitStepArgs {
   // z2 partial sums, z2part[row tile][16][ld] = W2[:, tile rows] . a1[tile rows, :] (v_mfma_f32_16x16x4
   // on the activated accumulators), so the head never re-reads a1 for z2 (mlp_split_fwd1_z2_chunks)
   float* z2part = nullptr;
+  // wide layers: bf16 copies of the shard (Xw = Xw_base + off*P, [n][P]; XTw = XTw_base + off, [P+1][ldxt])
+  // for the direct-to-LDS GEMM engine (glds_gemm.h); nullptr: the register-staged engine reads the uint8s
+  const void* Xw = nullptr;
+  const void* XTw = nullptr;
 };
 
 // number of z2 row-tile partials mlp_split_fwd1 writes for `a` (0: the forward does not produce them)
 int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a);
+// true when the weight-gradient launch of this (whole-layer) step reads dZ1 in fp32 and splits it in
+// registers (rega_gemm.h): the head then writes fp32 dZ1 and no dZ1 planes
+bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a);
 
 // flag slots (workgroup tiles) of the fused-all-reduce wgrad launch for a P-H layer with the all-ones
 // feature; -1 when above `cap`

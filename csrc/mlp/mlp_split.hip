@@ -3,6 +3,8 @@
 
 #include <algorithm>
 
+#include "glds_gemm.h"
+#include "rega_gemm.h"
 #include "lds_gemm.h"
 #include "mma_tile.h"
 
@@ -630,6 +632,289 @@ __global__ __launch_bounds__(NT) void wgrad_big_kernel(SplitStepArgs a, int tn, 
                                       a.w1_row0 + (id / tn) * BM, (id % tn) * BN, epi, lds_dyn);
 }
 
+// ---- the same two GEMMs on the direct-to-LDS engine (glds_gemm.h): bf16 copies of X / XT as B.
+// Epilogues are written out here (not element functors): every operand they need is loaded BEFORE the K
+// loop, out-of-range elements go to the kOOB offset (loads return 0, stores are dropped), no branches.
+__device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void st_bf16(__amdgpu_buffer_rsrc_t r, int off, bf16 v) {
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, v), r, off, 0, 0);
+}
+
+// a1 = sigmoid(W1 X + b1) and (z2p != nullptr) the head's z2 partials of this tile's rows:
+// z2p[row tile][class][col] = sum over the tile rows h of W2[class][h] a1[h][col]
+template <int BM, int BN, int NPW>
+__global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn) {
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  using G = GldsGeom<BM, BN>;
+  constexpr int MB = G::MB, NB = G::NB;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (id / tn) * BM, n0 = (id % tn) * BN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
+  const int rw = m0 + wr * G::WM, cw = n0 + wc * G::WN;  // this wave's first row / column
+  const int H = a.H, n = a.n, C = a.C;
+  const bool z2 = a.z2part != nullptr;
+  // epilogue operands, issued before the K loop: b1 of this lane's rows, W2[class fr][those rows]
+  const __amdgpu_buffer_rsrc_t rb1 = make_rsrc(a.b1), rw2 = make_rsrc(a.W2);
+  float bb[MB][4], w2[MB][4];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = rw + 16 * mb + 4 * fg + i;
+      bb[mb][i] = buf_load1<float>(rb1, h < H ? h * 4 : kOOB);
+      w2[mb][i] = buf_load1<float>(rw2, (z2 && fr < C && h < H) ? (fr * H + h) * 4 : kOOB);
+    }
+  f32x4 acc[MB][NB];
+  glds_gemm_mainloop<BM, BN, NPW>(static_cast<const bf16*>(a.W1p), a.P, H * a.P * (int)sizeof(bf16),
+                                  static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
+        const float sv = sigm(acc[mb][nb][i] * a.xscale + bb[mb][i]);
+        acc[mb][nb][i] = sv;
+        st_f32(ra1, (row < H && col < n) ? (row * a.ld + col) * 4 : kOOB, sv);
+      }
+  if (!z2) return;
+  // z2 partials on the f32 MFMA: step i of block mb takes B[k = fg][n = fr] = a1(row rw + 16 mb + 4 fg + i,
+  // col fr) -- exactly accumulator element i -- and A[m = fr][k = fg] = W2[class fr][that row]; the 4 row
+  // waves are summed through LDS (all K-loop reads of lds_dyn are done after the barrier)
+  f32x4 z[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) z[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2[mb][i], acc[mb][nb][i], z[nb], 0, 0, 0);
+  __syncthreads();
+  f32x4* red = reinterpret_cast<f32x4*>(lds_dyn);  // [4][2][NB][64]
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) red[((wr * 2 + wc) * NB + nb) * 64 + lane] = z[nb];
+  __syncthreads();
+  if (wr != 0) return;
+  const int tile = m0 / BM;
+  const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    f32x4 sz = red[(wc * NB + nb) * 64 + lane];
+#pragma unroll
+    for (int r = 1; r < G::WRN; ++r) sz += red[((r * 2 + wc) * NB + nb) * 64 + lane];
+    const int col = cw + 16 * nb + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      st_f32(rz, col < n ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, sz[i]);
+  }
+}
+
+// dW1 = dZ1 XT (+ the all-ones feature column P = db1) with the fused reg + SGD + bf16-plane refresh (sgd)
+// or the pre-scaled gradient (sgd == 0); the dW2 / db2 role workgroups ride in the same launch
+template <int BM, int BN, int NPZ>
+__global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  if ((int)blockIdx.x >= tbig) {  // the dW2 / db2 roles riding in this launch
+    wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
+                reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)));
+    return;
+  }
+  using G = GldsGeom<BM, BN>;
+  constexpr int MB = G::MB, NB = G::NB;
+  const int id = xcd_remap(blockIdx.x, tbig);
+  const int m0 = a.w1_row0 + (id / tn) * BM, n0 = (id % tn) * BN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
+  const int rw = m0 + wr * G::WM, cw = n0 + wc * G::WN;
+  const int M = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows, P = a.P;
+  const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
+  // the weights this lane updates (and b1 of its rows, for the all-ones column), before the K loop
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
+  float w[MB][NB][4], bb[MB][4];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rw + 16 * mb + 4 * fg + i;
+      bb[mb][i] = buf_load1<float>(rb1, row < M ? row * 4 : kOOB);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int col = cw + 16 * nb + fr;
+        w[mb][nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
+      }
+    }
+  f32x4 acc[MB][NB];
+  glds_gemm_mainloop<BM, BN, NPZ>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
+                                  static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0, n0, lds_dyn,
+                                  acc);
+  const size_t plane = (size_t)a.H * P;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
+        const float v = acc[mb][nb][i];
+        const bool in = row < M && col < P;
+        const int idx = row * P + col;
+        const float wv = w[mb][nb][i];
+        const float g = v * xs + reg * wv;
+        if (a.sgd) {
+          const float nw = wv - lr * g;
+          st_f32(rW, in ? idx * 4 : kOOB, nw);
+          float r = nw;
+#pragma unroll
+          for (int p = 0; p < NPZ; ++p) {  // the W1 planes have the dZ1 planes' count (npw == npz)
+            const bf16 hb = __float2bfloat16(r);
+            st_bf16(rp, in ? (int)((p * plane + idx) * 2) : kOOB, hb);
+            r -= __bfloat162float(hb);
+          }
+        } else {
+          st_f32(rg, in ? idx * 4 : kOOB, g);
+        }
+        if (a.bias_col && col == P && row < M) {  // all-ones feature: db1 (no input scale, no regulariser)
+          if (a.sgd) a.b1[row] = bb[mb][i] - lr * v;
+          else a.gb1[row] = v;
+        }
+      }
+}
+
+// a1 = sigmoid(W1 X + b1) on the A-in-registers engine (rega_gemm.h): W1 read as fp32 and split into the
+// exact bf16 planes in registers (AT = float), or the bf16 plane 0 (AT = bf16, split1); z2 partials of
+// this 128-row tile as in fwd1_glds_kernel
+template <typename AT, int BN, int NKS>
+__global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn) {
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  constexpr int NB = RegaGeom<BN>::NB, BM = RegaGeom<BN>::BM;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (id / tn) * BM, n0 = (id % tn) * BN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int rw = m0 + 16 * wave;
+  const int H = a.H, n = a.n, C = a.C;
+  const bool z2 = a.z2part != nullptr;
+  const __amdgpu_buffer_rsrc_t rb1 = make_rsrc(a.b1), rw2 = make_rsrc(a.W2);
+  float bb[4], w2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int h = rw + 4 * fg + i;
+    bb[i] = buf_load1<float>(rb1, h < H ? h * 4 : kOOB);
+    w2[i] = buf_load1<float>(rw2, (z2 && fr < C && h < H) ? (fr * H + h) * 4 : kOOB);
+  }
+  f32x4 acc[NB];
+  const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.W1) : reinterpret_cast<const AT*>(a.W1p);
+  rega_gemm_mainloop<AT, BN, NKS>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rw + 4 * fg + i, col = n0 + 16 * nb + fr;
+      const float sv = sigm(acc[nb][i] * a.xscale + bb[i]);
+      acc[nb][i] = sv;
+      st_f32(ra1, (row < H && col < n) ? (row * a.ld + col) * 4 : kOOB, sv);
+    }
+  if (!z2) return;
+  f32x4 z[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    z[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2[i], acc[nb][i], z[nb], 0, 0, 0);
+  }
+  __syncthreads();
+  f32x4* red = reinterpret_cast<f32x4*>(lds_dyn);  // [8 waves][NB][64]
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) red[(wave * NB + nb) * 64 + lane] = z[nb];
+  __syncthreads();
+  // wave w sums column block nb = w (NB == 8 == waves)
+  static_assert(NB == 8, "one column block per wave in the z2 reduction");
+  f32x4 sz = red[wave * 64 + lane];
+#pragma unroll
+  for (int r = 1; r < 8; ++r) sz += red[(r * NB + wave) * 64 + lane];
+  const int col = n0 + 16 * wave + fr;
+  const int tile = m0 / BM;
+  const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) st_f32(rz, col < n ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, sz[i]);
+}
+
+// dW1 = dZ1 XT on the A-in-registers engine: dZ1 read as fp32 (AT = float; the head writes it instead of
+// the three bf16 planes: 4 B per element stored and loaded instead of 6) or as its one bf16 plane (split1),
+// with wgrad_glds_kernel's fused reg + SGD + plane-refresh epilogue; the dW2 / db2 roles ride along
+template <typename AT, int NKS>
+__global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  if ((int)blockIdx.x >= tbig) {
+    wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
+                reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)));
+    return;
+  }
+  constexpr int NB = RegaGeom<128>::NB, BM = RegaGeom<128>::BM, NP = sizeof(AT) == 4 ? 3 : 1;
+  const int id = xcd_remap(blockIdx.x, tbig);
+  const int m0 = a.w1_row0 + (id / tn) * BM, n0 = (id % tn) * 128;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int rw = m0 + 16 * wave;
+  const int M = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows, P = a.P;
+  const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
+  float w[NB][4], bb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = rw + 4 * fg + i;
+    bb[i] = buf_load1<float>(rb1, row < M ? row * 4 : kOOB);
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int col = n0 + 16 * nb + fr;
+      w[nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
+    }
+  }
+  f32x4 acc[NB];
+  const AT* A = NP == 3 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
+  rega_gemm_mainloop<AT, 128, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0,
+                                   n0, lds_dyn, acc);
+  const size_t plane = (size_t)a.H * P;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rw + 4 * fg + i, col = n0 + 16 * nb + fr;
+      const float v = acc[nb][i];
+      const bool in = row < M && col < P;
+      const int idx = row * P + col;
+      const float wv = w[nb][i];
+      const float g = v * xs + reg * wv;
+      if (a.sgd) {
+        const float nw = wv - lr * g;
+        st_f32(rW, in ? idx * 4 : kOOB, nw);
+        float r = nw;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {  // the W1 planes (npw == npz)
+          const bf16 hb = __float2bfloat16(r);
+          st_bf16(rp, in ? (int)((p * plane + idx) * 2) : kOOB, hb);
+          r -= __bfloat162float(hb);
+        }
+      } else {
+        st_f32(rg, in ? idx * 4 : kOOB, g);
+      }
+      if (a.bias_col && col == P && row < M) {  // all-ones feature: db1
+        if (a.sgd) a.b1[row] = bb[i] - lr * v;
+        else a.gb1[row] = v;
+      }
+    }
+}
+
 template <auto Kern>
 void set_lds_limit(int bytes) {
   static bool done = false;  // one attribute call per kernel instantiation
@@ -653,6 +938,93 @@ bool big_fwd_ok(const SplitStepArgs& a) {
 }
 bool big_wgrad_ok(const SplitStepArgs& a) {
   return a.H >= kBigMinH && a.n % 16 == 0 && a.ld % 8 == 0 && a.ldxt % 16 == 0 && al16(a.dZ1p) && al16(a.XT);
+}
+// the direct-to-LDS engine: bf16 copies present, rows a whole number of 16-byte chunks, 16-byte bases
+bool glds_fwd_ok(const SplitStepArgs& a) {
+  return a.H >= kBigMinH && a.Xw && a.P % 8 == 0 && al16(a.W1p) && al16(a.Xw);
+}
+bool glds_wgrad_ok(const SplitStepArgs& a) {
+  return a.H >= kBigMinH && a.npw == a.npz && a.XTw && a.n % 8 == 0 && a.ld % 8 == 0 && a.ldxt % 8 == 0 && al16(a.dZ1p) &&
+         al16(a.XTw);
+}
+
+// 128x128 tiles when that still gives ~200+ workgroups, else 64x64 (same choice as the register-staged
+// engine, so mlp_split_fwd1_z2_chunks holds for both)
+// the A-in-registers engine: 128 x 128 tiles only, and only when they still give ~200+ workgroups
+bool rega_fwd_ok(const SplitStepArgs& a) {
+  return glds_fwd_ok(a) && cdiv(a.H, 128) * cdiv(a.n, 128) >= 192 && a.P % 4 == 0 && al16(a.W1);
+}
+
+template <typename AT, int NKS>
+void launch_fwd1_rega_k(const SplitStepArgs& a, hipStream_t s) {
+  constexpr int L = std::max(ra::lds_bytes<128>(), 8 * 8 * 64 * 16);  // (z2 reduction scratch)
+  set_lds_limit<fwd1_rega_kernel<AT, 128, NKS>>(L);
+  fwd1_rega_kernel<AT, 128, NKS><<<cdiv(a.H, 128) * cdiv(a.n, 128), 512, L, s>>>(a, cdiv(a.n, 128));
+}
+
+// K = P = 784 (MNIST) is 25 stages of 32: the fully unrolled K loop; anything else the runtime loop
+template <typename AT>
+void launch_fwd1_rega(const SplitStepArgs& a, hipStream_t s) {
+  if (cdiv(a.P, ra::kBK) == 25) launch_fwd1_rega_k<AT, 25>(a, s);
+  else launch_fwd1_rega_k<AT, 0>(a, s);
+}
+
+template <int NP>
+void launch_fwd1_glds(const SplitStepArgs& a, hipStream_t s) {
+  const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
+  if (t128 >= 192) {
+    constexpr int L = gl::lds_bytes<128, 128, NP>();
+    set_lds_limit<fwd1_glds_kernel<128, 128, NP>>(L);
+    fwd1_glds_kernel<128, 128, NP><<<t128, 512, L, s>>>(a, cdiv(a.n, 128));
+  } else {
+    constexpr int L = std::max(gl::lds_bytes<64, 64, NP>(), 4 * 2 * 2 * 64 * 16);  // (tile hook scratch)
+    set_lds_limit<fwd1_glds_kernel<64, 64, NP>>(L);
+    const int tn = cdiv(a.n, 64);
+    fwd1_glds_kernel<64, 64, NP><<<cdiv(a.H, 64) * tn, 512, L, s>>>(a, tn);
+  }
+}
+
+// the A-in-registers dW1 (and the head writing fp32 dZ1 instead of its planes, split3): wide layers whose
+// full 128 x 128 dW1 tiling gives ~200+ workgroups.  Decided on the whole layer (not the row range of a
+// bucketed call) so the head and every wgrad call of a step agree on what dZ1 form exists.
+bool rega_wgrad_ok(const SplitStepArgs& a) {
+  return a.H >= kBigMinH && a.npw == a.npz && a.XTw && cdiv(a.H, 128) * cdiv(a.P + a.bias_col, 128) >= 192 &&
+         a.n % 8 == 0 && a.ld % 8 == 0 && a.ldxt % 8 == 0 && al16(a.XTw) && al16(a.W1) &&
+         (a.npz == 3 ? (a.dZ1 != nullptr && al16(a.dZ1)) : al16(a.dZ1p));
+}
+
+template <typename AT, int NKS>
+void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
+  const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
+  const int tn = cdiv(a.P + a.bias_col, 128), tbig = cdiv(rows, 128) * tn;
+  constexpr int L = std::max(ra::lds_bytes<128>(), kWKS * 4 * 64 * (int)sizeof(float) + 16);
+  set_lds_limit<wgrad_rega_kernel<AT, NKS>>(L);
+  wgrad_rega_kernel<AT, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
+}
+
+template <typename AT>
+void launch_wgrad_rega(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
+  if (cdiv(a.n, ra::kBK) == 25) launch_wgrad_rega_k<AT, 25>(a, t2, tb, s);
+  else launch_wgrad_rega_k<AT, 0>(a, t2, tb, s);
+}
+
+template <int NP>
+void launch_wgrad_glds(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
+  const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
+  const int NW = a.P + a.bias_col;
+  const int t128 = cdiv(rows, 128) * cdiv(NW, 128);
+  constexpr int kRoleLds = kWKS * 4 * 64 * (int)sizeof(float) + 16;
+  if (t128 >= 192) {
+    constexpr int L = std::max(gl::lds_bytes<128, 128, NP>(), kRoleLds);
+    set_lds_limit<wgrad_glds_kernel<128, 128, NP>>(L);
+    wgrad_glds_kernel<128, 128, NP><<<t128 + t2 + tb, 512, L, s>>>(a, cdiv(NW, 128), t128, t2);
+  } else {
+    constexpr int L = std::max(gl::lds_bytes<64, 64, NP>(), kRoleLds);
+    set_lds_limit<wgrad_glds_kernel<64, 64, NP>>(L);
+    const int tn = cdiv(NW, 64);
+    const int t64 = cdiv(rows, 64) * tn;
+    wgrad_glds_kernel<64, 64, NP><<<t64 + t2 + tb, 512, L, s>>>(a, tn, t64, t2);
+  }
 }
 
 // 128x128 tiles when that still gives ~200+ workgroups, else 64x64
@@ -733,8 +1105,10 @@ void launch_fwdhead_nc(const SplitStepArgs& a, hipStream_t s) {
 
 int mlp_split_fwdhead_blocks(int n) { return cdiv(n, kFHCols); }
 
+bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a) { return a.npz == 3 && rega_wgrad_ok(a); }
+
 int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a) {
-  if (!a.z2part || a.C > 16 || a.n <= 0 || !big_fwd_ok(a)) return 0;
+  if (!a.z2part || a.C > 16 || a.n <= 0 || !(glds_fwd_ok(a) || big_fwd_ok(a))) return 0;
   const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
   return t128 >= 192 ? cdiv(a.H, 128) : cdiv(a.H, 64);  // must match launch_fwd1_big_nt's tile choice
 }
@@ -744,6 +1118,18 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
   CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
               "split path: operand too large for 32-bit buffer offsets");
   CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
+  if (rega_fwd_ok(a)) {
+    if (a.npw == 3) launch_fwd1_rega<float>(a, s);
+    else launch_fwd1_rega<bf16>(a, s);
+    CME_LAUNCH_CHECK(s);
+    return;
+  }
+  if (glds_fwd_ok(a)) {
+    if (a.npw == 3) launch_fwd1_glds<3>(a, s);
+    else launch_fwd1_glds<1>(a, s);
+    CME_LAUNCH_CHECK(s);
+    return;
+  }
   if (big_fwd_ok(a)) {
     if (a.npw == 3) launch_fwd1_big<3>(a, s);
     else launch_fwd1_big<1>(a, s);
@@ -786,6 +1172,18 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
     // workgroups: one launch and its boundary fewer, and they run on the CUs the dW1 tiles leave idle
     const int t2f = do_roles ? cdiv(a.H, 16) : 0;
     const int tbf = do_roles ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
+    if (rega_wgrad_ok(a)) {
+      if (a.npz == 3) launch_wgrad_rega<float>(a, t2f, tbf, s);
+      else launch_wgrad_rega<bf16>(a, t2f, tbf, s);
+      CME_LAUNCH_CHECK(s);
+      return;
+    }
+    if (glds_wgrad_ok(a)) {
+      if (a.npz == 3) launch_wgrad_glds<3>(a, t2f, tbf, s);
+      else launch_wgrad_glds<1>(a, t2f, tbf, s);
+      CME_LAUNCH_CHECK(s);
+      return;
+    }
     if (a.npz == 3) launch_wgrad_big<3>(a, t2f, tbf, s);
     else launch_wgrad_big<1>(a, t2f, tbf, s);
     CME_LAUNCH_CHECK(s);

@@ -365,3 +365,34 @@ def test_tensor_parallel_gpu_matches_data_parallel(H, R):
         for i in range(2):
             assert np.abs(nets[r].W[i] - ref.W[i]).max() / np.abs(ref.W[i]).max() < 1e-5
             assert np.abs(nets[r].b[i] - ref.b[i]).max() < 1e-6
+
+
+@pytest.mark.parametrize("dt,path", [("f32", "split3"), ("bf16", "split1")])
+@pytest.mark.parametrize("H,n", [(4096, 800), (1024, 800), (512, 160), (700, 96)])
+def test_wide_engines_agree_with_register_staged_engine(dt, path, H, n):
+    """The wide engines -- A-in-registers (rega_gemm.h, fp32 W1 split in registers; H >= 2048 forward) /
+    direct-to-LDS (glds_gemm.h) on the bf16 copies of X / XT, and the register-staged lds_gemm.h on the
+    uint8 copies -- run the same MFMA sequence per accumulator (k in 32-deep steps, planes innermost):
+    a1 must agree BITWISE.  The head's z2 partials are summed over a different wave layout (8 x 16 rows
+    vs 4 x 32), so D, the gradients and the step agree to fp32 rounding."""
+    x, y = synthetic_mnist(2 * n + 64, seed=11)
+    nn = NeuralNetwork([784, H, 10])
+    out = []
+    for glds in (True, False):
+        e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", path=path)
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        assert e.Xw is not None and e.XTw is not None
+        s = e._hip_step()
+        if not glds:
+            s.Xw = s.XTw = 0
+        e.run(64, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
+        g = (e.a1[:, :n].clone(), e.grads.clone())
+        e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+        torch.cuda.synchronize()
+        out.append(g + (e.params.clone(),))
+        recon = e.W1p.float().sum(0)  # the planes track the fp32 master exactly / rounded
+        assert torch.equal(recon, e.W1 if path == "split3" else e.W1.to(torch.bfloat16).float())
+    assert torch.equal(out[0][0], out[1][0])  # a1
+    for u, v in zip(out[0][1:], out[1][1:]):
+        assert _rel(u.float(), v.float()) < (1e-5 if path == "split3" else 1e-3)  # split1: bf16 dZ1
