@@ -791,56 +791,69 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
 // a1 = sigmoid(W1 X + b1) on the A-in-registers engine (rega_gemm.h): W1 read as fp32 and split into the
 // exact bf16 planes in registers (AT = float), or the bf16 plane 0 (AT = bf16, split1); z2 partials of
 // this 128-row tile as in fwd1_glds_kernel
-template <typename AT, int BN, int NKS>
+template <typename AT, int WC, int NKS>
 __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
-  constexpr int NB = RegaGeom<BN>::NB, BM = RegaGeom<BN>::BM;
+  using G = RegaGeom<128, WC>;
+  constexpr int MB = G::MB, NB = G::NB, WR = G::WR, BM = G::BM;
   const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (id / tn) * BM, n0 = (id % tn) * BN;
+  const int m0 = (id / tn) * BM, n0 = (id % tn) * 128;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int fr = lane & 15, fg = lane >> 4;
-  const int rw = m0 + 16 * wave;
+  const int wr = wave / WC, wc = wave % WC, fr = lane & 15, fg = lane >> 4;
+  const int rw = m0 + 16 * MB * wr, cw = n0 + 16 * NB * wc;  // this wave's first row / column
   const int H = a.H, n = a.n, C = a.C;
   const bool z2 = a.z2part != nullptr;
   const __amdgpu_buffer_rsrc_t rb1 = make_rsrc(a.b1), rw2 = make_rsrc(a.W2);
-  float bb[4], w2[4];
+  float bb[MB][4], w2[MB][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int h = rw + 4 * fg + i;
-    bb[i] = buf_load1<float>(rb1, h < H ? h * 4 : kOOB);
-    w2[i] = buf_load1<float>(rw2, (z2 && fr < C && h < H) ? (fr * H + h) * 4 : kOOB);
-  }
-  f32x4 acc[NB];
-  const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.W1) : reinterpret_cast<const AT*>(a.W1p);
-  rega_gemm_mainloop<AT, BN, NKS>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
-  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb)
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int row = rw + 4 * fg + i, col = n0 + 16 * nb + fr;
-      const float sv = sigm(acc[nb][i] * a.xscale + bb[i]);
-      acc[nb][i] = sv;
-      st_f32(ra1, (row < H && col < n) ? (row * a.ld + col) * 4 : kOOB, sv);
+      const int h = rw + 16 * mb + 4 * fg + i;
+      bb[mb][i] = buf_load1<float>(rb1, h < H ? h * 4 : kOOB);
+      w2[mb][i] = buf_load1<float>(rw2, (z2 && fr < C && h < H) ? (fr * H + h) * 4 : kOOB);
     }
+  f32x4 acc[MB][NB];
+  const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.W1) : reinterpret_cast<const AT*>(a.W1p);
+  rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn,
+                                       acc);
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
+        const float sv = sigm(acc[mb][nb][i] * a.xscale + bb[mb][i]);
+        acc[mb][nb][i] = sv;
+        st_f32(ra1, (row < H && col < n) ? (row * a.ld + col) * 4 : kOOB, sv);
+      }
   if (!z2) return;
+  // z2 partials on the f32 MFMA: step i of block mb takes B[k = fg][n = fr] = a1(row rw + 16 mb + 4 fg + i,
+  // col fr) -- exactly accumulator element i -- and A[m = fr][k = fg] = W2[class fr][that row]; the WR row
+  // waves are summed through LDS (every K-loop read of lds_dyn is done after the barrier)
   f32x4 z[NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     z[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2[i], acc[nb][i], z[nb], 0, 0, 0);
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2[mb][i], acc[mb][nb][i], z[nb], 0, 0, 0);
   }
   __syncthreads();
-  f32x4* red = reinterpret_cast<f32x4*>(lds_dyn);  // [8 waves][NB][64]
+  f32x4* red = reinterpret_cast<f32x4*>(lds_dyn);  // [WR][WC][NB][64]
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb) red[(wave * NB + nb) * 64 + lane] = z[nb];
+  for (int nb = 0; nb < NB; ++nb) red[((wr * WC + wc) * NB + nb) * 64 + lane] = z[nb];
   __syncthreads();
-  // wave w sums column block nb = w (NB == 8 == waves)
-  static_assert(NB == 8, "one column block per wave in the z2 reduction");
-  f32x4 sz = red[wave * 64 + lane];
+  // the tile's 8 column blocks, one per wave
+  static_assert(WC * NB == 8, "8 column blocks of 16");
+  const int oc = wave / NB, onb = wave % NB;
+  f32x4 sz = red[(oc * NB + onb) * 64 + lane];
 #pragma unroll
-  for (int r = 1; r < 8; ++r) sz += red[(r * NB + wave) * 64 + lane];
+  for (int r = 1; r < WR; ++r) sz += red[((r * WC + oc) * NB + onb) * 64 + lane];
   const int col = n0 + 16 * wave + fr;
   const int tile = m0 / BM;
   const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
@@ -851,7 +864,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn)
 // dW1 = dZ1 XT on the A-in-registers engine: dZ1 read as fp32 (AT = float; the head writes it instead of
 // the three bf16 planes: 4 B per element stored and loaded instead of 6) or as its one bf16 plane (split1),
 // with wgrad_glds_kernel's fused reg + SGD + plane-refresh epilogue; the dW2 / db2 roles ride along
-template <typename AT, int NKS>
+template <typename AT, int WC, int NKS>
 __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {
@@ -859,60 +872,65 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
                 reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)));
     return;
   }
-  constexpr int NB = RegaGeom<128>::NB, BM = RegaGeom<128>::BM, NP = sizeof(AT) == 4 ? 3 : 1;
+  using G = RegaGeom<128, WC>;
+  constexpr int MB = G::MB, NB = G::NB, BM = G::BM, NP = sizeof(AT) == 4 ? 3 : 1;
   const int id = xcd_remap(blockIdx.x, tbig);
   const int m0 = a.w1_row0 + (id / tn) * BM, n0 = (id % tn) * 128;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int fr = lane & 15, fg = lane >> 4;
-  const int rw = m0 + 16 * wave;
+  const int wr = wave / WC, wc = wave % WC, fr = lane & 15, fg = lane >> 4;
+  const int rw = m0 + 16 * MB * wr, cw = n0 + 16 * NB * wc;
   const int M = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows, P = a.P;
   const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
-  float w[NB][4], bb[4];
+  float w[MB][NB][4], bb[MB][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = rw + 4 * fg + i;
-    bb[i] = buf_load1<float>(rb1, row < M ? row * 4 : kOOB);
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const int col = n0 + 16 * nb + fr;
-      w[nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
+    for (int i = 0; i < 4; ++i) {
+      const int row = rw + 16 * mb + 4 * fg + i;
+      bb[mb][i] = buf_load1<float>(rb1, row < M ? row * 4 : kOOB);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int col = cw + 16 * nb + fr;
+        w[mb][nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
+      }
     }
-  }
-  f32x4 acc[NB];
+  f32x4 acc[MB][NB];
   const AT* A = NP == 3 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
-  rega_gemm_mainloop<AT, 128, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0,
-                                   n0, lds_dyn, acc);
+  rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n,
+                                       m0, n0, lds_dyn, acc);
   const size_t plane = (size_t)a.H * P;
   const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb)
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = rw + 4 * fg + i, col = n0 + 16 * nb + fr;
-      const float v = acc[nb][i];
-      const bool in = row < M && col < P;
-      const int idx = row * P + col;
-      const float wv = w[nb][i];
-      const float g = v * xs + reg * wv;
-      if (a.sgd) {
-        const float nw = wv - lr * g;
-        st_f32(rW, in ? idx * 4 : kOOB, nw);
-        float r = nw;
+    for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-        for (int p = 0; p < NP; ++p) {  // the W1 planes (npw == npz)
-          const bf16 hb = __float2bfloat16(r);
-          st_bf16(rp, in ? (int)((p * plane + idx) * 2) : kOOB, hb);
-          r -= __bfloat162float(hb);
+      for (int i = 0; i < 4; ++i) {
+        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
+        const float v = acc[mb][nb][i];
+        const bool in = row < M && col < P;
+        const int idx = row * P + col;
+        const float wv = w[mb][nb][i];
+        const float g = v * xs + reg * wv;
+        if (a.sgd) {
+          const float nw = wv - lr * g;
+          st_f32(rW, in ? idx * 4 : kOOB, nw);
+          float r = nw;
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {  // the W1 planes (npw == npz)
+            const bf16 hb = __float2bfloat16(r);
+            st_bf16(rp, in ? (int)((p * plane + idx) * 2) : kOOB, hb);
+            r -= __bfloat162float(hb);
+          }
+        } else {
+          st_f32(rg, in ? idx * 4 : kOOB, g);
         }
-      } else {
-        st_f32(rg, in ? idx * 4 : kOOB, g);
+        if (a.bias_col && col == P && row < M) {  // all-ones feature: db1
+          if (a.sgd) a.b1[row] = bb[mb][i] - lr * v;
+          else a.gb1[row] = v;
+        }
       }
-      if (a.bias_col && col == P && row < M) {  // all-ones feature: db1
-        if (a.sgd) a.b1[row] = bb[i] - lr * v;
-        else a.gb1[row] = v;
-      }
-    }
 }
 
 template <auto Kern>
@@ -955,11 +973,13 @@ bool rega_fwd_ok(const SplitStepArgs& a) {
   return glds_fwd_ok(a) && cdiv(a.H, 128) * cdiv(a.n, 128) >= 192 && a.P % 4 == 0 && al16(a.W1);
 }
 
+constexpr int kRegaWC = 1;  // wave layout of the A-in-registers kernels: 8 (rows) x 1 (bench/micro/rega_ablate.hip: WC = 2 splits every A value twice, +25 % at H = 4096)
+
 template <typename AT, int NKS>
 void launch_fwd1_rega_k(const SplitStepArgs& a, hipStream_t s) {
   constexpr int L = std::max(ra::lds_bytes<128>(), 8 * 8 * 64 * 16);  // (z2 reduction scratch)
-  set_lds_limit<fwd1_rega_kernel<AT, 128, NKS>>(L);
-  fwd1_rega_kernel<AT, 128, NKS><<<cdiv(a.H, 128) * cdiv(a.n, 128), 512, L, s>>>(a, cdiv(a.n, 128));
+  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS>>(L);
+  fwd1_rega_kernel<AT, kRegaWC, NKS><<<cdiv(a.H, 128) * cdiv(a.n, 128), 512, L, s>>>(a, cdiv(a.n, 128));
 }
 
 // K = P = 784 (MNIST) is 25 stages of 32: the fully unrolled K loop; anything else the runtime loop
@@ -998,8 +1018,8 @@ void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) 
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int tn = cdiv(a.P + a.bias_col, 128), tbig = cdiv(rows, 128) * tn;
   constexpr int L = std::max(ra::lds_bytes<128>(), kWKS * 4 * 64 * (int)sizeof(float) + 16);
-  set_lds_limit<wgrad_rega_kernel<AT, NKS>>(L);
-  wgrad_rega_kernel<AT, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
+  set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS>>(L);
+  wgrad_rega_kernel<AT, kRegaWC, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
 }
 
 template <typename AT>

@@ -28,7 +28,7 @@ namespace ra {
 
 constexpr int kBK = 32;
 constexpr int kRowB = kBK * 2;  // LDS bytes per B row per stage (bf16)
-constexpr int kBufs = 4;        // B LDS buffers and A register slots; 3 stages in flight
+constexpr int kBufs = 5;        // B LDS buffers and A register slots; 4 stages in flight
 
 template <int BN>
 constexpr int lds_bytes() {
@@ -37,15 +37,11 @@ constexpr int lds_bytes() {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <typename AT>
-struct AFrag;
-template <>
-struct AFrag<float> {
-  u32x4 v[2];  // 8 fp32
-};
-template <>
-struct AFrag<__hip_bfloat16> {
-  u32x4 v[1];  // 8 bf16
+// one stage's A operand of one lane: MB row blocks x 8 k-values (fp32: two dwordx4 per block; bf16: one)
+template <typename AT, int MB>
+struct AFrag {
+  static constexpr int Q = (sizeof(AT) == 4 ? 2 : 1) * MB;  // dwordx4 per lane
+  u32x4 v[Q];
 };
 
 // A fragment loads are inline asm, hidden from hipcc's vmcnt bookkeeping (cdna_hip_programming.md §5
@@ -60,19 +56,20 @@ __device__ __forceinline__ u32x4 load16_asm(__amdgpu_buffer_rsrc_t r, int voff) 
   return v;
 }
 
-template <int N, typename AT>
-__device__ __forceinline__ void wait_vm_regs(AFrag<AT>& f) {
+template <int N, typename AT, int MB>
+__device__ __forceinline__ void wait_vm_regs(AFrag<AT, MB>& f) {
   static_assert(N >= 0 && N < 64, "vmcnt range");
-  if constexpr (sizeof(AT) == 4)
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(f.v[0]), "+v"(f.v[1]) : "n"(N) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(f.v[0]) : "n"(N) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+  for (int q = 0; q < AFrag<AT, MB>::Q; ++q) asm volatile("" : "+v"(f.v[q]));
 }
 
-// the three exact bf16 planes of 8 fp32 values
-__device__ __forceinline__ void split3(const AFrag<float>& f, bf16x8_t& hi, bf16x8_t& mid, bf16x8_t& lo) {
+// the three exact bf16 planes of 8 fp32 values (two dwordx4)
+__device__ __forceinline__ void split3(const u32x4& w0, const u32x4& w1, bf16x8_t& hi, bf16x8_t& mid,
+                                       bf16x8_t& lo) {
   float x[8];
-  __builtin_memcpy(x, f.v, 32);
+  __builtin_memcpy(x, &w0, 16);
+  __builtin_memcpy(x + 4, &w1, 16);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const __bf16 h = (__bf16)x[j];
@@ -87,41 +84,55 @@ __device__ __forceinline__ void split3(const AFrag<float>& f, bf16x8_t& hi, bf16
 
 }  // namespace ra
 
-template <int BN>
+// 8 waves as WR (rows) x WC (columns): wave (wr, wc) owns rows m0 + wr * 16 * MB + [0, 16 * MB) and
+// columns n0 + wc * 16 * NB + [0, 16 * NB).  WC = 1: each wave 16 rows x all BN columns (every wave reads
+// the whole B stage from LDS: 8 KB per wave per stage at BN = 128); WC = 2: 32 rows x BN / 2 columns (half
+// the B fragment reads, each A row block loaded by the two column waves -- the second load hits L1).
+template <int BN, int WC = 1>
 struct RegaGeom {
-  static constexpr int BM = 128, NB = BN / 16;
+  static constexpr int BM = 128, WR = 8 / WC, MB = WC, NB = BN / (16 * WC);
+  static_assert(WR * 16 * MB == BM && NB >= 1, "8 waves cover 128 rows");
 };
 
-// K loop of the BM(=128) x BN tile at (m0, n0) into acc[NB] (zeroed here): C[m][n] = sum_k A[m][k] B[n][k].
-// AT = float: A is fp32 split into NPA (= 3) exact bf16 planes on the fly; AT = bf16: A is one bf16
-// plane (NPA = 1).  B is bf16.  Requirements (launcher): K % 8 == 0, lda % 4 == 0 (fp32) / % 8 (bf16),
-// ldb % 8 == 0, 16-byte aligned bases.  Ends with this wave's LDS reads retired (other waves may still
-// read `lds`: __syncthreads() before reusing it).
+// K loop of the 128 x BN tile at (m0, n0) into acc[MB][NB] (zeroed here): C[m][n] = sum_k A[m][k] B[n][k].
+// AT = float: A is fp32 split into 3 exact bf16 planes on the fly; AT = bf16: A is one bf16 plane.  B is
+// bf16.  Requirements (launcher): K % 8 == 0, lda % 4 == 0 (fp32) / % 8 (bf16), ldb % 8 == 0, 16-byte
+// aligned bases.  Ends with this wave's LDS reads retired (other waves may still read `lds`:
+// __syncthreads() before reusing it).
 // NKS > 0: exactly NKS stages (K in ((NKS-1)*32, NKS*32]), loop fully unrolled -- with a runtime trip
 // count hipcc's vmcnt tracking merges at the back-edge and drains every load in flight (vmcnt(0)) once
 // per trip before the A registers are used.
-template <typename AT, int BN, int NKS = 0>
+// ABLATE (bench/micro/rega_ablate.hip only): 1 = no MFMA (fragments still read and split, kept live),
+// 2 = no loads after the prologue (the MFMAs run on whatever the ring holds)
+template <typename AT, int BN, int WC = 1, int NKS = 0, int ABLATE = 0>
 __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int lda,
                                                    const __hip_bfloat16* __restrict__ B, int ldb, int M, int N,
                                                    int K, int m0, int n0, char* __restrict__ lds,
-                                                   f32x4 (&acc)[RegaGeom<BN>::NB]) {
+                                                   f32x4 (&acc)[RegaGeom<BN, WC>::MB][RegaGeom<BN, WC>::NB]) {
   using namespace ra;
-  constexpr int NB = RegaGeom<BN>::NB, NW = 8;
+  using G = RegaGeom<BN, WC>;
+  constexpr int MB = G::MB, NB = G::NB, NW = 8;
   constexpr bool F32 = sizeof(AT) == 4;
   constexpr int SB = BN * kRowB;  // B bytes per stage
   static_assert(SB % (1024 * NW) == 0, "B DMA instructions must divide over the 8 waves");
   constexpr int LB = SB / 1024 / NW;            // B DMA instructions per wave per stage
-  constexpr int LA = F32 ? 2 : 1;               // A loads per lane per stage
+  constexpr int LA = AFrag<AT, MB>::Q;          // A loads per lane per stage
   constexpr int LS = LB + LA;                   // vmcnt per stage per wave
+  using AF = AFrag<AT, MB>;
 
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave / WC, wc = wave % WC;
   const int fr = lane & 15, fg = lane >> 4;
   const __amdgpu_buffer_rsrc_t rsa = make_rsrc(A), rsb = make_rsrc(B);
 
-  // A: row m0 + 16 wave + fr, k = 8 fg .. 8 fg + 7 of each stage
-  const int arow = m0 + 16 * wave + fr;
-  const int abase = arow < M ? (arow * lda + 8 * fg) * (int)sizeof(AT) : -1;
+  // A: rows m0 + 16 (MB wr + mb) + fr, k = 8 fg .. 8 fg + 7 of each stage
+  int abase[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int arow = m0 + 16 * (MB * wr + mb) + fr;
+    abase[mb] = arow < M ? (arow * lda + 8 * fg) * (int)sizeof(AT) : -1;
+  }
   // B DMA: chunk c = wave + 8 j of 16 rows; lane -> row lane >> 2, physical slot lane & 3 holding logical
   // k-chunk slot ^ ((row >> 2) & 3)
   const int dr = lane >> 2, dkc = (lane & 3) ^ ((dr >> 2) & 3);
@@ -134,73 +145,110 @@ __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int
     blds[j] = rb16 * kRowB;
   }
 
-  auto issue = [&](int kt, AFrag<AT>& fa) {
+  auto issue = [&](int kt, AF& fa) {
     const int k0 = kt * kBK;
     char* base = lds + (kt % kBufs) * SB;
     const bool bk = k0 + dkc * 8 < K;
 #pragma unroll
     for (int j = 0; j < LB; ++j) gl::dma16(rsb, base + blds[j], (bsrc[j] >= 0 && bk) ? bsrc[j] + k0 * 2 : kOOB);
-    const int ao = (abase >= 0 && k0 + 8 * fg < K) ? abase + k0 * (int)sizeof(AT) : kOOB;
-    fa.v[0] = load16_asm<0>(rsa, ao);
-    if constexpr (LA == 2) fa.v[1] = load16_asm<16>(rsa, ao);
+    const bool ak = k0 + 8 * fg < K;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int ao = (abase[mb] >= 0 && ak) ? abase[mb] + k0 * (int)sizeof(AT) : kOOB;
+      if constexpr (F32) {
+        fa.v[2 * mb] = load16_asm<0>(rsa, ao);
+        fa.v[2 * mb + 1] = load16_asm<16>(rsa, ao);
+      } else {
+        fa.v[mb] = load16_asm<0>(rsa, ao);
+      }
+    }
   };
 
 #pragma unroll
-  for (int j = 0; j < NB; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int frag = fr * kRowB + ((fg ^ ((fr >> 2) & 3)) << 4);
-  auto compute = [&](int kt, const AFrag<AT>& fa) {
+  const int frag = (wc * 16 * NB + fr) * kRowB + ((fg ^ ((fr >> 2) & 3)) << 4);
+  // one stage's MFMA operands in registers: NB B fragments (LDS) and the A planes (split of the A ring slot)
+  constexpr int NPL = F32 ? 3 : 1;
+  struct Frags {
+    bf16x8_t b[NB];
+    bf16x8_t a[MB][NPL];
+  };
+  auto load_frags = [&](int kt, Frags& F, const AF& fa) {
     const char* sB = lds + (kt % kBufs) * SB + frag;
-    bf16x8_t bf[NB];
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) bf[nb] = *reinterpret_cast<const bf16x8_t*>(sB + nb * 16 * kRowB);
-    if constexpr (F32) {
-      bf16x8_t h, m, l;
-      split3(fa, h, m, l);
+    for (int nb = 0; nb < NB; ++nb) F.b[nb] = *reinterpret_cast<const bf16x8_t*>(sB + nb * 16 * kRowB);
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(h, bf[nb], acc[nb], 0, 0, 0);
-        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(m, bf[nb], acc[nb], 0, 0, 0);
-        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(l, bf[nb], acc[nb], 0, 0, 0);
-      }
+    for (int mb = 0; mb < MB; ++mb) {
+      if constexpr (F32) split3(fa.v[2 * mb], fa.v[2 * mb + 1], F.a[mb][0], F.a[mb][1], F.a[mb][2]);
+      else __builtin_memcpy(&F.a[mb][0], &fa.v[mb], 16);
+    }
+  };
+  auto mma = [&](const Frags& F) {
+    if constexpr (ABLATE == 1) {
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) asm volatile("" ::"v"(F.b[nb]));
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) asm volatile("" ::"v"(F.a[mb][p]));
     } else {
-      bf16x8_t a;
-      __builtin_memcpy(&a, fa.v, 16);
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bf[nb], acc[nb], 0, 0, 0);
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int p = 0; p < NPL; ++p)  // planes innermost: hi, mid, lo into the same accumulator
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.a[mb][p], F.b[nb], acc[mb][nb], 0, 0, 0);
     }
   };
 
   const int nk = NKS > 0 ? NKS : (K + kBK - 1) / kBK;
-  AFrag<AT> ring[kBufs];
+  AF ring[kBufs];
+  Frags F[2];
+  // stage s landed for this wave, with `younger` later stages allowed to stay in flight
+  auto wait_stage = [&](int younger, AF& slot) {
+    if (younger >= 3) wait_vm_regs<3 * LS>(slot);
+    else if (younger == 2) wait_vm_regs<2 * LS>(slot);
+    else if (younger == 1) wait_vm_regs<LS>(slot);
+    else wait_vm_regs<0>(slot);
+  };
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
   asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs just written -> the asm loads read them
 #pragma unroll
   for (int s = 0; s < kBufs - 1; ++s)
     if (s < nk) issue(s, ring[s]);
+  wait_stage(min(kBufs - 2, nk - 1), ring[0]);
+  barrier();
+  load_frags(0, F[0], ring[0]);
 
-  auto stage = [&](int kt, int d) {
-    const int younger = min(kBufs - 2, nk - 1 - kt);
-    if (younger >= 2) wait_vm_regs<2 * LS>(ring[d]);
-    else if (younger == 1) wait_vm_regs<LS>(ring[d]);
-    else wait_vm_regs<0>(ring[d]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    // stage kt + 3 reuses B buffer (kt - 1) % 4 (every wave is past its reads: the barrier) and A slot
-    // (kt + 3) % 4 == (kt - 1) % 4, consumed by the previous stage's compute
-    if (kt + kBufs - 1 < nk) issue(kt + kBufs - 1, ring[(d + kBufs - 1) % kBufs]);
-    compute(kt, ring[d]);
+  // Stage kt: its operands are already in registers (F[kt & 1], read during stage kt-1).  Wait for stage
+  // kt+1 to land, barrier (it is visible to every wave; every wave's reads of stage kt-1's buffer are
+  // retired), refill that buffer with stage kt+kBufs-1, read stage kt+1's fragments into the other
+  // register set, and multiply stage kt.
+  auto stage = [&](int kt, int slot_next, Frags& Fcur, Frags& Fnext) {
+    if (kt + 1 < nk) wait_stage(min(kBufs - 3, nk - 2 - kt), ring[slot_next]);
+    barrier();
+    if (ABLATE != 2 && kt + kBufs - 1 < nk) issue(kt + kBufs - 1, ring[(slot_next + kBufs - 2) % kBufs]);
+    if (kt + 1 < nk) load_frags(kt + 1, Fnext, ring[slot_next]);
+    mma(Fcur);
   };
   if constexpr (NKS > 0) {
 #pragma unroll
-    for (int kt = 0; kt < NKS; ++kt) stage(kt, kt % kBufs);
+    for (int kt = 0; kt < NKS; ++kt) stage(kt, (kt + 1) % kBufs, F[kt & 1], F[(kt + 1) & 1]);
   } else {
-    // 4 stages per trip so every ring slot index is a compile-time constant
-    for (int k4 = 0; k4 < nk; k4 += kBufs) {
+    // 2 * kBufs stages per trip: every ring slot and register set index is a compile-time constant
+    for (int k0 = 0; k0 < nk; k0 += 2 * kBufs) {
 #pragma unroll
-      for (int d = 0; d < kBufs; ++d) {
-        if (k4 + d >= nk) break;
-        stage(k4 + d, d);
+      for (int d = 0; d < 2 * kBufs; ++d) {
+        if (k0 + d >= nk) break;
+        stage(k0 + d, (d + 1) % kBufs, F[d & 1], F[(d + 1) & 1]);
       }
     }
   }
