@@ -44,6 +44,9 @@ def parse(argv=None):
     ap.add_argument("--scaling", default="weak", choices=["strong", "weak"])
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--executor", default="auto", choices=["auto", "graph", "eager"],
+                    help="auto: the native C++ step loop where a step is pure device work (one process, or the "
+                         "xGMI-fused all-reduce), else captured HIP graphs; graph: always graphs")
     ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl", "host"],
                     help="gradient sync for N>1: xGMI peer kernel with fused SGD (auto/xgmi), RCCL all-reduce, "
                          "or host-staged gloo (reference-equivalent)")
@@ -87,7 +90,8 @@ def main(argv=None) -> int:
     def prepare(allreduce: str):
         """Trainer + captured graphs + W warm-up steps.  Returns (trainer, timed plans)."""
         tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=global_batch,
-                                 backend=a.backend, use_graphs=not a.no_graphs, allreduce=allreduce)
+                                 backend=a.backend, use_graphs=not a.no_graphs, allreduce=allreduce,
+                                 executor="eager" if a.no_graphs else a.executor)
         tr.load(x, y)
         full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == global_batch]
         if not full:
@@ -102,7 +106,8 @@ def main(argv=None) -> int:
             return out
 
         warm_plans, timed_plans = plans_for(a.warmup), plans_for(a.steps)
-        if tr.use_graphs:  # capture outside the timed region (graphs are cached by plan)
+        native = all(tr.native_plan(p) is not None for p in warm_plans + timed_plans)
+        if tr.use_graphs and not native:  # capture outside the timed region (graphs are cached by plan)
             try:
                 for p in {tuple(p.steps): p for p in warm_plans + timed_plans}.values():
                     tr.capture(p, lr, reg)
@@ -130,15 +135,18 @@ def main(argv=None) -> int:
                 print("warning: xGMI all-reduce peer wait timed out in warm-up; re-running on RCCL", file=sys.stderr)
             tr.close()
             tr, timed_plans = prepare("rccl")
+    native_exec = all(tr.native_plan(p) is not None for p in timed_plans)
+    runners = [tr.plan_runner(p, lr, reg) for p in timed_plans]  # resolved before the clock starts
     torch.cuda.synchronize(device)
     comm.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for p in timed_plans:
-        tr.run_plan(p, lr, reg)
+    for run in runners:
+        run()
     torch.cuda.synchronize(device)
     comm.barrier()
-    torch.cuda.synchronize(device)
+    if R > 1:  # an RCCL barrier is GPU work; one process has nothing left to wait for
+        torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
     dt = comm.allreduce_scalar(dt, op="max")
 
@@ -168,7 +176,9 @@ def main(argv=None) -> int:
             "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": global_batch, "seq_len": None,
                        "parallelism": f"dp{R}", "per_gpu_batch": global_batch // R, "backend": a.backend,
                        "mode": a.mode,
-                       "hip_graphs": tr.use_graphs, "allreduce": tr.allreduce_impl, "params_finite": not bad,
+                       "hip_graphs": tr.use_graphs and not native_exec,
+                       "executor": "native" if native_exec else ("graph" if tr.use_graphs else "eager"),
+                       "allreduce": tr.allreduce_impl, "params_finite": not bad,
                        "comm_ok": not comm_failed},
         }
         if not ok:

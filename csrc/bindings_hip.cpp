@@ -197,6 +197,24 @@ struct MlpStep {
     if (parts & 2) cme::mlp_wgrad(d, w, S(stream));
   }
 
+  // Native step loop: `count` consecutive global batches of B samples starting at gstart0 (wrapping to 0
+  // when a batch would pass N_end), this rank's shard [gstart + shard_off, +n) of each, every kernel
+  // launched from here with no Python between steps.  sgd = 1: single process, SGD fused into wgrad;
+  // sgd = 2: the xGMI all-reduce + SGD fused into wgrad (set_xgmi).  The eager counterpart of a captured
+  // epoch graph: the first kernel starts one launch after the call instead of after a whole-graph
+  // submission (bench/launch_overhead.py: ~7 us less fixed cost per timed run, equal per-step cost).
+  void run_steps(int64_t gstart0, int64_t count, int64_t B, int64_t shard_off, int n, int64_t N_end, double scale,
+                 double reg, double lr, int sgd, uintptr_t stream) {
+    CME_REQUIRE(count >= 0 && n > 0 && n <= ld && B >= n && N_end >= B && (sgd == 1 || sgd == 2),
+                "MlpStep.run_steps: bad step plan");
+    int64_t gs = gstart0;
+    for (int64_t i = 0; i < count; ++i) {
+      if (gs + B > N_end) gs = 0;
+      run(gs + shard_off, n, scale, reg, lr, sgd, 0, stream, 3);
+      gs += B;
+    }
+  }
+
   // Weight-gradient pieces of a step whose forward + head already ran (parts=1): used by the
   // trainer to overlap per-bucket all-reduces with the rest of the backward pass.
   // parts bit0 = dW1 rows [row0, row0+rows), bit1 = dW2 + bias gradients.  Split paths only.
@@ -367,6 +385,10 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("bias_col", &MlpStep::bias_col)
       .def("set_xgmi", &MlpStep::set_xgmi, py::arg("desc"), py::arg("slots"), py::arg("off_b1"), py::arg("off_W2"),
            py::arg("off_b2"))
+      .def("run_steps", &MlpStep::run_steps, py::arg("gstart0"), py::arg("count"), py::arg("B"), py::arg("shard_off"),
+           py::arg("n"), py::arg("N_end"), py::arg("scale"), py::arg("reg"), py::arg("lr"), py::arg("sgd"),
+           py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
       .def("run_wgrad", &MlpStep::run_wgrad, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"),
            py::arg("lr"), py::arg("sgd"), py::arg("parts"), py::arg("row0"), py::arg("rows"), py::arg("stream"))
       .def_readwrite("npw", &MlpStep::npw)

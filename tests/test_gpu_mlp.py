@@ -396,3 +396,23 @@ def test_wide_engines_agree_with_register_staged_engine(dt, path, H, n):
     assert torch.equal(out[0][0], out[1][0])  # a1
     for u, v in zip(out[0][1:], out[1][1:]):
         assert _rel(u.float(), v.float()) < (1e-5 if path == "split3" else 1e-3)  # split1: bf16 dZ1
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_native_step_loop_equals_graph_replay(dt):
+    """MlpStep.run_steps (the native C++ step loop run_plan uses for consecutive full batches) launches the
+    same kernels as the captured graph: bitwise-identical parameters, including the wrap past the end of
+    the dataset."""
+    from cme213_sp18_amd.parallel.trainer import EpochPlan
+    x, y = synthetic_mnist(4000, seed=4)
+    nn = NeuralNetwork([784, 100, 10])
+    plan = EpochPlan([(800 * (i % 5), 800) for i in range(7)])  # 5 batches, then wraps to 0
+    out = []
+    for executor in ("auto", "graph"):
+        t = DataParallelTrainer(nn.copy(), dtype=dt, executor=executor)
+        t.load(x, y)
+        assert (t.native_plan(plan) is not None) == (executor == "auto")
+        t.run_plan(plan, 0.01, 1e-4)
+        torch.cuda.synchronize()
+        out.append(t.engine.params.clone())
+    assert torch.equal(out[0], out[1])
