@@ -155,7 +155,8 @@ def main(argv=None) -> int:
     finite = bool(torch.isfinite(tr.engine.params).all().item())
     bad = comm.allreduce_scalar(0.0 if finite else 1.0, op="max") > 0
     comm_failed = tr.comm_failed()
-    ok = not bad and not comm_failed
+    kerr = comm.allreduce_scalar(1.0 if tr.engine.kernel_error() else 0.0, op="max") > 0
+    ok = not bad and not comm_failed and not kerr
     # strong scaling drops the remainder columns when R does not divide the batch (trainer.shard)
     images = a.steps * (global_batch // R) * R
     value = images / dt
@@ -182,7 +183,8 @@ def main(argv=None) -> int:
                        "comm_ok": not comm_failed},
         }
         if not ok:
-            rec["invalid"] = "non-finite parameters" if bad else "an xGMI peer wait timed out"
+            rec["invalid"] = ("non-finite parameters" if bad else "an xGMI peer wait timed out" if comm_failed
+                              else "a forward+head workgroup wait timed out")
         print(json.dumps(rec), flush=True)
     shutdown()
     return 0 if ok else 1

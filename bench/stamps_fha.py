@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Timeline of the all-gather forward + head launch (mlp_fwd1_head_ag) from s_memrealtime stamps (100 MHz):
+per workgroup entry -> GEMM + z2 partial published -> all tm workgroups of its column tile arrived ->
+dZ1 stored.  Diagnostic.
+
+    python bench/stamps_fha.py [--n 800] [--hidden 100]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=800)
+    ap.add_argument("--hidden", type=int, default=100)
+    a = ap.parse_args(argv)
+    import numpy as np
+    import torch
+
+    from cme213_sp18_amd import NeuralNetwork
+    from cme213_sp18_amd.parallel import MlpEngine
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    x, y = synthetic_mnist(4000, seed=0)
+    nn = NeuralNetwork([784, a.hidden, 10])
+    e = MlpEngine(nn.H, dtype="f32", max_cols=a.n, device="cuda", path="split3")
+    e.set_params(*nn.params)
+    e.load_dataset(x, y)
+    step = e._hip_step()
+    assert step.fh_allgather == 1
+    st = torch.cuda.current_stream().cuda_stream
+    buf = torch.zeros(4096 * 4, dtype=torch.int64, device="cuda")
+    pct = lambda v: [round(float(np.percentile(v, q)), 3) for q in (0, 50, 90, 100)]  # noqa: E731
+    for rep in range(4):
+        for _ in range(20):
+            step.run(0, a.n, 1.0 / a.n, 1e-4, 0.0, 1, 0, st, 3)
+        torch.cuda.synchronize()
+        buf.zero_()
+        step.stamps = buf.data_ptr()
+        step.run(0, a.n, 1.0 / a.n, 1e-4, 0.0, 1, 0, st, 1)
+        step.stamps = 0
+        torch.cuda.synchronize()
+        s = buf.view(-1, 4).cpu().numpy().astype(np.int64)
+        s = s[s[:, 0] > 0]
+        t0 = s[:, 0].min()
+        rel = (s - t0) * 10.0 / 1000.0
+        print(json.dumps({"wgs": int(len(s)), "entry": pct(rel[:, 0]), "published": pct(rel[:, 1]),
+                          "all_arrived": pct(rel[:, 2]), "wait": pct(rel[:, 2] - rel[:, 1]), "end": pct(rel[:, 3])}))
+
+
+if __name__ == "__main__":
+    main()

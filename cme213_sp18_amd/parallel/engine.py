@@ -119,6 +119,9 @@ class MlpEngine:
         self._alloc_acts(max_cols)
         self._step = None
         self._xgmi_fuse = None
+        # H <= 128 split path: the forward + head launch in its all-gather form (every workgroup of the
+        # launch must be resident at once; DataParallelTrainer turns it off when processes share a GPU)
+        self.fh_allgather = True
 
     def _configure_path(self):
         dev = self.device
@@ -155,8 +158,15 @@ class MlpEngine:
         # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
         # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
         self.fh_counters = None
+        self.ag_counters = self.ag_slabs = self.ag_err = None
         if self.backend == "hip" and self.np and H <= 128 and C <= 16:
-            self.fh_counters = torch.zeros((ld + 31) // 32, dtype=torch.int32, device=dev)
+            tiles = (ld + 31) // 32
+            self.fh_counters = torch.zeros(tiles, dtype=torch.int32, device=dev)
+            # all-gather form (mlp_fwd1_head_ag): monotonic uint64 tile counters, z2 partial slabs
+            # [tile][8 row tiles][16 classes][32 columns], and the timed-out-wait word
+            self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)  # one 256-B line each
+            self.ag_slabs = torch.zeros(tiles * 8 * 16 * 32, dtype=torch.float32, device=dev)
+            self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._step = None
 
     def load_dataset(self, x, labels, normalize: bool = False):
@@ -229,6 +239,16 @@ class MlpEngine:
             elif self.dtype == "bf16":
                 self.W1g.copy_(self.W1.to(torch.bfloat16))
 
+    def set_fh_allgather(self, on: bool) -> None:
+        self.fh_allgather = bool(on)
+        if self._step is not None:
+            self._step.fh_allgather = int(self.fh_allgather)
+
+    def kernel_error(self) -> bool:
+        """True if a forward + head launch's wait for the workgroups of its column tile timed out (the
+        all-gather form; its outputs were then not trusted).  Reads a device word: synchronises."""
+        return self.ag_err is not None and bool(self.ag_err.item())
+
     def join(self):
         """Kept for API stability: every kernel of a step runs on the caller's stream, nothing to join."""
 
@@ -270,6 +290,10 @@ class MlpEngine:
             if self.fh_counters is not None:
                 s.fh_counters = self.fh_counters.data_ptr()
                 s.fh_tiles = int(self.fh_counters.numel())
+                s.ag_counters = self.ag_counters.data_ptr()
+                s.ag_slabs = self.ag_slabs.data_ptr()
+                s.ag_err = self.ag_err.data_ptr()
+                s.fh_allgather = int(self.fh_allgather)
             if self.np and self.XT is not None and self.XT.shape[0] == self.P + 1:
                 s.bias_col = 1
             if self._xgmi_fuse is not None and s.bias_col:

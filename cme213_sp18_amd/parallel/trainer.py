@@ -90,7 +90,16 @@ class DataParallelTrainer:
                                 path=path)
         self.engine.set_params(*nn.params)
         self._graphs: dict = {}
+        self._sharing = None
         self.iter = 0
+        # the all-gather forward + head launch waits for the other workgroups of its own launch: every
+        # workgroup must be resident at once, which several processes sharing a GPU (each launch spinning
+        # while the other's holds CUs) cannot promise -- one process per GPU keeps it
+        from .comm import TorchDistComm
+
+        if (self.R > 1 and isinstance(self.comm, TorchDistComm) and self.engine.device.type == "cuda"
+                and self._gpu_sharing() > 1):
+            self.engine.set_fh_allgather(False)
         from ..utils.tracing import Roctx
 
         self.roctx = Roctx()       # CME_ROCTX=1: epoch / phase ranges for rocprofv3 --marker-trace
@@ -173,20 +182,26 @@ class DataParallelTrainer:
             return None
         return xb
 
+    def _gpu_sharing(self) -> int:
+        """How many ranks of the group run on this rank's GPU (1 = one process per GPU).  Collective."""
+        import torch.distributed as dist
+
+        if self._sharing is None:
+            dev = self.engine.device
+            props = torch.cuda.get_device_properties(dev)
+            ident = str(getattr(props, "uuid", "")) or f"{os.environ.get('HIP_VISIBLE_DEVICES', '')}:{dev.index}"
+            ids = [None] * self.R
+            dist.all_gather_object(ids, (os.uname().nodename, ident), group=self.comm.group)
+            self._sharing = sum(1 for x in ids if x == ids[self.rank])
+        return self._sharing
+
     def _fused_fits(self, tiles: int) -> bool:
         """Every wgrad tile waits for the same tile of its peers, so all tiles of all ranks SHARING a
         GPU must be resident at once (2 workgroups of 512 threads per CU at the kernel's occupancy).
         One rank per GPU always fits (~180 tiles at H=100 on 256 CUs); the several-ranks-on-one-GPU
         rehearsal only with 2 ranks.  Collective."""
-        import torch.distributed as dist
-
-        dev = self.engine.device
-        props = torch.cuda.get_device_properties(dev)
-        ident = str(getattr(props, "uuid", "")) or f"{os.environ.get('HIP_VISIBLE_DEVICES', '')}:{dev.index}"
-        ids = [None] * self.R
-        dist.all_gather_object(ids, (os.uname().nodename, ident), group=self.comm.group)
-        sharing = sum(1 for x in ids if x == ids[self.rank])
-        return self._all_true(sharing * tiles <= 2 * props.multi_processor_count)
+        props = torch.cuda.get_device_properties(self.engine.device)
+        return self._all_true(self._gpu_sharing() * tiles <= 2 * props.multi_processor_count)
 
     def _all_true(self, v: bool) -> bool:
         import torch.distributed as dist

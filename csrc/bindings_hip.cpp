@@ -53,6 +53,10 @@ struct MlpStep {
   // head (mlp_fwd1_head); 0: separate fwd1 + head kernels
   uintptr_t fh_counters = 0;
   int fh_tiles = 0;
+  // the all-gather form of that launch (mlp_fwd1_head_ag): uint64 counters, z2 partial slabs and an error
+  // word (>= fh_tiles each); fh_allgather = 1 selects it when all three are set
+  uintptr_t ag_counters = 0, ag_slabs = 0, ag_err = 0;
+  int fh_allgather = 0;
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
   void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2) {
@@ -137,7 +141,10 @@ struct MlpStep {
           h.loss_partial = a.loss_partial; h.shift = shift; h.mode = cme::HEAD_TRAIN;
           h.z2part = P_<float>(z2p);
           h.stamps = hstamps ? reinterpret_cast<unsigned long long*>(hstamps) : nullptr;
-          if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
+          if (fh_allgather && ag_counters && ag_slabs && ag_err && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {
+            cme::mlp_fwd1_head_ag(a, h, P_<unsigned long long>(ag_counters), P_<float>(ag_slabs), P_<int>(ag_err),
+                                  fh_tiles, S(stream));
+          } else if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
             cme::mlp_fwd1_head(a, h, P_<unsigned>(fh_counters), fh_tiles, S(stream));
           } else {
             // wide layers: the forward GEMM also leaves the head's z2 partials (unless only the head runs)
@@ -372,6 +379,10 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("loss", &MlpStep::loss)
       .def_readwrite("fh_counters", &MlpStep::fh_counters)
       .def_readwrite("fh_tiles", &MlpStep::fh_tiles)
+      .def_readwrite("ag_counters", &MlpStep::ag_counters)
+      .def_readwrite("ag_slabs", &MlpStep::ag_slabs)
+      .def_readwrite("ag_err", &MlpStep::ag_err)
+      .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
       .def("tp_forward", &MlpStep::tp_forward)
       .def("tp_head", &MlpStep::tp_head)
       .def_readwrite("shift", &MlpStep::shift)

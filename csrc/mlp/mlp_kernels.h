@@ -62,6 +62,12 @@ void mlp_head(DType dt, const HeadArgs& a, hipStream_t stream);
 // zero-initialised uint32 (one per 32-column tile; each launch leaves them at 0 again).
 bool mlp_fwd1_head_ok(const SplitStepArgs& f, const HeadArgs& h);
 void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters, int max_tiles, hipStream_t s);
+// the same launch in the all-gather form (every row-tile workgroup of a column tile sums the tile's z2
+// partials and forms dZ1 for its own rows): counters >= max_tiles * 32 uint64 (one 256-byte line per tile,
+// only ever incremented), slabs
+// >= max_tiles * 8 * 16 * 32 floats, err: set to 1 if a wait for the tile's workgroups timed out
+void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long long* counters, float* slabs,
+                      int* err, int max_tiles, hipStream_t s);
 int mlp_head_num_blocks(int n);
 
 struct WgradArgs {

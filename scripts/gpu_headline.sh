@@ -8,10 +8,13 @@ O=gpurun_out/headline
 mkdir -p $O
 echo "== tests"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_mlp.py -m gpu -x -q \
-  -k "native or graph" --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+  --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+echo "== kbench"
+timeout -k 10 120 python bench/kbench.py --hidden 100 --cols 800 --cfg f32:split3 bf16:split1 > $O/kbench.log 2>&1 || { tail -5 $O/kbench.log; exit 1; }
+grep -v amdgpu $O/kbench.log | cut -c1-260
 echo "== launch overhead"
-timeout -k 10 200 python bench/launch_overhead.py > $O/launch_overhead.jsonl 2>&1 && timeout -k 10 200 python bench/launch_overhead.py --spin >> $O/launch_overhead.jsonl 2>&1 || { tail -5 $O/launch_overhead.jsonl; exit 1; }
+timeout -k 10 200 python bench/launch_overhead.py > $O/launch_overhead.jsonl 2>&1 || { tail -5 $O/launch_overhead.jsonl; exit 1; }
 grep -v amdgpu $O/launch_overhead.jsonl
 for args in "--steps 20 --warmup 5" "--steps 20 --warmup 5" "--steps 20 --warmup 5 --executor graph" "--steps 20 --warmup 5 --executor graph" "--steps 4000 --warmup 400"; do
   echo "== bench $args"

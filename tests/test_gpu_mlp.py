@@ -274,6 +274,7 @@ def test_fwd1_head_single_launch_matches_two_launches(dtype, H, n):
     outs = []
     for single in (True, False):
         e = MlpEngine((784, H, 10), dtype, max_cols=n, device="cuda")
+        e.set_fh_allgather(False)  # the last-arriver form (the all-gather form: its own test)
         if not single:
             e.fh_counters = None
             e._step = None
@@ -416,3 +417,38 @@ def test_native_step_loop_equals_graph_replay(dt):
         torch.cuda.synchronize()
         out.append(t.engine.params.clone())
     assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("H,n", [(100, 800), (100, 100), (128, 513), (37, 45), (16, 32)])
+def test_fwd1_head_allgather_matches_last_arriver(dtype, H, n):
+    """mlp_fwd1_head_ag (every row-tile workgroup sums the column tile's z2 partials and forms dZ1 for its
+    own rows) against the last-arriver launch over several SGD steps: a1 bitwise, the rest to fp32
+    rounding (z2 is summed in another order); D, dZ1 planes, loss and params vs the fp32 reference; the
+    monotonic tile counters advance by exactly tm per launch and no wait timed out."""
+    x, y = synthetic_mnist(2 * n + 7, seed=H)
+    rng = np.random.default_rng(H + n)
+    W1 = rng.standard_normal((H, 784)) * 0.01
+    W2 = rng.standard_normal((10, H)) * 0.01
+    b1 = rng.standard_normal(H) * 0.1
+    b2 = rng.standard_normal(10) * 0.1
+    outs = []
+    for ag in (True, False):
+        e = MlpEngine((784, H, 10), dtype, max_cols=n, device="cuda")
+        e.set_fh_allgather(ag)
+        e.load_dataset(x, y, normalize=True)
+        e.set_params(W1, b1, W2, b2)
+        steps = (0, n, 7, 0)
+        for step, off in enumerate(steps):
+            e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True, with_loss=step == 3)
+        torch.cuda.synchronize()
+        outs.append([t.clone().cpu() for t in (e.a1[:, :n], e.D[:, :n], e.dZ1[:, :n], e.params)] + [e.loss_sum()])
+        if ag:
+            tm, tn = (H + 15) // 16, (n + 31) // 32
+            assert not e.kernel_error()
+            assert e.ag_counters.view(-1, 32)[:tn, 0].tolist() == [tm * len(steps)] * tn
+    a, b = outs
+    tol = 1e-5 if dtype == "f32" else 2e-3
+    for ta, tb in zip(a[:-1], b[:-1]):
+        assert _rel(ta, tb) < tol
+    assert abs(a[-1] - b[-1]) / abs(b[-1]) < 1e-5
