@@ -56,12 +56,14 @@ def sum_even_odd_parallel(v) -> tuple[int, int]:
     return tuple(int(x) for x in host().sum_even_odd(np.ascontiguousarray(v, np.uint32), True))
 
 
-def sum_even_odd_gpu(v: torch.Tensor) -> torch.Tensor:
-    """(even_sum, odd_sum) as a uint64-valued int64 tensor of 2, computed by a wave-reduction kernel."""
+def sum_even_odd_gpu(v: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """(even_sum, odd_sum) as a uint64-valued int64 tensor of 2 (a zeroing memset node + one
+    wave-reduction kernel).  ``out``: a preallocated int64 tensor of 2 (timed loops allocate nothing)."""
     require_cuda(v)
     if v.dtype not in (torch.int32, torch.uint32):
         raise TypeError("sum_even_odd_gpu: need a 32-bit integer tensor")
-    out = torch.empty(2, dtype=torch.int64, device=v.device)
+    if out is None:
+        out = torch.empty(2, dtype=torch.int64, device=v.device)
     kernels().sum_even_odd(v.data_ptr(), v.numel(), out.data_ptr(), stream_handle())
     return out
 

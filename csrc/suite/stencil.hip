@@ -6,8 +6,8 @@
 //   variant 0 global : one thread per interior point
 //   variant 1 loop   : each thread walks ROWS consecutive y points keeping the
 //                      2b+1-tall column window in registers (1 new load per row)
-//   variant 2 lds    : (64 x 16) tile + b-wide halo staged in LDS, every
-//                      stencil read served from LDS
+//   variant 2 lds    : (256 x 32) tile + b-wide halo staged in LDS once with
+//                      16-byte loads, every stencil read served from LDS
 //   variant 3 vec    : 4 x-points per lane with 16-byte loads/stores + the
 //                      register column window (fewest instructions per byte)
 #include <algorithm>
@@ -148,32 +148,72 @@ __device__ __forceinline__ void stencil_vec_body(float* __restrict__ next, const
   }
 }
 
-constexpr int kTX = 64, kTY = 16;
 constexpr int kVecRows = 8;
+
+// variant 2 "lds": a 256 x 32 interior tile + its b-wide halo staged into LDS ONCE with 16-byte buffer
+// loads (every grid value of the tile read from memory once: (256 + 2b)(32 + 2b) / (256 * 32) = 1.29x at
+// order 8, vs 1.75x for vec's three overlapping float4 loads per output row), then each lane forms 4 x
+// points x 8 rows from LDS: per row the centre line as 3 x ds_read_b128 and the new bottom row's 4 values,
+// with the (2b+1)-tall column window in registers.
+constexpr int kLTX = 256, kLTY = 32;
 
 template <int ORDER>
 __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
                                                  int gy, int nx, int ny, float xcfl, float ycfl, int tbx, int tby) {
   constexpr int B = Coef<ORDER>::B;
-  constexpr int W = kTX + 2 * B, Hh = kTY + 2 * B;
-  __shared__ float tile[Hh][W + 1];
-  const int bx = tbx * kTX, by = tby * kTY;  // interior-coordinate origin
-  // stage the tile + halo: grid rows by .. by+Hh-1, cols bx .. bx+W-1 (grid coordinates)
-  for (int idx = threadIdx.y * 64 + threadIdx.x; idx < Hh * W; idx += 256) {
-    const int r = idx / W, cc = idx - r * W;
-    const int gr = by + r, gc = bx + cc;
-    tile[r][cc] = (gr < gy && gc < gx) ? curr[(int64_t)gr * gx + gc] : 0.f;
+  constexpr int W4 = (kLTX + 2 * B + 3) / 4 + (B < 4 ? 1 : 0);  // staged float4 per row (+1: 3-wide reads)
+  constexpr int HH = kLTY + 2 * B;
+  __shared__ f32x4 tile[HH][W4];
+  const int c0 = tbx * kLTX, r0 = tby * kLTY;  // grid column / row of staged (0, 0)
+  const __amdgpu_buffer_rsrc_t rc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(curr), (short)0, (int)((int64_t)gx * gy * 4), 0x00020000);
+  const int tid = threadIdx.y * 64 + threadIdx.x;
+  for (int idx = tid; idx < HH * W4; idx += 256) {
+    const int r = idx / W4, q = idx - r * W4;
+    const int gr = r0 + r, gc = c0 + 4 * q;
+    // out-of-grid rows / columns past the row read 0 or the next row's first values: never used
+    tile[r][q] = ld4(rc, gr < gy ? (int64_t)gr * gx + gc : (int64_t)0x7FFFFFF0 / 4);
   }
   __syncthreads();
-  const int lx = threadIdx.x;
-  for (int ly = threadIdx.y; ly < kTY; ly += 4) {
-    const int x = bx + lx, y = by + ly;
-    if (x < nx && y < ny) {
-      const int tr = ly + B, tc = lx + B;
-      next[(int64_t)(y + B) * gx + (x + B)] = apply_stencil<ORDER>(
-          tile[tr][tc], [&](int k) { return tile[tr][tc + k]; }, [&](int k) { return tile[tr + k][tc]; }, xcfl,
-          ycfl);
+  const int lane = threadIdx.x, xl = 4 * lane;  // interior local columns xl .. xl + 3
+  const int y0 = threadIdx.y * 8;
+  if (c0 + xl >= nx || r0 + y0 >= ny) return;
+  const float* t = reinterpret_cast<const float*>(&tile[0][0]);
+  constexpr int WP = W4 * 4;  // floats per staged row
+  // staged (row, col) of interior local (y, x): (y + B, x + B)
+  float win[2 * B + 1][4];
+#pragma unroll
+  for (int k = 0; k < 2 * B; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) win[k][j] = t[(y0 + k) * WP + xl + B + j];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int y = y0 + r;
+    if (r0 + y >= ny) break;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) win[2 * B][j] = t[(y + 2 * B) * WP + xl + B + j];
+    float line[12];  // staged columns xl .. xl + 11 of the centre row
+    const f32x4* lp = reinterpret_cast<const f32x4*>(t + (y + B) * WP + xl);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const f32x4 v = lp[q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) line[4 * q + j] = v[j];
     }
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = apply_stencil<ORDER>(
+          line[B + j], [&](int k) { return line[B + j + k]; }, [&](int k) { return win[B + k][j]; }, xcfl, ycfl);
+    const int gyy = r0 + y + B, gxx = c0 + xl + B;
+    float* dst = next + (int64_t)gyy * gx + gxx;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (c0 + xl + j < nx) dst[j] = o[j];
+#pragma unroll
+    for (int k = 0; k < 2 * B; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) win[k][j] = win[k + 1][j];
   }
 }
 
@@ -229,8 +269,8 @@ void launch_v(float* next, const float* curr, int gx, int gy, float xcfl, float 
               hipStream_t s) {
   constexpr int B = Coef<ORDER>::B;
   const int nx = gx - 2 * B, ny = gy - 2 * B;
-  const int rows_per_block = VARIANT == 0 ? 4 : (VARIANT == 1 ? 4 * 8 : (VARIANT == 2 ? kTY : 4 * kVecRows));
-  const int cols_per_block = VARIANT == 3 ? 256 : 64;
+  const int rows_per_block = VARIANT == 0 ? 4 : (VARIANT == 1 ? 4 * 8 : (VARIANT == 2 ? kLTY : 4 * kVecRows));
+  const int cols_per_block = VARIANT >= 2 ? 256 : 64;
   const int nbx = (nx + cols_per_block - 1) / cols_per_block, nby = (ny + rows_per_block - 1) / rows_per_block;
   const int nint = nbx * nby;
   const int64_t bc_cells_total = 2 * ((int64_t)gx * B + (int64_t)(gy - 2 * B) * B);

@@ -157,6 +157,9 @@ void pagerank_propagate(const uint32_t* indptr, const uint32_t* edges, const flo
 }
 
 void sum_even_odd(const uint32_t* v, int64_t n, unsigned long long* sums, hipStream_t s) {
+  // (a self-resetting single-kernel form -- returning atomics + last-ticket publish, no memset -- measured
+  // 54 us vs 42 us per call at 30M: the serial atomic round trips of the last workgroup cost more than
+  // the memset node)
   HIP_CHECK(hipMemsetAsync(sums, 0, 2 * sizeof(unsigned long long), s));
   if (n <= 0) return;
   CME_REQUIRE((reinterpret_cast<uintptr_t>(v) & 15) == 0, "sum_even_odd: input must be 16-byte aligned");

@@ -25,6 +25,16 @@ def test_sum_even_odd_gpu(n):
     assert tuple(got) == hw1.sum_even_odd_parallel(v)
 
 
+def test_sum_even_odd_gpu_repeated_calls_rearm():
+    """Back-to-back calls of different inputs (and an empty one)
+    each return their own sums, into a preallocated output."""
+    out = torch.empty(2, dtype=torch.int64, device="cuda")
+    for n in (3, 1_000_003, 0, 77):
+        v = hw1.init_sum_input(n, seed=n + 1) if n else np.zeros(0, np.uint32)
+        got = hw1.sum_even_odd_gpu(torch.from_numpy(v.view(np.int32)).cuda(), out).cpu().tolist()
+        assert tuple(got) == (hw1.sum_even_odd_parallel(v) if n else (0, 0))
+
+
 @pytest.mark.parametrize("n", [1, 100, 4096, 4097, 40000, 1 << 22, 3_000_001])
 def test_radix_sort_gpu(n):
     keys = np.random.default_rng(n).integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
