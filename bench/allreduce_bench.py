@@ -38,7 +38,8 @@ MLP_BUCKETS = {"mlp_h100": 784 * 100 + 100 + 10 * 100 + 10,
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--paths", nargs="*", default=["rccl", "xgmi"], choices=["rccl", "xgmi"])
+    ap.add_argument("--paths", nargs="*", default=["rccl", "xgmi", "xgmi-bf16"], choices=["rccl", "xgmi", "xgmi-bf16"],
+                    help="xgmi-bf16: fp32 gradients over a bf16 wire (half the bytes), summed in fp32")
     ap.add_argument("--min-bytes", type=int, default=4 << 10)
     ap.add_argument("--max-bytes", type=int, default=64 << 20)
     ap.add_argument("--xgmi-max-bytes", type=int, default=16 << 20, help="largest bucket tried on the xGMI path")
@@ -106,12 +107,16 @@ def main(argv=None) -> int:
                 ok = bool(torch.allclose(t.double(), expect, rtol=1e-6))
                 sec = time_calls(lambda: comm.allreduce_(t), comm, device, a.iters, a.warmup)
             else:
-                if n * eb > a.xgmi_max_bytes:
+                if n * eb > a.xgmi_max_bytes or (path == "xgmi-bf16" and dt != torch.float32):
                     continue
                 from cme213_sp18_amd.parallel.xgmi import XgmiBucket
 
+                wire = torch.bfloat16 if path == "xgmi-bf16" else dt
+                if path == "xgmi-bf16":  # what crosses the wire is bf16(base * (rank + 1)), summed in fp32
+                    expect = sum((base * (r + 1)).to(torch.bfloat16).double() for r in range(R))
+                    rec["wire_bytes"] = n * 2
                 try:  # collective: on an IPC failure every rank skips this size together
-                    xb = XgmiBucket(comm.group, rank, R, n, dt, device, self_test=False)
+                    xb = XgmiBucket(comm.group, rank, R, n, dt, device, self_test=False, wire=wire)
                 except RuntimeError as ex:
                     rec["error"] = str(ex)
                     records.append(rec)
@@ -126,6 +131,7 @@ def main(argv=None) -> int:
                 rec["peer_wait_timeouts"] = xb.error()
                 ok = ok and rec["peer_wait_timeouts"] == 0
                 xb.close()
+                expect = base.double() * (R * (R + 1) / 2)
             rec["correct"] = comm.allreduce_scalar(0.0 if ok else 1.0, op="max") == 0.0
             rec["us"] = round(sec * 1e6, 3)
             algbw = n * eb / sec / 1e9

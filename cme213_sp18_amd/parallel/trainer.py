@@ -65,7 +65,8 @@ class DataParallelTrainer:
     def __init__(self, nn, comm: Communicator | None = None, device=None, dtype: str = "f32",
                  batch_size: int = 800, backend: str = "hip", shift: bool = True, use_graphs: bool = True,
                  normalize: bool = False, path: str = "auto", allreduce: str = "auto", overlap: bool = True,
-                 overlap_chunks: int = 0, fuse_allreduce: bool = True, executor: str = "auto"):
+                 overlap_chunks: int = 0, fuse_allreduce: bool = True, executor: str = "auto",
+                 grad_wire: str = "auto"):
         self.nn = nn
         # how run_plan enqueues a plan: "auto" = the native C++ step loop (MlpStep.run_steps) for plans of
         # consecutive full batches on the fused paths (pure device work), else the captured HIP graph;
@@ -73,6 +74,13 @@ class DataParallelTrainer:
         if executor not in ("auto", "graph", "eager"):
             raise ValueError("executor must be auto, graph or eager")
         self.executor = executor
+        # element type of the gradients on the xGMI wire: "f32" (exact), "bf16" (half the bytes, summed in
+        # fp32 after the pull), "auto" = bf16 for the bf16 compute path (its GEMM operands are bf16 already)
+        # when that is what brings the bucket under XGMI_AUTO_MAX_BYTES (784-1024-10: 3.3 -> 1.6 MB), else
+        # the parameter dtype (small buckets keep the exact, wgrad-fused all-reduce)
+        if grad_wire not in ("auto", "f32", "bf16"):
+            raise ValueError("grad_wire must be auto, f32 or bf16")
+        self.grad_wire = grad_wire
         # RCCL path: dW1 row chunks all-reduced while the next chunk is computed (0: ~BUCKET_BYTES each).
         # Setting it also forces the overlapped path with ONE rank of a real process group (nccl world 1),
         # so a one-GPU box exercises the side-stream + graph-captured backward.
@@ -110,7 +118,7 @@ class DataParallelTrainer:
         # bitwise comparison with the separate-kernel step has passed on every rank
         self._xgmi_fused = None
         self.fused_allreduce = False
-        if self.xgmi is not None and fuse_allreduce:
+        if self.xgmi is not None and fuse_allreduce and self.xgmi.wire == self.engine.params.dtype:
             slots = self.engine.fused_allreduce_slots()
             if slots and self.engine.params.dtype == torch.float32 and self._fused_fits(slots):
                 from .xgmi import XgmiBucket
@@ -135,7 +143,8 @@ class DataParallelTrainer:
                           and len(self._buckets()) > 1)
         self._comm_stream = torch.cuda.Stream(self.engine.device) if self._bucketed else None
         self.allreduce_impl = "none" if self.R == 1 else (
-            "xgmi" if self.xgmi is not None else "host-gloo" if allreduce == "host" else self.comm.name)
+            ("xgmi-bf16wire" if self.xgmi.wire == torch.bfloat16 else "xgmi") if self.xgmi is not None
+            else "host-gloo" if allreduce == "host" else self.comm.name)
 
     def _setup_xgmi(self, mode: str):
         """Peer-to-peer fused all-reduce+SGD (parallel/xgmi.py) when every rank is a GPU on this node.
@@ -166,10 +175,18 @@ class DataParallelTrainer:
             return None
         # one-shot: every rank pulls all R-1 peer buckets over its links -- the win for latency-bound
         # buckets (318 KB at H=100); past a few MB the ring/tree of RCCL moves fewer bytes per link
-        if mode == "auto" and e.params.numel() * e.params.element_size() > XGMI_AUTO_MAX_BYTES:
+        # (docs/PERFORMANCE.md "Communication policy"); the bytes that count are the WIRE bytes
+        fp_bytes = e.params.numel() * e.params.element_size()
+        bf16_wire = e.params.dtype == torch.float32 and (
+            self.grad_wire == "bf16" or (self.grad_wire == "auto" and self.dtype == "bf16"
+                                         and fp_bytes > XGMI_AUTO_MAX_BYTES))
+        wire = torch.bfloat16 if bf16_wire else e.params.dtype
+        wire_bytes = e.params.numel() * torch.tensor([], dtype=wire).element_size()
+        if mode == "auto" and wire_bytes > XGMI_AUTO_MAX_BYTES:
             return None
         try:
-            xb = XgmiBucket(self.comm.group, self.rank, self.R, e.params.numel(), e.params.dtype, e.device)
+            xb = XgmiBucket(self.comm.group, self.rank, self.R, e.params.numel(), e.params.dtype, e.device,
+                            wire=wire)
         except Exception as ex:  # IPC unavailable: every rank sees the same failure at the same point
             if mode == "xgmi":
                 raise

@@ -34,24 +34,30 @@ class XgmiBucket:
     MODE_ALLREDUCE = 1
 
     def __init__(self, group, rank: int, world: int, numel: int, dtype: torch.dtype, device, self_test: bool = True,
-                 flag_slots: int = 0):
+                 flag_slots: int = 0, wire: torch.dtype | None = None):
+        """wire: the element type in the IPC buffers -- ``dtype`` (default), or torch.bfloat16 for float32
+        gradients (half the bytes over xGMI; every rank sums the R bf16 values in fp32, in rank order)."""
         import torch.distributed as dist
 
         if world > hip().comm.MAX_RANKS:
             raise ValueError(f"xGMI all-reduce supports at most {hip().comm.MAX_RANKS} ranks")
         if dtype not in (torch.float32, torch.float64):
             raise TypeError("xGMI bucket: float32 or float64")
-        self.rank, self.world, self.numel, self.dtype = rank, world, int(numel), dtype
+        wire = dtype if wire is None else wire
+        if wire not in (dtype, torch.bfloat16) or (wire == torch.bfloat16 and dtype != torch.float32):
+            raise TypeError("xGMI bucket: the wire is the gradient dtype, or bf16 for float32 gradients")
+        self.rank, self.world, self.numel, self.dtype, self.wire = rank, world, int(numel), dtype, wire
         self.group = group
         self.device = torch.device(device)
-        self.code = 1 if dtype == torch.float64 else 0
+        self.code = 1 if dtype == torch.float64 else (2 if wire == torch.bfloat16 else 0)
+        elt = {torch.float64: 8, torch.float32: 4, torch.bfloat16: 2}[wire]
         self.c = None
         with torch.cuda.device(self.device):
             # every step that can fail on one rank is followed by a collective agreement, so a local
             # IPC failure makes ALL ranks give up together instead of leaving peers in a collective
             mine, err = None, None
             try:
-                self.c = hip().comm.XgmiComm(rank, world, self.numel, 8 if self.code else 4, int(flag_slots))
+                self.c = hip().comm.XgmiComm(rank, world, self.numel, elt, int(flag_slots))
                 mine = self.c.handles()
             except Exception as ex:  # noqa: BLE001 - reported collectively below
                 err = f"rank {rank}: {ex}"
@@ -86,7 +92,8 @@ class XgmiBucket:
         n = self.numel
         base = torch.arange(n, dtype=torch.float64, device=self.device) % 1000
         g = ((self.rank + 1) * 0.25 + base / 1024).to(self.dtype)
-        exp = sum(((r + 1) * 0.25 + base / 1024).to(self.dtype).double() for r in range(self.world))
+        # what crosses the wire is g rounded to the wire type; the sum of R of those is exact in fp32
+        exp = sum(((r + 1) * 0.25 + base / 1024).to(self.dtype).to(self.wire).double() for r in range(self.world))
         good = True
         for _ in range(3):  # exercises both buffer halves and the epoch counters
             t = g.clone()

@@ -91,7 +91,8 @@ class XgmiComm {
   XgmiComm(int rank, int world, int64_t n, int elt_bytes, int64_t flag_slots = 0) {
     CME_REQUIRE(world >= 1 && world <= kMaxRanks, "XgmiComm: 1 <= world <= 8");
     CME_REQUIRE(rank >= 0 && rank < world, "XgmiComm: bad rank");
-    CME_REQUIRE(elt_bytes == 4 || elt_bytes == 8, "XgmiComm: f32 or f64");
+    CME_REQUIRE(elt_bytes == 2 || elt_bytes == 4 || elt_bytes == 8, "XgmiComm: bf16 wire, f32 or f64");
+    elt_ = elt_bytes;
     d_.rank = rank;
     d_.world = world;
     d_.n = n;
@@ -151,6 +152,8 @@ class XgmiComm {
            int64_t n, uintptr_t stream) {
     CME_REQUIRE(ready_ || d_.world == 1, "XgmiComm.run: open() the peer handles first");
     CME_REQUIRE(n == d_.n, "XgmiComm.run: element count differs from the one the buffers were sized for");
+    CME_REQUIRE((dtype == 0 && elt_ == 4) || (dtype == 1 && elt_ == 8) || (dtype == 2 && elt_ == 2),
+                "XgmiComm.run: dtype does not match the buffer's wire element size");
     xgmi_allreduce(d_, dtype, reinterpret_cast<const void*>(grads), reinterpret_cast<void*>(params), lr,
                    reinterpret_cast<void*>(planes), np, w1n, mode, reinterpret_cast<hipStream_t>(stream));
   }
@@ -198,6 +201,7 @@ class XgmiComm {
   size_t flag_bytes() const { return (size_t)nblocks_ * kMaxRanks * sizeof(uint32_t); }
   XgmiDesc d_;
   int64_t nblocks_ = 0;
+  int elt_ = 4;  // wire element bytes: 2 (bf16), 4 (f32), 8 (f64)
   size_t flags_off_ = 0, sig_off_ = 0, alloc_bytes_ = 0;
   Signature sig_{};
   bool ready_ = false;

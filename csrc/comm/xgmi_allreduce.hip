@@ -22,6 +22,7 @@
 #include <hip/hip_bf16.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "../common/hip_common.h"
 #include "xgmi_allreduce.h"
@@ -36,12 +37,14 @@ constexpr int kChunk = kThreads * kVec;       // elements per block
 constexpr int64_t kMaxGrid = 256;             // one block per CU: always resident, even with several ranks per GPU
 constexpr uint32_t kSpinLimit = 1u << 22;     // ~seconds, then flag an error instead of hanging
 
-template <typename T>
+// T: gradient / parameter type; W: the wire type in the IPC buffers (T, or bf16 for fp32 gradients:
+// half the bytes over xGMI, summed in fp32 after the pull)
+template <typename T, typename W = T>
 struct Args {
   const T* grads;
   T* params;
-  T* mybuf;
-  const T* peers[kMaxRanks];
+  W* mybuf;
+  const W* peers[kMaxRanks];
   uint32_t* myflags;
   uint32_t* peerflags[kMaxRanks];
   uint32_t* epochs;
@@ -61,7 +64,10 @@ __device__ __forceinline__ U peer_load(const void* base, int64_t off) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
                                                                       0x7FFFFFFF, 0x00020000);
   U out;
-  if constexpr (sizeof(U) == 4) {
+  if constexpr (sizeof(U) == 2) {
+    const auto w = __builtin_amdgcn_raw_buffer_load_b16(rs, (int)off, 0, kSysCoherent);
+    __builtin_memcpy(&out, &w, 2);
+  } else if constexpr (sizeof(U) == 4) {
     const auto w = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, kSysCoherent);
     __builtin_memcpy(&out, &w, 4);
   } else if constexpr (sizeof(U) == 8) {
@@ -89,8 +95,8 @@ __device__ __forceinline__ void store_planes(float v, __hip_bfloat16* base, int6
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void update_one(const Args<T>& a, int64_t i, T sum) {
+template <typename T, typename W>
+__device__ __forceinline__ void update_one(const Args<T, W>& a, int64_t i, T sum) {
   if (a.mode == kModeAllReduce) {
     const_cast<T*>(a.grads)[i] = sum;
     return;
@@ -105,8 +111,19 @@ __device__ __forceinline__ void update_one(const Args<T>& a, int64_t i, T sum) {
 
 // One chunk (kChunk elements) through copy -> release -> signal -> wait -> reduce -> update.
 // s_sync[0]: this chunk's epoch, s_sync[1]: 1 when the chunk must not be applied (block-uniform via LDS)
-template <typename T>
-__device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* s_sync) {
+template <typename W, typename T>
+__device__ __forceinline__ W to_wire(T x) {
+  if constexpr (std::is_same_v<W, T>) return x;
+  else return __float2bfloat16((float)x);
+}
+template <typename T, typename W>
+__device__ __forceinline__ T from_wire(W x) {
+  if constexpr (std::is_same_v<W, T>) return x;
+  else return (T)__bfloat162float(x);
+}
+
+template <typename T, typename W>
+__device__ __forceinline__ void do_chunk(const Args<T, W>& a, int64_t c, uint32_t* s_sync) {
   const int t = threadIdx.x;
   if (t == 0) {
     s_sync[0] = a.epochs[c] + 1;
@@ -123,30 +140,44 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
   //    bytes are in memory, not in this XCD's L2, once the store has retired; every wave drains its
   //    stores (vmcnt(0)) before the barrier that precedes the flag stores
   using V = T __attribute__((ext_vector_type(kVec)));
+  struct WV {
+    W e[kVec];
+  };  // one thread's elements on the wire (16 B for fp32, 8 B for bf16, 32 B for fp64)
   const bool full = i0 + kVec <= a.n;  // every vector but the last partial one
   const __amdgpu_buffer_rsrc_t rmine = __builtin_amdgcn_make_buffer_rsrc(a.mybuf, (short)0, 0x7FFFFFFF, 0x00020000);
+  auto store_w = [&](const void* src, int bytes, int64_t byte_off) {
+    if (bytes == 2) {
+      unsigned short w;
+      __builtin_memcpy(&w, src, 2);
+      __builtin_amdgcn_raw_buffer_store_b16(w, rmine, (int)byte_off, 0, kSysCoherent);
+    } else if (bytes == 4) {
+      unsigned w;
+      __builtin_memcpy(&w, src, 4);
+      __builtin_amdgcn_raw_buffer_store_b32(w, rmine, (int)byte_off, 0, kSysCoherent);
+    } else if (bytes == 8) {
+      __attribute__((ext_vector_type(2))) unsigned w;
+      __builtin_memcpy(&w, src, 8);
+      __builtin_amdgcn_raw_buffer_store_b64(w, rmine, (int)byte_off, 0, kSysCoherent);
+    } else {
+      for (int q = 0; q < bytes / 16; ++q) {
+        __attribute__((ext_vector_type(4))) unsigned w;
+        __builtin_memcpy(&w, static_cast<const char*>(src) + 16 * q, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(w, rmine, (int)byte_off + 16 * q, 0, kSysCoherent);
+      }
+    }
+  };
   if (full) {
     const V v = *reinterpret_cast<const V*>(a.grads + i0);
+    WV w;
 #pragma unroll
-    for (int q = 0; q < (int)(sizeof(V) / 16); ++q) {
-      uint4 w;
-      __builtin_memcpy(&w, reinterpret_cast<const char*>(&v) + 16 * q, 16);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, w),
-                                             rmine, (int)((half + i0) * (int64_t)sizeof(T)) + 16 * q, 0,
-                                             kSysCoherent);
-    }
+    for (int k = 0; k < kVec; ++k) w.e[k] = to_wire<W>(v[k]);
+    store_w(&w, (int)sizeof(WV), (half + i0) * (int64_t)sizeof(W));
   } else {
 #pragma unroll
     for (int k = 0; k < kVec; ++k)
       if (i0 + k < a.n) {
-        const T x = a.grads[i0 + k];
-        if constexpr (sizeof(T) == 8) {
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x),
-                                                rmine, (int)((half + i0 + k) * 8), 0, kSysCoherent);
-        } else {
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, x), rmine, (int)((half + i0 + k) * 4), 0,
-                                                kSysCoherent);
-        }
+        const W x = to_wire<W>(a.grads[i0 + k]);
+        store_w(&x, (int)sizeof(W), (half + i0 + k) * (int64_t)sizeof(W));
       }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -183,7 +214,10 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
 #pragma unroll
     for (int r = 0; r < kMaxRanks; ++r) {
       if (r >= a.world) break;
-      V v = peer_load<V>(a.peers[r], (half + i0) * (int64_t)sizeof(T));
+      const WV w = peer_load<WV>(a.peers[r], (half + i0) * (int64_t)sizeof(W));
+      V v;
+#pragma unroll
+      for (int k = 0; k < kVec; ++k) v[k] = from_wire<T>(w.e[k]);
       acc = r == 0 ? v : acc + v;
     }
 #pragma unroll
@@ -191,8 +225,9 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
   } else {
     for (int k = 0; k < kVec; ++k) {
       if (i0 + k >= a.n) break;
-      T acc = peer_load<T>(a.peers[0], (half + i0 + k) * (int64_t)sizeof(T));
-      for (int r = 1; r < a.world; ++r) acc += peer_load<T>(a.peers[r], (half + i0 + k) * (int64_t)sizeof(T));
+      T acc = from_wire<T>(peer_load<W>(a.peers[0], (half + i0 + k) * (int64_t)sizeof(W)));
+      for (int r = 1; r < a.world; ++r)
+        acc += from_wire<T>(peer_load<W>(a.peers[r], (half + i0 + k) * (int64_t)sizeof(W)));
       update_one(a, i0 + k, acc);
     }
   }
@@ -201,8 +236,8 @@ __device__ __forceinline__ void do_chunk(const Args<T>& a, int64_t c, uint32_t* 
 
 // Grid-stride over chunks with a capped grid: a block only ever waits on the
 // same chunk of its peers, and the capped grid is always fully resident.
-template <typename T>
-__global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(Args<T> a, int64_t nchunks) {
+template <typename T, typename W>
+__global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(Args<T, W> a, int64_t nchunks) {
   __shared__ uint32_t s_sync[2];
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     do_chunk(a, c, s_sync);
@@ -225,14 +260,15 @@ void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* param
   const int64_t nchunks = xgmi_num_blocks(d.n);
   if (nchunks == 0) return;
   const unsigned grid = (unsigned)std::min<int64_t>(nchunks, kMaxGrid);
-  auto fill = [&](auto* tag) {
+  auto fill = [&](auto* tag, auto* wtag) {
     using T = std::remove_pointer_t<decltype(tag)>;
-    Args<T> a{};
+    using W = std::remove_pointer_t<decltype(wtag)>;
+    Args<T, W> a{};
     a.grads = static_cast<const T*>(grads);
     a.params = static_cast<T*>(params);
-    a.mybuf = static_cast<T*>(d.mybuf);
+    a.mybuf = static_cast<W*>(d.mybuf);
     for (int r = 0; r < d.world; ++r) {
-      a.peers[r] = static_cast<const T*>(d.peers[r]);
+      a.peers[r] = static_cast<const W*>(d.peers[r]);
       a.peerflags[r] = d.peerflags[r];
     }
     a.myflags = d.myflags;
@@ -247,10 +283,11 @@ void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* param
     a.rank = d.rank;
     a.world = d.world;
     a.mode = mode;
-    xgmi_allreduce_kernel<T><<<grid, kThreads, 0, s>>>(a, nchunks);
+    xgmi_allreduce_kernel<T, W><<<grid, kThreads, 0, s>>>(a, nchunks);
   };
-  if (dtype == 1) fill((double*)nullptr);
-  else fill((float*)nullptr);
+  if (dtype == 1) fill((double*)nullptr, (double*)nullptr);
+  else if (dtype == 2) fill((float*)nullptr, (__hip_bfloat16*)nullptr);
+  else fill((float*)nullptr, (float*)nullptr);
   CME_LAUNCH_CHECK(s);
 }
 

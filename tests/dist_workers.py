@@ -298,6 +298,8 @@ DP_MODES = (  # (name, H, trainer kwargs)
     ("xgmi", 100, dict(allreduce="xgmi", fuse_allreduce=False)),
     ("rccl", 100, dict(allreduce="rccl")),
     ("rccl-bucketed", 4096, dict(allreduce="rccl", overlap_chunks=4)),
+    # BASELINE config 5's shape: the bf16 path's 3.3 MB fp32 gradient over a bf16 xGMI wire (1.6 MB)
+    ("xgmi-bf16wire", 1024, dict(allreduce="xgmi", dtype="bf16")),
     ("host", 100, dict(allreduce="host")),
 )
 
@@ -332,7 +334,8 @@ def multigpu_dp_worker(rank, world, comm, device, out_dir, modes, scalings, step
             tr.train(1, 0.05, 1e-4)
             got = tr.engine.params.detach().double().cpu()
             tr.close()
-            single = DataParallelTrainer(ref, device=device, batch_size=B, use_graphs=True)  # one process
+            single = DataParallelTrainer(ref, device=device, batch_size=B, use_graphs=True,  # one process
+                                         dtype=kw.get("dtype", "f32"))
             single.load(x, y)
             single.train(1, 0.05, 1e-4)
             want = single.engine.params.detach().double().cpu()

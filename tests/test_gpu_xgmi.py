@@ -54,7 +54,7 @@ def test_allreduce_bench_two_ranks_shared_gpu(tmp_path):
     out = tmp_path / "ar.json"
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29661",
-                        os.path.join(ROOT, "bench", "allreduce_bench.py"), "--paths", "xgmi", "--max-bytes",
+                        os.path.join(ROOT, "bench", "allreduce_bench.py"), "--paths", "xgmi", "xgmi-bf16", "--max-bytes",
                         str(1 << 20), "--iters", "5", "--json", str(out)],
                        capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, CME_SHARED_GPU="1", OMP_NUM_THREADS="2"))
@@ -91,7 +91,7 @@ def test_xgmi_stalled_peer_applies_nothing_and_fails_everywhere(tmp_path):
 def test_dp_paths_shared_gpu_rehearsal(tmp_path):
     """The one-rank-per-GPU DP test's worker, rehearsed with 2 ranks sharing GPU 0 over gloo (every path
     except RCCL itself): replicas bitwise equal, result == the single-process run of the same global batch."""
-    _run_multigpu(tmp_path, 2, "gloo", ("xgmi-fused", "xgmi", "rccl", "host"), ("weak", "strong"),
+    _run_multigpu(tmp_path, 2, "gloo", ("xgmi-fused", "xgmi", "xgmi-bf16wire", "rccl", "host"), ("weak", "strong"),
                   dict(os.environ, CME_SHARED_GPU="1", OMP_NUM_THREADS="2"))
 
 
@@ -107,7 +107,8 @@ def _run_multigpu(tmp_path, world, backend, modes, scalings, env):
     for key, v in res.items():
         assert v["replicas_equal"], (key, v)
         assert v["moved"] > 0, (key, v)
-        assert v["rel_vs_single"] <= 2e-6, (key, v)
+        # fp32 paths: reassociation only; the bf16 wire rounds each rank's gradient to bf16 (2^-9)
+        assert v["rel_vs_single"] <= (2e-3 if "bf16wire" in key else 2e-6), (key, v)
         if key.startswith("xgmi"):
             assert v["impl"] == key.split("/")[0], (key, v)
 
@@ -128,5 +129,5 @@ def test_dp_one_rank_per_gpu(tmp_path, world):
     graph, host-staged) at weak and strong scaling against the single-process run of the same global batch."""
     if _gpus() < world:
         pytest.skip(f"needs {world} GPUs, {_gpus()} visible")
-    modes = ("xgmi-fused", "xgmi", "rccl", "rccl-bucketed", "host")
+    modes = ("xgmi-fused", "xgmi", "xgmi-bf16wire", "rccl", "rccl-bucketed", "host")
     _run_multigpu(tmp_path, world, "nccl", modes, ("weak", "strong"), dict(os.environ, OMP_NUM_THREADS="2"))
