@@ -79,7 +79,8 @@ def run(cfg: TrainConfig) -> dict:
             if rank == 0:
                 from .ops.gemm import benchmark_gemm
 
-                benchmark_gemm(device=device)
+                # the reference's fp64 benchmark first, then the MI355X dtypes (fp32, bf16)
+                benchmark_gemm(device=device, dtypes=(torch.float64, torch.float32, torch.bfloat16))
             return {}
         log0(rank, f"num_neuron={cfg.num_neuron}, reg={cfg.reg}, learning_rate={cfg.learning_rate}, "
                    f"num_epochs={cfg.num_epochs}, batch_size={cfg.batch_size}, dtype={cfg.dtype}")
