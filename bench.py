@@ -130,9 +130,12 @@ def main(argv=None) -> int:
         # a bounded peer wait that timed out during the warm-up (the xGMI protocol misbehaving on this
         # node) -> every rank drops to RCCL together, from the initial weights, before anything is timed
         forced = os.environ.get("CME_BENCH_TEST_FALLBACK") == "1"  # test hook: take the fallback
-        if tr.comm_failed() or comm.allreduce_scalar(float(forced), op="max") > 0:
+        failed = tr.comm_failed()
+        diverged = not failed and not tr.replicas_agree()  # a stale peer read would show up here
+        if failed or diverged or comm.allreduce_scalar(float(forced), op="max") > 0:
             if rank == 0:
-                print("warning: xGMI all-reduce peer wait timed out in warm-up; re-running on RCCL", file=sys.stderr)
+                why = "replicas diverged" if diverged else "peer wait timed out" if failed else "forced"
+                print(f"warning: xGMI all-reduce failed in warm-up ({why}); re-running on RCCL", file=sys.stderr)
             tr.close()
             tr, timed_plans = prepare("rccl")
     native_exec = all(tr.native_plan(p) is not None for p in timed_plans)
@@ -156,7 +159,8 @@ def main(argv=None) -> int:
     bad = comm.allreduce_scalar(0.0 if finite else 1.0, op="max") > 0
     comm_failed = tr.comm_failed()
     kerr = comm.allreduce_scalar(1.0 if tr.engine.kernel_error() else 0.0, op="max") > 0
-    ok = not bad and not comm_failed and not kerr
+    agree = tr.replicas_agree()
+    ok = not bad and not comm_failed and not kerr and agree
     # strong scaling drops the remainder columns when R does not divide the batch (trainer.shard)
     images = a.steps * (global_batch // R) * R
     value = images / dt
@@ -180,11 +184,12 @@ def main(argv=None) -> int:
                        "hip_graphs": tr.use_graphs and not native_exec,
                        "executor": "native" if native_exec else ("graph" if tr.use_graphs else "eager"),
                        "allreduce": tr.allreduce_impl, "params_finite": not bad,
-                       "comm_ok": not comm_failed},
+                       "comm_ok": not comm_failed, "replicas_bitwise_equal": agree},
         }
         if not ok:
             rec["invalid"] = ("non-finite parameters" if bad else "an xGMI peer wait timed out" if comm_failed
-                              else "a forward+head workgroup wait timed out")
+                              else "a forward+head workgroup wait timed out" if kerr
+                              else "replicas diverged across ranks")
         print(json.dumps(rec), flush=True)
     shutdown()
     return 0 if ok else 1

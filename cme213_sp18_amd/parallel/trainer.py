@@ -242,6 +242,23 @@ class DataParallelTrainer:
             return local
         return self.comm.allreduce_scalar(1.0 if local else 0.0, op="max") > 0
 
+    def replicas_agree(self) -> bool:
+        """Collective: True when every rank holds BITWISE the same parameters.  Every all-reduce path sums in
+        a rank-independent order (xGMI: rank order on every rank; RCCL/host: one result broadcast), so
+        weak- and strong-scaling replicas must agree exactly; a stale peer read in the xGMI hand-off would
+        show up here as a mismatch rather than as a hang."""
+        if self.R == 1:
+            return True
+        p = self.engine.params.detach().reshape(-1)
+        w = p.view(torch.int32) if p.element_size() == 4 else p.view(torch.int16) if p.element_size() == 2 \
+            else p.view(torch.int64)
+        w = w.to(torch.int64)
+        idx = torch.arange(1, w.numel() + 1, device=w.device, dtype=torch.int64)
+        # two position-weighted sums, folded below 2^52 so they travel exactly as float64
+        h = [int(w.sum().item()) % (1 << 52), int(((w % 65521) * (idx % 65519)).sum().item()) % (1 << 52)]
+        return all(self.comm.allreduce_scalar(float(v), op="max") == self.comm.allreduce_scalar(float(v), op="min")
+                   for v in h)
+
     def assert_comm_ok(self) -> None:
         """Collective: raise CommFailure on every rank together if any rank's peer wait timed out."""
         if (self.xgmi is not None or self._xgmi_fused is not None) and self.comm_failed():

@@ -183,11 +183,12 @@ __device__ __forceinline__ void do_chunk(const Args<T, W>& a, int64_t c, uint32_
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // 2. signal every peer that my chunk c of this epoch is ready: a system-scope RELEASE store (L2
-  //    write-back before the flag) by the signalling lanes of wave 0; the barrier above makes every
-  //    wave's stores part of what it releases
+  // 2. signal every peer that my chunk c of this epoch is ready: a RELAXED system-scope flag store by the
+  //    signalling lanes of wave 0.  Everything a peer reads was stored write-through at system scope and
+  //    drained by every wave before the barrier above, so a release (a write-back of the whole L2's other
+  //    dirty lines, per block) orders nothing more; bench.py checks the replicas bitwise after warm-up.
   if (t < a.world)
-    __hip_atomic_store(a.peerflags[t] + c * kMaxRanks + a.rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.peerflags[t] + c * kMaxRanks + a.rank, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // 3. wait for every peer's chunk c (bounded)
   if (t < a.world) {
     uint32_t spins = 0;
@@ -206,7 +207,7 @@ __device__ __forceinline__ void do_chunk(const Args<T, W>& a, int64_t c, uint32_
 
   // 4. sum the R gradients of my elements in rank order, 5. update.
   //    Peer data is read with system-coherent loads (sc0 sc1), i.e. as relaxed system-scope atomics,
-  //    issued only after the peer's release-ordered flag was observed: no acquire fence (an L2
+  //    issued only after the peer's flag (behind its drained write-through stores) was observed: no acquire fence (an L2
   //    invalidation per block) is needed -- and a line of a peer buffer cached by this agent two
   //    epochs ago is never served again (a peer mapped on the SAME device is local memory to the L2).
   if (full) {

@@ -97,6 +97,34 @@ def test_remainder_columns_are_dropped_like_reference():
     assert np.abs(res[0].W[0] - W1).max() / np.abs(W1).max() < 1e-12
 
 
+def test_replicas_agree_detects_a_single_flipped_bit():
+    """bench.py's divergence check (DataParallelTrainer.replicas_agree): True after data-parallel
+    training, False when one rank's parameters differ in one low bit."""
+    world = 3
+    comms = LoopbackComm.create(world)
+    x, y = synthetic_mnist(1600, seed=11)
+    out = [None] * world
+
+    def work(r, flip):
+        torch.set_num_threads(1)
+        tr = DataParallelTrainer(NeuralNetwork([784, 16, 10]), comm=comms[r], device="cpu", dtype="f32",
+                                 batch_size=800, backend="torch", use_graphs=False)
+        tr.load(x, y)
+        tr.train(1, 0.05, 1e-4)
+        same = tr.replicas_agree()
+        if flip and r == 2:
+            bits = tr.engine.params.view(torch.int32)
+            bits[5] ^= 1
+        out[r] = (same, tr.replicas_agree())
+
+    ts = [threading.Thread(target=work, args=(r, True)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert all(o == (True, False) for o in out)
+
+
 def test_shard_math():
     nn = NeuralNetwork([784, 8, 10])
     comms = LoopbackComm.create(3)
