@@ -21,6 +21,8 @@ Two interchangeable compute backends execute a step:
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -285,6 +287,9 @@ class MlpEngine:
                 s.npw = s.npz = self.np
                 s.W1p = self.W1p.data_ptr()
                 s.dZ1p = self.dZ1p.data_ptr()
+                # split3 operand forms of the small-layer GEMMs (SplitStepArgs.a_fp32; measurement override)
+                if os.environ.get("CME_A_FP32"):
+                    s.a_fp32 = int(os.environ["CME_A_FP32"])
             if self.z2buf is not None:
                 s.z2p = self.z2buf.data_ptr()
             if self.fh_counters is not None:

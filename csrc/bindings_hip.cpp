@@ -90,6 +90,12 @@ struct MlpStep {
   }
   float xscale = 1.f;    // split path: inputs are uint8 * xscale
   uintptr_t W1p = 0, dZ1p = 0;
+  // split3 small layers: bit0 fp32 W1, bit1 fp32 dZ1 split in registers (SplitStepArgs.a_fp32).  -1 = by
+  // measurement (bench/kbench.py +a<bits>): fp32 W1 always (one split per weight per column tile is cheaper
+  // than pulling 6 B); fp32 dZ1 only above H = 128, where the separate head's plane stores cost ~2 us at
+  // H = 300 -- at H <= 128 the all-gather head stores planes cheaply and the 25-fold re-split of dZ1 in the
+  // dW1 tiles costs +0.5 us (VALU: 4 cycles per wave64 op on the 16-lane SIMD)
+  int a_fp32 = -1;
 
   cme::SplitStepArgs split_args(int64_t off, int n, double scale, double reg, double lr, int sgd,
                                 int with_loss) const {
@@ -111,6 +117,7 @@ struct MlpStep {
     a.scale = scale; a.reg = reg; a.lr = lr; a.sgd = sgd; a.shift = shift; a.mode = 0;
     a.stamps = reinterpret_cast<unsigned long long*>(stamps);
     a.bias_col = bias_col;
+    a.a_fp32 = a_fp32 >= 0 ? a_fp32 : (H <= 128 ? 1 : 3);
     return a;
   }
 
@@ -141,6 +148,9 @@ struct MlpStep {
           h.loss_partial = a.loss_partial; h.shift = shift; h.mode = cme::HEAD_TRAIN;
           h.z2part = P_<float>(z2p);
           h.stamps = hstamps ? reinterpret_cast<unsigned long long*>(hstamps) : nullptr;
+          // the dW1 GEMM splits fp32 dZ1 in registers: the head writes fp32 dZ1 and no planes
+          const bool dz32 = cme::mlp_split_wgrad_fp32_dz(a);
+          if (dz32) h.dZ1_planes = nullptr;
           if (fh_allgather && ag_counters && ag_slabs && ag_err && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {
             cme::mlp_fwd1_head_ag(a, h, P_<unsigned long long>(ag_counters), P_<float>(ag_slabs), P_<int>(ag_err),
                                   fh_tiles, S(stream));
@@ -156,10 +166,7 @@ struct MlpStep {
             // the dW1 GEMM over the planes): skip those 4 B/element of HBM writes
             if (h.z2_chunks > 0 && bias_col) h.dZ1 = nullptr;
             // ... unless the dW1 GEMM splits fp32 dZ1 in registers: then fp32 dZ1 and no planes
-            if (cme::mlp_split_wgrad_fp32_dz(a)) {
-              h.dZ1 = a.dZ1;
-              h.dZ1_planes = nullptr;
-            }
+            if (dz32) h.dZ1 = a.dZ1;
             if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
           }
         }
@@ -383,6 +390,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_slabs", &MlpStep::ag_slabs)
       .def_readwrite("ag_err", &MlpStep::ag_err)
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
+      .def_readwrite("a_fp32", &MlpStep::a_fp32)
       .def("tp_forward", &MlpStep::tp_forward)
       .def("tp_head", &MlpStep::tp_head)
       .def_readwrite("shift", &MlpStep::shift)

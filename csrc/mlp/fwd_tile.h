@@ -1,0 +1,26 @@
+// The forward GEMM tile of the small-layer kernels (fwd1_split_kernel, fwd1_head_kernel,
+// fwd1_head_ag_kernel): a1 tile = W1[rows] . X[cols]^T on the wave-split-K engine (mma_tile.h), W1 either
+// from its stored bf16 planes or (AF, split3) straight from fp32 W1, split into the exact planes in
+// registers -- 4 B per weight through the CU's ~50 GB/s L2 fill instead of 6 B.
+#pragma once
+
+#include "mlp_split.h"
+#include "mma_tile.h"
+
+namespace cme {
+
+template <int NPW, int NB, int VEC, int U, bool AF, class Epi>
+__device__ __forceinline__ void fwd_tile(const SplitStepArgs& f, const TileGeom& g, Epi& epi, float* red,
+                                         unsigned long long* stamps = nullptr) {
+  const uint8_t* X = static_cast<const uint8_t*>(f.X);
+  if constexpr (AF) {
+    static_assert(NPW == 3, "fp32 W1 is split into three planes");
+    wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t>(f.W1, f.P, X, f.P, g, epi, red, 0, stamps);
+  } else {
+    wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, NPW, uint8_t>(
+        static_cast<const __hip_bfloat16*>(f.W1p), f.P, X, f.P, g, epi, red, f.H * f.P * (int)sizeof(__hip_bfloat16),
+        stamps);
+  }
+}
+
+}  // namespace cme

@@ -4,6 +4,7 @@
 #include "mlp_split.h"
 
 #include "mma_tile.h"
+#include "fwd_tile.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -528,7 +529,7 @@ struct EpiSigWT {
 
 // NBT 16-column blocks per a1 tile (32 or 64 columns; a 64-column tile halves the W1-plane re-reads
 // through L2 at half the workgroups, but serialises two head passes in the last arriver)
-template <int NPW, int VEC, int NBT>
+template <int NPW, int VEC, int NBT, bool AF>
 __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArgs h, unsigned* __restrict__ counters,
                                                         int tm, int tn) {
   constexpr int kCols = 16 * NBT;
@@ -548,9 +549,7 @@ __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArg
   head32_stage(h, threadIdx.x, L);
   TileGeom g{f.H, f.n, f.P, rt * 16, ct * kCols};
   EpiSigWT epi{f.b1, f.a1, f.ld, f.xscale, {}};
-  wsk_tile<__hip_bfloat16, 1, NBT, 8, true, true, VEC, NBT == 2 ? 4 : 2, NPW, uint8_t>(
-      static_cast<const __hip_bfloat16*>(f.W1p), f.P, static_cast<const uint8_t*>(f.X), f.P, g, epi, red,
-      f.H * f.P * (int)sizeof(__hip_bfloat16));
+  fwd_tile<NPW, NBT, VEC, NBT == 2 ? 4 : 2, AF>(f, g, epi, red);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
   __syncthreads();
   stamp(1);
@@ -610,7 +609,7 @@ struct EpiSigLds {
   }
 };
 
-template <int NPW, int VEC>
+template <int NPW, int VEC, bool AF>
 __global__ __launch_bounds__(512) void fwd1_head_ag_kernel(SplitStepArgs f, HeadArgs h,
                                                            unsigned long long* __restrict__ counters,
                                                            float* __restrict__ slabs, int* __restrict__ err, int tm,
@@ -638,9 +637,7 @@ __global__ __launch_bounds__(512) void fwd1_head_ag_kernel(SplitStepArgs f, Head
   }
   TileGeom g{H, n, f.P, r0, c0};
   EpiSigLds epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
-  wsk_tile<__hip_bfloat16, 1, 2, 8, true, true, VEC, 4, NPW, uint8_t>(
-      static_cast<const __hip_bfloat16*>(f.W1p), f.P, static_cast<const uint8_t*>(f.X), f.P, g, epi, red,
-      H * f.P * (int)sizeof(__hip_bfloat16));
+  fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red);
   // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
   // they are masked below.
   // ---- 1. z2 partial for (class c, column col), one per thread, published write-through
@@ -1416,13 +1413,14 @@ void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters
   constexpr int nbt = 2;
   const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 16 * nbt);
   CME_REQUIRE(counters != nullptr && tn <= max_tiles, "fwd1_head: counter array too small");
-  const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 && reinterpret_cast<uintptr_t>(f.W1p) % 16 == 0 &&
-                   f.P % 8 == 0;
+  const bool af = mlp_split_fwd_fp32_w(f);
+  const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(af ? (const void*)f.W1 : f.W1p) % 16 == 0 && f.P % 8 == 0;
   const int nwg = 8 * tm * cdiv(tn, 8);
-#define CME_FH(np)                                                                         \
-  if (vec) fwd1_head_kernel<np, 1, nbt><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);       \
-  else fwd1_head_kernel<np, 0, nbt><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);
-  if (f.npw == 3) { CME_FH(3) } else { CME_FH(1) }
+#define CME_FH(np, af)                                                                     \
+  if (vec) fwd1_head_kernel<np, 1, nbt, af><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);   \
+  else fwd1_head_kernel<np, 0, nbt, af><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);
+  if (af) { CME_FH(3, true) } else if (f.npw == 3) { CME_FH(3, false) } else { CME_FH(1, false) }
 #undef CME_FH
   CME_LAUNCH_CHECK(s);
 }
@@ -1436,13 +1434,14 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
   const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32);
   CME_REQUIRE(tm <= 8, "fwd1_head_ag: H <= 128");
   CME_REQUIRE(counters && slabs && err && tn <= max_tiles, "fwd1_head_ag: counter / slab arrays too small");
-  const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 && reinterpret_cast<uintptr_t>(f.W1p) % 16 == 0 &&
-                   f.P % 8 == 0;
+  const bool af = mlp_split_fwd_fp32_w(f);
+  const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(af ? (const void*)f.W1 : f.W1p) % 16 == 0 && f.P % 8 == 0;
   const int nwg = 8 * tm * cdiv(tn, 8);
-#define CME_FHA(np)                                                                                 \
-  if (vec) fwd1_head_ag_kernel<np, 1><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);      \
-  else fwd1_head_ag_kernel<np, 0><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);
-  if (f.npw == 3) { CME_FHA(3) } else { CME_FHA(1) }
+#define CME_FHA(np, af)                                                                             \
+  if (vec) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
+  else fwd1_head_ag_kernel<np, 0, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);
+  if (af) { CME_FHA(3, true) } else if (f.npw == 3) { CME_FHA(3, false) } else { CME_FHA(1, false) }
 #undef CME_FHA
   CME_LAUNCH_CHECK(s);
 }

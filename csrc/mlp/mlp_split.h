@@ -78,7 +78,14 @@ struct SplitStepArgs {
   // for the direct-to-LDS GEMM engine (glds_gemm.h); nullptr: the register-staged engine reads the uint8s
   const void* Xw = nullptr;
   const void* XTw = nullptr;
+  // small layers (wave-split-K kernels), split3 only: bit0 = the forward GEMM reads fp32 W1, bit1 = the dW1
+  // GEMM reads fp32 dZ1 (4 B per element, split into the exact bf16 planes in registers; the head then
+  // writes no dZ1 planes); clear bits: the stored planes (6 B per element, split once by their writer)
+  int a_fp32 = 1;
 };
+
+// the small-layer forward GEMM reads fp32 W1 (split in registers) instead of the W1 planes
+bool mlp_split_fwd_fp32_w(const SplitStepArgs& a);
 
 // number of z2 row-tile partials mlp_split_fwd1 writes for `a` (0: the forward does not produce them)
 int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a);

@@ -7,6 +7,7 @@
 #include "rega_gemm.h"
 #include "lds_gemm.h"
 #include "mma_tile.h"
+#include "fwd_tile.h"
 
 namespace cme {
 
@@ -219,16 +220,14 @@ struct EpiSig {
   }
 };
 
-template <int NPW, int VEC>
+template <int NPW, int VEC, bool AF>
 __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a, int tiles_n) {
+  static_assert(kF1MB == 1 && kF1KS == 8, "fwd_tile: one 16-row block, 8 K-waves");
   __shared__ __attribute__((aligned(16))) float red[kF1KS * kF1MB * kF1NB * 4 * 64];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   TileGeom g{a.H, a.n, a.P, (bid / tiles_n) * 16 * kF1MB, (bid % tiles_n) * 16 * kF1NB};
   EpiSig epi{a.b1, a.a1, a.ld, a.xscale, {}};
-  constexpr int U = 4;
-  wsk_tile<bf16, kF1MB, kF1NB, kF1KS, true, true, VEC, U, NPW, uint8_t>(static_cast<const bf16*>(a.W1p), a.P,
-                                                               static_cast<const uint8_t*>(a.X), a.P, g, epi, red,
-                                                               a.H * a.P * (int)sizeof(bf16), a.stamps);
+  fwd_tile<NPW, kF1NB, VEC, 4, AF>(a, g, epi, red, a.stamps);
 }
 
 
@@ -385,7 +384,8 @@ struct EpiW1 {
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
                                             uint32_t* s_xf);
 
-template <int NPZ, int VEC>
+// AF (split3): dZ1 read in fp32 and split into its exact planes in registers (the head then writes no planes)
+template <int NPZ, int VEC, bool AF>
 __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
   __shared__ uint32_t s_xf[2];
@@ -406,9 +406,13 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.npw, reg, lr,
               a.xscale, {}, a.b1, gb, live ? 1 : 0};
     constexpr int U = 4;
-    wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
-                                                              static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
-                                                              red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
+    if constexpr (AF)
+      wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, 3, uint8_t>(a.dZ1, a.ld, static_cast<const uint8_t*>(a.XT),
+                                                                       a.ldxt, g, epi, red, 0, a.stamps);
+    else
+      wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
+                                                                static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
+                                                                red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
     if (live && xf_exchange(a.xf, bid, s_xf)) {  // all-reduced with the peers: SGD + bf16 planes
       const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf.npad;
       constexpr int TW = 16 * kWNB;
@@ -1128,7 +1132,20 @@ void launch_fwdhead_nc(const SplitStepArgs& a, hipStream_t s) {
 
 int mlp_split_fwdhead_blocks(int n) { return cdiv(n, kFHCols); }
 
-bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a) { return a.npz == 3 && rega_wgrad_ok(a); }
+// the wave-split-K dW1 reads fp32 dZ1 (split3, a_fp32, 16-byte rows)
+bool small_wgrad_fp32_ok(const SplitStepArgs& a) {
+  return a.npz == 3 && (a.a_fp32 & 2) && a.dZ1 != nullptr && al16(a.dZ1) && a.ld % 4 == 0;
+}
+
+// Decided on the whole step (not the row range of a bucketed call; the xGMI-fused launch always takes the
+// wave-split-K kernel) so that the head and every wgrad call of a step agree on what dZ1 form exists.
+bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a) {
+  if (a.npz != 3) return false;
+  const bool big = big_wgrad_ok(a) && a.xf.world == 0;
+  return big ? rega_wgrad_ok(a) : small_wgrad_fp32_ok(a);
+}
+
+bool mlp_split_fwd_fp32_w(const SplitStepArgs& a) { return a.npw == 3 && (a.a_fp32 & 1) && a.W1 != nullptr && al16(a.W1); }
 
 int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a) {
   if (!a.z2part || a.C > 16 || a.n <= 0 || !(glds_fwd_ok(a) || big_fwd_ok(a))) return 0;
@@ -1160,12 +1177,13 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
     return;
   }
   const int tn = cdiv(a.n, 16 * kF1NB), tm = cdiv(a.H, 16 * kF1MB);
-  const bool vec = al4(a.X) && al16(a.W1p) && a.P % 8 == 0;
+  const bool af = mlp_split_fwd_fp32_w(a);
+  const bool vec = al4(a.X) && al16(af ? (const void*)a.W1 : a.W1p) && a.P % 8 == 0;
   const dim3 grid(tm * tn);
-#define CME_F1(np)                                                                         \
-  if (vec) fwd1_split_kernel<np, 1><<<grid, 64 * kF1KS, 0, s>>>(a, tn);                   \
-  else fwd1_split_kernel<np, 0><<<grid, 64 * kF1KS, 0, s>>>(a, tn);
-  if (a.npw == 3) { CME_F1(3) } else { CME_F1(1) }
+#define CME_F1(np, af)                                                                     \
+  if (vec) fwd1_split_kernel<np, 1, af><<<grid, 64 * kF1KS, 0, s>>>(a, tn);               \
+  else fwd1_split_kernel<np, 0, af><<<grid, 64 * kF1KS, 0, s>>>(a, tn);
+  if (af) { CME_F1(3, true) } else if (a.npw == 3) { CME_F1(3, false) } else { CME_F1(1, false) }
 #undef CME_F1
   CME_LAUNCH_CHECK(s);
 }
@@ -1226,14 +1244,16 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
     return;
   }
   // dZ1 planes: 16-byte vectors when n % 8 == 0, 8-byte halves when n % 4 == 0; XT bytes need 4-byte rows
-  const bool base_ok = al16(a.dZ1p) && al4(a.XT) && a.ld % 8 == 0 && a.ldxt % 4 == 0;
+  // (fp32 dZ1: 2 x 16-byte vectors when n % 8 == 0, else element loads -- mma_tile.h VA)
+  const bool af = small_wgrad_fp32_ok(a);
+  const bool base_ok = al16(af ? (const void*)a.dZ1 : a.dZ1p) && al4(a.XT) && a.ld % 8 == 0 && a.ldxt % 4 == 0;
   const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? 1 : (a.n % 4 == 0 ? 2 : 0));
   const dim3 grid(t1 + t2 + tb);
-#define CME_WG(npz)                                                                   \
-  if (vec == 1) wgrad_split_kernel<npz, 1><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);      \
-  else if (vec == 2) wgrad_split_kernel<npz, 2><<<grid, kWT, 0, s>>>(a, t1, t1n, t2); \
-  else wgrad_split_kernel<npz, 0><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);
-  if (a.npz == 3) { CME_WG(3) } else { CME_WG(1) }
+#define CME_WG(npz, af)                                                                   \
+  if (vec == 1) wgrad_split_kernel<npz, 1, af><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);      \
+  else if (vec == 2) wgrad_split_kernel<npz, 2, af><<<grid, kWT, 0, s>>>(a, t1, t1n, t2); \
+  else wgrad_split_kernel<npz, 0, af><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);
+  if (af) { CME_WG(3, true) } else if (a.npz == 3) { CME_WG(3, false) } else { CME_WG(1, false) }
 #undef CME_WG
   CME_LAUNCH_CHECK(s);
 }

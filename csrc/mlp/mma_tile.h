@@ -165,6 +165,44 @@ __device__ __forceinline__ unsigned int u8x2_to_bf16x2(unsigned int w, int hi) {
   return (__builtin_bit_cast(unsigned int, f0) >> 16) | (__builtin_bit_cast(unsigned int, f1) & 0xffff0000u);
 }
 
+// The same 8 bytes as two raw words (VEC != 0) or 8 byte-loads (VEC == 0, one byte per word), widened later
+// by widen_u8: the burst loads of wsk_tile stay ahead of every wait (widening right after the load makes
+// hipcc wait for the bytes in the middle of the burst -- two memory round trips instead of one).
+template <int VEC>
+struct U8Raw {
+  unsigned int w[VEC != 0 ? 2 : 8];
+};
+
+template <int VEC>
+__device__ __forceinline__ void load_u8_raw(__amdgpu_buffer_rsrc_t rs, int ld, int r, int rmax, int k, int kend,
+                                            U8Raw<VEC>& out) {
+  const bool rok = r < rmax;
+  if constexpr (VEC != 0) {
+    const int base = r * ld + k;
+    out.w[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, (rok && k + 4 <= kend) ? base : kOOB, 0, 0);
+    out.w[1] = __builtin_amdgcn_raw_buffer_load_b32(rs, (rok && k + 8 <= kend) ? base + 4 : kOOB, 0, 0);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      out.w[j] = __builtin_amdgcn_raw_buffer_load_b8(rs, (rok && k + j < kend) ? r * ld + k + j : kOOB, 0, 0);
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void widen_u8(const U8Raw<VEC>& in, __hip_bfloat16 (&out)[8]) {
+  unsigned int w[4];
+  if constexpr (VEC != 0) {
+    w[0] = u8x2_to_bf16x2(in.w[0], 0);
+    w[1] = u8x2_to_bf16x2(in.w[0], 1);
+    w[2] = u8x2_to_bf16x2(in.w[1], 0);
+    w[3] = u8x2_to_bf16x2(in.w[1], 1);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = u8x2_to_bf16x2(in.w[2 * q] | (in.w[2 * q + 1] << 8), 0);
+  }
+  __builtin_memcpy(out, w, 16);
+}
+
 template <int VEC>
 __device__ __forceinline__ void load_frag_u8(__amdgpu_buffer_rsrc_t rs, int ld, int r, int rmax, int k, int kend,
                                              __hip_bfloat16 (&out)[8]) {
@@ -188,6 +226,33 @@ __device__ __forceinline__ void load_frag_u8(__amdgpu_buffer_rsrc_t rs, int ld, 
     for (int q = 0; q < 4; ++q) w[q] = u8x2_to_bf16x2(b[2 * q] | (b[2 * q + 1] << 8), 0);
   }
   __builtin_memcpy(out, w, 16);
+}
+
+// Exact split of V fp32 values into NP bf16 planes BY TRUNCATION (x = hi + mid + lo for NP = 3):
+// hi = the top 16 bits of x, r = x - hi (exact: < 2^-7 ulp-relative, <= 16 significant bits),
+// mid = the top 16 bits of r, lo = r - mid (exact, <= 8 significant bits: a bf16).  Cheaper than the
+// round-to-nearest split (an AND and a SUB per plane; packing takes the upper halves directly) and just
+// as exact: 3 bf16 significands hold the 24 of an fp32.  NP = 1 is NOT exact (a truncated bf16); the
+// callers use this only for NP = 3.
+template <int NP, int V>
+__device__ __forceinline__ void split_trunc(const float (&x)[V], __hip_bfloat16 (&p)[NP][V]) {
+  static_assert(V % 2 == 0, "pairs of values per 32-bit word");
+  unsigned w[NP][V / 2];
+#pragma unroll
+  for (int j = 0; j < V; j += 2) {
+    unsigned cur0 = __builtin_bit_cast(unsigned, x[j]), cur1 = __builtin_bit_cast(unsigned, x[j + 1]);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      w[q][j / 2] = (cur0 >> 16) | (cur1 & 0xffff0000u);
+      if (q + 1 < NP) {
+        const float r0 = __builtin_bit_cast(float, cur0) - __builtin_bit_cast(float, cur0 & 0xffff0000u);
+        const float r1 = __builtin_bit_cast(float, cur1) - __builtin_bit_cast(float, cur1 & 0xffff0000u);
+        cur0 = __builtin_bit_cast(unsigned, r0);
+        cur1 = __builtin_bit_cast(unsigned, r1);
+      }
+    }
+  }
+  __builtin_memcpy(p, w, sizeof(w));
 }
 
 constexpr int kEpiMaxQ = 16;  // max output elements per thread in a tile epilogue
@@ -218,9 +283,12 @@ struct TileGeom {
 // reduction barrier and at the end: stamps[(block*KS + wave)*4 + i].
 //
 // TB = uint8_t (with T = bf16): the B operand is raw bytes, widened in registers.
+// TA = float (with T = bf16, NPA = 3, AK): A is the fp32 operand itself, 4 B per element pulled instead of
+// the 6 B of three stored planes, split into its exact planes in registers (split_trunc) while the MFMAs
+// of the previous unroll step run.
 template <typename T, int MB, int NB, int KS, bool AK, bool BK, int VEC, int U, int NPA = 1, typename TB = T,
-          class Epi>
-__device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const TB* __restrict__ B, int ldb,
+          typename TA = T, class Epi>
+__device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, const TB* __restrict__ B, int ldb,
                                          TileGeom g, Epi& epi,
                                          typename MmaTraits<T>::acc_t* __restrict__ red, int plane_bytes = 0,
                                          unsigned long long* stamps = nullptr) {
@@ -283,22 +351,33 @@ __device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const
   const int kbeg = wave * cpw * KC;
   const int kend = min(g.K, (wave + 1) * cpw * KC);
 
+  constexpr bool AF32 = std::is_same_v<TA, float> && !std::is_same_v<T, float>;
+  static_assert(!AF32 || (std::is_same_v<T, __hip_bfloat16> && NPA == 3 && AK), "fp32 A: split3 bf16, K-contiguous");
+  constexpr int VA = VEC == 1 ? 1 : 0;  // fp32 A: 2 x 16-byte loads, or element loads
   for (int kc = kbeg; kc < kend; kc += KC * U) {
     T af[U][NPA][MB][V];
+    float ar[AF32 ? U : 1][MB][V];
     T bf[U][NB][V];
+    constexpr bool BU8 = std::is_same_v<TB, uint8_t>;
+    U8Raw<VEC> braw[BU8 ? U : 1][NB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = kc + u * KC + V * grp;
+      if constexpr (AF32) {
 #pragma unroll
-      for (int p = 0; p < NPA; ++p)
+        for (int i = 0; i < MB; ++i) load_frag<float, V, true, VA>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, ar[u][i]);
+      } else {
 #pragma unroll
-        for (int i = 0; i < MB; ++i)
-          load_frag<T, V, AK, VEC>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, af[u][p][i], p * plane_bytes);
+        for (int p = 0; p < NPA; ++p)
+#pragma unroll
+          for (int i = 0; i < MB; ++i)
+            load_frag<T, V, AK, VEC>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, af[u][p][i], p * plane_bytes);
+      }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         if constexpr (std::is_same_v<TB, uint8_t>) {
           static_assert(std::is_same_v<T, __hip_bfloat16> && BK, "u8 B operand: bf16 MFMA, K-contiguous");
-          load_frag_u8<VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, bf[u][j]);
+          load_u8_raw<VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, braw[u][j]);
         } else {
           load_frag<T, V, BK, VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, bf[u][j]);
         }
@@ -310,13 +389,29 @@ __device__ __forceinline__ void wsk_tile(const T* __restrict__ A, int lda, const
     // vmcnt(0) waits per wave in fwd1).  With it: one wait ladder per burst.
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      if constexpr (BU8) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) widen_u8<VEC>(braw[u][j], bf[u][j]);
+      }
+      if constexpr (AF32) {
+#pragma unroll
+        for (int i = 0; i < MB; ++i) {
+          T pl[NPA][V];
+          split_trunc<NPA, V>(ar[u][i], pl);
+#pragma unroll
+          for (int p = 0; p < NPA; ++p)
+#pragma unroll
+            for (int v = 0; v < V; ++v) af[u][p][i][v] = pl[p][v];
+        }
+      }
 #pragma unroll
       for (int p = 0; p < NPA; ++p)
 #pragma unroll
         for (int i = 0; i < MB; ++i)
 #pragma unroll
           for (int j = 0; j < NB; ++j) Tr::mma(af[u][p][i], bf[u][j], acc[i][j]);
+    }
   }
 
   if (st) {  // make the K-loop stamp wait for the MFMA results

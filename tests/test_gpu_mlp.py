@@ -457,6 +457,35 @@ def test_fwd1_head_allgather_matches_last_arriver(dtype, H, n):
     assert abs(a[-1] - b[-1]) / abs(b[-1]) < 1e-5
 
 
+@pytest.mark.parametrize("H,n", [(100, 800), (100, 37), (128, 513), (300, 100)])
+def test_fp32_operands_split_in_registers_match_stored_planes(H, n):
+    """split3 small layers: the GEMMs reading fp32 W1 / dZ1 and splitting them into their exact bf16 planes
+    in registers (mma_tile.h split_trunc, the default) against the same kernels reading the stored
+    round-to-nearest planes.  Every product is exact either way; only the fp32 accumulation order differs.
+    On the fp32 path the head writes no dZ1 planes (a poisoned plane buffer stays untouched)."""
+    x, y = synthetic_mnist(2 * n + 7, seed=H)
+    rng = np.random.default_rng(H + n)
+    W1 = rng.standard_normal((H, 784)) * 0.01
+    W2 = rng.standard_normal((10, H)) * 0.01
+    b1 = rng.standard_normal(H) * 0.1
+    b2 = rng.standard_normal(10) * 0.1
+    outs = []
+    for a32 in (3, 0):  # SplitStepArgs.a_fp32: bit0 fp32 W1, bit1 fp32 dZ1
+        e = MlpEngine((784, H, 10), "f32", max_cols=n, device="cuda")
+        e.load_dataset(x, y, normalize=True)
+        e.set_params(W1, b1, W2, b2)
+        e._hip_step().a_fp32 = a32
+        e.dZ1p.fill_(7.0)
+        for step, off in enumerate((0, n, 7, 0)):
+            e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True, with_loss=step == 3)
+        torch.cuda.synchronize()
+        if a32 & 2:
+            assert bool((e.dZ1p == 7.0).all())
+        outs.append([t.clone().cpu() for t in (e.a1[:, :n], e.D[:, :n], e.dZ1[:, :n], e.params)])
+    for ta, tb in zip(*outs):
+        assert _rel(ta, tb) < 2e-6
+
+
 @pytest.mark.parametrize("path", ["split3", "mfma"])
 @pytest.mark.parametrize("n", [800, 100, 37])
 @pytest.mark.parametrize("H", [100, 300, 1024, 4096])
