@@ -246,6 +246,18 @@ class MlpEngine:
         if self._step is not None:
             self._step.fh_allgather = int(self.fh_allgather)
 
+    def w1_planes_maintained(self) -> bool:
+        """True when the W1 bf16 planes track the fp32 master after every update.  Below H = 512 the split3
+        forward kernels read fp32 W1 and split it in registers, so the update stops refreshing the planes
+        (csrc/mlp/mlp_split.hip mlp_split_w1_planes_read); refresh_w1_planes() rebuilds them on demand."""
+        return bool(self.np) and self.backend == "hip" and bool(self._hip_step().w1_planes_read())
+
+    def refresh_w1_planes(self) -> None:
+        """Rebuild the W1 planes from the fp32 master (exact split3 / rounded split1)."""
+        if self.np and self.backend == "hip":
+            hip().split_planes(self.W1.data_ptr(), self.W1p.data_ptr(), self.W1.numel(), self.np,
+                               torch.cuda.current_stream(self.device).cuda_stream)
+
     def kernel_error(self) -> bool:
         """True if a forward + head launch's wait for the workgroups of its column tile timed out (the
         all-gather form; its outputs were then not trusted).  Reads a device word: synchronises."""

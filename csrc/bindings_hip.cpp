@@ -391,6 +391,10 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_err", &MlpStep::ag_err)
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
       .def_readwrite("a_fp32", &MlpStep::a_fp32)
+      .def("w1_planes_read",
+           [](const MlpStep& st) {  // a forward kernel of this step reads the W1 planes (else: not refreshed)
+             return st.split != 0 && cme::mlp_split_w1_planes_read(st.split_args(0, st.ld, 1.0, 0.0, 0.0, 1, 0));
+           })
       .def("tp_forward", &MlpStep::tp_forward)
       .def("tp_head", &MlpStep::tp_head)
       .def_readwrite("shift", &MlpStep::shift)

@@ -82,7 +82,11 @@ struct SplitStepArgs {
   // GEMM reads fp32 dZ1 (4 B per element, split into the exact bf16 planes in registers; the head then
   // writes no dZ1 planes); clear bits: the stored planes (6 B per element, split once by their writer)
   int a_fp32 = 1;
+  int w1_planes = 1;  // (set by mlp_split_wgrad) the small-layer W1 update refreshes the W1 planes
 };
+
+// true when a forward kernel of this configuration reads the W1 planes (false: fp32 W1 everywhere)
+bool mlp_split_w1_planes_read(const SplitStepArgs& a);
 
 // the small-layer forward GEMM reads fp32 W1 (split in registers) instead of the W1 planes
 bool mlp_split_fwd_fp32_w(const SplitStepArgs& a);

@@ -37,7 +37,7 @@ constexpr int kFHT = 64 * kFHKS;
 // ======================================================================
 // Kernel A: forward + head for 16 samples, all hidden units.
 // ======================================================================
-template <int NPW, int NPZ, int NC, int VEC>
+template <int NPW, int NPZ, int NC, int VEC, bool AF>
 __global__ __launch_bounds__(kFHT) void fwdhead_kernel(SplitStepArgs a) {
   __shared__ __attribute__((aligned(16))) float red[kFHKS * kFHMB * 4 * 64];  // 64 KB split-K partials
   __shared__ float a1s[kFHMB * 16][kFHCols + 1];  // a1 of the current H-chunk
@@ -87,8 +87,11 @@ __global__ __launch_bounds__(kFHT) void fwdhead_kernel(SplitStepArgs a) {
     } epi{a.b1 + m0, a.a1 + (size_t)m0 * ld, a1s, w2s, zp, ld, b0, a.xscale, {}};
     TileGeom g{M, a.n, P, 0, b0};
     constexpr int U = NPW == 3 ? 1 : 2;  // keep one burst of loads <= ~100 VGPRs
-    wsk_tile<bf16, kFHMB, 1, kFHKS, true, true, VEC, U, NPW, uint8_t>(W1p + (size_t)m0 * P, P, X, P, g, epi, red,
-                                                             H * P * (int)sizeof(bf16));
+    if constexpr (AF)  // fp32 W1 split in registers (mma_tile.h)
+      wsk_tile<bf16, kFHMB, 1, kFHKS, true, true, VEC, U, 3, uint8_t>(a.W1 + (size_t)m0 * P, P, X, P, g, epi, red);
+    else
+      wsk_tile<bf16, kFHMB, 1, kFHKS, true, true, VEC, U, NPW, uint8_t>(W1p + (size_t)m0 * P, P, X, P, g, epi, red,
+                                                               H * P * (int)sizeof(bf16));
   }
   // ---- z2 = W2 a1 + b2 for the 16 columns: reduce the per-thread partials
 #pragma unroll
@@ -372,7 +375,7 @@ struct EpiW1 {
       const float nw = w - lr * g;
       W1[i] = nw;
       if (npw == 3) split_store<3>(nw, W1p, plane, i);
-      else split_store<1>(nw, W1p, plane, i);
+      else if (npw == 1) split_store<1>(nw, W1p, plane, i);  // (0: no forward kernel reads the planes)
     } else if (sys) {
       xf_store(gW1, (int64_t)i, g);
     } else {
@@ -403,7 +406,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(s_xf[0] & 1u) * a.xf.npad;
       gb = gw + a.xf.off_b1;
     }
-    EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.npw, reg, lr,
+    EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.w1_planes ? a.npw : 0, reg, lr,
               a.xscale, {}, a.b1, gb, live ? 1 : 0};
     constexpr int U = 4;
     if constexpr (AF)
@@ -423,6 +426,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
           const int64_t i = (int64_t)row * a.P + col;
           const float w = a.W1[i] - lr * xf_sum(a.xf, half + i);
           a.W1[i] = w;
+          if (!a.w1_planes) continue;
           if (a.npw == 3) split_store<3>(w, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
           else split_store<1>(w, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
         } else {
@@ -1116,10 +1120,16 @@ void launch_wgrad_big(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
 
 template <int NPW, int NPZ, int NC>
 void launch_fwdhead(const SplitStepArgs& a, hipStream_t s) {
-  const bool vec = al4(a.X) && al16(a.W1p) && a.P % 8 == 0;
+  const bool af = NPW == 3 && mlp_split_fwd_fp32_w(a);
+  const bool vec = al4(a.X) && al16(af ? (const void*)a.W1 : a.W1p) && a.P % 8 == 0;
   const dim3 grid(cdiv(a.n, kFHCols));
-  if (vec) fwdhead_kernel<NPW, NPZ, NC, 1><<<grid, kFHT, 0, s>>>(a);
-  else fwdhead_kernel<NPW, NPZ, NC, 0><<<grid, kFHT, 0, s>>>(a);
+  if (af) {
+    if (vec) fwdhead_kernel<NPW, NPZ, NC, 1, NPW == 3><<<grid, kFHT, 0, s>>>(a);
+    else fwdhead_kernel<NPW, NPZ, NC, 0, NPW == 3><<<grid, kFHT, 0, s>>>(a);
+  } else {
+    if (vec) fwdhead_kernel<NPW, NPZ, NC, 1, false><<<grid, kFHT, 0, s>>>(a);
+    else fwdhead_kernel<NPW, NPZ, NC, 0, false><<<grid, kFHT, 0, s>>>(a);
+  }
 }
 
 template <int NPW, int NPZ>
@@ -1146,6 +1156,10 @@ bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a) {
 }
 
 bool mlp_split_fwd_fp32_w(const SplitStepArgs& a) { return a.npw == 3 && (a.a_fp32 & 1) && a.W1 != nullptr && al16(a.W1); }
+
+// below kBigMinH every forward kernel (fwd1_split, fwd1_head(_ag), fwdhead) takes fp32 W1 when
+// mlp_split_fwd_fp32_w holds: nothing reads the W1 planes, so the weight update stops refreshing them
+bool mlp_split_w1_planes_read(const SplitStepArgs& a) { return a.H >= kBigMinH || !mlp_split_fwd_fp32_w(a); }
 
 int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a) {
   if (!a.z2part || a.C > 16 || a.n <= 0 || !(glds_fwd_ok(a) || big_fwd_ok(a))) return 0;
@@ -1249,10 +1263,12 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   const bool base_ok = al16(af ? (const void*)a.dZ1 : a.dZ1p) && al4(a.XT) && a.ld % 8 == 0 && a.ldxt % 4 == 0;
   const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? 1 : (a.n % 4 == 0 ? 2 : 0));
   const dim3 grid(t1 + t2 + tb);
+  SplitStepArgs b = a;
+  b.w1_planes = mlp_split_w1_planes_read(a) ? 1 : 0;
 #define CME_WG(npz, af)                                                                   \
-  if (vec == 1) wgrad_split_kernel<npz, 1, af><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);      \
-  else if (vec == 2) wgrad_split_kernel<npz, 2, af><<<grid, kWT, 0, s>>>(a, t1, t1n, t2); \
-  else wgrad_split_kernel<npz, 0, af><<<grid, kWT, 0, s>>>(a, t1, t1n, t2);
+  if (vec == 1) wgrad_split_kernel<npz, 1, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);      \
+  else if (vec == 2) wgrad_split_kernel<npz, 2, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \
+  else wgrad_split_kernel<npz, 0, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
   if (af) { CME_WG(3, true) } else if (a.npz == 3) { CME_WG(3, false) } else { CME_WG(1, false) }
 #undef CME_WG
   CME_LAUNCH_CHECK(s);
