@@ -1,0 +1,228 @@
+// Forward GEMM + head, all-gather form (H <= 128): the body of fwd1_head_ag_kernel (mlp_kernels.hip).
+//
+// The 16 x 32 a1 tiles of the forward GEMM; each of the tm row-tile workgroups of a 32-column tile
+//   1. forms its z2 partial W2[:, its 16 rows] . a1[its rows, cols] (16 classes x 32 columns) and publishes
+//      it: sc1 (write-through) stores, vmcnt(0), barrier, one agent-scope add to the tile's 64-bit counter;
+//   2. waits (one lane, returning-atomic polls, s_sleep, bounded) until all tm adds of this launch are in --
+//      counters only grow, each launch adds exactly tm per tile, so the target is the next multiple of tm;
+//   3. sums the tm partials in row-tile order (sc1 loads: bit-identical z2 in every workgroup), softmax,
+//      D (row tile 0 stores it and the loss partial);
+//   4. forms dZ1 for ITS OWN 16 rows from the a1 tile it still holds in LDS and stores it (fp32 and / or
+//      the bf16 planes, two columns per 4-byte word).
+// The hand-off is MI355X_MICROARCH.md's table's first row (sc1 stores, vmcnt(0) in every storing wave,
+// barrier, one agent add per workgroup, sc1 loads after the poll).  Requires every workgroup of the launch
+// to be resident at once; a wait that outlasts kAgSpinLimit sets *err (the launch's results are then not
+// trusted: MlpEngine.kernel_error()).
+#pragma once
+
+#include "fwd_tile.h"
+#include "mlp_kernels.h"
+#include "mlp_split.h"
+#include "mma_tile.h"
+
+namespace cme {
+
+constexpr uint32_t kAgSpinLimit = 1u << 22;
+constexpr int kAgCounterStride = 32;  // uint64 words: one 256-byte line per tile counter (polls and adds of
+                                      // different tiles must not share a line)
+
+__device__ __forceinline__ float ag_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
+
+template <int AUX>
+struct EpiSigLds {
+  const float* b1;
+  float* a1;
+  float (*a1s)[33];  // [16][32 + 1] this workgroup's a1 tile
+  int ld, r0, c0;
+  float xscale;
+  float pre[kEpiMaxQ];
+  __device__ __forceinline__ void prefetch(int q, int row, int, bool ok) {
+    pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
+  }
+  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
+    const float s = ag_sigmoid(v * xscale + pre[q]);
+    a1s[row - r0][col - c0] = s;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), make_rsrc(a1), (row * ld + col) * 4, 0,
+                                          AUX);
+  }
+};
+
+// blk: the workgroup's slot in the XCD-grouped grid (the hardware XCD is blk & 7).  red: >= 8 * 2 * 4 * 64
+// floats of LDS.
+template <int NPW, int VEC, bool AF>
+__device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs& h,
+                                         unsigned long long* __restrict__ counters, float* __restrict__ slabs,
+                                         int* __restrict__ err, int tm, int tn, int blk, float* red) {
+  constexpr int kCols = 32;
+  constexpr int AUX = 0;  // cache policy of the a1 / D / dZ1 stores
+  __shared__ float a1s[16][kCols + 1];
+  __shared__ float w2s[16][17];        // W2[class][row of this tile], zero past C / H
+  __shared__ float b2s[16];
+  __shared__ float zs[16][kCols + 1];  // z2 (+ b2), then D
+  __shared__ float ls[kCols];
+  __shared__ int s_bad;
+  const int xcd = blk & 7, slot = blk >> 3;
+  const int ct = xcd + 8 * (slot / tm), rt = slot % tm;
+  if (ct >= tn) return;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
+  const int t = threadIdx.x, H = f.H, C = h.C, n = f.n;
+  const int r0 = rt * 16, c0 = ct * kCols;
+  unsigned long long* st = f.stamps ? f.stamps + (size_t)blk * 4 : nullptr;  // diagnostics only
+  auto stamp = [&](int i) {
+    if (st && t == 0) st[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  // W2 slice of this tile's rows (read by the z2 partial and by dZ1) and b2; wsk_tile's barrier orders them
+  if (t < 256) {
+    const int c = t >> 4, r = t & 15;
+    w2s[c][r] = buf_load1<float>(make_rsrc(h.W2), (c < C && r0 + r < H) ? (c * H + r0 + r) * 4 : kOOB);
+  } else if (t < 256 + 16) {
+    const int c = t - 256;
+    b2s[c] = buf_load1<float>(make_rsrc(h.b2), c < C ? c * 4 : kOOB);
+  }
+  TileGeom g{H, n, f.P, r0, c0};
+  EpiSigLds<AUX> epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
+  fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red);
+  // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
+  // they are masked below.
+  // ---- 1. z2 partial for (class c, column col), one per thread, published write-through
+  const int c = t >> 5, col = t & 31;
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z += (r0 + r < H && c0 + col < n) ? w2s[c][r] * a1s[r][col] : 0.f;
+    float* slab = slabs + (size_t)(ct * tm + rt) * 16 * kCols;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, z), make_rsrc(slab), (c * kCols + col) * 4,
+                                          0, kSc1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
+  __syncthreads();
+  stamp(1);
+  // ---- 2. one add per workgroup, then wait for the tile's tm adds of this launch
+  if (t == 0) {
+    unsigned long long* cnt = counters + (size_t)ct * kAgCounterStride;
+    const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long target = (old / (unsigned)tm + 1) * (unsigned)tm;
+    uint32_t spins = 0;
+    int bad = 0;
+    // polled with a returning atomic (add 0): served where the adds are performed, never from a
+    // possibly stale L2 copy of the line (measured: sc1 load polls saw the last adds only ~20 us late)
+    while (old + 1 < target &&
+           __hip_atomic_fetch_add(cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++spins > kAgSpinLimit) {
+        bad = 1;
+        atomicExch(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    s_bad = bad;
+  }
+  __syncthreads();
+  stamp(2);
+  // ---- 3. z2 = sum of the tm partials (row-tile order: the same bits in every workgroup) + b2
+  {
+    // (the descriptor is built from the uniform slab base: a per-lane base makes hipcc waterfall every
+    // load over the 64 distinct descriptors -- measured +21 us)
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(slabs + (size_t)ct * tm * 16 * kCols);
+    const int lo = (c * kCols + col) * 4;
+    float v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      v[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                           rs, r < tm ? lo + r * 16 * kCols * 4 : kOOB, 0, kSc1));
+    float z = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) z += v[r];
+    zs[c][col] = z + b2s[c];
+  }
+  __syncthreads();
+  // softmax + cross-entropy gradient: 16 lanes (classes) per column, 4 columns per wave
+  {
+    const int col2 = t >> 4, cls = t & 15;
+    const int gcol = c0 + col2;
+    const bool cval = gcol < n;
+    const float z = zs[cls][col2];
+    float m = cls < C ? z : -3.402823466e38f;
+    if (h.shift) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    } else {
+      m = 0.f;
+    }
+    const float e = cls < C ? __expf(z - m) : 0.f;
+    float ssum = e;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) ssum += __shfl_xor(ssum, o, 64);
+    const int lab = cval ? h.labels[gcol] : -1;
+    const float yh = e / ssum;
+    const bool hit = cls == lab;
+    const float d = (cval && cls < C) ? (yh - (hit ? 1.f : 0.f)) * (float)h.scale : 0.f;
+    __syncthreads();  // every lane has read zs before it is overwritten with D
+    zs[cls][col2] = d;
+    if (rt == 0)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, d), make_rsrc(h.D),
+                                            (cval && cls < C) ? (cls * h.ldd + gcol) * 4 : kOOB, 0, AUX);
+    if (rt == 0 && h.loss_partial) {
+      float lp = (cval && hit) ? -__logf(yh) : 0.f;
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) lp += __shfl_xor(lp, o, 64);
+      if (cls == 0) ls[col2] = lp;
+    }
+  }
+  __syncthreads();
+  if (rt == 0 && h.loss_partial && t < 2) {  // one partial per 16 columns (the column head's layout)
+    const int vb = ct * 2 + t;
+    if (vb * 16 < n) {
+      float sl = 0.f;
+      for (int k = 0; k < 16; ++k) sl += ls[t * 16 + k];
+      h.loss_partial[vb] = sl;
+    }
+  }
+  if (s_bad) return;  // (zs holds D) a timed-out wait: nothing more is written
+  // ---- 4. dZ1 = (W2^T D) .* a1 .* (1 - a1) for this tile's 16 rows, one element per thread
+  {
+    const int r = t >> 5;  // (col as above)
+    const int row = r0 + r, gcol = c0 + col;
+    const bool rok = row < H, ok = rok && gcol < n;
+    float dz = 0.f;
+    if (ok) {
+      float da = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) da += w2s[k][r] * zs[k][col];
+      const float x = a1s[r][col];
+      dz = da * x * (1.f - x);
+    }
+    const size_t zi = (size_t)row * h.ldz + gcol;
+    if (h.dZ1)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dz), make_rsrc(h.dZ1),
+                                            ok ? (int)(zi * 4) : kOOB, 0, AUX);
+    // the planes two columns per 4-byte word: lanes col and col ^ 1 (same row) both split both values;
+    // the even lane stores the even planes' words, the odd lane the odd ones (the pair's second column
+    // lies inside the ld padding when it is past n; the dW1 GEMM never reads past n)
+    const float dzn = __shfl_xor(dz, 1, 64);
+    if (h.dZ1_planes) {
+      const float ve = (col & 1) ? dzn : dz, vo = (col & 1) ? dz : dzn;
+      const int ce = gcol & ~1;
+      const bool pok = rok && ce < n;
+      const __amdgpu_buffer_rsrc_t rp = make_rsrc(h.dZ1_planes);
+      const size_t pstride = (size_t)H * h.ldz;
+      float re = ve, ro = vo;
+      for (int p = 0; p < h.npz; ++p) {
+        const __hip_bfloat16 qe = __float2bfloat16(re), qo = __float2bfloat16(ro);
+        re -= __bfloat162float(qe);
+        ro -= __bfloat162float(qo);
+        const unsigned w = (unsigned)__builtin_bit_cast(unsigned short, qe) |
+                           ((unsigned)__builtin_bit_cast(unsigned short, qo) << 16);
+        const int off = (int)((p * pstride + (size_t)row * h.ldz + ce) * 2);
+        if ((p & 1) == (col & 1)) __builtin_amdgcn_raw_buffer_store_b32(w, rp, pok ? off : kOOB, 0, AUX);
+      }
+    }
+  }
+  if (st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    stamp(3);
+  }
+}
+
+}  // namespace cme

@@ -95,6 +95,7 @@ __device__ __forceinline__ __hip_bfloat16 zero_val<__hip_bfloat16>() { return __
 // hipcc branch around every load and wait vmcnt(0) per element -- measured:
 // a 10x100x800 dW2 took 17 us that way.)
 constexpr int kOOB = 0x7FFFFFF0;
+constexpr int kSc1 = 16;  // buffer cache-policy bit sc1: write-through stores / L1-bypassing loads
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, kOOB, 0x00020000);
