@@ -152,9 +152,11 @@ class MlpEngine:
             self.dZ1p = None
             self.dZ1g = torch.zeros(H, ld, dtype=torch.bfloat16, device=dev) if self.dtype == "bf16" else self.dZ1
         # wide layers: scratch for the split-H z2 partial sums of the two-kernel head
-        self.z2buf = None
+        self.z2buf = self.dw2buf = None
         if self.backend == "hip" and H >= 512 and self.pdt == torch.float32:
             self.z2buf = torch.zeros(int(hip().head_big_scratch_floats(H, ld)), dtype=torch.float32, device=dev)
+            # dW2 partials the wide head leaves per 32-column tile ([tile][16][H]) for the weight-gradient launch
+            self.dw2buf = torch.zeros((ld + 31) // 32 * 16 * H, dtype=torch.float32, device=dev)
         nblk = (ld + 15) // 16
         self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
         # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
@@ -304,6 +306,8 @@ class MlpEngine:
                     s.a_fp32 = int(os.environ["CME_A_FP32"])
             if self.z2buf is not None:
                 s.z2p = self.z2buf.data_ptr()
+                if self.dw2buf is not None and os.environ.get("CME_DW2_FROM_HEAD", "1") != "0":  # (A/B toggle)
+                    s.dw2p = self.dw2buf.data_ptr()
             if self.fh_counters is not None:
                 s.fh_counters = self.fh_counters.data_ptr()
                 s.fh_tiles = int(self.fh_counters.numel())

@@ -48,6 +48,7 @@ struct MlpStep {
   uintptr_t stamps = 0;  // diagnostics only
   uintptr_t hstamps = 0;  // diagnostics only: head-block stamps
   uintptr_t z2p = 0;     // wide-layer head scratch (head_big_scratch_floats), 0: column head
+  uintptr_t dw2p = 0;    // wide layers: dW2 partials [cdiv(ld, 32)][16][H] left by the head (0: the dW2 GEMM)
   int bias_col = 0;      // XT has an all-ones feature row P: db1 comes out of the dW1 GEMM
   // split path, H <= 128: uint32 tile counters (>= fh_tiles, zeroed) enable the single-launch forward +
   // head (mlp_fwd1_head); 0: separate fwd1 + head kernels
@@ -167,6 +168,10 @@ struct MlpStep {
             if (h.z2_chunks > 0 && bias_col) h.dZ1 = nullptr;
             // ... unless the dW1 GEMM splits fp32 dZ1 in registers: then fp32 dZ1 and no planes
             if (dz32) h.dZ1 = a.dZ1;
+            if (h.z2_chunks > 0 && dw2p && !(parts & 4)) {  // the head leaves dW2 partials for the wgrad launch
+              h.dw2part = P_<float>(dw2p);
+              a.dw2part = h.dw2part;
+            }
             if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
           }
         }
@@ -240,6 +245,11 @@ struct MlpStep {
     a.wg_parts = parts;
     a.w1_row0 = row0;
     a.w1_rows = rows;
+    if (dw2p && z2p) {  // the forward + head half (run(parts=1)) of this step left dW2 partials: same test as run()
+      cme::SplitStepArgs f = a;
+      f.z2part = P_<float>(z2p);
+      if (cme::mlp_split_fwd1_z2_chunks(f) > 0) a.dw2part = P_<float>(dw2p);
+    }
     cme::mlp_split_wgrad(a, S(stream));
   }
 
@@ -405,6 +415,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("hstamps", &MlpStep::hstamps)
       .def_readwrite("xscale", &MlpStep::xscale)
       .def_readwrite("z2p", &MlpStep::z2p)
+      .def_readwrite("dw2p", &MlpStep::dw2p)
       .def_readwrite("bias_col", &MlpStep::bias_col)
       .def("set_xgmi", &MlpStep::set_xgmi, py::arg("desc"), py::arg("slots"), py::arg("off_b1"), py::arg("off_W2"),
            py::arg("off_b2"))

@@ -52,6 +52,10 @@ struct HeadArgs {
   int z2_chunks = 0;
   // diagnostics only: s_memrealtime stamps [block][8] (bench/stamps_fh.py)
   unsigned long long* stamps = nullptr;
+  // wide head (z2_chunks > 0) only: when set, each 32-column tile also leaves its dW2 partial
+  // dw2part[column tile][16][H] = D[:, tile cols] . a1[:, tile cols]^T (classes < C) for the weight-gradient
+  // launch to sum (SplitStepArgs::dw2part)
+  float* dw2part = nullptr;
 };
 int64_t head_big_scratch_floats(int H, int n);
 

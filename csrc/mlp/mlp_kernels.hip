@@ -777,11 +777,11 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
     float v[kZ2Burst];
 #pragma unroll
     for (int u = 0; u < kZ2Burst; ++u)
-      v[u] = buf_load1<float>(rz, (zcol < a.n && u < a.z2_chunks) ? ((u * 16 + zc) * ld + zcol) * 4 : kOOB);
+      v[u] = buf_load1<float>(rz, (zcol < a.n && u < a.z2_chunks && zc < C) ? ((u * 16 + zc) * ld + zcol) * 4 : kOOB);
 #pragma unroll
     for (int u = 0; u < kZ2Burst; ++u) zsum += v[u];
-    for (int k = kZ2Burst; k < a.z2_chunks; ++k)
-      zsum += buf_load1<float>(rz, zcol < a.n ? ((k * 16 + zc) * ld + zcol) * 4 : kOOB);
+    for (int k = kZ2Burst; k < a.z2_chunks; ++k)  // (classes past C: never stored, read as the range-checked 0)
+      zsum += buf_load1<float>(rz, (zcol < a.n && zc < C) ? ((k * 16 + zc) * ld + zcol) * 4 : kOOB);
   }
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.W2), ra = make_rsrc(a.a1);
   float wv[RT][4], xv[RT][2][4];
@@ -924,6 +924,30 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (a.dw2part) {
+      // this column tile's share of dW2: P[c][h] = sum over its 32 columns of D[c][col] a1[h][col], one
+      // 16 x 16 x 32 v_mfma_f32_16x16x4_f32 chain per 16 rows (A = D from LDS, B = the a1 tile staged
+      // through this wave's LDS tile); the weight-gradient launch sums the column tiles' partials instead
+      // of re-reading all of a1 (mlp_split.hip wgrad_roles)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ts[w][4 * g + j][cb * 16 + c16] = xv[rt][cb][j];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      f32x4 pw = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8)
+        pw = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[c16][4 * s8 + g], ts[w][c16][4 * s8 + g], pw, 0, 0, 0);
+      const int hh = row0 + rt * 16 + c16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r < C && hh < H) a.dw2part[((size_t)ct * 16 + 4 * g + r) * H + hh] = pw[r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
   }
 }
 

@@ -458,10 +458,26 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf.npad;
     if (live) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
     EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, live ? 1 : 0, reg, lr, {}};
-    if (a.n % 4 == 0)
+    if (a.dw2part) {  // the head's per-column-tile partials, summed in tile order (16 rows x C classes)
+      const int nct = (a.n + 31) / 32, e = threadIdx.x, c = e >> 4, h = tb * 16 + (e & 15);
+      const bool ok = e < 256 && c < a.C && h < a.H;
+      epi.prefetch(0, c, h, ok);
+      const __amdgpu_buffer_rsrc_t rp = make_rsrc(a.dw2part);
+      float v = 0.f;
+      for (int k0 = 0; k0 < nct; k0 += 8) {
+        float pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          pv[u] = buf_load1<float>(rp, (ok && k0 + u < nct) ? (((k0 + u) * 16 + c) * a.H + h) * 4 : kOOB);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += pv[u];
+      }
+      if (ok) epi(0, c, h, v);
+    } else if (a.n % 4 == 0) {
       wsk_tile<float, 1, 1, kWKS, true, true, 1, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red);
-    else
+    } else {
       wsk_tile<float, 1, 1, kWKS, true, true, 0, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red);
+    }
     if (!live) return;
     const bool with_b2 = tb == 0;  // db2 (fused mode has no separate bias role): one wave per class
     if (with_b2) {
@@ -580,7 +596,8 @@ struct EpiSigBig {
       const int col = col0 + 16 * nb + fr;
       if (col < N) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) z2p[((size_t)tile * 16 + 4 * fg + i) * ld + col] = s[i];
+        for (int i = 0; i < 4; ++i)
+          if (4 * fg + i < C) z2p[((size_t)tile * 16 + 4 * fg + i) * ld + col] = s[i];  // (past C: zero, unread)
       }
     }
   }
@@ -722,8 +739,8 @@ __global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn)
     for (int r = 1; r < G::WRN; ++r) sz += red[((r * 2 + wc) * NB + nb) * 64 + lane];
     const int col = cw + 16 * nb + fr;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      st_f32(rz, col < n ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, sz[i]);
+    for (int i = 0; i < 4; ++i)  // (classes past C are zero: not stored, the head does not read them)
+      st_f32(rz, (col < n && 4 * fg + i < a.C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, sz[i]);
   }
 }
 
@@ -869,7 +886,8 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn)
   const int tile = m0 / BM;
   const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) st_f32(rz, col < n ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, sz[i]);
+  for (int i = 0; i < 4; ++i)  // (classes past C are zero: not stored, the head does not read them)
+    st_f32(rz, (col < n && 4 * fg + i < C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, sz[i]);
 }
 
 // dW1 = dZ1 XT on the A-in-registers engine: dZ1 read as fp32 (AT = float; the head writes it instead of
