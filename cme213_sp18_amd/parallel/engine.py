@@ -21,8 +21,6 @@ Two interchangeable compute backends execute a step:
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import torch
 
@@ -301,12 +299,9 @@ class MlpEngine:
                 s.npw = s.npz = self.np
                 s.W1p = self.W1p.data_ptr()
                 s.dZ1p = self.dZ1p.data_ptr()
-                # split3 operand forms of the small-layer GEMMs (SplitStepArgs.a_fp32; measurement override)
-                if os.environ.get("CME_A_FP32"):
-                    s.a_fp32 = int(os.environ["CME_A_FP32"])
             if self.z2buf is not None:
                 s.z2p = self.z2buf.data_ptr()
-                if self.dw2buf is not None and os.environ.get("CME_DW2_FROM_HEAD", "1") != "0":  # (A/B toggle)
+                if self.dw2buf is not None:
                     s.dw2p = self.dw2buf.data_ptr()
             if self.fh_counters is not None:
                 s.fh_counters = self.fh_counters.data_ptr()

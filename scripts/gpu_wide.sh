@@ -10,15 +10,13 @@ echo "== tests"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_mlp.py tests/test_gpu_dist.py tests/test_tensor_parallel.py -m gpu -x -q --timeout 120 \
   --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -5 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-echo "== kbench (dW2 from the head's partials: on, then off)"
-for d in 1 0; do
-  CME_DW2_FROM_HEAD=$d timeout -k 10 240 python bench/kbench.py --hidden 4096 1024 --cols 800 --cfg f32:split3 bf16:split1 \
-    --json $O/kbench$d.json > $O/kbench$d.log 2>&1 || { tail -20 $O/kbench$d.log; exit 1; }
-  grep -v amdgpu.ids $O/kbench$d.log | python3 -c "
+echo "== kbench"
+timeout -k 10 240 python bench/kbench.py --hidden 4096 1024 --cols 800 --cfg f32:split3 bf16:split1 \
+  --json $O/kbench.json > $O/kbench.log 2>&1 || { tail -20 $O/kbench.log; exit 1; }
+grep -v amdgpu.ids $O/kbench.log | python3 -c "
 import sys,json
 for l in sys.stdin:
-    r=json.loads(l); print('dw2head=$d', {k:v for k,v in r.items() if k.endswith('_us') or k in ('dtype','H')})"
-done
+    r=json.loads(l); print({k:v for k,v in r.items() if k.endswith('_us') or k in ('dtype','H')})"
 echo "== gemm vs vendor (training shapes)"
 timeout -k 10 240 python bench/gemm_vs_vendor.py --only training --json $O/gemm_training.json > $O/gemm.log 2>&1 \
   || { tail -20 $O/gemm.log; exit 1; }
