@@ -28,7 +28,6 @@ constexpr int kAgCounterStride = 32;  // uint64 words: one 256-byte line per til
 
 __device__ __forceinline__ float ag_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
 
-template <int AUX>
 struct EpiSigLds {
   const float* b1;
   float* a1;
@@ -42,8 +41,7 @@ struct EpiSigLds {
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     const float s = ag_sigmoid(v * xscale + pre[q]);
     a1s[row - r0][col - c0] = s;
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), make_rsrc(a1), (row * ld + col) * 4, 0,
-                                          AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), make_rsrc(a1), (row * ld + col) * 4, 0, 0);
   }
 };
 
@@ -54,7 +52,6 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
                                          unsigned long long* __restrict__ counters, float* __restrict__ slabs,
                                          int* __restrict__ err, int tm, int tn, int blk, float* red) {
   constexpr int kCols = 32;
-  constexpr int AUX = 0;  // cache policy of the a1 / D / dZ1 stores
   __shared__ float a1s[16][kCols + 1];
   __shared__ float w2s[16][17];        // W2[class][row of this tile], zero past C / H
   __shared__ float b2s[16];
@@ -80,7 +77,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     b2s[c] = buf_load1<float>(make_rsrc(h.b2), c < C ? c * 4 : kOOB);
   }
   TileGeom g{H, n, f.P, r0, c0};
-  EpiSigLds<AUX> epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
+  EpiSigLds epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
   fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red);
   // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
   // they are masked below.
@@ -161,7 +158,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     zs[cls][col2] = d;
     if (rt == 0)
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, d), make_rsrc(h.D),
-                                            (cval && cls < C) ? (cls * h.ldd + gcol) * 4 : kOOB, 0, AUX);
+                                            (cval && cls < C) ? (cls * h.ldd + gcol) * 4 : kOOB, 0, 0);
     if (rt == 0 && h.loss_partial) {
       float lp = (cval && hit) ? -__logf(yh) : 0.f;
 #pragma unroll
@@ -195,7 +192,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     const size_t zi = (size_t)row * h.ldz + gcol;
     if (h.dZ1)
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dz), make_rsrc(h.dZ1),
-                                            ok ? (int)(zi * 4) : kOOB, 0, AUX);
+                                            ok ? (int)(zi * 4) : kOOB, 0, 0);
     // the planes two columns per 4-byte word: lanes col and col ^ 1 (same row) both split both values;
     // the even lane stores the even planes' words, the odd lane the odd ones (the pair's second column
     // lies inside the ld padding when it is past n; the dW1 GEMM never reads past n)
@@ -214,7 +211,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
         const unsigned w = (unsigned)__builtin_bit_cast(unsigned short, qe) |
                            ((unsigned)__builtin_bit_cast(unsigned short, qo) << 16);
         const int off = (int)((p * pstride + (size_t)row * h.ldz + ce) * 2);
-        if ((p & 1) == (col & 1)) __builtin_amdgcn_raw_buffer_store_b32(w, rp, pok ? off : kOOB, 0, AUX);
+        if ((p & 1) == (col & 1)) __builtin_amdgcn_raw_buffer_store_b32(w, rp, pok ? off : kOOB, 0, 0);
       }
     }
   }
