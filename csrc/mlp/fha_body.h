@@ -68,6 +68,10 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     if (st && t == 0) st[i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
+  // the label of this thread's softmax column (t >> 4), fetched now: loaded where the softmax uses it, it was
+  // a dependent memory round trip after the all-gather wait
+  const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(
+      make_rsrc(h.labels), c0 + (t >> 4) < n ? (c0 + (t >> 4)) * 4 : kOOB, 0, 0);
   // W2 slice of this tile's rows (read by the z2 partial and by dZ1) and b2; wsk_tile's barrier orders them
   if (t < 256) {
     const int c = t >> 4, r = t & 15;
@@ -150,7 +154,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     float ssum = e;
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) ssum += __shfl_xor(ssum, o, 64);
-    const int lab = cval ? h.labels[gcol] : -1;
+    const int lab = cval ? lab_pre : -1;
     const float yh = e / ssum;
     const bool hit = cls == lab;
     const float d = (cval && cls < C) ? (yh - (hit ? 1.f : 0.f)) * (float)h.scale : 0.f;

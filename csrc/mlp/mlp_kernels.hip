@@ -765,8 +765,16 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
   const int rb = blockIdx.x % nrb, ct = blockIdx.x / nrb;
   const int H = a.H, C = a.C, ld = a.lda;
   const int row0 = (rb * 8 + w) * 16 * RT;
+  auto hstamp = [&](int i) {  // diagnostics (HeadArgs::stamps, bench/stamps_hw.py): wave 0 lane 0 of the block
+    if (a.stamps && t == 0) a.stamps[(size_t)blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+  hstamp(0);
   // ---- one burst: the z2 partial sums of (class t>>5, column t&31), W2^T operands, a1 of the tiles
   const int zc = t >> 5, zcol = ct * kHWCols + (t & 31);
+  // the label of softmax column t, fetched with the burst: loaded where it is used it was a dependent
+  // memory round trip inside the single-wave softmax (bench/stamps_hw.py: softmax phase 2.3 us)
+  const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(
+      make_rsrc(a.labels), (t < kHWCols && ct * kHWCols + t < a.n) ? (ct * kHWCols + t) * 4 : kOOB, 0, 0);
   const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
   float zsum = 0.f;
   {
@@ -784,28 +792,31 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
       zsum += buf_load1<float>(rz, (zcol < a.n && zc < C) ? ((k * 16 + zc) * ld + zcol) * 4 : kOOB);
   }
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.W2), ra = make_rsrc(a.a1);
-  float wv[RT][4], xv[RT][2][4];
+  // a1: each wave's 16 x 32 tiles as two 16-byte loads per lane (row lane >> 2, 8 columns from (lane & 3) * 8),
+  // re-read from the wave's LDS tile in the MFMA layout below -- 4x fewer load instructions than 4-byte loads
+  // in that layout (rows ld apart).  Columns past n (inside the ld padding) hold finite stale values or zeros:
+  // they only meet D = 0 or masked stores.
+  const int sr = lane >> 2, sc = (lane & 3) * 8;
+  float wv[RT][4];
+  f32x4 xr[RT][2];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const int hA = row0 + rt * 16 + c16;
 #pragma unroll
     for (int i = 0; i < 4; ++i) wv[rt][i] = buf_load1<float>(rw, (4 * g + i < C && hA < H) ? ((4 * g + i) * H + hA) * 4 : kOOB);
+    const int h = row0 + rt * 16 + sr, col = ct * kHWCols + sc;
+    const int off = (h < H && col < ld) ? (h * ld + col) * 4 : kOOB;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int col = ct * kHWCols + cb * 16 + c16;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int h = row0 + rt * 16 + 4 * g + j;
-        xv[rt][cb][j] = buf_load1<float>(ra, (h < H && col < a.n) ? (h * ld + col) * 4 : kOOB);
-      }
-    }
+    for (int q = 0; q < 2; ++q)
+      xr[rt][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 16 * q, 0));
   }
   zs[zc][t & 31] = zsum + (zc < C ? static_cast<const float*>(a.b2)[zc < C ? zc : 0] : 0.f);
   __syncthreads();
+  hstamp(1);
   if (t < kHWCols) {  // ---- softmax / loss / D for column t
     const int col = ct * kHWCols + t;
     const bool ok = col < a.n;
-    const int lab = ok ? a.labels[col] : -1;
+    const int lab = ok ? lab_pre : -1;
     float m = 0.f;
     if (a.shift) {
       m = zs[0][t];
@@ -830,6 +841,7 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
     ls[t] = lp;
   }
   __syncthreads();
+  hstamp(2);
   if (rb == 0 && a.loss_partial && t < 2) {  // the column head's layout: one partial per 16 columns
     const int vb = ct * 2 + t;
     if (vb * 16 < a.n) {
@@ -851,11 +863,40 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
   // The MFMA leaves each lane 4 ROWS of one column; stored straight from there every plane store is a
   // 2-byte scatter (32-byte row pieces).  The tile goes through this wave's LDS tile instead and comes
   // back as 8 consecutive columns per lane: one 16-byte store per plane (64-byte row pieces).
-  const int sr = lane >> 2, sc = (lane & 3) * 8;
   const int scol = ct * kHWCols + sc;
   const bool vec = a.ldz % 8 == 0;  // 16-byte aligned rows (ld is padded to 16)
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
+    // this row tile's a1, row-major into the wave's LDS tile, then read back in the MFMA C layout
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ts[w][sr][sc + 4 * q + u] = xr[rt][q][u];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float xv[2][4];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[cb][j] = ts[w][4 * g + j][cb * 16 + c16];
+    if (a.dw2part) {
+      // this column tile's share of dW2: P[c][h] = sum over its 32 columns of D[c][col] a1[h][col], one
+      // 16 x 16 x 32 v_mfma_f32_16x16x4_f32 chain per 16 rows (A = D from LDS, B = the row-major a1 tile);
+      // the weight-gradient launch sums the column tiles' partials instead of re-reading all of a1
+      // (mlp_split.hip wgrad_roles)
+      f32x4 pw = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8)
+        pw = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[c16][4 * s8 + g], ts[w][c16][4 * s8 + g], pw, 0, 0, 0);
+      const int hh = row0 + rt * 16 + c16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r < C && hh < H) a.dw2part[((size_t)ct * 16 + 4 * g + r) * H + hh] = pw[r];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // every read of the a1 tile is done
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       f32x4 r = {0.f, 0.f, 0.f, 0.f};
@@ -863,7 +904,7 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
       for (int i = 0; i < 4; ++i) r = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[rt][i], dv[cb][i], r, 0, 0, 0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float x = xv[rt][cb][j];
+        const float x = xv[cb][j];
         ts[w][4 * g + j][cb * 16 + c16] = r[j] * x * (1.f - x);
       }
     }
@@ -924,30 +965,10 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (a.dw2part) {
-      // this column tile's share of dW2: P[c][h] = sum over its 32 columns of D[c][col] a1[h][col], one
-      // 16 x 16 x 32 v_mfma_f32_16x16x4_f32 chain per 16 rows (A = D from LDS, B = the a1 tile staged
-      // through this wave's LDS tile); the weight-gradient launch sums the column tiles' partials instead
-      // of re-reading all of a1 (mlp_split.hip wgrad_roles)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ts[w][4 * g + j][cb * 16 + c16] = xv[rt][cb][j];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      f32x4 pw = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s8 = 0; s8 < 8; ++s8)
-        pw = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[c16][4 * s8 + g], ts[w][c16][4 * s8 + g], pw, 0, 0, 0);
-      const int hh = row0 + rt * 16 + c16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (4 * g + r < C && hh < H) a.dw2part[((size_t)ct * 16 + 4 * g + r) * H + hh] = pw[r];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+  }
+  if (a.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    hstamp(3);
   }
 }
 
