@@ -30,7 +30,15 @@ def main(argv=None):
     x, y = synthetic_mnist(4000, seed=0)
     nn = NeuralNetwork([784, a.hidden, 10])
     pct = lambda v: [round(float(np.percentile(v, q)), 3) for q in (0, 50, 90, 100)]  # noqa: E731
-    for a32 in (3, 1, 3, 1):
+    def xcd_remap(orig, nwg):  # csrc/common/hip_common.h
+        if nwg <= 8:
+            return orig
+        q, r, x = nwg // 8, nwg % 8, orig % 8
+        return (x * (q + 1) if x < r else r * (q + 1) + (x - r) * q) + orig // 8
+
+    t1n = (785 + 31) // 32
+    t1 = ((a.hidden + 15) // 16) * t1n
+    for a32 in (1, 1):
         e = MlpEngine(nn.H, dtype="f32", max_cols=a.n, device="cuda", path="split3")
         e.set_params(*nn.params)
         e.load_dataset(x, y)
@@ -51,6 +59,17 @@ def main(argv=None):
         rel = (s - t0) * 10.0 / 1000.0
         print(json.dumps({"a_fp32": a32, "waves": int(len(s)), "entry": pct(rel[:, 0]), "kloop_done": pct(rel[:, 1]),
                           "kloop": pct(rel[:, 1] - rel[:, 0]), "reduced": pct(rel[:, 2]), "end": pct(rel[:, 3])}))
+        # per workgroup (wave 0): which dW1 tiles end last -- (row tile, column tile, XCD, end us)
+        raw = buf.view(-1, 8, 4)[:t1].cpu().numpy().astype(np.int64)
+        ends = [((raw[b, :, 3].max() - t0) * 10.0 / 1000.0, b) for b in range(t1) if raw[b, 0, 0] > 0]
+        ends.sort(reverse=True)
+        slow = [{"row_tile": xcd_remap(b, t1) // t1n, "col_tile": xcd_remap(b, t1) % t1n, "xcd": b % 8,
+                 "end_us": round(float(t_), 2)} for t_, b in ends[:12]]
+        cols = {}
+        for t_, b in ends:
+            cols.setdefault(xcd_remap(b, t1) % t1n, []).append(float(t_))
+        print(json.dumps({"slowest": slow, "median_end_by_col_tile": {k: round(float(np.median(v)), 2)
+                                                                     for k, v in sorted(cols.items())}}), flush=True)
 
 
 if __name__ == "__main__":

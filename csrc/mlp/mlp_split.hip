@@ -359,11 +359,13 @@ struct EpiW1 {
   float* gb1;
   int sys;  // gradients into a peer-visible IPC buffer (write-through)
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
-    pre[q] = buf_load1<float>(make_rsrc(W1), (ok && col < P) ? (row * P + col) * 4 : kOOB);
+    // (the all-ones feature column P: b1[row], so its update is not a dependent load after the K loop)
+    if (col == P) pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
+    else pre[q] = buf_load1<float>(make_rsrc(W1), (ok && col < P) ? (row * P + col) * 4 : kOOB);
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     if (col == P) {  // the all-ones feature: db1[row] (no input scale, no regulariser)
-      if (sgd) b1[row] -= lr * v;
+      if (sgd) b1[row] = pre[q] - lr * v;
       else if (sys) xf_store(gb1, row, v);
       else gb1[row] = v;
       return;

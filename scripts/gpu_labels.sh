@@ -11,6 +11,8 @@ timeout -k 10 120 python bench/stamps_hw.py > $O/stamps_hw.jsonl 2>&1 || { tail 
 grep -v amdgpu $O/stamps_hw.jsonl | tail -2
 timeout -k 10 120 python bench/stamps_fha.py > $O/stamps_fha.jsonl 2>&1 || { tail -5 $O/stamps_fha.jsonl; exit 1; }
 grep -v amdgpu $O/stamps_fha.jsonl | tail -2
+timeout -k 10 120 python bench/stamps_wgrad.py > $O/stamps_wgrad.jsonl 2>&1 || { tail -5 $O/stamps_wgrad.jsonl; exit 1; }
+grep -v amdgpu $O/stamps_wgrad.jsonl | tail -2
 timeout -k 10 300 python bench/kbench.py --hidden 100 4096 1024 --cols 800 --cfg f32:split3 bf16:split1 > $O/kbench.log 2>&1 \
   || { tail -5 $O/kbench.log; exit 1; }
 grep -v amdgpu $O/kbench.log | python3 -c "
