@@ -52,6 +52,17 @@ def main(argv=None):
         rel = (s - t0) * 10.0 / 1000.0
         print(json.dumps({"wgs": int(len(s)), "entry": pct(rel[:, 0]), "published": pct(rel[:, 1]),
                           "all_arrived": pct(rel[:, 2]), "wait": pct(rel[:, 2] - rel[:, 1]), "end": pct(rel[:, 3])}))
+        if rep == 3:  # per column tile (XCD-grouped grid: block b -> xcd b & 7, slot b >> 3, ct = xcd + 8 (slot // tm))
+            tm = (a.hidden + 15) // 16
+            allv = buf.view(-1, 4).cpu().numpy().astype(np.int64)
+            per = {}
+            for b in range(allv.shape[0]):
+                if allv[b, 0] <= 0:
+                    continue
+                ct = (b & 7) + 8 * ((b >> 3) // tm)
+                per.setdefault(ct, []).append(((allv[b, 0] - t0) / 100.0, (allv[b, 3] - t0) / 100.0))
+            print(json.dumps({str(ct): {"last_entry": round(max(e for e, _ in v), 2), "last_end": round(max(x for _, x in v), 2)}
+                              for ct, v in sorted(per.items())}), flush=True)
 
 
 if __name__ == "__main__":
