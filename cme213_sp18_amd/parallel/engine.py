@@ -122,6 +122,7 @@ class MlpEngine:
         # H <= 128 split path: the forward + head launch in its all-gather form (every workgroup of the
         # launch must be resident at once; DataParallelTrainer turns it off when processes share a GPU)
         self.fh_allgather = True
+        self.store_a1 = True
 
     def _configure_path(self):
         dev = self.device
@@ -168,6 +169,12 @@ class MlpEngine:
             # [tile][8 row tiles][16 classes][32 columns], and the timed-out-wait word
             self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)  # one 256-B line each
             self.ag_slabs = torch.zeros(tiles * 8 * 16 * 32, dtype=torch.float32, device=dev)
+            self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
+        elif self.backend == "hip" and self.np and H >= 1024 and C <= 16 and self.dw2buf is not None:
+            # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_rega_ag) uses one
+            # monotonic counter per column tile and the timed-out-wait word
+            tiles = (ld + 31) // 32
+            self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._step = None
 
@@ -246,6 +253,13 @@ class MlpEngine:
         if self._step is not None:
             self._step.fh_allgather = int(self.fh_allgather)
 
+    def set_store_a1(self, on: bool) -> None:
+        """Wide split layers with the head fused into the forward launch: False skips the a1 store (no kernel
+        of the training step reads a1 there: dZ1 and the dW2 partials come out of the same launch)."""
+        self.store_a1 = bool(on)
+        if self._step is not None:
+            self._step.store_a1 = int(self.store_a1)
+
     def w1_planes_maintained(self) -> bool:
         """True when the W1 bf16 planes track the fp32 master after every update.  Below H = 512 the split3
         forward kernels read fp32 W1 and split it in registers, so the update stops refreshing the planes
@@ -310,6 +324,12 @@ class MlpEngine:
                 s.ag_slabs = self.ag_slabs.data_ptr()
                 s.ag_err = self.ag_err.data_ptr()
                 s.fh_allgather = int(self.fh_allgather)
+            elif self.ag_counters is not None:
+                s.fh_tiles = int(self.ag_counters.numel()) // 32
+                s.ag_counters = self.ag_counters.data_ptr()
+                s.ag_err = self.ag_err.data_ptr()
+                s.fh_allgather = int(self.fh_allgather)
+            s.store_a1 = int(self.store_a1)
             if self.np and self.XT is not None and self.XT.shape[0] == self.P + 1:
                 s.bias_col = 1
             if self._xgmi_fuse is not None and s.bias_col:

@@ -97,6 +97,9 @@ class DataParallelTrainer:
         self.engine = MlpEngine(nn.H, dtype=dtype, max_cols=max_cols, device=device, backend=backend, shift=shift,
                                 path=path)
         self.engine.set_params(*nn.params)
+        # training reads nothing of a1 after a step: the wide fused forward + head launch skips its 13 MB store
+        # at H = 4096 (bench/wide_ag_ab.py: -1.4 us/step fp32, -2.1 us bf16)
+        self.engine.set_store_a1(False)
         self._graphs: dict = {}
         self._sharing = None
         self.iter = 0

@@ -58,6 +58,11 @@ struct MlpStep {
   // word (>= fh_tiles each); fh_allgather = 1 selects it when all three are set
   uintptr_t ag_counters = 0, ag_slabs = 0, ag_err = 0;
   int fh_allgather = 0;
+  // wide split layers: the all-gather head fused into the forward launch (fh_allgather, ag_counters, ag_err;
+  // mlp_fwd1_rega_ag) leaves dW2 partials per 128 columns (32 from head_wide_kernel): what run_wgrad sums
+  int dw2_cols_last = 32;
+  int store_a1 = 1;  // the fused wide head: 0 skips the a1 store (nothing in the step reads it)
+  int ag_xcd_grouped = 0;  // the fused wide head's grid: 1 = each column tile on one XCD (RegaAgArgs)
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
   void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2) {
@@ -161,7 +166,6 @@ struct MlpStep {
             // wide layers: the forward GEMM also leaves the head's z2 partials (unless only the head runs)
             cme::SplitStepArgs f = a;
             f.z2part = (z2p && !(parts & 8)) ? P_<float>(z2p) : nullptr;
-            if (!(parts & 8)) cme::mlp_split_fwd1(f, S(stream));
             h.z2_chunks = f.z2part ? cme::mlp_split_fwd1_z2_chunks(f) : 0;
             // with the all-ones XT feature nothing reads dZ1 in fp32 on the wide path (db1 comes out of
             // the dW1 GEMM over the planes): skip those 4 B/element of HBM writes
@@ -172,7 +176,16 @@ struct MlpStep {
               h.dw2part = P_<float>(dw2p);
               a.dw2part = h.dw2part;
             }
-            if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
+            if (fh_allgather && ag_counters && ag_err && h.dw2part && !(parts & 12) &&
+                cme::mlp_fwd1_rega_ag_ok(f, h)) {  // one launch: forward GEMM + the all-gather head
+              cme::mlp_fwd1_rega_ag(f, h, P_<unsigned long long>(ag_counters), fh_tiles, P_<int>(ag_err),
+                                    store_a1, ag_xcd_grouped, S(stream));
+              a.dw2_cols = 128;
+            } else {
+              if (!(parts & 8)) cme::mlp_split_fwd1(f, S(stream));
+              if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
+            }
+            dw2_cols_last = a.dw2_cols;
           }
         }
       }
@@ -248,7 +261,10 @@ struct MlpStep {
     if (dw2p && z2p) {  // the forward + head half (run(parts=1)) of this step left dW2 partials: same test as run()
       cme::SplitStepArgs f = a;
       f.z2part = P_<float>(z2p);
-      if (cme::mlp_split_fwd1_z2_chunks(f) > 0) a.dw2part = P_<float>(dw2p);
+      if (cme::mlp_split_fwd1_z2_chunks(f) > 0) {
+        a.dw2part = P_<float>(dw2p);
+        a.dw2_cols = dw2_cols_last;
+      }
     }
     cme::mlp_split_wgrad(a, S(stream));
   }
@@ -400,6 +416,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_slabs", &MlpStep::ag_slabs)
       .def_readwrite("ag_err", &MlpStep::ag_err)
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
+      .def_readwrite("store_a1", &MlpStep::store_a1)
+      .def_readwrite("ag_xcd_grouped", &MlpStep::ag_xcd_grouped)
       .def_readwrite("a_fp32", &MlpStep::a_fp32)
       .def("w1_planes_read",
            [](const MlpStep& st) {  // a forward kernel of this step reads the W1 planes (else: not refreshed)

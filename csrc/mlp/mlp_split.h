@@ -85,6 +85,7 @@ struct SplitStepArgs {
   // wide layers: the head left dW2 partials [cdiv(n, 32)][16][H] (HeadArgs::dw2part); the dW2 role then sums
   // them in column-tile order instead of forming D . a1^T from all of a1
   float* dw2part = nullptr;
+  int dw2_cols = 32;  // columns per dW2 partial: 32 (head_wide_kernel), 128 (the fused all-gather head)
   int w1_planes = 1;  // (set by mlp_split_wgrad) the small-layer W1 update refreshes the W1 planes
 };
 
@@ -107,6 +108,14 @@ int mlp_split_fused_tiles(int P, int H, int cap);
 void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);
 // tiled forward only: a1 = sigmoid(W1 X + b1) (pair with mlp_head for the 3-kernel step)
 void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s);
+// wide layers: the forward GEMM with the head fused in (all-gather form, fwd1_rega_kernel<..., AG>): one
+// launch leaves a1 (store_a1), D, the loss partials, dZ1 (fp32 and / or planes) and the dW2 partials per
+// 128-column tile (h.dw2part; the weight-gradient launch then needs a.dw2_cols = 128).  Every workgroup must
+// be resident at once (off when processes share a GPU); a timed-out wait sets *err.
+struct HeadArgs;
+bool mlp_fwd1_rega_ag_ok(const SplitStepArgs& a, const HeadArgs& h);
+void mlp_fwd1_rega_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long long* counters, int max_tiles,
+                      int* err, int store_a1, int xcd_grouped, hipStream_t s);
 void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s);
 int mlp_split_fwdhead_blocks(int n);
 

@@ -1,5 +1,6 @@
 // Split-bf16 MLP step kernels (see mlp_split.h for the numerics argument).
 #include "mlp_split.h"
+#include "mlp_kernels.h"
 
 #include <algorithm>
 
@@ -461,7 +462,7 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     if (live) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
     EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, live ? 1 : 0, reg, lr, {}};
     if (a.dw2part) {  // the head's per-column-tile partials, summed in tile order (16 rows x C classes)
-      const int nct = (a.n + 31) / 32, e = threadIdx.x, c = e >> 4, h = tb * 16 + (e & 15);
+      const int nct = (a.n + a.dw2_cols - 1) / a.dw2_cols, e = threadIdx.x, c = e >> 4, h = tb * 16 + (e & 15);
       const bool ok = e < 256 && c < a.C && h < a.H;
       epi.prefetch(0, c, h, ok);
       const __amdgpu_buffer_rsrc_t rp = make_rsrc(a.dw2part);
@@ -818,16 +819,231 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
       }
 }
 
+// ---- wide layers: the head fused into the A-in-registers forward launch (all-gather form, H >= 1024).
+// Every 128 x 128 a1 tile is still in its workgroup's accumulators when the forward GEMM ends, so instead of
+// storing z2 partials for head_wide_kernel to reduce (and re-reading all of a1 there), the tm row-tile
+// workgroups of a column tile hand off twice through one monotonic counter per column tile:
+//   1. every workgroup publishes its z2 partial (sc1 stores above, vmcnt(0), barrier, one agent add), then
+//      waits for the tm adds of this launch;
+//   2. row tile rt < 8 reduces columns n0 + 16 rt .. +15 (the tm partials in tile order, + b2), forms
+//      softmax / D / the loss partial of those 16 columns exactly as head_wide_kernel does (same operation
+//      order: bit-identical D, loss and dZ1), stores D sc1, vmcnt(0), barrier, second add;
+//   3. after the 2 tm adds every workgroup reads the tile's 16 x 128 D (sc1 loads) and forms dZ1 = (W2^T D)
+//      .* a1 .* (1 - a1) for its own 128 x 128 tile on the f32 MFMA, plus the tile's dW2 partial
+//      D . a1^T (SplitStepArgs::dw2_cols = 128).
+// The hand-off is MI355X_MICROARCH.md's table's first row (sc1 stores drained before one agent add per
+// workgroup, returning-atomic polls, barrier, sc1 loads), one workgroup per CU (the launcher's LDS request
+// and <= 32 workgroups per XCD).  Every workgroup must be resident at once; a wait past kRegaAgSpinLimit sets *err
+// (MlpEngine.kernel_error()) and the workgroup writes nothing more -- the counter still gets both adds, so
+// later launches stay aligned.
+struct RegaAgArgs {
+  HeadArgs h{};
+  unsigned long long* counters = nullptr;  // [column tile * kRegaAgCounterStride], monotonic
+  int* err = nullptr;
+  int store_a1 = 1;  // 0: a1 is not stored (nothing after the fused head reads it)
+  int tm = 0;        // row tiles
+  // 1: XCD-grouped grid (8 * tm * cdiv(tn, 8) workgroups, each column tile on one XCD); 0: the plain forward's
+  // xcd_remap grid (tm * tn workgroups; a column tile's row tiles span XCDs -- the hand-off crosses L2s)
+  int xcd_grouped = 0;
+};
+constexpr int kRegaAgCounterStride = 32;  // uint64 words: one 256-byte line per column-tile counter
+constexpr uint32_t kRegaAgSpinLimit = 1u << 22;
+constexpr int kAgLd = 132;  // LDS row pitch (floats) of the D tile and the per-wave a1 tiles: conflict-free
+constexpr int kRegaAgLdsBytes = (16 * kAgLd + 8 * 16 * kAgLd + 16 * 17 + 16 + 4) * 4;
+
+// one lane: 1 when the counter did not reach `target` within the spin bound (and *err is set)
+__device__ __forceinline__ int rega_ag_wait(unsigned long long* cnt, unsigned long long target, int* err) {
+  uint32_t spins = 0;
+  // polled with a returning atomic (add 0): served where the adds are performed, never a stale L2 copy
+  while (__hip_atomic_fetch_add(cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (++spins > kRegaAgSpinLimit) {
+      atomicExch(err, 1);
+      return 1;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return 0;
+}
+
+__device__ __forceinline__ void ag_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// a1v[nb][j] = a1(row rw + 4 fg + j, column n0 + 16 nb + fr) of this wave; tm row tiles; ct = column tile
+__device__ __forceinline__ void rega_head_ag(const SplitStepArgs& a, const RegaAgArgs& g, const f32x4 (&a1v)[8],
+                                             char* lds, int m0, int n0, int rw, int tm, int ct) {
+  const HeadArgs& h = g.h;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, fr = lane & 15, fg = lane >> 4;
+  const int H = a.H, n = a.n, C = a.C, rt = m0 / 128;
+  float* Ds = reinterpret_cast<float*>(lds);    // [16][kAgLd] the column tile's D
+  float* ts = Ds + 16 * kAgLd + wave * 16 * kAgLd;  // [16][kAgLd] this wave's a1 rows
+  float* zs = Ds + 16 * kAgLd + 8 * 16 * kAgLd;     // [16][17] z2 (+ b2) of the reduced 16 columns
+  float* ls = zs + 16 * 17;                         // [16] loss of those columns
+  int* sflag = reinterpret_cast<int*>(ls + 16);
+  // independent loads first: the W2^T operand of dZ1 (class 4 fg + i, row rw + fr), the reducer's labels, b2
+  float wv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    wv[i] = buf_load1<float>(make_rsrc(a.W2), (4 * fg + i < C && rw + fr < H) ? ((4 * fg + i) * H + rw + fr) * 4 : kOOB);
+  const int u0 = n0 + 16 * rt;  // the 16 columns row tile rt < 8 reduces
+  const bool red = rt < 8 && u0 < n;
+  const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(
+      make_rsrc(h.labels), (red && t < 16 && u0 + t < n) ? (u0 + t) * 4 : kOOB, 0, 0);
+  const int zc = t >> 4, zcol = u0 + (t & 15);
+  const float b2v = buf_load1<float>(make_rsrc(h.b2), (red && t < 256 && zc < C) ? zc * 4 : kOOB);
+  // ---- hand-off 1: this tile's z2 partial is published
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
+  __syncthreads();  // (and every read of the z2 reduction scratch in lds is done)
+  unsigned long long* cnt = g.counters + (size_t)ct * kRegaAgCounterStride;
+  unsigned long long base = 0;
+  if (t == 0) {
+    const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base = old / (2ull * (unsigned)tm) * (2ull * (unsigned)tm);
+    sflag[0] = rega_ag_wait(cnt, base + (unsigned)tm, g.err);
+  }
+  __syncthreads();
+  const bool bad1 = sflag[0] != 0;
+  // ---- reduce-scatter: softmax / loss / D of columns u0 .. u0 + 15
+  if (red && !bad1) {
+    if (t < 256) {
+      const bool ok = zc < C && zcol < n;
+      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
+      constexpr int kBurst = 32;
+      float v[kBurst];
+#pragma unroll
+      for (int k = 0; k < kBurst; ++k)
+        v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             rz, (ok && k < tm) ? ((k * 16 + zc) * a.ld + zcol) * 4 : kOOB, 0, kSc1));
+      float zsum = 0.f;
+#pragma unroll
+      for (int k = 0; k < kBurst; ++k) zsum += v[k];
+      for (int k = kBurst; k < tm; ++k)
+        zsum += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rz, ok ? ((k * 16 + zc) * a.ld + zcol) * 4 : kOOB, 0, kSc1));
+      zs[zc * 17 + (t & 15)] = zsum + (zc < C ? b2v : 0.f);
+    }
+    __syncthreads();
+    if (t < 16) {  // head_wide_kernel's softmax arithmetic, in its order
+      const int col = u0 + t;
+      const bool ok = col < n;
+      const int lab = ok ? lab_pre : -1;
+      float m = 0.f;
+      if (h.shift) {
+        m = zs[t];
+        for (int c = 1; c < C; ++c) m = fmaxf(m, zs[c * 17 + t]);
+      }
+      float e[16], sum = 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        e[c] = c < C ? __expf(zs[c * 17 + t] - m) : 0.f;
+        sum += e[c];
+      }
+      const float inv = 1.f / sum, sc = (float)h.scale;
+      float lp = 0.f;
+      const __amdgpu_buffer_rsrc_t rd = make_rsrc(h.D);
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const float y = e[c] * inv;
+        if (c == lab) lp = -__logf(y);
+        const float d = (ok && c < C) ? (y - (c == lab ? 1.f : 0.f)) * sc : 0.f;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, d), rd,
+                                              (ok && c < C) ? (c * h.ldd + col) * 4 : kOOB, 0, kSc1);
+      }
+      ls[t] = lp;
+    }
+    __syncthreads();
+    if (t == 0 && h.loss_partial) {  // the column head's layout: one partial per 16 columns
+      float s = 0.f;
+      for (int k = 0; k < 16; ++k) s += ls[k];
+      h.loss_partial[u0 / 16] = s;
+    }
+  }
+  // ---- hand-off 2: D of the reduced columns is published; wait for all tm row tiles' D
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (also after a timeout)
+    sflag[1] = bad1 ? 1 : rega_ag_wait(cnt, base + 2ull * (unsigned)tm, g.err);
+  }
+  __syncthreads();
+  if (sflag[1]) return;  // workgroup-uniform
+  {
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(h.D);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 512 * q, c = e >> 7, j = e & 127, col = n0 + j;
+      Ds[c * kAgLd + j] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rd, (c < C && col < n) ? (c * h.ldd + col) * 4 : kOOB, 0, kSc1));
+    }
+  }
+  // this wave's a1 rows, row-major, for the dW2 partial's B operand
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ts[(4 * fg + j) * kAgLd + 16 * nb + fr] = a1v[nb][j];
+  __syncthreads();
+  if (h.dw2part) {
+    // P[c][row rw + fr] = sum over the tile's 128 columns of D[c][col] a1[row][col] (head_wide_kernel's
+    // chain over 128 columns instead of 32): A = D, B = the row-major a1 rows
+    f32x4 pw = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 32; ++s)
+      pw = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[fr * kAgLd + 4 * s + fg], ts[fr * kAgLd + 4 * s + fg], pw, 0, 0, 0);
+    const int hh = rw + fr;
+    const __amdgpu_buffer_rsrc_t rp = make_rsrc(h.dw2part);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      st_f32(rp, (4 * fg + r < C && hh < H) ? ((ct * 16 + 4 * fg + r) * H + hh) * 4 : kOOB, pw[r]);
+  }
+  const __amdgpu_buffer_rsrc_t rdz = make_rsrc(h.dZ1), rpl = make_rsrc(h.dZ1_planes);
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb) {
+    f32x4 r = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      r = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i], Ds[(4 * fg + i) * kAgLd + 16 * nb + fr], r, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = a1v[nb][j];
+      float dz = r[j] * x * (1.f - x);
+      const int row = rw + 4 * fg + j, col = n0 + 16 * nb + fr;
+      const bool ok = row < H && col < n;
+      if (h.dZ1) st_f32(rdz, ok ? (row * h.ldz + col) * 4 : kOOB, dz);
+      if (h.dZ1_planes)
+        for (int p = 0; p < h.npz; ++p) {
+          const bf16 q = __float2bfloat16(dz);
+          st_bf16(rpl, ok ? ((p * H + row) * h.ldz + col) * 2 : kOOB, q);
+          dz -= __bfloat162float(q);
+        }
+    }
+  }
+}
+
 // a1 = sigmoid(W1 X + b1) on the A-in-registers engine (rega_gemm.h): W1 read as fp32 and split into the
 // exact bf16 planes in registers (AT = float), or the bf16 plane 0 (AT = bf16, split1); z2 partials of
 // this 128-row tile as in fwd1_glds_kernel
-template <typename AT, int WC, int NKS>
-__global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn) {
+template <typename AT, int WC, int NKS, bool AG = false>
+__global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn, RegaAgArgs ag = {}) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   using G = RegaGeom<128, WC>;
   constexpr int MB = G::MB, NB = G::NB, WR = G::WR, BM = G::BM;
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (id / tn) * BM, n0 = (id % tn) * 128;
+  int m0, n0;
+  if (AG && ag.xcd_grouped) {
+    // XCD-grouped grid (hardware XCD = blockIdx % 8): the tm row tiles of a column tile share one XCD, so
+    // both hand-offs stay inside one L2 (the form fwd1_head_ag_kernel runs) -- but every XCD then reads all
+    // of W1; padding workgroups leave
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int ct = xcd + 8 * (slot / ag.tm), rt = slot % ag.tm;
+    if (ct >= tn) return;
+    m0 = rt * BM;
+    n0 = ct * 128;
+  } else {
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    m0 = (id / tn) * BM;
+    n0 = (id % tn) * 128;
+  }
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave / WC, wc = wave % WC, fr = lane & 15, fg = lane >> 4;
   const int rw = m0 + 16 * MB * wr, cw = n0 + 16 * NB * wc;  // this wave's first row / column
@@ -857,7 +1073,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn)
         const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
         const float sv = sigm(acc[mb][nb][i] * a.xscale + bb[mb][i]);
         acc[mb][nb][i] = sv;
-        st_f32(ra1, (row < H && col < n) ? (row * a.ld + col) * 4 : kOOB, sv);
+        if (!AG || ag.store_a1) st_f32(ra1, (row < H && col < n) ? (row * a.ld + col) * 4 : kOOB, sv);
       }
   if (!z2) return;
   // z2 partials on the f32 MFMA: step i of block mb takes B[k = fg][n = fr] = a1(row rw + 16 mb + 4 fg + i,
@@ -888,8 +1104,21 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn)
   const int tile = m0 / BM;
   const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)  // (classes past C are zero: not stored, the head does not read them)
-    st_f32(rz, (col < n && 4 * fg + i < C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, sz[i]);
+  for (int i = 0; i < 4; ++i) {  // (classes past C are zero: not stored, the head does not read them)
+    // (the element is copied to a scalar first: hipcc (ROCm 7.2) lowered __builtin_bit_cast of the vector
+    // element sz[i] to element 0 for every i -- all four z2 rows stored the same value)
+    const float zv = sz[i];
+    __builtin_amdgcn_raw_buffer_store_b32(
+        __builtin_bit_cast(unsigned, zv), rz,
+        (col < n && 4 * fg + i < C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, 0, AG ? kSc1 : 0);
+  }
+  if constexpr (AG) {
+    static_assert(MB == 1 && NB == 8, "all-gather head: 8 row waves of 16 rows x 128 columns");
+    f32x4 a1v[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) a1v[nb] = acc[0][nb];
+    rega_head_ag(a, ag, a1v, lds_dyn, m0, n0, rw, ag.tm, n0 / 128);
+  }
 }
 
 // dW1 = dZ1 XT on the A-in-registers engine: dZ1 read as fp32 (AT = float; the head writes it instead of
@@ -1011,6 +1240,15 @@ void launch_fwd1_rega_k(const SplitStepArgs& a, hipStream_t s) {
   constexpr int L = std::max(ra::lds_bytes<128>(), 8 * 8 * 64 * 16);  // (z2 reduction scratch)
   set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS>>(L);
   fwd1_rega_kernel<AT, kRegaWC, NKS><<<cdiv(a.H, 128) * cdiv(a.n, 128), 512, L, s>>>(a, cdiv(a.n, 128));
+}
+
+// the fused all-gather head: > 80 KB of LDS keeps it at one workgroup per CU (the hand-off's measured form)
+template <typename AT, int NKS>
+void launch_fwd1_rega_ag_k(const SplitStepArgs& a, const RegaAgArgs& g, hipStream_t s) {
+  constexpr int L = std::max({ra::lds_bytes<128>(), 8 * 8 * 64 * 16, kRegaAgLdsBytes, 84 * 1024});
+  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true>>(L);
+  const int tn = cdiv(a.n, 128), grid = g.xcd_grouped ? 8 * g.tm * cdiv(tn, 8) : g.tm * tn;
+  fwd1_rega_kernel<AT, kRegaWC, NKS, true><<<grid, 512, L, s>>>(a, tn, g);
 }
 
 // K = P = 784 (MNIST) is 25 stages of 32: the fully unrolled K loop; anything else the runtime loop
@@ -1185,6 +1423,52 @@ int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a) {
   if (!a.z2part || a.C > 16 || a.n <= 0 || !(glds_fwd_ok(a) || big_fwd_ok(a))) return 0;
   const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
   return t128 >= 192 ? cdiv(a.H, 128) : cdiv(a.H, 64);  // must match launch_fwd1_big_nt's tile choice
+}
+
+namespace {
+int device_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) HIP_CHECK(hipDeviceGetAttribute(&cached[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  return cached[dev];
+}
+}  // namespace
+
+bool mlp_fwd1_rega_ag_ok(const SplitStepArgs& a, const HeadArgs& h) {
+  const int tm = cdiv(a.H, 128), tn = cdiv(a.n, 128);
+  return a.n > 0 && rega_fwd_ok(a) && a.z2part != nullptr && h.mode == HEAD_TRAIN && a.C >= 1 && a.C <= 16 &&
+         h.C == a.C && h.H == a.H && h.n == a.n && h.W2 == a.W2 && tm >= 8 && tm * cdiv(tn, 8) <= device_cu_count() / 8 && tm * tn <= device_cu_count() &&
+         h.dZ1_bf16 == nullptr && (h.dZ1 || h.dZ1_planes) && h.D && h.labels && h.b2 && h.dw2part &&
+         (int64_t)a.H * h.ldz * 4 < (int64_t)kOOB && (int64_t)h.npz * a.H * h.ldz * 2 < (int64_t)kOOB &&
+         (int64_t)16 * tn * a.H * 4 < (int64_t)kOOB && (int64_t)16 * h.ldd * 4 < (int64_t)kOOB &&
+         (int64_t)tm * 16 * a.ld * 4 < (int64_t)kOOB;
+}
+
+void mlp_fwd1_rega_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long long* counters, int max_tiles,
+                      int* err, int store_a1, int xcd_grouped, hipStream_t s) {
+  CME_REQUIRE(mlp_fwd1_rega_ag_ok(a, h), "fwd1_rega_ag: wide split path (128 x 128 A-in-registers tiles, "
+                                         ">= 8 row tiles, <= 32 per XCD), train-mode head, C <= 16");
+  CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
+              "fwd1_rega_ag: operand too large for 32-bit buffer offsets");
+  CME_REQUIRE(counters && err && cdiv(a.n, 128) <= max_tiles, "fwd1_rega_ag: counter array too small");
+  RegaAgArgs g;
+  g.h = h;
+  g.counters = counters;
+  g.err = err;
+  g.store_a1 = store_a1;
+  g.tm = cdiv(a.H, 128);
+  g.xcd_grouped = xcd_grouped;
+  const bool k25 = cdiv(a.P, ra::kBK) == 25;
+  if (a.npw == 3) {
+    if (k25) launch_fwd1_rega_ag_k<float, 25>(a, g, s);
+    else launch_fwd1_rega_ag_k<float, 0>(a, g, s);
+  } else {
+    if (k25) launch_fwd1_rega_ag_k<bf16, 25>(a, g, s);
+    else launch_fwd1_rega_ag_k<bf16, 0>(a, g, s);
+  }
+  CME_LAUNCH_CHECK(s);
 }
 
 void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {

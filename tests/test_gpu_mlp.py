@@ -531,3 +531,53 @@ def test_split3_multi_epoch_drift_vs_fp64_oracle():
     for i in range(2):
         assert np.abs(par.W[i] - seq.W[i]).max() / np.abs(seq.W[i]).max() < 5e-6
         assert np.abs(par.b[i] - seq.b[i]).max() / np.abs(seq.b[i]).max() < 5e-6
+
+
+@pytest.mark.parametrize("dt,path", [("f32", "split3"), ("bf16", "split1")])
+@pytest.mark.parametrize("H,n", [(4096, 800), (4096, 777), (3072, 1024)])
+def test_wide_fused_allgather_head_matches_head_kernel(dt, path, H, n):
+    """Wide layers: the head fused into the A-in-registers forward launch (mlp_fwd1_rega_ag: two hand-offs
+    per 128-column tile, row tiles 0-7 each reduce 16 columns' z2 partials) against the forward launch +
+    head_wide_kernel.  Same arithmetic in the same order: a1, D, dZ1 (fp32 / planes), the loss and every
+    gradient but dW2 BITWISE; dW2 sums 128-column partials instead of 32-column ones (fp32 rounding).
+    Then SGD steps agree to rounding, the column-tile counters advance by 2 tm per launch, no wait timed
+    out, and store_a1=False leaves a1 untouched with identical results."""
+    x, y = synthetic_mnist(2 * n + 64, seed=13)
+    nn = NeuralNetwork([784, H, 10])
+    tm, tn = (H + 127) // 128, (n + 127) // 128
+    outs = []
+    for mode in ("ag", "head", "ag_noa1", "agx"):
+        e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", path=path)
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        e.set_fh_allgather(mode != "head")
+        e._hip_step().ag_xcd_grouped = int(mode == "agx")  # each column tile's hand-offs inside one XCD
+        if mode == "ag_noa1":
+            e.set_store_a1(False)
+            e.a1.fill_(7.0)
+        e.run(64, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
+        torch.cuda.synchronize()
+        first = [e.a1[:, :n].clone(), e.D[:, :n].clone(), e.dZ1[:, :n].clone(), e.dZ1p[:, :, :n].clone(),
+                 e.gW1.clone(), e.gb1.clone(), e.gb2.clone(), e.gW2.clone(), e.loss_sum()]
+        for off in (0, n, 32):
+            e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+        torch.cuda.synchronize()
+        outs.append((first, e.params.clone()))
+        if mode != "head":
+            assert e.ag_counters is not None and not e.kernel_error()
+            assert e.ag_counters.view(-1, 32)[:tn, 0].tolist() == [2 * tm * 4] * tn
+        if mode == "ag_noa1":
+            assert bool((e.a1 == 7.0).all())
+    (fa, pa), (fh, ph), (fn, pn), (fx, px) = outs
+    names = ("a1", "D", "dZ1", "dZ1p", "gW1", "gb1", "gb2")
+    bad = [(nm, _rel(fa[i].float(), fh[i].float())) for i, nm in enumerate(names) if not torch.equal(fa[i], fh[i])]
+    assert not bad, bad
+    assert _rel(fa[7], fh[7]) < 1e-5  # gW2
+    assert fa[8] == fh[8]  # loss
+    assert _rel(pa, ph) < (1e-5 if path == "split3" else 1e-3)
+    for i in range(1, 9):
+        assert torch.equal(fn[i], fa[i]) if torch.is_tensor(fn[i]) else fn[i] == fa[i]
+    assert torch.equal(pn, pa)
+    for i in range(8):
+        assert torch.equal(fx[i], fa[i]), i
+    assert torch.equal(px, pa)
