@@ -170,8 +170,8 @@ class MlpEngine:
             self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)  # one 256-B line each
             self.ag_slabs = torch.zeros(tiles * 8 * 16 * 32, dtype=torch.float32, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
-        elif self.backend == "hip" and self.np and H >= 1024 and C <= 16 and self.dw2buf is not None:
-            # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_rega_ag) uses one
+        elif self.backend == "hip" and self.np and H >= 512 and C <= 16 and self.dw2buf is not None:
+            # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_wide_ag) uses one
             # monotonic counter per column tile and the timed-out-wait word
             tiles = (ld + 31) // 32
             self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)

@@ -59,10 +59,11 @@ struct MlpStep {
   uintptr_t ag_counters = 0, ag_slabs = 0, ag_err = 0;
   int fh_allgather = 0;
   // wide split layers: the all-gather head fused into the forward launch (fh_allgather, ag_counters, ag_err;
-  // mlp_fwd1_rega_ag) leaves dW2 partials per 128 columns (32 from head_wide_kernel): what run_wgrad sums
+  // mlp_fwd1_wide_ag) leaves dW2 partials per 128 / 64 columns (32 from head_wide_kernel): what run_wgrad sums
   int dw2_cols_last = 32;
   int store_a1 = 1;  // the fused wide head: 0 skips the a1 store (nothing in the step reads it)
   int ag_xcd_grouped = 0;  // the fused wide head's grid: 1 = each column tile on one XCD (RegaAgArgs)
+  int ag_tiles64 = 0;      // 1: the fused wide head also on the 64 x 64 tiling (measured no faster)
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
   void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2) {
@@ -177,10 +178,10 @@ struct MlpStep {
               a.dw2part = h.dw2part;
             }
             if (fh_allgather && ag_counters && ag_err && h.dw2part && !(parts & 12) &&
-                cme::mlp_fwd1_rega_ag_ok(f, h)) {  // one launch: forward GEMM + the all-gather head
-              cme::mlp_fwd1_rega_ag(f, h, P_<unsigned long long>(ag_counters), fh_tiles, P_<int>(ag_err),
-                                    store_a1, ag_xcd_grouped, S(stream));
-              a.dw2_cols = 128;
+                cme::mlp_fwd1_wide_ag_ok(f, h, ag_tiles64)) {  // one launch: forward GEMM + the all-gather head
+              a.dw2_cols = cme::mlp_fwd1_wide_ag(f, h, P_<unsigned long long>(ag_counters), fh_tiles,
+                                                 P_<int>(ag_err), store_a1, ag_xcd_grouped, ag_tiles64,
+                                                 S(stream));
             } else {
               if (!(parts & 8)) cme::mlp_split_fwd1(f, S(stream));
               if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
@@ -418,6 +419,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
       .def_readwrite("store_a1", &MlpStep::store_a1)
       .def_readwrite("ag_xcd_grouped", &MlpStep::ag_xcd_grouped)
+      .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
       .def_readwrite("a_fp32", &MlpStep::a_fp32)
       .def("w1_planes_read",
            [](const MlpStep& st) {  // a forward kernel of this step reads the W1 planes (else: not refreshed)

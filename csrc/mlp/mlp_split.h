@@ -108,14 +108,16 @@ int mlp_split_fused_tiles(int P, int H, int cap);
 void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);
 // tiled forward only: a1 = sigmoid(W1 X + b1) (pair with mlp_head for the 3-kernel step)
 void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s);
-// wide layers: the forward GEMM with the head fused in (all-gather form, fwd1_rega_kernel<..., AG>): one
-// launch leaves a1 (store_a1), D, the loss partials, dZ1 (fp32 and / or planes) and the dW2 partials per
-// 128-column tile (h.dw2part; the weight-gradient launch then needs a.dw2_cols = 128).  Every workgroup must
-// be resident at once (off when processes share a GPU); a timed-out wait sets *err.
+// wide layers: the forward GEMM with the head fused in (all-gather form; fwd1_rega_kernel<..., AG> on 128 x 128
+// tiles, fwd1_glds_kernel<64, 64, ..., AG> on 64 x 64): one launch leaves a1 (store_a1), D, the loss partials,
+// dZ1 (fp32 and / or planes) and the dW2 partials per column tile (h.dw2part).  Returns the tile width: the
+// weight-gradient launch then needs a.dw2_cols = it.  Every workgroup must be resident at once (off when
+// processes share a GPU); a timed-out wait sets *err.
 struct HeadArgs;
-bool mlp_fwd1_rega_ag_ok(const SplitStepArgs& a, const HeadArgs& h);
-void mlp_fwd1_rega_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long long* counters, int max_tiles,
-                      int* err, int store_a1, int xcd_grouped, hipStream_t s);
+// allow64: also the 64 x 64 tiling (measured no faster; tests)
+bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64);
+int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long long* counters, int max_tiles,
+                     int* err, int store_a1, int xcd_grouped, int allow64, hipStream_t s);
 void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s);
 int mlp_split_fwdhead_blocks(int n);
 

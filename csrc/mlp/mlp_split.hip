@@ -673,152 +673,6 @@ __device__ __forceinline__ void st_bf16(__amdgpu_buffer_rsrc_t r, int off, bf16 
   __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, v), r, off, 0, 0);
 }
 
-// a1 = sigmoid(W1 X + b1) and (z2p != nullptr) the head's z2 partials of this tile's rows:
-// z2p[row tile][class][col] = sum over the tile rows h of W2[class][h] a1[h][col]
-template <int BM, int BN, int NPW>
-__global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn) {
-  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
-  using G = GldsGeom<BM, BN>;
-  constexpr int MB = G::MB, NB = G::NB;
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (id / tn) * BM, n0 = (id % tn) * BN;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
-  const int rw = m0 + wr * G::WM, cw = n0 + wc * G::WN;  // this wave's first row / column
-  const int H = a.H, n = a.n, C = a.C;
-  const bool z2 = a.z2part != nullptr;
-  // epilogue operands, issued before the K loop: b1 of this lane's rows, W2[class fr][those rows]
-  const __amdgpu_buffer_rsrc_t rb1 = make_rsrc(a.b1), rw2 = make_rsrc(a.W2);
-  float bb[MB][4], w2[MB][4];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int h = rw + 16 * mb + 4 * fg + i;
-      bb[mb][i] = buf_load1<float>(rb1, h < H ? h * 4 : kOOB);
-      w2[mb][i] = buf_load1<float>(rw2, (z2 && fr < C && h < H) ? (fr * H + h) * 4 : kOOB);
-    }
-  f32x4 acc[MB][NB];
-  glds_gemm_mainloop<BM, BN, NPW>(static_cast<const bf16*>(a.W1p), a.P, H * a.P * (int)sizeof(bf16),
-                                  static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
-  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
-        const float sv = sigm(acc[mb][nb][i] * a.xscale + bb[mb][i]);
-        acc[mb][nb][i] = sv;
-        st_f32(ra1, (row < H && col < n) ? (row * a.ld + col) * 4 : kOOB, sv);
-      }
-  if (!z2) return;
-  // z2 partials on the f32 MFMA: step i of block mb takes B[k = fg][n = fr] = a1(row rw + 16 mb + 4 fg + i,
-  // col fr) -- exactly accumulator element i -- and A[m = fr][k = fg] = W2[class fr][that row]; the 4 row
-  // waves are summed through LDS (all K-loop reads of lds_dyn are done after the barrier)
-  f32x4 z[NB];
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) z[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-        z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2[mb][i], acc[mb][nb][i], z[nb], 0, 0, 0);
-  __syncthreads();
-  f32x4* red = reinterpret_cast<f32x4*>(lds_dyn);  // [4][2][NB][64]
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) red[((wr * 2 + wc) * NB + nb) * 64 + lane] = z[nb];
-  __syncthreads();
-  if (wr != 0) return;
-  const int tile = m0 / BM;
-  const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) {
-    f32x4 sz = red[(wc * NB + nb) * 64 + lane];
-#pragma unroll
-    for (int r = 1; r < G::WRN; ++r) sz += red[((r * 2 + wc) * NB + nb) * 64 + lane];
-    const int col = cw + 16 * nb + fr;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)  // (classes past C are zero: not stored, the head does not read them)
-      st_f32(rz, (col < n && 4 * fg + i < a.C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, sz[i]);
-  }
-}
-
-// dW1 = dZ1 XT (+ the all-ones feature column P = db1) with the fused reg + SGD + bf16-plane refresh (sgd)
-// or the pre-scaled gradient (sgd == 0); the dW2 / db2 role workgroups ride in the same launch
-template <int BM, int BN, int NPZ>
-__global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
-  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
-  if ((int)blockIdx.x >= tbig) {  // the dW2 / db2 roles riding in this launch
-    wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
-                reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)));
-    return;
-  }
-  using G = GldsGeom<BM, BN>;
-  constexpr int MB = G::MB, NB = G::NB;
-  const int id = xcd_remap(blockIdx.x, tbig);
-  const int m0 = a.w1_row0 + (id / tn) * BM, n0 = (id % tn) * BN;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
-  const int rw = m0 + wr * G::WM, cw = n0 + wc * G::WN;
-  const int M = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows, P = a.P;
-  const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
-  // the weights this lane updates (and b1 of its rows, for the all-ones column), before the K loop
-  const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
-  float w[MB][NB][4], bb[MB][4];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = rw + 16 * mb + 4 * fg + i;
-      bb[mb][i] = buf_load1<float>(rb1, row < M ? row * 4 : kOOB);
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        const int col = cw + 16 * nb + fr;
-        w[mb][nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
-      }
-    }
-  f32x4 acc[MB][NB];
-  glds_gemm_mainloop<BM, BN, NPZ>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
-                                  static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0, n0, lds_dyn,
-                                  acc);
-  const size_t plane = (size_t)a.H * P;
-  const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
-        const float v = acc[mb][nb][i];
-        const bool in = row < M && col < P;
-        const int idx = row * P + col;
-        const float wv = w[mb][nb][i];
-        const float g = v * xs + reg * wv;
-        if (a.sgd) {
-          const float nw = wv - lr * g;
-          st_f32(rW, in ? idx * 4 : kOOB, nw);
-          float r = nw;
-#pragma unroll
-          for (int p = 0; p < NPZ; ++p) {  // the W1 planes have the dZ1 planes' count (npw == npz)
-            const bf16 hb = __float2bfloat16(r);
-            st_bf16(rp, in ? (int)((p * plane + idx) * 2) : kOOB, hb);
-            r -= __bfloat162float(hb);
-          }
-        } else {
-          st_f32(rg, in ? idx * 4 : kOOB, g);
-        }
-        if (a.bias_col && col == P && row < M) {  // all-ones feature: db1 (no input scale, no regulariser)
-          if (a.sgd) a.b1[row] = bb[mb][i] - lr * v;
-          else a.gb1[row] = v;
-        }
-      }
-}
-
 // ---- wide layers: the head fused into the A-in-registers forward launch (all-gather form, H >= 1024).
 // Every 128 x 128 a1 tile is still in its workgroup's accumulators when the forward GEMM ends, so instead of
 // storing z2 partials for head_wide_kernel to reduce (and re-reading all of a1 there), the tm row-tile
@@ -848,8 +702,12 @@ struct RegaAgArgs {
 };
 constexpr int kRegaAgCounterStride = 32;  // uint64 words: one 256-byte line per column-tile counter
 constexpr uint32_t kRegaAgSpinLimit = 1u << 22;
-constexpr int kAgLd = 132;  // LDS row pitch (floats) of the D tile and the per-wave a1 tiles: conflict-free
-constexpr int kRegaAgLdsBytes = (16 * kAgLd + 8 * 16 * kAgLd + 16 * 17 + 16 + 4) * 4;
+// LDS of the fused head for a BM x BN tile: the D tile [16][BN + 4], the a1 tile [BM][BN + 4] (row pitch BN + 4:
+// conflict-free MFMA-layout reads), z2 [16][17], loss [16], 2 flags
+template <int BM, int BN>
+constexpr int wide_ag_lds_bytes() {
+  return (16 * (BN + 4) + BM * (BN + 4) + 16 * 17 + 16 + 4) * 4;
+}
 
 // one lane: 1 when the counter did not reach `target` within the spin bound (and *err is set)
 __device__ __forceinline__ int rega_ag_wait(unsigned long long* cnt, unsigned long long target, int* err) {
@@ -871,15 +729,19 @@ __device__ __forceinline__ void ag_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// a1v[nb][j] = a1(row rw + 4 fg + j, column n0 + 16 nb + fr) of this wave; tm row tiles; ct = column tile
-__device__ __forceinline__ void rega_head_ag(const SplitStepArgs& a, const RegaAgArgs& g, const f32x4 (&a1v)[8],
-                                             char* lds, int m0, int n0, int rw, int tm, int ct) {
+// BM x BN tile at (m0, n0); this wave holds a1v[nb][j] = a1(row rw + 4 fg + j, column cw + 16 nb + fr) (16 rows x
+// 16 NB columns); tm row tiles; ct = column tile.  BN / 16 row tiles reduce 16 columns each (tm >= BN / 16).
+template <int BM, int BN, int NB>
+__device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaAgArgs& g, const f32x4 (&a1v)[NB],
+                                             char* lds, int m0, int n0, int rw, int cw, int tm, int ct) {
+  constexpr int LD = BN + 4, NU = BN / 16, NDS = 16 * BN / 512;
+  static_assert(NDS * 512 == 16 * BN && BM % 16 == 0 && BM / 16 <= 8, "tile shape");
   const HeadArgs& h = g.h;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, fr = lane & 15, fg = lane >> 4;
   const int H = a.H, n = a.n, C = a.C, rt = m0 / 128;
-  float* Ds = reinterpret_cast<float*>(lds);    // [16][kAgLd] the column tile's D
-  float* ts = Ds + 16 * kAgLd + wave * 16 * kAgLd;  // [16][kAgLd] this wave's a1 rows
-  float* zs = Ds + 16 * kAgLd + 8 * 16 * kAgLd;     // [16][17] z2 (+ b2) of the reduced 16 columns
+  float* Ds = reinterpret_cast<float*>(lds);  // [16][LD] the column tile's D
+  float* ts = Ds + 16 * LD;                     // [BM][LD] the a1 tile
+  float* zs = ts + BM * LD;                     // [16][17] z2 (+ b2) of the reduced 16 columns
   float* ls = zs + 16 * 17;                         // [16] loss of those columns
   int* sflag = reinterpret_cast<int*>(ls + 16);
   // independent loads first: the W2^T operand of dZ1 (class 4 fg + i, row rw + fr), the reducer's labels, b2
@@ -887,8 +749,8 @@ __device__ __forceinline__ void rega_head_ag(const SplitStepArgs& a, const RegaA
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     wv[i] = buf_load1<float>(make_rsrc(a.W2), (4 * fg + i < C && rw + fr < H) ? ((4 * fg + i) * H + rw + fr) * 4 : kOOB);
-  const int u0 = n0 + 16 * rt;  // the 16 columns row tile rt < 8 reduces
-  const bool red = rt < 8 && u0 < n;
+  const int u0 = n0 + 16 * rt;  // the 16 columns row tile rt < NU reduces
+  const bool red = rt < NU && u0 < n;
   const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(
       make_rsrc(h.labels), (red && t < 16 && u0 + t < n) ? (u0 + t) * 4 : kOOB, 0, 0);
   const int zc = t >> 4, zcol = u0 + (t & 15);
@@ -972,26 +834,27 @@ __device__ __forceinline__ void rega_head_ag(const SplitStepArgs& a, const RegaA
   {
     const __amdgpu_buffer_rsrc_t rd = make_rsrc(h.D);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = t + 512 * q, c = e >> 7, j = e & 127, col = n0 + j;
-      Ds[c * kAgLd + j] = __builtin_bit_cast(
+    for (int q = 0; q < NDS; ++q) {
+      const int e = t + 512 * q, c = e / BN, j = e % BN, col = n0 + j;
+      Ds[c * LD + j] = __builtin_bit_cast(
           float, __builtin_amdgcn_raw_buffer_load_b32(rd, (c < C && col < n) ? (c * h.ldd + col) * 4 : kOOB, 0, kSc1));
     }
   }
-  // this wave's a1 rows, row-major, for the dW2 partial's B operand
+  // this wave's a1 block into the row-major a1 tile, for the dW2 partial's B operand
 #pragma unroll
-  for (int nb = 0; nb < 8; ++nb)
+  for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ts[(4 * fg + j) * kAgLd + 16 * nb + fr] = a1v[nb][j];
+    for (int j = 0; j < 4; ++j) ts[(rw - m0 + 4 * fg + j) * LD + cw - n0 + 16 * nb + fr] = a1v[nb][j];
   __syncthreads();
-  if (h.dw2part) {
-    // P[c][row rw + fr] = sum over the tile's 128 columns of D[c][col] a1[row][col] (head_wide_kernel's
-    // chain over 128 columns instead of 32): A = D, B = the row-major a1 rows
+  if (h.dw2part && wave < BM / 16) {
+    // P[c][row m0 + 16 wave + fr] = sum over the tile's BN columns of D[c][col] a1[row][col] (head_wide_kernel's
+    // chain over BN columns instead of 32): A = D, B = the row-major a1 rows
+    const float* tr = ts + 16 * wave * LD;
     f32x4 pw = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 32; ++s)
-      pw = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[fr * kAgLd + 4 * s + fg], ts[fr * kAgLd + 4 * s + fg], pw, 0, 0, 0);
-    const int hh = rw + fr;
+    for (int s = 0; s < BN / 4; ++s)
+      pw = __builtin_amdgcn_mfma_f32_16x16x4f32(Ds[fr * LD + 4 * s + fg], tr[fr * LD + 4 * s + fg], pw, 0, 0, 0);
+    const int hh = m0 + 16 * wave + fr;
     const __amdgpu_buffer_rsrc_t rp = make_rsrc(h.dw2part);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -999,16 +862,16 @@ __device__ __forceinline__ void rega_head_ag(const SplitStepArgs& a, const RegaA
   }
   const __amdgpu_buffer_rsrc_t rdz = make_rsrc(h.dZ1), rpl = make_rsrc(h.dZ1_planes);
 #pragma unroll
-  for (int nb = 0; nb < 8; ++nb) {
+  for (int nb = 0; nb < NB; ++nb) {
     f32x4 r = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      r = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i], Ds[(4 * fg + i) * kAgLd + 16 * nb + fr], r, 0, 0, 0);
+      r = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i], Ds[(4 * fg + i) * LD + cw - n0 + 16 * nb + fr], r, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float x = a1v[nb][j];
       float dz = r[j] * x * (1.f - x);
-      const int row = rw + 4 * fg + j, col = n0 + 16 * nb + fr;
+      const int row = rw + 4 * fg + j, col = cw + 16 * nb + fr;
       const bool ok = row < H && col < n;
       if (h.dZ1) st_f32(rdz, ok ? (row * h.ldz + col) * 4 : kOOB, dz);
       if (h.dZ1_planes)
@@ -1019,6 +882,164 @@ __device__ __forceinline__ void rega_head_ag(const SplitStepArgs& a, const RegaA
         }
     }
   }
+}
+
+// a1 = sigmoid(W1 X + b1) and (z2p != nullptr) the head's z2 partials of this tile's rows:
+// z2p[row tile][class][col] = sum over the tile rows h of W2[class][h] a1[h][col]
+template <int BM, int BN, int NPW, bool AG = false>
+__global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn, RegaAgArgs ag = {}) {
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  using G = GldsGeom<BM, BN>;
+  constexpr int MB = G::MB, NB = G::NB;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (id / tn) * BM, n0 = (id % tn) * BN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
+  const int rw = m0 + wr * G::WM, cw = n0 + wc * G::WN;  // this wave's first row / column
+  const int H = a.H, n = a.n, C = a.C;
+  const bool z2 = a.z2part != nullptr;
+  // epilogue operands, issued before the K loop: b1 of this lane's rows, W2[class fr][those rows]
+  const __amdgpu_buffer_rsrc_t rb1 = make_rsrc(a.b1), rw2 = make_rsrc(a.W2);
+  float bb[MB][4], w2[MB][4];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = rw + 16 * mb + 4 * fg + i;
+      bb[mb][i] = buf_load1<float>(rb1, h < H ? h * 4 : kOOB);
+      w2[mb][i] = buf_load1<float>(rw2, (z2 && fr < C && h < H) ? (fr * H + h) * 4 : kOOB);
+    }
+  f32x4 acc[MB][NB];
+  glds_gemm_mainloop<BM, BN, NPW>(static_cast<const bf16*>(a.W1p), a.P, H * a.P * (int)sizeof(bf16),
+                                  static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
+  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
+        const float sv = sigm(acc[mb][nb][i] * a.xscale + bb[mb][i]);
+        acc[mb][nb][i] = sv;
+        if (!AG || ag.store_a1) st_f32(ra1, (row < H && col < n) ? (row * a.ld + col) * 4 : kOOB, sv);
+      }
+  if (!z2) return;
+  // z2 partials on the f32 MFMA: step i of block mb takes B[k = fg][n = fr] = a1(row rw + 16 mb + 4 fg + i,
+  // col fr) -- exactly accumulator element i -- and A[m = fr][k = fg] = W2[class fr][that row]; the 4 row
+  // waves are summed through LDS (all K-loop reads of lds_dyn are done after the barrier)
+  f32x4 z[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) z[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2[mb][i], acc[mb][nb][i], z[nb], 0, 0, 0);
+  __syncthreads();
+  f32x4* red = reinterpret_cast<f32x4*>(lds_dyn);  // [4][2][NB][64]
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) red[((wr * 2 + wc) * NB + nb) * 64 + lane] = z[nb];
+  __syncthreads();
+  if (wr == 0) {
+    const int tile = m0 / BM;
+    const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      f32x4 sz = red[(wc * NB + nb) * 64 + lane];
+#pragma unroll
+      for (int r = 1; r < G::WRN; ++r) sz += red[((r * 2 + wc) * NB + nb) * 64 + lane];
+      const int col = cw + 16 * nb + fr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // (classes past C are zero: not stored, the head does not read them)
+        const float zv = sz[i];      // (a scalar copy: see fwd1_rega_kernel)
+        __builtin_amdgcn_raw_buffer_store_b32(
+            __builtin_bit_cast(unsigned, zv), rz,
+            (col < n && 4 * fg + i < a.C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, 0, AG ? kSc1 : 0);
+      }
+    }
+  }
+  if constexpr (AG) {
+    static_assert(MB == 1 && BM == 64 && BN == 64, "fused head: the 64 x 64 tiling (4 x 2 waves of 16 x 32)");
+    f32x4 a1v[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) a1v[nb] = acc[0][nb];
+    wide_head_ag<BM, BN, NB>(a, ag, a1v, lds_dyn, m0, n0, rw, cw, ag.tm, n0 / BN);
+  }
+}
+
+// dW1 = dZ1 XT (+ the all-ones feature column P = db1) with the fused reg + SGD + bf16-plane refresh (sgd)
+// or the pre-scaled gradient (sgd == 0); the dW2 / db2 role workgroups ride in the same launch
+template <int BM, int BN, int NPZ>
+__global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
+  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
+  if ((int)blockIdx.x >= tbig) {  // the dW2 / db2 roles riding in this launch
+    wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
+                reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)));
+    return;
+  }
+  using G = GldsGeom<BM, BN>;
+  constexpr int MB = G::MB, NB = G::NB;
+  const int id = xcd_remap(blockIdx.x, tbig);
+  const int m0 = a.w1_row0 + (id / tn) * BM, n0 = (id % tn) * BN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
+  const int rw = m0 + wr * G::WM, cw = n0 + wc * G::WN;
+  const int M = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows, P = a.P;
+  const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
+  // the weights this lane updates (and b1 of its rows, for the all-ones column), before the K loop
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
+  float w[MB][NB][4], bb[MB][4];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rw + 16 * mb + 4 * fg + i;
+      bb[mb][i] = buf_load1<float>(rb1, row < M ? row * 4 : kOOB);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int col = cw + 16 * nb + fr;
+        w[mb][nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
+      }
+    }
+  f32x4 acc[MB][NB];
+  glds_gemm_mainloop<BM, BN, NPZ>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
+                                  static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0, n0, lds_dyn,
+                                  acc);
+  const size_t plane = (size_t)a.H * P;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
+        const float v = acc[mb][nb][i];
+        const bool in = row < M && col < P;
+        const int idx = row * P + col;
+        const float wv = w[mb][nb][i];
+        const float g = v * xs + reg * wv;
+        if (a.sgd) {
+          const float nw = wv - lr * g;
+          st_f32(rW, in ? idx * 4 : kOOB, nw);
+          float r = nw;
+#pragma unroll
+          for (int p = 0; p < NPZ; ++p) {  // the W1 planes have the dZ1 planes' count (npw == npz)
+            const bf16 hb = __float2bfloat16(r);
+            st_bf16(rp, in ? (int)((p * plane + idx) * 2) : kOOB, hb);
+            r -= __bfloat162float(hb);
+          }
+        } else {
+          st_f32(rg, in ? idx * 4 : kOOB, g);
+        }
+        if (a.bias_col && col == P && row < M) {  // all-ones feature: db1 (no input scale, no regulariser)
+          if (a.sgd) a.b1[row] = bb[mb][i] - lr * v;
+          else a.gb1[row] = v;
+        }
+      }
 }
 
 // a1 = sigmoid(W1 X + b1) on the A-in-registers engine (rega_gemm.h): W1 read as fp32 and split into the
@@ -1117,7 +1138,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
     f32x4 a1v[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) a1v[nb] = acc[0][nb];
-    rega_head_ag(a, ag, a1v, lds_dyn, m0, n0, rw, ag.tm, n0 / 128);
+    wide_head_ag<128, 128, NB>(a, ag, a1v, lds_dyn, m0, n0, rw, cw, ag.tm, n0 / 128);
   }
 }
 
@@ -1245,7 +1266,7 @@ void launch_fwd1_rega_k(const SplitStepArgs& a, hipStream_t s) {
 // the fused all-gather head: > 80 KB of LDS keeps it at one workgroup per CU (the hand-off's measured form)
 template <typename AT, int NKS>
 void launch_fwd1_rega_ag_k(const SplitStepArgs& a, const RegaAgArgs& g, hipStream_t s) {
-  constexpr int L = std::max({ra::lds_bytes<128>(), 8 * 8 * 64 * 16, kRegaAgLdsBytes, 84 * 1024});
+  constexpr int L = std::max({ra::lds_bytes<128>(), 8 * 8 * 64 * 16, wide_ag_lds_bytes<128, 128>(), 84 * 1024});
   set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true>>(L);
   const int tn = cdiv(a.n, 128), grid = g.xcd_grouped ? 8 * g.tm * cdiv(tn, 8) : g.tm * tn;
   fwd1_rega_kernel<AT, kRegaWC, NKS, true><<<grid, 512, L, s>>>(a, tn, g);
@@ -1436,39 +1457,67 @@ int device_cu_count() {
 }
 }  // namespace
 
-bool mlp_fwd1_rega_ag_ok(const SplitStepArgs& a, const HeadArgs& h) {
-  const int tm = cdiv(a.H, 128), tn = cdiv(a.n, 128);
-  return a.n > 0 && rega_fwd_ok(a) && a.z2part != nullptr && h.mode == HEAD_TRAIN && a.C >= 1 && a.C <= 16 &&
-         h.C == a.C && h.H == a.H && h.n == a.n && h.W2 == a.W2 && tm >= 8 && tm * cdiv(tn, 8) <= device_cu_count() / 8 && tm * tn <= device_cu_count() &&
-         h.dZ1_bf16 == nullptr && (h.dZ1 || h.dZ1_planes) && h.D && h.labels && h.b2 && h.dw2part &&
+// the tile the fused head runs on: 128 (A-in-registers engine), 64 (the direct-to-LDS 64 x 64 tiling), 0 (none)
+// (64 x 64 measured no faster than forward + head_wide_kernel at 784-1024-10: 33.2 vs 32.9 us f32, 25.40 vs
+// 25.39 us bf16, profiles/wide_ag_ab_r2.jsonl -- taken only on request, MlpStep.ag_tiles64)
+static int wide_ag_bm(const SplitStepArgs& a, int allow64) {
+  if (rega_fwd_ok(a)) return 128;
+  if (allow64 && glds_fwd_ok(a) && cdiv(a.H, 128) * cdiv(a.n, 128) < 192) return 64;
+  return 0;
+}
+
+bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64) {
+  const int bm = wide_ag_bm(a, allow64);
+  if (bm == 0 || a.n <= 0) return false;
+  const int tm = cdiv(a.H, bm), tn = cdiv(a.n, bm);
+  return a.z2part != nullptr && h.mode == HEAD_TRAIN && a.C >= 1 && a.C <= 16 && h.C == a.C && h.H == a.H &&
+         h.n == a.n && h.W2 == a.W2 && tm >= bm / 16 && tm * tn <= device_cu_count() && h.dZ1_bf16 == nullptr &&
+         (h.dZ1 || h.dZ1_planes) && h.D && h.labels && h.b2 && h.dw2part &&
          (int64_t)a.H * h.ldz * 4 < (int64_t)kOOB && (int64_t)h.npz * a.H * h.ldz * 2 < (int64_t)kOOB &&
          (int64_t)16 * tn * a.H * 4 < (int64_t)kOOB && (int64_t)16 * h.ldd * 4 < (int64_t)kOOB &&
          (int64_t)tm * 16 * a.ld * 4 < (int64_t)kOOB;
 }
 
-void mlp_fwd1_rega_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long long* counters, int max_tiles,
-                      int* err, int store_a1, int xcd_grouped, hipStream_t s) {
-  CME_REQUIRE(mlp_fwd1_rega_ag_ok(a, h), "fwd1_rega_ag: wide split path (128 x 128 A-in-registers tiles, "
-                                         ">= 8 row tiles, <= 32 per XCD), train-mode head, C <= 16");
+template <int NP>
+void launch_fwd1_glds64_ag(const SplitStepArgs& a, const RegaAgArgs& g, hipStream_t s) {
+  constexpr int L = std::max({gl::lds_bytes<64, 64, NP>(), 4 * 2 * 2 * 64 * 16, wide_ag_lds_bytes<64, 64>(), 84 * 1024});
+  set_lds_limit<fwd1_glds_kernel<64, 64, NP, true>>(L);
+  const int tn = cdiv(a.n, 64);
+  fwd1_glds_kernel<64, 64, NP, true><<<g.tm * tn, 512, L, s>>>(a, tn, g);
+}
+
+int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long long* counters, int max_tiles,
+                     int* err, int store_a1, int xcd_grouped, int allow64, hipStream_t s) {
+  CME_REQUIRE(mlp_fwd1_wide_ag_ok(a, h, allow64), "fwd1_wide_ag: wide split path (128 x 128 A-in-registers or 64 x 64 "
+                                         "direct-to-LDS tiles, grid <= CU count), train-mode head, C <= 16");
   CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
-              "fwd1_rega_ag: operand too large for 32-bit buffer offsets");
-  CME_REQUIRE(counters && err && cdiv(a.n, 128) <= max_tiles, "fwd1_rega_ag: counter array too small");
+              "fwd1_wide_ag: operand too large for 32-bit buffer offsets");
+  const int bm = wide_ag_bm(a, allow64);
+  CME_REQUIRE(counters && err && cdiv(a.n, bm) <= max_tiles, "fwd1_wide_ag: counter array too small");
   RegaAgArgs g;
   g.h = h;
   g.counters = counters;
   g.err = err;
   g.store_a1 = store_a1;
-  g.tm = cdiv(a.H, 128);
-  g.xcd_grouped = xcd_grouped;
-  const bool k25 = cdiv(a.P, ra::kBK) == 25;
-  if (a.npw == 3) {
-    if (k25) launch_fwd1_rega_ag_k<float, 25>(a, g, s);
-    else launch_fwd1_rega_ag_k<float, 0>(a, g, s);
+  g.tm = cdiv(a.H, bm);
+  // the XCD-grouped grid needs a column tile's tm workgroups on one XCD's 32 CUs (128 x 128 tiles only)
+  g.xcd_grouped = xcd_grouped && bm == 128 && g.tm * cdiv(cdiv(a.n, 128), 8) <= device_cu_count() / 8;
+  if (bm == 128) {
+    const bool k25 = cdiv(a.P, ra::kBK) == 25;
+    if (a.npw == 3) {
+      if (k25) launch_fwd1_rega_ag_k<float, 25>(a, g, s);
+      else launch_fwd1_rega_ag_k<float, 0>(a, g, s);
+    } else {
+      if (k25) launch_fwd1_rega_ag_k<bf16, 25>(a, g, s);
+      else launch_fwd1_rega_ag_k<bf16, 0>(a, g, s);
+    }
+  } else if (a.npw == 3) {
+    launch_fwd1_glds64_ag<3>(a, g, s);
   } else {
-    if (k25) launch_fwd1_rega_ag_k<bf16, 25>(a, g, s);
-    else launch_fwd1_rega_ag_k<bf16, 0>(a, g, s);
+    launch_fwd1_glds64_ag<1>(a, g, s);
   }
   CME_LAUNCH_CHECK(s);
+  return bm;
 }
 
 void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {

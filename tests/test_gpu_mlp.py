@@ -534,17 +534,18 @@ def test_split3_multi_epoch_drift_vs_fp64_oracle():
 
 
 @pytest.mark.parametrize("dt,path", [("f32", "split3"), ("bf16", "split1")])
-@pytest.mark.parametrize("H,n", [(4096, 800), (4096, 777), (3072, 1024)])
+@pytest.mark.parametrize("H,n", [(4096, 800), (4096, 777), (3072, 1024), (1024, 800), (512, 160), (700, 96)])
 def test_wide_fused_allgather_head_matches_head_kernel(dt, path, H, n):
-    """Wide layers: the head fused into the A-in-registers forward launch (mlp_fwd1_rega_ag: two hand-offs
-    per 128-column tile, row tiles 0-7 each reduce 16 columns' z2 partials) against the forward launch +
-    head_wide_kernel.  Same arithmetic in the same order: a1, D, dZ1 (fp32 / planes), the loss and every
+    """Wide layers: the head fused into the forward launch (mlp_fwd1_wide_ag: the A-in-registers 128 x 128
+    tiles, or the direct-to-LDS 64 x 64 tiles below ~200 such tiles; two hand-offs per column tile, row tiles
+    0 .. BN/16-1 each reduce 16 columns' z2 partials) against the forward launch + head_wide_kernel.  Same arithmetic in the same order: a1, D, dZ1 (fp32 / planes), the loss and every
     gradient but dW2 BITWISE; dW2 sums 128-column partials instead of 32-column ones (fp32 rounding).
     Then SGD steps agree to rounding, the column-tile counters advance by 2 tm per launch, no wait timed
     out, and store_a1=False leaves a1 untouched with identical results."""
     x, y = synthetic_mnist(2 * n + 64, seed=13)
     nn = NeuralNetwork([784, H, 10])
-    tm, tn = (H + 127) // 128, (n + 127) // 128
+    bm = 128 if ((H + 127) // 128) * ((n + 127) // 128) >= 192 else 64
+    tm, tn = (H + bm - 1) // bm, (n + bm - 1) // bm
     outs = []
     for mode in ("ag", "head", "ag_noa1", "agx"):
         e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", path=path)
@@ -552,6 +553,7 @@ def test_wide_fused_allgather_head_matches_head_kernel(dt, path, H, n):
         e.load_dataset(x, y)
         e.set_fh_allgather(mode != "head")
         e._hip_step().ag_xcd_grouped = int(mode == "agx")  # each column tile's hand-offs inside one XCD
+        e._hip_step().ag_tiles64 = 1  # the 64 x 64 tiling too (off by default: measured no faster)
         if mode == "ag_noa1":
             e.set_store_a1(False)
             e.a1.fill_(7.0)
