@@ -860,7 +860,10 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
     for (int r = 0; r < 4; ++r)
       st_f32(rp, (4 * fg + r < C && hh < H) ? ((ct * 16 + 4 * fg + r) * H + hh) * 4 : kOOB, pw[r]);
   }
-  const __amdgpu_buffer_rsrc_t rdz = make_rsrc(h.dZ1), rpl = make_rsrc(h.dZ1_planes);
+  // dZ1 of this wave's block, written over its a1 block in the LDS tile (every dW2 read of it is done after the
+  // barrier), then read back as 4 consecutive columns per lane: 16-byte fp32 stores / 8-byte plane stores along
+  // rows instead of a 4-byte (2-byte) scatter in the MFMA layout
+  __syncthreads();
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     f32x4 r = {0.f, 0.f, 0.f, 0.f};
@@ -870,16 +873,53 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float x = a1v[nb][j];
-      float dz = r[j] * x * (1.f - x);
-      const int row = rw + 4 * fg + j, col = cw + 16 * nb + fr;
-      const bool ok = row < H && col < n;
-      if (h.dZ1) st_f32(rdz, ok ? (row * h.ldz + col) * 4 : kOOB, dz);
-      if (h.dZ1_planes)
-        for (int p = 0; p < h.npz; ++p) {
-          const bf16 q = __float2bfloat16(dz);
-          st_bf16(rpl, ok ? ((p * H + row) * h.ldz + col) * 2 : kOOB, q);
-          dz -= __bfloat162float(q);
+      ts[(rw - m0 + 4 * fg + j) * LD + cw - n0 + 16 * nb + fr] = r[j] * x * (1.f - x);
+    }
+  }
+  ag_wave_sync();  // (each wave re-reads only its own block)
+  constexpr int CPR = 4 * NB;  // 4-column chunks per row of the wave's block
+  const __amdgpu_buffer_rsrc_t rdz = make_rsrc(h.dZ1), rpl = make_rsrc(h.dZ1_planes);
+#pragma unroll
+  for (int q = 0; q < 16 * CPR / 64; ++q) {
+    const int c = q * 64 + lane, rr = c / CPR, c4 = (c % CPR) * 4;
+    const int row = rw + rr, col = cw + c4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(ts + (rw - m0 + rr) * LD + cw - n0 + c4);
+    const bool rok = row < H, full = rok && col + 4 <= n;
+    if (h.dZ1) {
+      if (full) {
+        __attribute__((ext_vector_type(4))) unsigned w;
+        __builtin_memcpy(&w, &v, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(w, rdz, (row * h.ldz + col) * 4, 0, 0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float ve = v[e];
+          st_f32(rdz, (rok && col + e < n) ? (row * h.ldz + col + e) * 4 : kOOB, ve);
         }
+      }
+    }
+    if (h.dZ1_planes) {
+      float rem[4] = {v[0], v[1], v[2], v[3]};
+      for (int p = 0; p < h.npz; ++p) {
+        unsigned short qb[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bf16 qv = __float2bfloat16(rem[e]);
+          qb[e] = __builtin_bit_cast(unsigned short, qv);
+          rem[e] -= __bfloat162float(qv);
+        }
+        const int base = ((p * H + row) * h.ldz + col) * 2;
+        if (full) {
+          __attribute__((ext_vector_type(2))) unsigned w;
+          w.x = (unsigned)qb[0] | ((unsigned)qb[1] << 16);
+          w.y = (unsigned)qb[2] | ((unsigned)qb[3] << 16);
+          __builtin_amdgcn_raw_buffer_store_b64(w, rpl, base, 0, 0);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            __builtin_amdgcn_raw_buffer_store_b16(qb[e], rpl, (rok && col + e < n) ? base + 2 * e : kOOB, 0, 0);
+        }
+      }
     }
   }
 }
