@@ -44,6 +44,11 @@ class CommFailure(RuntimeError):
     """Raised on every rank together when a peer-to-peer all-reduce wait timed out on any rank."""
 
 
+class KernelHandoffTimeout(RuntimeError):
+    """A forward + head launch in its all-gather form (H <= 128, or the fused wide head) waited past its bound
+    for the other workgroups of its column tile (engine.kernel_error()): that launch's outputs are not trusted."""
+
+
 @dataclass
 class EpochPlan:
     steps: list  # [(start, length)]
@@ -263,10 +268,21 @@ class DataParallelTrainer:
                    for v in h)
 
     def assert_comm_ok(self) -> None:
-        """Collective: raise CommFailure on every rank together if any rank's peer wait timed out."""
+        """Collective: raise CommFailure on every rank together if any rank's peer wait timed out, and
+        KernelHandoffTimeout if any rank's all-gather forward + head launch timed out waiting for its tile."""
         if (self.xgmi is not None or self._xgmi_fused is not None) and self.comm_failed():
             raise CommFailure(f"rank {self.rank}: an xGMI all-reduce peer wait timed out on some rank "
                               "(a rank stalled or died); no rank applied the affected update")
+        if self._allgather_live():
+            local = self.engine.kernel_error()
+            bad = local if self.R == 1 else self.comm.allreduce_scalar(1.0 if local else 0.0, op="max") > 0
+            if bad:
+                raise KernelHandoffTimeout(f"rank {self.rank}: an all-gather forward + head launch timed out "
+                                           "waiting for its column tile on some rank; its outputs are not trusted")
+
+    def _allgather_live(self) -> bool:
+        e = self.engine
+        return e.backend == "hip" and e.ag_err is not None and bool(e.fh_allgather)
 
     def close(self) -> None:
         """Collective: release the xGMI IPC buckets (every rank must call it)."""
@@ -590,6 +606,7 @@ class DataParallelTrainer:
             err_file = open(os.path.join(outdir, "CpuGpuDiff.txt"), "w" if self.iter == 0 else "a")
             own_file = True
         xgmi_live = self.xgmi is not None or self._xgmi_fused is not None
+        ag_live = self._allgather_live()  # all-gather forward + head launches: their timeout flag, per epoch
         host_needed = print_every > 0 or debug or self.profiler is not None
         dev = self.engine.device
         if dev.type == "cuda":
@@ -606,7 +623,7 @@ class DataParallelTrainer:
                     maybe_fault(self.iter, len(plan.steps))
                     with self.roctx.range(f"epoch {epoch}"):
                         self.run_plan(plan, lr, reg)
-                    if xgmi_live:
+                    if xgmi_live or ag_live:
                         self.assert_comm_ok()  # syncs; every rank raises together
                     self.iter += len(plan.steps)
                     stats.steps += len(plan.steps)
@@ -637,7 +654,7 @@ class DataParallelTrainer:
                     self.iter += 1
                     stats.steps += 1
                     stats.images += (ln // self.R) * self.R
-                if xgmi_live:
+                if xgmi_live or ag_live:
                     self.assert_comm_ok()
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)

@@ -583,3 +583,20 @@ def test_wide_fused_allgather_head_matches_head_kernel(dt, path, H, n):
     for i in range(8):
         assert torch.equal(fx[i], fa[i]), i
     assert torch.equal(px, pa)
+
+
+@pytest.mark.parametrize("H", [100, 4096])
+def test_allgather_timeout_flag_raises_in_train(H):
+    """A forward + head launch in its all-gather form that timed out waiting for its column tile leaves the
+    engine's error word set; train() checks it after every epoch (DataParallelTrainer.assert_comm_ok) and
+    raises instead of training on from untrusted D / dZ1."""
+    from cme213_sp18_amd.parallel.trainer import KernelHandoffTimeout
+
+    x, y = synthetic_mnist(1600, seed=2)
+    tr = DataParallelTrainer(NeuralNetwork([784, H, 10]), dtype="f32", batch_size=800)
+    tr.load(x, y)
+    tr.train(1, 0.01, 1e-4)  # clean epoch: no raise
+    assert tr._allgather_live() and not tr.engine.kernel_error()
+    tr.engine.ag_err.fill_(1)  # what a timed-out wait leaves behind
+    with pytest.raises(KernelHandoffTimeout):
+        tr.train(1, 0.01, 1e-4)
