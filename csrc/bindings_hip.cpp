@@ -63,7 +63,10 @@ struct MlpStep {
   int dw2_cols_last = 32;
   int store_a1 = 1;  // the fused wide head: 0 skips the a1 store (nothing in the step reads it)
   int ag_xcd_grouped = 0;  // the fused wide head's grid: 1 = each column tile on one XCD (RegaAgArgs)
-  int ag_tiles64 = 0;      // 1: the fused wide head also on the 64 x 64 tiling (measured no faster)
+  // the fused wide head on the 64 x 64 tiling (H = 512-1024): -1 = when a1 is not stored (measured faster only
+  // then: profiles/wide_fused_head_r2.md), 1 = always, 0 = never
+  int ag_tiles64 = -1;
+  int ag64() const { return ag_tiles64 >= 0 ? ag_tiles64 : (store_a1 ? 0 : 1); }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
   void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2) {
@@ -178,9 +181,9 @@ struct MlpStep {
               a.dw2part = h.dw2part;
             }
             if (fh_allgather && ag_counters && ag_err && h.dw2part && !(parts & 12) &&
-                cme::mlp_fwd1_wide_ag_ok(f, h, ag_tiles64)) {  // one launch: forward GEMM + the all-gather head
+                cme::mlp_fwd1_wide_ag_ok(f, h, ag64())) {  // one launch: forward GEMM + the all-gather head
               a.dw2_cols = cme::mlp_fwd1_wide_ag(f, h, P_<unsigned long long>(ag_counters), fh_tiles,
-                                                 P_<int>(ag_err), store_a1, ag_xcd_grouped, ag_tiles64,
+                                                 P_<int>(ag_err), store_a1, ag_xcd_grouped, ag64(),
                                                  S(stream));
             } else {
               if (!(parts & 8)) cme::mlp_split_fwd1(f, S(stream));

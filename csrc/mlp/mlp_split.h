@@ -114,7 +114,7 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s);
 // weight-gradient launch then needs a.dw2_cols = it.  Every workgroup must be resident at once (off when
 // processes share a GPU); a timed-out wait sets *err.
 struct HeadArgs;
-// allow64: also the 64 x 64 tiling (measured no faster; tests)
+// allow64: also the 64 x 64 tiling (MlpStep.ag_tiles64: by default only when a1 is not stored)
 bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64);
 int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long long* counters, int max_tiles,
                      int* err, int store_a1, int xcd_grouped, int allow64, hipStream_t s);

@@ -1498,8 +1498,8 @@ int device_cu_count() {
 }  // namespace
 
 // the tile the fused head runs on: 128 (A-in-registers engine), 64 (the direct-to-LDS 64 x 64 tiling), 0 (none)
-// (64 x 64 measured no faster than forward + head_wide_kernel at 784-1024-10: 33.2 vs 32.9 us f32, 25.40 vs
-// 25.39 us bf16, profiles/wide_ag_ab_r2.jsonl -- taken only on request, MlpStep.ag_tiles64)
+// (64 x 64: faster than forward + head_wide_kernel only without the a1 store -- 784-1024-10 bf16 25.33 -> 25.06 us,
+// 784-512-10 f32 32.20 -> 31.13 us, profiles/wide_ag_ab_64_r2.jsonl; MlpStep.ag_tiles64 decides)
 static int wide_ag_bm(const SplitStepArgs& a, int allow64) {
   if (rega_fwd_ok(a)) return 128;
   if (allow64 && glds_fwd_ok(a) && cdiv(a.H, 128) * cdiv(a.n, 128) < 192) return 64;
