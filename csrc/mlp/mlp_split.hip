@@ -738,7 +738,7 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
   static_assert(NDS * 512 == 16 * BN && BM % 16 == 0 && BM / 16 <= 8, "tile shape");
   const HeadArgs& h = g.h;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, fr = lane & 15, fg = lane >> 4;
-  const int H = a.H, n = a.n, C = a.C, rt = m0 / 128;
+  const int H = a.H, n = a.n, C = a.C, rt = m0 / BM;
   float* Ds = reinterpret_cast<float*>(lds);  // [16][LD] the column tile's D
   float* ts = Ds + 16 * LD;                     // [BM][LD] the a1 tile
   float* zs = ts + BM * LD;                     // [16][17] z2 (+ b2) of the reduced 16 columns
