@@ -2,7 +2,11 @@
 """Headline benchmark: MNIST images/sec, 784-100-10 MLP, batch=800, on N MI355X.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it
-is launched under ``torch.distributed.run`` (one rank per GPU, RCCL).  W untimed
+runs under ``torch.distributed.run`` (one rank per GPU, RCCL) -- started by the
+driver, or, when no launcher started this process, by bench.py itself (a child
+launcher).  Every rank checks that the job is N ranks on N distinct GPUs and
+exits non-zero WITHOUT a record otherwise (ranks_seen / devices_distinct are in
+the record, with the measured all-reduce time of the step's bucket).  W untimed
 warm-up steps, then EXACTLY K timed optimizer steps bracketed by barrier +
 synchronize on both sides; the max time over ranks is reported; rank 0 prints
 one JSON line.
@@ -63,24 +67,41 @@ def parse(argv=None):
 
 
 def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
     a = parse(argv)
     if a.mode == "reference":
         a.backend, a.no_graphs, a.allreduce = "torch", True, "host"
+    from cme213_sp18_amd.parallel.launcher import PlacementError, self_launch
+
+    # --gpus N without a launcher: start the N ranks here (a child torch.distributed.run, before any GPU
+    # call in this process) and pass their exit code through; rank 0 of the child job prints the record
+    try:
+        rc = self_launch(a.gpus, argv, script=os.path.abspath(__file__), need_gpus=a.backend == "hip")
+    except PlacementError as ex:
+        print(f"error: {ex}; no record", file=sys.stderr, flush=True)
+        return 2
+    if rc is not None:
+        return rc
+
     import numpy as np
     import torch
 
     from cme213_sp18_amd.models.mlp import NeuralNetwork
-    from cme213_sp18_amd.parallel.launcher import init_distributed, shutdown
+    from cme213_sp18_amd.parallel.launcher import init_distributed, shutdown, verify_placement
     from cme213_sp18_amd.parallel.trainer import DataParallelTrainer, EpochPlan
     from cme213_sp18_amd.utils.data import synthetic_mnist
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if world_env != a.gpus:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE", file=sys.stderr)
     comm, device = init_distributed()
     R, rank = comm.world_size, comm.rank
+    try:  # the job must be exactly --gpus ranks on --gpus distinct GPUs, or it measures nothing
+        placement = verify_placement(comm, device, a.gpus)
+    except PlacementError as ex:
+        print(f"[rank {rank}] error: {ex}; no record", file=sys.stderr, flush=True)
+        shutdown()
+        return 2
+    sync = (lambda: torch.cuda.synchronize(device)) if device.type == "cuda" else (lambda: None)
     if a.parallel == "tp":
-        return run_tp(a, comm, device)
+        return run_tp(a, comm, device, placement, sync)
     global_batch = a.batch * R if a.scaling == "weak" else a.batch
 
     x, y = synthetic_mnist(a.train_size, seed=0)  # identical on every rank, no broadcast
@@ -117,14 +138,14 @@ def main(argv=None) -> int:
                 tr._graphs.clear()
         # every rank done capturing before the first warm-up step: with the xGMI all-reduce a step waits
         # (bounded) for its peers' same step, so a rank still capturing would count against that bound
-        torch.cuda.synchronize(device)
+        sync()
         comm.barrier()
         for p in warm_plans:
             tr.run_plan(p, lr, reg)
         return tr, timed_plans
 
     tr, timed_plans = prepare(a.allreduce)
-    torch.cuda.synchronize(device)
+    sync()
     comm.barrier()
     if tr.allreduce_impl.startswith("xgmi") and a.allreduce == "auto":
         # a bounded peer wait that timed out during the warm-up (the xGMI protocol misbehaving on this
@@ -140,16 +161,16 @@ def main(argv=None) -> int:
             tr, timed_plans = prepare("rccl")
     native_exec = all(tr.native_plan(p) is not None for p in timed_plans)
     runners = [tr.plan_runner(p, lr, reg) for p in timed_plans]  # resolved before the clock starts
-    torch.cuda.synchronize(device)
+    sync()
     comm.barrier()
-    torch.cuda.synchronize(device)
+    sync()
     t0 = time.perf_counter()
     for run in runners:
         run()
-    torch.cuda.synchronize(device)
+    sync()
     comm.barrier()
     if R > 1:  # an RCCL barrier is GPU work; one process has nothing left to wait for
-        torch.cuda.synchronize(device)
+        sync()
     dt = time.perf_counter() - t0
     dt = comm.allreduce_scalar(dt, op="max")
 
@@ -161,6 +182,7 @@ def main(argv=None) -> int:
     kerr = comm.allreduce_scalar(1.0 if tr.engine.kernel_error() else 0.0, op="max") > 0
     agree = tr.replicas_agree()
     ok = not bad and not comm_failed and not kerr and agree
+    ar = measure_allreduce(tr, comm, sync) if ok else {}
     # strong scaling drops the remainder columns when R does not divide the batch (trainer.shard)
     images = a.steps * (global_batch // R) * R
     value = images / dt
@@ -184,7 +206,7 @@ def main(argv=None) -> int:
                        "hip_graphs": tr.use_graphs and not native_exec,
                        "executor": "native" if native_exec else ("graph" if tr.use_graphs else "eager"),
                        "allreduce": tr.allreduce_impl, "params_finite": not bad,
-                       "comm_ok": not comm_failed, "replicas_bitwise_equal": agree},
+                       "comm_ok": not comm_failed, "replicas_bitwise_equal": agree, **placement, **ar},
         }
         if not ok:
             rec["invalid"] = ("non-finite parameters" if bad else "an xGMI peer wait timed out" if comm_failed
@@ -195,7 +217,46 @@ def main(argv=None) -> int:
     return 0 if ok else 1
 
 
-def run_tp(a, comm, device) -> int:
+def measure_allreduce(tr, comm, sync, iters: int = 20) -> dict:
+    """After the timed run: the per-call time of the step's gradient all-reduce on its own (the same
+    implementation and bucket bytes, max over ranks), so a scaling curve can be split into compute and
+    communication.  The xGMI forms are timed through their one-shot kernel (the fused form runs the same
+    protocol inside the wgrad launch); the overlapped RCCL backward through one whole-bucket all-reduce."""
+    import torch
+
+    if comm.world_size == 1:
+        return {"allreduce_us": None}
+    e = tr.engine
+    buf = torch.zeros_like(e.grads)
+    if tr.xgmi is not None:
+        fn, wire = (lambda: tr.xgmi.allreduce_(buf)), tr.xgmi.wire
+    elif tr.allreduce_mode == "host":
+        import torch.distributed as dist
+
+        def fn():
+            g = buf.cpu()
+            dist.all_reduce(g, group=tr._host_group)
+            buf.copy_(g)
+        wire = buf.dtype
+    else:
+        fn, wire = (lambda: comm.allreduce_(buf)), buf.dtype
+    for _ in range(3):
+        fn()
+    sync()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    sync()
+    us = comm.allreduce_scalar(1e6 * (time.perf_counter() - t0) / iters, op="max")
+    nbytes = buf.numel() * torch.tensor([], dtype=wire).element_size()
+    R = comm.world_size
+    return {"allreduce_us": round(us, 2), "allreduce_bytes": int(nbytes),
+            "allreduce_busbw_GBps": round(2 * (R - 1) / R * nbytes / (us * 1e-6) / 1e9, 2)}
+
+
+def run_tp(a, comm, device, placement, sync) -> int:
     """Hidden-sharded tensor-parallel step (parallel/tensor_parallel.py): fixed model and global batch
     (strong scaling), K timed steps bracketed by barrier + synchronize, max over ranks."""
     import torch
@@ -230,15 +291,15 @@ def run_tp(a, comm, device) -> int:
             tr.capture(p, lr, reg)
     for p in warm:
         tr.run_plan(p, lr, reg, use_graphs=graphs)
-    torch.cuda.synchronize(device)
+    sync()
     comm.barrier()
-    torch.cuda.synchronize(device)
+    sync()
     t0 = time.perf_counter()
     for p in timed:
         tr.run_plan(p, lr, reg, use_graphs=graphs)
-    torch.cuda.synchronize(device)
+    sync()
     comm.barrier()
-    torch.cuda.synchronize(device)
+    sync()
     dt = comm.allreduce_scalar(time.perf_counter() - t0, op="max")
     ok = comm.allreduce_scalar(0.0 if bool(torch.isfinite(tr.engine.params).all().item()) else 1.0, op="max") == 0
     value = a.steps * B / dt
@@ -251,7 +312,7 @@ def run_tp(a, comm, device) -> int:
             "data": "synthetic (MNIST-shaped 784-dim uint8 images, random-init weights)",
             "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": B, "seq_len": None,
                        "parallelism": f"tp{R}", "hidden_per_gpu": a.hidden // R, "backend": a.backend,
-                       "hip_graphs": graphs, "params_finite": ok},
+                       "hip_graphs": graphs, "params_finite": ok, **placement},
         }), flush=True)
     shutdown()
     return 0 if ok else 1

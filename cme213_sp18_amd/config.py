@@ -47,6 +47,8 @@ class TrainConfig:
     profile: bool = False       # per-phase event timing + roctx ranges (eager steps), summary at the end
     overlap_chunks: int = 0     # RCCL path: dW1 all-reduce row chunks overlapped with the backward (0 = auto)
     parallel: str = "dp"        # dp (reference scheme) | tp (hidden-dimension tensor parallel, wide layers)
+    gpus: int = 0               # ranks (one per GPU); 0 = WORLD_SIZE of the launcher, else 1.  N > 1 without a
+                                # launcher: the CLI starts the N ranks itself (parallel/launcher.self_launch)
 
     @property
     def H(self):
@@ -112,6 +114,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--parallel", choices=["dp", "tp"],
                     help="dp: data parallel (default); tp: shard the hidden layer over the ranks (one z2 all-reduce "
                          "per step, every rank runs the whole global batch)")
+    ap.add_argument("--gpus", type=int,
+                    help="number of ranks, one per GPU (the reference's mpirun -np N); started here when no "
+                         "launcher started this process")
     ap.add_argument("--overlap-chunks", type=int,
                     help="RCCL path: number of dW1 row chunks all-reduced while the backward runs (0 = auto)")
     return ap
@@ -126,6 +131,10 @@ def parse_config(argv=None) -> TrainConfig:
             setattr(cfg, k, v)
     for k, v in explicit.items():
         setattr(cfg, k.replace("-", "_"), v)
+    if cfg.gpus <= 0:
+        import os
+
+        cfg.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     if cfg.grade in GRADE_PRESETS:
         for k, v in GRADE_PRESETS[cfg.grade].items():
             setattr(cfg, k, v)

@@ -106,8 +106,10 @@ def numgrad(nn: NeuralNetwork, X, labels, reg: float, shift: bool = True) -> Gra
 
 def train(nn: NeuralNetwork, X, labels, learning_rate: float, reg: float = 0.0, epochs: int = 15,
           batch_size: int = 800, grad_check: bool = False, print_every: int = -1, debug: bool = False,
-          outdir: str = "Outputs", shift: bool = True, ckpt_precision: int = 12) -> list[float]:
+          outdir: str = "Outputs", shift: bool = True, ckpt_precision: int = 12, iter0: int = 0) -> list[float]:
     """Sequential fp64 minibatch SGD on the CPU -- the oracle (neural_network.cpp:219-279).
+
+    ``iter0``: the iteration counter at the start -- a resumed run continues the loss / snapshot numbering.
 
     ``grad_check`` runs a numerical gradient check on the first batch (the
     reference's threshold of 1000 made it a no-op; we assert a real bound).
@@ -124,4 +126,4 @@ def train(nn: NeuralNetwork, X, labels, learning_rate: float, reg: float = 0.0, 
         if not gradcheck(ng, g):
             raise AssertionError("gradient check failed")
     return list(cpu().train(*nn.params, X, labels, float(learning_rate), float(reg), int(epochs), int(batch_size),
-                            int(print_every), bool(debug), outdir, shift, int(ckpt_precision)))
+                            int(print_every), bool(debug), outdir, shift, int(ckpt_precision), int(iter0)))

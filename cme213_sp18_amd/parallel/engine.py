@@ -42,11 +42,14 @@ def gemm_dtype(dtype: str) -> torch.dtype:
 
 
 class FlatLayout:
-    """Offsets of W1, b1, W2, b2 inside the flat arena (each 64-element aligned)."""
+    """Offsets of W1, b1, W2, b2 inside the flat arena (each 64-element aligned), then one STATUS element:
+    in the gradient bucket it is 0 for a trusted step and 1 when this rank's forward + head launch timed out
+    (csrc/mlp/mlp_split.h SplitStepArgs::gstatus); the all-reduce sums it with the gradients and the SGD
+    kernels apply nothing when it is non-zero.  The parameter arena's copy stays 0."""
 
     def __init__(self, P: int, H: int, C: int):
         self.P, self.H, self.C = P, H, C
-        sizes = [H * P, H, C * H, C]
+        sizes = [H * P, H, C * H, C, 1]
         self.offsets = []
         o = 0
         for s in sizes:
@@ -54,6 +57,7 @@ class FlatLayout:
             o += _round_up(s, _ALIGN)
         self.sizes = sizes
         self.total = o
+        self.status = self.offsets[4]
 
     def views(self, flat: torch.Tensor):
         P, H, C = self.P, self.H, self.C
@@ -105,6 +109,7 @@ class MlpEngine:
         self.grads = torch.zeros(self.layout.total, dtype=self.pdt, device=dev)
         self.W1, self.b1, self.W2, self.b2 = self.layout.views(self.params)
         self.gW1, self.gb1, self.gW2, self.gb2 = self.layout.views(self.grads)
+        self.status_index = self.layout.status  # the gradient bucket's status element (FlatLayout)
         self.X = None
         self.Xw = self.XTw = None  # wide-layer bf16 copies (load_dataset)
         self.XT = None
@@ -123,6 +128,7 @@ class MlpEngine:
         # launch must be resident at once; DataParallelTrainer turns it off when processes share a GPU)
         self.fh_allgather = True
         self.store_a1 = True
+        self._ag_test_skip, self._ag_spin_shift = -1, 22  # inject_handoff_timeout (tests)
 
     def _configure_path(self):
         dev = self.device
@@ -172,9 +178,10 @@ class MlpEngine:
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
         elif self.backend == "hip" and self.np and H >= 512 and C <= 16 and self.dw2buf is not None:
             # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_wide_ag) uses one
-            # monotonic counter per column tile and the timed-out-wait word
+            # monotonic counter per column tile -- a separate array per tiling (128 x 128 / 64 x 64) -- and
+            # the timed-out-wait word
             tiles = (ld + 31) // 32
-            self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)
+            self.ag_counters = torch.zeros(2 * tiles * 32, dtype=torch.int64, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self._step = None
 
@@ -272,6 +279,15 @@ class MlpEngine:
             hip().split_planes(self.W1.data_ptr(), self.W1p.data_ptr(), self.W1.numel(), self.np,
                                torch.cuda.current_stream(self.device).cuda_stream)
 
+    def inject_handoff_timeout(self, row_tile: int = 0, spin_shift: int = 14) -> None:
+        """TEST HOOK: from the next step on, row tile ``row_tile`` of column tile 0 leaves its counter add out
+        of every all-gather forward + head launch, so that tile's wait really times out (after 2^spin_shift
+        polls).  ``row_tile=-1`` turns it off.  A timed-out launch sets the sticky error word: this engine then
+        applies no further update (kernel_error(), KernelHandoffTimeout) -- make a new engine afterwards."""
+        self._ag_test_skip, self._ag_spin_shift = int(row_tile), int(spin_shift)
+        if self._step is not None:
+            self._step.ag_test_skip, self._step.ag_spin_shift = self._ag_test_skip, self._ag_spin_shift
+
     def kernel_error(self) -> bool:
         """True if a forward + head launch's wait for the workgroups of its column tile timed out (the
         all-gather form; its outputs were then not trusted).  Reads a device word: synchronises."""
@@ -301,6 +317,7 @@ class MlpEngine:
             s.XTw = self.XTw.data_ptr() if loaded and self.XTw is not None else 0
             s.N = self.num_samples if loaded else 0
             s.W1, s.b1, s.W2, s.b2 = (t.data_ptr() for t in (self.W1, self.b1, self.W2, self.b2))
+            s.gstatus = self.grads[self.status_index:].data_ptr()
             s.W1g = self.W1g.data_ptr()
             s.gW1, s.gb1, s.gW2, s.gb2 = (t.data_ptr() for t in (self.gW1, self.gb1, self.gW2, self.gb2))
             s.a1, s.D, s.dZ1, s.dZ1g = (t.data_ptr() for t in (self.a1, self.D, self.dZ1, self.dZ1g))
@@ -325,11 +342,12 @@ class MlpEngine:
                 s.ag_err = self.ag_err.data_ptr()
                 s.fh_allgather = int(self.fh_allgather)
             elif self.ag_counters is not None:
-                s.fh_tiles = int(self.ag_counters.numel()) // 32
+                s.fh_tiles = int(self.ag_counters.numel()) // 64  # [2 tilings][tiles][32]
                 s.ag_counters = self.ag_counters.data_ptr()
                 s.ag_err = self.ag_err.data_ptr()
                 s.fh_allgather = int(self.fh_allgather)
             s.store_a1 = int(self.store_a1)
+            s.ag_test_skip, s.ag_spin_shift = self._ag_test_skip, self._ag_spin_shift
             if self.np and self.XT is not None and self.XT.shape[0] == self.P + 1:
                 s.bias_col = 1
             if self._xgmi_fuse is not None and s.bias_col:
@@ -441,7 +459,8 @@ class MlpEngine:
         if self.backend == "hip" and self.np:
             hip().split_sgd(self.params.data_ptr(), self.grads.data_ptr(), self.layout.total, float(lr),
                             self.W1p.data_ptr(), self.H * self.P, self.np,
-                            torch.cuda.current_stream(self.device).cuda_stream)
+                            torch.cuda.current_stream(self.device).cuda_stream,
+                            self.grads[self.status_index:].data_ptr())
         elif self.backend == "hip":
             stream = torch.cuda.current_stream(self.device).cuda_stream
             shadow = self.W1g.data_ptr() if self.dtype == "bf16" else 0

@@ -113,9 +113,11 @@ class DataParallelTrainer:
         # while the other's holds CUs) cannot promise -- one process per GPU keeps it
         from .comm import TorchDistComm
 
-        if (self.R > 1 and isinstance(self.comm, TorchDistComm) and self.engine.device.type == "cuda"
-                and self._gpu_sharing() > 1):
-            self.engine.set_fh_allgather(False)
+        # -- agreed by every rank (with uneven placement some ranks would otherwise take the all-gather form
+        # and its epoch-end timeout check, a collective, while others do not: mismatched collectives)
+        if self.R > 1 and isinstance(self.comm, TorchDistComm) and self.engine.device.type == "cuda":
+            one_per_gpu = self._gpu_sharing() == 1  # (collective, like _all_true: every rank calls both)
+            self.engine.set_fh_allgather(self._all_true(one_per_gpu and self.engine.fh_allgather))
         from ..utils.tracing import Roctx
 
         self.roctx = Roctx()       # CME_ROCTX=1: epoch / phase ranges for rocprofv3 --marker-trace
@@ -212,11 +214,10 @@ class DataParallelTrainer:
         import torch.distributed as dist
 
         if self._sharing is None:
-            dev = self.engine.device
-            props = torch.cuda.get_device_properties(dev)
-            ident = str(getattr(props, "uuid", "")) or f"{os.environ.get('HIP_VISIBLE_DEVICES', '')}:{dev.index}"
+            from .launcher import device_identity
+
             ids = [None] * self.R
-            dist.all_gather_object(ids, (os.uname().nodename, ident), group=self.comm.group)
+            dist.all_gather_object(ids, device_identity(self.engine.device), group=self.comm.group)
             self._sharing = sum(1 for x in ids if x == ids[self.rank])
         return self._sharing
 
@@ -268,17 +269,23 @@ class DataParallelTrainer:
                    for v in h)
 
     def assert_comm_ok(self) -> None:
-        """Collective: raise CommFailure on every rank together if any rank's peer wait timed out, and
-        KernelHandoffTimeout if any rank's all-gather forward + head launch timed out waiting for its tile."""
-        if (self.xgmi is not None or self._xgmi_fused is not None) and self.comm_failed():
-            raise CommFailure(f"rank {self.rank}: an xGMI all-reduce peer wait timed out on some rank "
-                              "(a rank stalled or died); no rank applied the affected update")
+        """Collective: raise KernelHandoffTimeout on every rank together if any rank's all-gather forward +
+        head launch timed out waiting for its tile, and CommFailure if any rank's xGMI peer wait timed out.
+        Either way NO rank applied the affected update or any later one: a timed-out launch's rank stops
+        updating (the weight-gradient launch reads the sticky error word) and marks its gradient bucket (the
+        status element, so RCCL / host all-reduces make every rank skip the SGD) or stops taking part in the
+        xGMI exchange (its peers' waits time out and apply nothing).  The hand-off check comes first: it is
+        the cause when both fire."""
         if self._allgather_live():
             local = self.engine.kernel_error()
             bad = local if self.R == 1 else self.comm.allreduce_scalar(1.0 if local else 0.0, op="max") > 0
             if bad:
                 raise KernelHandoffTimeout(f"rank {self.rank}: an all-gather forward + head launch timed out "
-                                           "waiting for its column tile on some rank; its outputs are not trusted")
+                                           "waiting for its column tile on some rank; no rank applied that step "
+                                           "or any later one")
+        if (self.xgmi is not None or self._xgmi_fused is not None) and self.comm_failed():
+            raise CommFailure(f"rank {self.rank}: an xGMI all-reduce peer wait timed out on some rank "
+                              "(a rank stalled or died); no rank applied the affected update")
 
     def _allgather_live(self) -> bool:
         e = self.engine
@@ -315,7 +322,7 @@ class DataParallelTrainer:
             planes, np_ = e.W1p, e.np
         elif e.dtype == "bf16":  # bf16 path: single-rounded shadow of W1
             planes, np_ = e.W1g, 1
-        self.xgmi.sgd_(e.grads, e.params, lr, planes, np_, e.H * e.P)
+        self.xgmi.sgd_(e.grads, e.params, lr, planes, np_, e.H * e.P, status_index=e.status_index)
 
     # ---------------------------------------------------------------- data
     def load(self, x_train, y_train):
@@ -658,6 +665,10 @@ class DataParallelTrainer:
                     self.assert_comm_ok()
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
+            if xgmi_live and not self.replicas_agree():
+                # the xGMI hand-off's ordering rests on write-through stores (csrc/comm/xgmi_allreduce.hip):
+                # a stale peer read would leave the replicas different -- checked bitwise once per train()
+                raise CommFailure(f"rank {self.rank}: replicas differ after xGMI data-parallel training")
             self.comm.barrier()
         finally:
             if own_file:

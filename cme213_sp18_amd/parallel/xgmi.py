@@ -111,12 +111,15 @@ class XgmiBucket:
         self.c.run(self.code, t.data_ptr(), 0, 0.0, 0, 0, 0, self.MODE_ALLREDUCE, self.numel, self._stream())
 
     def sgd_(self, grads: torch.Tensor, params: torch.Tensor, lr: float, planes: torch.Tensor | None = None,
-             np_: int = 0, w1n: int = 0) -> None:
-        """params -= lr * sum_ranks(grads); refresh bf16 planes ([np_][w1n]) of the first w1n params."""
+             np_: int = 0, w1n: int = 0, status_index: int | None = None) -> None:
+        """params -= lr * sum_ranks(grads); refresh bf16 planes ([np_][w1n]) of the first w1n params.
+        status_index: the bucket's status element -- non-zero (this rank's step is untrusted) makes this
+        rank take no part, so every peer's wait times out and no rank applies the step."""
         assert grads.numel() == self.numel == params.numel()
         pl = planes.data_ptr() if planes is not None else 0
+        st = grads[status_index:].data_ptr() if status_index is not None else 0
         self.c.run(self.code, grads.data_ptr(), params.data_ptr(), float(lr), pl, np_ if pl else 0, w1n,
-                   self.MODE_SGD, self.numel, self._stream())
+                   self.MODE_SGD, self.numel, self._stream(), st)
 
     def error(self) -> int:
         return int(self.c.error())

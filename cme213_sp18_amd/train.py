@@ -2,8 +2,9 @@
 
     python -m cme213_sp18_amd.train -g 1                      # grade preset 1 (fp64 parity)
     python -m cme213_sp18_amd.train -n 100 -e 5 -p 10         # f32 split-bf16 engine, print loss
+    python -m cme213_sp18_amd.train --preset 8gpu_wide --gpus 8   # 8 ranks, one per GPU, RCCL/xGMI
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
-        -m cme213_sp18_amd.train --preset 8gpu_wide           # one rank per GPU, RCCL
+        -m cme213_sp18_amd.train --preset 8gpu_wide           # the same under an external launcher
 
 Flow: bootstrap (one process per GPU, device = LOCAL_RANK) -> data (identical on
 every rank, uploaded once per GPU) -> optional sequential fp64 CPU training on
@@ -58,7 +59,7 @@ def run(cfg: TrainConfig) -> dict:
 
     from .models import mlp
     from .models.mlp import NeuralNetwork
-    from .parallel.launcher import init_distributed, shutdown
+    from .parallel.launcher import PlacementError, init_distributed, shutdown, verify_placement
     from .parallel.trainer import DataParallelTrainer
     from .utils.checkpoint import checkNNErrors, load_checkpoint, save_checkpoint
     from .utils.common import precision, save_label
@@ -69,9 +70,15 @@ def run(cfg: TrainConfig) -> dict:
         backend = "torch"
     comm, device = init_distributed("gloo" if backend == "torch" else None, timeout_s=cfg.comm_timeout)
     rank, world = comm.rank, comm.world_size
+    try:  # exactly --gpus ranks, on distinct GPUs (CME_SHARED_GPU=1: the shared-GPU rehearsal)
+        placement = verify_placement(comm, device, cfg.gpus)
+    except PlacementError as ex:
+        print(f"[rank {rank}] error: {ex}", file=sys.stderr, flush=True)
+        shutdown()
+        raise SystemExit(2)
     jlog = JsonLog(cfg.log_json, rank)
     try:
-        jlog({"event": "config", "world": world, "device": str(device), **{
+        jlog({"event": "config", "world": world, "device": str(device), **placement, **{
             k: v for k, v in vars(cfg).items() if isinstance(v, (int, float, str, bool))}})
         log0(rank, f"Number of processes = {world}")
         log0(rank, f"Device = {device} ({torch.cuda.get_device_name(device) if device.type == 'cuda' else 'cpu'})")
@@ -103,7 +110,8 @@ def run(cfg: TrainConfig) -> dict:
             log0(rank, "Start Sequential Training")
             t = time.perf_counter()
             mlp.train(seq_nn, xs, ds.y_train, cfg.learning_rate, cfg.reg, cfg.num_epochs, cfg.batch_size,
-                      False, cfg.print_every, cfg.debug, cfg.outdir, cfg.softmax_shift, cfg.ckpt_precision)
+                      False, cfg.print_every, cfg.debug, cfg.outdir, cfg.softmax_shift, cfg.ckpt_precision,
+                      iter0=int(meta.get("iter", 0)))
             out["seq_seconds"] = time.perf_counter() - t
             log0(rank, f"Time for Sequential Training: {out['seq_seconds']:.6f} seconds")
             out["seq_dev_precision"] = precision(mlp.predict(seq_nn, xd, cfg.softmax_shift), ds.y_dev)
@@ -126,6 +134,9 @@ def run(cfg: TrainConfig) -> dict:
                                      normalize=cfg.normalize, path=cfg.path, allreduce=cfg.allreduce,
                                      overlap_chunks=cfg.overlap_chunks)
         tr.load(ds.x_train, ds.y_train)
+        # a resumed run continues the iteration counter (loss lines, -d diff rows and the print_flag
+        # schedule pick up where the checkpoint left off; CpuGpuDiff.txt is appended to, not truncated)
+        tr.iter = int(meta.get("iter", 0))
         if cfg.profile:
             tr.enable_profiling()
         fault = parse_fault(cfg.fault_inject)
@@ -193,7 +204,17 @@ def run(cfg: TrainConfig) -> dict:
 
 
 def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
     cfg = parse_config(argv)
+    from .parallel.launcher import PlacementError, self_launch
+
+    try:  # --gpus N and no launcher: run the N ranks (a child launcher) and return their status
+        rc = self_launch(cfg.gpus, argv, module="cme213_sp18_amd.train", need_gpus=False)
+    except PlacementError as ex:
+        print(f"error: {ex}", file=sys.stderr, flush=True)
+        return 2
+    if rc is not None:
+        return rc
     out = run(cfg)
     if out and int(os.environ.get("RANK", "0")) == 0:
         print(json.dumps({k: (float(v) if isinstance(v, (np.floating,)) else v) for k, v in out.items()}))

@@ -117,12 +117,12 @@ PYBIND11_MODULE(_cpu, m) {
       "train",
       [](py::array_t<double> W1, py::array_t<double> b1, py::array_t<double> W2, py::array_t<double> b2, f64arr X,
          i32arr labels, double lr, double reg, int epochs, int batch, int print_every, bool debug,
-         std::string outdir, bool shift, int ckpt_precision) {
+         std::string outdir, bool shift, int ckpt_precision, int iter0) {
         auto v = view(W1, b1, W2, b2);
         check_x(X, v.P);
         cme::cpu::TrainOpts o;
         o.lr = lr; o.reg = reg; o.epochs = epochs; o.batch = batch; o.print_every = print_every;
-        o.debug = debug; o.outdir = outdir; o.shift = shift; o.ckpt_precision = ckpt_precision;
+        o.debug = debug; o.outdir = outdir; o.shift = shift; o.ckpt_precision = ckpt_precision; o.iter0 = iter0;
         std::vector<double> losses;
         {
           py::gil_scoped_release r;
@@ -132,7 +132,8 @@ PYBIND11_MODULE(_cpu, m) {
       },
       py::arg("W1"), py::arg("b1"), py::arg("W2"), py::arg("b2"), py::arg("X"), py::arg("labels"), py::arg("lr"),
       py::arg("reg"), py::arg("epochs"), py::arg("batch"), py::arg("print_every") = 0, py::arg("debug") = false,
-      py::arg("outdir") = "Outputs", py::arg("shift") = true, py::arg("ckpt_precision") = 12);
+      py::arg("outdir") = "Outputs", py::arg("shift") = true, py::arg("ckpt_precision") = 12,
+      py::arg("iter0") = 0);
 
   // ---------------------------------------------------------------- I/O
   m.def(

@@ -58,6 +58,11 @@ struct MlpStep {
   // word (>= fh_tiles each); fh_allgather = 1 selects it when all three are set
   uintptr_t ag_counters = 0, ag_slabs = 0, ag_err = 0;
   int fh_allgather = 0;
+  // the gradient bucket's status element (float, after b2): written by the wgrad launch in gradient mode
+  uintptr_t gstatus = 0;
+  // the all-gather hand-offs' wait bound (2^ag_spin_shift polls) and the forced-timeout test hook
+  // (SplitStepArgs::ag_test_skip; -1 off)
+  int ag_spin_shift = 22, ag_test_skip = -1;
   // wide split layers: the all-gather head fused into the forward launch (fh_allgather, ag_counters, ag_err;
   // mlp_fwd1_wide_ag) leaves dW2 partials per 128 / 64 columns (32 from head_wide_kernel): what run_wgrad sums
   int dw2_cols_last = 32;
@@ -128,6 +133,11 @@ struct MlpStep {
     a.stamps = reinterpret_cast<unsigned long long*>(stamps);
     a.bias_col = bias_col;
     a.a_fp32 = a_fp32 >= 0 ? a_fp32 : (H <= 128 ? 1 : 3);
+    // a timed-out all-gather forward + head launch (sticky word) makes every later update a no-op
+    a.ag_err = P_<const int>(ag_err);
+    a.gstatus = P_<float>(gstatus);
+    a.ag_spin_shift = ag_spin_shift;
+    a.ag_test_skip = ag_test_skip;
     return a;
   }
 
@@ -161,7 +171,8 @@ struct MlpStep {
           // the dW1 GEMM splits fp32 dZ1 in registers: the head writes fp32 dZ1 and no planes
           const bool dz32 = cme::mlp_split_wgrad_fp32_dz(a);
           if (dz32) h.dZ1_planes = nullptr;
-          if (fh_allgather && ag_counters && ag_slabs && ag_err && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {
+          if (fh_allgather && ag_counters && ag_slabs && ag_err && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h) &&
+              cme::mlp_fwd1_head_ag_fits(a)) {
             cme::mlp_fwd1_head_ag(a, h, P_<unsigned long long>(ag_counters), P_<float>(ag_slabs), P_<int>(ag_err),
                                   fh_tiles, S(stream));
           } else if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
@@ -420,6 +431,9 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_slabs", &MlpStep::ag_slabs)
       .def_readwrite("ag_err", &MlpStep::ag_err)
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
+      .def_readwrite("gstatus", &MlpStep::gstatus)
+      .def_readwrite("ag_spin_shift", &MlpStep::ag_spin_shift)
+      .def_readwrite("ag_test_skip", &MlpStep::ag_test_skip)
       .def_readwrite("store_a1", &MlpStep::store_a1)
       .def_readwrite("ag_xcd_grouped", &MlpStep::ag_xcd_grouped)
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
@@ -476,11 +490,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def(
       "split_sgd",
       [](uintptr_t params, uintptr_t grads, int64_t count, double lr, uintptr_t W1p, int64_t w1n, int npw,
-         uintptr_t s) {
-        cme::mlp_split_sgd(P<float>(params), P<const float>(grads), count, lr, P<void>(W1p), w1n, npw, S(s));
+         uintptr_t s, uintptr_t status) {
+        cme::mlp_split_sgd(P<float>(params), P<const float>(grads), count, lr, P<void>(W1p), w1n, npw, S(s),
+                           P<const float>(status));
       },
       py::arg("params"), py::arg("grads"), py::arg("count"), py::arg("lr"), py::arg("W1p"), py::arg("w1n"),
-      py::arg("npw"), py::arg("stream") = 0);
+      py::arg("npw"), py::arg("stream") = 0, py::arg("status") = 0);
   m.def("split_fwdhead_blocks", &cme::mlp_split_fwdhead_blocks);
   m.def("mlp_split_fused_tiles", &cme::mlp_split_fused_tiles, py::arg("P"), py::arg("H"), py::arg("cap"));
 

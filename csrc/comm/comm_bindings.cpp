@@ -149,13 +149,14 @@ class XgmiComm {
   }
 
   void run(int dtype, uintptr_t grads, uintptr_t params, double lr, uintptr_t planes, int np, int64_t w1n, int mode,
-           int64_t n, uintptr_t stream) {
+           int64_t n, uintptr_t stream, uintptr_t status) {
     CME_REQUIRE(ready_ || d_.world == 1, "XgmiComm.run: open() the peer handles first");
     CME_REQUIRE(n == d_.n, "XgmiComm.run: element count differs from the one the buffers were sized for");
     CME_REQUIRE((dtype == 0 && elt_ == 4) || (dtype == 1 && elt_ == 8) || (dtype == 2 && elt_ == 2),
                 "XgmiComm.run: dtype does not match the buffer's wire element size");
     xgmi_allreduce(d_, dtype, reinterpret_cast<const void*>(grads), reinterpret_cast<void*>(params), lr,
-                   reinterpret_cast<void*>(planes), np, w1n, mode, reinterpret_cast<hipStream_t>(stream));
+                   reinterpret_cast<void*>(planes), np, w1n, mode, reinterpret_cast<hipStream_t>(stream),
+                   reinterpret_cast<const void*>(status));
   }
 
   int error() const {
@@ -221,7 +222,8 @@ void bind_comm(py::module_& m) {
       .def("handles", &XgmiComm::handles)
       .def("open", &XgmiComm::open)
       .def("run", &XgmiComm::run, py::arg("dtype"), py::arg("grads"), py::arg("params"), py::arg("lr"),
-           py::arg("planes"), py::arg("np"), py::arg("w1n"), py::arg("mode"), py::arg("n"), py::arg("stream"))
+           py::arg("planes"), py::arg("np"), py::arg("w1n"), py::arg("mode"), py::arg("n"), py::arg("stream"),
+           py::arg("status") = 0)
       .def("error", &XgmiComm::error)
       .def("close", &XgmiComm::close)
       .def("close_peers", &XgmiComm::close_peers)

@@ -29,7 +29,10 @@ int64_t xgmi_padded_count(int64_t n);
 int64_t xgmi_num_blocks(int64_t n);
 
 // dtype: 0 f32, 1 f64, 2 f32 gradients over a bf16 wire (the IPC buffers hold bf16; summed in fp32).  planes: bf16 [np][w1n] refreshed from the first w1n params (np 1 or 3), or null.
+// status: this rank's gradient status element (the T-typed word after b2, or null): non-zero = this rank's
+// step is untrusted -> the rank takes no part (publishes nothing, applies nothing); its peers' waits then
+// time out and apply nothing either, exactly as for a stalled rank.
 void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* params, double lr, void* planes, int np,
-                    int64_t w1n, int mode, hipStream_t s);
+                    int64_t w1n, int mode, hipStream_t s, const void* status = nullptr);
 
 }  // namespace cme::comm

@@ -54,6 +54,7 @@ struct Args {
   __hip_bfloat16* planes;
   int np;
   int rank, world, mode;
+  const T* status;  // this rank's gradient status element (null: none): non-zero = take no part
 };
 
 constexpr int kSysCoherent = 1 | 16;  // buffer-load cache policy sc0 | sc1 (system coherent)
@@ -128,7 +129,8 @@ __device__ __forceinline__ void do_chunk(const Args<T, W>& a, int64_t c, uint32_
   if (t == 0) {
     s_sync[0] = a.epochs[c] + 1;
     // an earlier wait of this rank timed out: the replicas may already disagree -> apply nothing more
-    s_sync[1] = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    s_sync[1] = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                (a.status && *a.status != T(0));  // (or this rank's own step is untrusted)
   }
   __syncthreads();
   if (s_sync[1]) return;
@@ -252,7 +254,7 @@ int64_t xgmi_padded_count(int64_t n) { return (n + kChunk - 1) / kChunk * kChunk
 int64_t xgmi_num_blocks(int64_t n) { return (n + kChunk - 1) / kChunk; }
 
 void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* params, double lr, void* planes, int np,
-                    int64_t w1n, int mode, hipStream_t s) {
+                    int64_t w1n, int mode, hipStream_t s, const void* status) {
   CME_REQUIRE(d.world >= 1 && d.world <= kMaxRanks, "xgmi_allreduce: 1 <= world <= 8");
   CME_REQUIRE(d.rank >= 0 && d.rank < d.world, "xgmi_allreduce: bad rank");
   CME_REQUIRE(d.npad == xgmi_padded_count(d.n), "xgmi_allreduce: descriptor count mismatch");
@@ -284,6 +286,7 @@ void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* param
     a.rank = d.rank;
     a.world = d.world;
     a.mode = mode;
+    a.status = static_cast<const T*>(status);
     xgmi_allreduce_kernel<T, W><<<grid, kThreads, 0, s>>>(a, nchunks);
   };
   if (dtype == 1) fill((double*)nullptr, (double*)nullptr);

@@ -178,7 +178,7 @@ std::vector<double> train(NetView net, const double* X, const int* labels, int N
   std::vector<double> dW1((size_t)H * P), db1(H), dW2((size_t)C * H), db2(C);
   std::vector<double> losses;
   if (o.debug) std::filesystem::create_directories(o.outdir + "/CPUmats");
-  int iter = 0;
+  int iter = o.iter0;
   for (int epoch = 0; epoch < o.epochs; ++epoch) {
     const int nb = (N + B - 1) / B;
     for (int batch = 0; batch < nb; ++batch) {

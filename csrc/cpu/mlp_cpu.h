@@ -49,6 +49,7 @@ struct TrainOpts {
   bool debug = false, shift = true;
   std::string outdir = "Outputs";
   int ckpt_precision = 12;  // raw_ascii format, see io.h
+  int iter0 = 0;            // iteration counter at the start (a resumed run continues the numbering)
 };
 
 // Minibatch SGD (neural_network.cpp:219-279): ceil(N/B) batches per epoch, the

@@ -4,15 +4,17 @@
 //   1. forms its z2 partial W2[:, its 16 rows] . a1[its rows, cols] (16 classes x 32 columns) and publishes
 //      it: sc1 (write-through) stores, vmcnt(0), barrier, one agent-scope add to the tile's 64-bit counter;
 //   2. waits (one lane, returning-atomic polls, s_sleep, bounded) until all tm adds of this launch are in --
-//      counters only grow, each launch adds exactly tm per tile, so the target is the next multiple of tm;
+//      counters only grow, each launch adds exactly tm per tile (tm = cdiv(H, 16) is fixed for an engine, and a
+//      workgroup whose wait timed out still added), so the target is the next multiple of tm;
 //   3. sums the tm partials in row-tile order (sc1 loads: bit-identical z2 in every workgroup), softmax,
 //      D (row tile 0 stores it and the loss partial);
 //   4. forms dZ1 for ITS OWN 16 rows from the a1 tile it still holds in LDS and stores it (fp32 and / or
 //      the bf16 planes, two columns per 4-byte word).
 // The hand-off is MI355X_MICROARCH.md's table's first row (sc1 stores, vmcnt(0) in every storing wave,
 // barrier, one agent add per workgroup, sc1 loads after the poll).  Requires every workgroup of the launch
-// to be resident at once; a wait that outlasts kAgSpinLimit sets *err (the launch's results are then not
-// trusted: MlpEngine.kernel_error()).
+// to be resident at once (mlp_fwd1_head_ag_fits); a wait that outlasts 2^ag_spin_shift polls sets *err: the
+// launch's results are not trusted, and the weight-gradient launch that follows reads *err and applies nothing
+// (SplitStepArgs::ag_err; MlpEngine.kernel_error(), KernelHandoffTimeout).
 #pragma once
 
 #include "fwd_tile.h"
@@ -22,7 +24,6 @@
 
 namespace cme {
 
-constexpr uint32_t kAgSpinLimit = 1u << 22;
 constexpr int kAgCounterStride = 32;  // uint64 words: one 256-byte line per tile counter (polls and adds of
                                       // different tiles must not share a line)
 
@@ -101,15 +102,18 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   // ---- 2. one add per workgroup, then wait for the tile's tm adds of this launch
   if (t == 0) {
     unsigned long long* cnt = counters + (size_t)ct * kAgCounterStride;
-    const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (test hook: one workgroup of column tile 0 leaves its add out, so that tile's wait really times out)
+    const unsigned long long inc = (f.ag_test_skip == rt && ct == 0) ? 0ull : 1ull;
+    const unsigned long long old = __hip_atomic_fetch_add(cnt, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long target = (old / (unsigned)tm + 1) * (unsigned)tm;
+    const uint32_t limit = 1u << f.ag_spin_shift;
     uint32_t spins = 0;
     int bad = 0;
     // polled with a returning atomic (add 0): served where the adds are performed, never from a
     // possibly stale L2 copy of the line (measured: sc1 load polls saw the last adds only ~20 us late)
-    while (old + 1 < target &&
+    while (old + inc < target &&
            __hip_atomic_fetch_add(cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++spins > kAgSpinLimit) {
+      if (++spins > limit) {
         bad = 1;
         atomicExch(err, 1);
         break;

@@ -72,6 +72,9 @@ void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters
 // >= max_tiles * 8 * 16 * 32 floats, err: set to 1 if a wait for the tile's workgroups timed out
 void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long long* counters, float* slabs,
                       int* err, int max_tiles, hipStream_t s);
+// the all-gather form's grid fits on the device at once (occupancy x CU count): every workgroup waits for the
+// others of its column tile, so a larger grid (a large per-GPU batch) must take the last-arriver form
+bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f);
 int mlp_head_num_blocks(int n);
 
 struct WgradArgs {

@@ -1288,6 +1288,36 @@ void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters
   CME_LAUNCH_CHECK(s);
 }
 
+namespace {
+template <auto Kern>
+int resident_per_cu(int threads) {  // workgroups of Kern one CU holds at once (static LDS only), cached
+  static int occ = -1;
+  if (occ < 0) HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, Kern, threads, 0));
+  return occ;
+}
+int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) HIP_CHECK(hipDeviceGetAttribute(&cached[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  return cached[dev];
+}
+}  // namespace
+
+bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f) {
+  if (f.n <= 0) return true;
+  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32), nwg = 8 * tm * cdiv(tn, 8);
+  const bool af = mlp_split_fwd_fp32_w(f);
+  const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(af ? (const void*)f.W1 : f.W1p) % 16 == 0 && f.P % 8 == 0;
+  int occ;
+  if (af) occ = vec ? resident_per_cu<fwd1_head_ag_kernel<3, 1, true>>(512) : resident_per_cu<fwd1_head_ag_kernel<3, 0, true>>(512);
+  else if (f.npw == 3) occ = vec ? resident_per_cu<fwd1_head_ag_kernel<3, 1, false>>(512) : resident_per_cu<fwd1_head_ag_kernel<3, 0, false>>(512);
+  else occ = vec ? resident_per_cu<fwd1_head_ag_kernel<1, 1, false>>(512) : resident_per_cu<fwd1_head_ag_kernel<1, 0, false>>(512);
+  return nwg <= occ * cu_count();
+}
+
 void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long long* counters, float* slabs,
                       int* err, int max_tiles, hipStream_t s) {
   if (f.n <= 0) return;
@@ -1297,6 +1327,8 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
   const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32);
   CME_REQUIRE(tm <= 8, "fwd1_head_ag: H <= 128");
   CME_REQUIRE(counters && slabs && err && tn <= max_tiles, "fwd1_head_ag: counter / slab arrays too small");
+  CME_REQUIRE(mlp_fwd1_head_ag_fits(f), "fwd1_head_ag: grid larger than the device holds at once (use the "
+                                        "last-arriver form, mlp_fwd1_head)");
   const bool af = mlp_split_fwd_fp32_w(f);
   const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 &&
                    reinterpret_cast<uintptr_t>(af ? (const void*)f.W1 : f.W1p) % 16 == 0 && f.P % 8 == 0;

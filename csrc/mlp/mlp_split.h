@@ -87,7 +87,20 @@ struct SplitStepArgs {
   float* dw2part = nullptr;
   int dw2_cols = 32;  // columns per dW2 partial: 32 (head_wide_kernel), 128 (the fused all-gather head)
   int w1_planes = 1;  // (set by mlp_split_wgrad) the small-layer W1 update refreshes the W1 planes
+  // The all-gather forward + head launches' timed-out-wait word (MlpEngine.ag_err).  The weight-gradient
+  // launch reads it and, when set, APPLIES NOTHING: no SGD / plane refresh (sgd = 1), no xGMI exchange (the
+  // fused all-reduce: this rank stops taking part, its peers time out), and the gradient status word below
+  // marks the bucket (sgd = 0) so the separate SGD / all-reduce kernels apply nothing on any rank.
+  const int* ag_err = nullptr;
+  // sgd = 0: the flat gradient bucket's status element (after b2): 0.f good, 1.f = this rank's step is
+  // untrusted.  Summed by the all-reduce with the gradients; the SGD kernels skip the update when non-zero.
+  float* gstatus = nullptr;
+  // the all-gather hand-off's wait bound (2^ag_spin_shift polls) and a TEST hook: row tile ag_test_skip of
+  // column tile 0 leaves out its (first) counter add, so that tile's wait really times out (-1: off)
+  int ag_spin_shift = 22;
+  int ag_test_skip = -1;
 };
+
 
 // true when a forward kernel of this configuration reads the W1 planes (false: fp32 W1 everywhere)
 bool mlp_split_w1_planes_read(const SplitStepArgs& a);
@@ -112,7 +125,7 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s);
 // tiles, fwd1_glds_kernel<64, 64, ..., AG> on 64 x 64): one launch leaves a1 (store_a1), D, the loss partials,
 // dZ1 (fp32 and / or planes) and the dW2 partials per column tile (h.dw2part).  Returns the tile width: the
 // weight-gradient launch then needs a.dw2_cols = it.  Every workgroup must be resident at once (off when
-// processes share a GPU); a timed-out wait sets *err.
+// processes share a GPU); a timed-out wait sets *err.  counters: [2][max_tiles][32] uint64 (one array per tiling).
 struct HeadArgs;
 // allow64: also the 64 x 64 tiling (MlpStep.ag_tiles64: by default only when a1 is not stored)
 bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64);
@@ -124,7 +137,8 @@ int mlp_split_fwdhead_blocks(int n);
 // planes[p][i] for i < n: exact np-way bf16 split of W[i] (np = 1: plain rounding).
 void mlp_split_planes(const float* W, void* planes, int64_t n, int np, hipStream_t s);
 // params[i] -= lr * grads[i]; then refresh the W1 planes (first w1_count params).
+// status: the bucket's status element (nullptr: none) -- non-zero (an untrusted step on some rank) skips the update
 void mlp_split_sgd(float* params, const float* grads, int64_t count, double lr, void* W1p, int64_t w1_count,
-                   int npw, hipStream_t s);
+                   int npw, hipStream_t s, const float* status = nullptr);
 
 }  // namespace cme

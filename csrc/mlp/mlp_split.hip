@@ -244,6 +244,20 @@ __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a,
 constexpr int kXfSys = 1 | 16;  // cache policy sc0 | sc1: system coherent
 constexpr uint32_t kXfSpinLimit = 1u << 22;
 
+// The forward + head launch of this step timed out (SplitStepArgs::ag_err): the word is loaded (a vector
+// atomic load from L2) BEFORE the K loop, like the epilogue's other operands, and tested only by the epilogue
+// (poisoned()), so its latency hides behind the loop.
+__device__ __forceinline__ int ag_err_load(const int* e) {
+  return e ? __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+}
+__device__ __forceinline__ bool poisoned(int v) { return __builtin_amdgcn_readfirstlane(v) != 0; }
+
+// sgd = 0: the dW1 launch marks the gradient bucket's status element (one lane of workgroup 0, after its
+// epilogue): 1.f when this rank's step is untrusted
+__device__ __forceinline__ void mark_status(const SplitStepArgs& a, int err) {
+  if (a.gstatus && blockIdx.x == 0 && threadIdx.x == 0) *a.gstatus = poisoned(err) ? 1.f : 0.f;
+}
+
 __device__ __forceinline__ void xf_store(float* base, int64_t idx, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), make_rsrc(base), (int)(idx * 4), 0, kXfSys);
 }
@@ -257,10 +271,11 @@ __device__ __forceinline__ float xf_load(const void* base, int64_t idx) {
 // A rank whose earlier wait timed out stops taking part altogether: it neither writes its IPC buffer (a
 // peer may still be reading the other epoch's half there) nor publishes flags nor applies updates, so
 // its peers time out too and every rank reports the error instead of stepping on stale data.
-__device__ __forceinline__ bool xf_begin(const XgmiFuse& x, int tile, uint32_t* s_xf) {
+// An untrusted step of this rank (its forward + head launch timed out: ag_err) is treated the same way.
+__device__ __forceinline__ bool xf_begin(const XgmiFuse& x, int tile, uint32_t* s_xf, const int* ag_err) {
   if (threadIdx.x == 0) {
     s_xf[0] = x.epochs[tile] + 1;
-    s_xf[1] = __hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    s_xf[1] = (__hip_atomic_load(x.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | ag_err_load(ag_err)) != 0;
   }
   __syncthreads();
   return s_xf[1] == 0;
@@ -335,14 +350,17 @@ struct EpiW2 {
   int sys;  // gradients into a peer-visible IPC buffer (write-through)
   float reg, lr;
   float pre[kEpiMaxQ];
+  const int* ag_err;  // the step's forward timed out: no update (the gradient goes to gW2, unused)
+  int perr = 0;
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
     pre[q] = buf_load1<float>(make_rsrc(W2), ok ? (row * H + col) * 4 : kOOB);
+    if (q == 0) perr = ag_err_load(ag_err);
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     const size_t i = (size_t)row * H + col;
     const float w = pre[q];
     const float g = v + reg * w;
-    if (sgd) W2[i] = w - lr * g;
+    if (sgd && !poisoned(perr)) W2[i] = w - lr * g;
     else if (sys) xf_store(gW2, (int64_t)i, g);
     else gW2[i] = g;
   }
@@ -359,14 +377,18 @@ struct EpiW1 {
   float* b1;
   float* gb1;
   int sys;  // gradients into a peer-visible IPC buffer (write-through)
+  const int* ag_err;  // the step's forward timed out: no update (the gradient goes to gW1, unused)
+  int perr = 0;
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
     // (the all-ones feature column P: b1[row], so its update is not a dependent load after the K loop)
     if (col == P) pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
     else pre[q] = buf_load1<float>(make_rsrc(W1), (ok && col < P) ? (row * P + col) * 4 : kOOB);
+    if (q == 0) perr = ag_err_load(ag_err);
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
+    const bool upd = sgd && !poisoned(perr);
     if (col == P) {  // the all-ones feature: db1[row] (no input scale, no regulariser)
-      if (sgd) b1[row] = pre[q] - lr * v;
+      if (upd) b1[row] = pre[q] - lr * v;
       else if (sys) xf_store(gb1, row, v);
       else gb1[row] = v;
       return;
@@ -374,7 +396,7 @@ struct EpiW1 {
     const size_t i = (size_t)row * P + col;
     const float w = pre[q];
     const float g = v * xscale + reg * w;
-    if (sgd) {
+    if (upd) {
       const float nw = w - lr * g;
       W1[i] = nw;
       if (npw == 3) split_store<3>(nw, W1p, plane, i);
@@ -404,13 +426,13 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     TileGeom g{r1, a.P + a.bias_col, a.n, a.w1_row0 + (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
     float *gw = a.gW1, *gb = a.gb1;
     // fused: gradients straight into this step's half of the IPC buffer (unless this rank is in error)
-    const bool live = fused && xf_begin(a.xf, bid, s_xf);
+    const bool live = fused && xf_begin(a.xf, bid, s_xf, a.ag_err);
     if (live) {
       gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(s_xf[0] & 1u) * a.xf.npad;
       gb = gw + a.xf.off_b1;
     }
     EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.w1_planes ? a.npw : 0, reg, lr,
-              a.xscale, {}, a.b1, gb, live ? 1 : 0};
+              a.xscale, {}, a.b1, gb, live ? 1 : 0, a.ag_err};
     constexpr int U = 4;
     if constexpr (AF)
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, 3, uint8_t>(a.dZ1, a.ld, static_cast<const uint8_t*>(a.XT),
@@ -438,6 +460,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       }
       xf_end(a.xf, bid, s_xf);
     }
+    mark_status(a, epi.perr);
     return;
   }
   wgrad_roles(a, bid, t1, t2, red, s_xf);
@@ -457,10 +480,10 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     const int tb = bid - t1;
     TileGeom g{a.C, a.H, a.n, 0, tb * 16};
     float* gw = a.gW2;
-    const bool live = fused && xf_begin(a.xf, bid, s_xf);
+    const bool live = fused && xf_begin(a.xf, bid, s_xf, a.ag_err);
     const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf.npad;
     if (live) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
-    EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, live ? 1 : 0, reg, lr, {}};
+    EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, live ? 1 : 0, reg, lr, {}, a.ag_err};
     if (a.dw2part) {  // the head's per-column-tile partials, summed in tile order (16 rows x C classes)
       const int nct = (a.n + a.dw2_cols - 1) / a.dw2_cols, e = threadIdx.x, c = e >> 4, h = tb * 16 + (e & 15);
       const bool ok = e < 256 && c < a.C && h < a.H;
@@ -511,11 +534,12 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
   const bool first = row < a.H;
   const float* src = first ? a.dZ1 + (size_t)row * a.ld : a.D + (size_t)(row - a.H) * a.ld;
   const float bpre = buf_load1<float>(make_rsrc(first ? a.b1 : a.b2), (first ? row : row - a.H) * 4);
+  const int perr = ag_err_load(a.ag_err);
   const float s = wave_sum(row_sum(src, a.n, lane));
   if (lane == 0) {
     float* bp = first ? a.b1 : a.b2;
     const int r = first ? row : row - a.H;
-    if (a.sgd) bp[r] = bpre - lr * s;
+    if (a.sgd && !poisoned(perr)) bp[r] = bpre - lr * s;
     else (first ? a.gb1 : a.gb2)[r] = s;
   }
 }
@@ -530,7 +554,9 @@ __global__ __launch_bounds__(256) void planes_kernel(const float* __restrict__ W
 template <int NP>
 __global__ __launch_bounds__(256) void sgd_planes_kernel(float* __restrict__ prm, const float* __restrict__ g,
                                                          int64_t n, float lr, bf16* __restrict__ planes,
-                                                         int64_t w1n) {
+                                                         int64_t w1n, const float* __restrict__ status) {
+  // the bucket's status element (summed over the ranks): some rank's step is untrusted -> no update anywhere
+  if (status && __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, *status)) != 0) return;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const float v = prm[i] - lr * g[i];
@@ -615,16 +641,18 @@ struct EpiW1Big {
   float reg, lr, xscale;
   float* b1;
   float* gb1;
+  int perr;  // ag_err, loaded before the K loop: no update when set
   __device__ __forceinline__ void operator()(int row, int col, float v) {
+    const bool upd = sgd && !poisoned(perr);
     if (col == P) {  // all-ones feature row of XT: db1
-      if (sgd) b1[row] -= lr * v;
+      if (upd) b1[row] -= lr * v;
       else gb1[row] = v;
       return;
     }
     const size_t i = (size_t)row * P + col;
     const float w = W1[i];
     const float g = v * xscale + reg * w;
-    if (sgd) {
+    if (upd) {
       const float nw = w - lr * g;
       W1[i] = nw;
       if (npw == 3) split_store<3>(nw, W1p, plane, i);
@@ -656,11 +684,12 @@ __global__ __launch_bounds__(NT) void wgrad_big_kernel(SplitStepArgs a, int tn, 
   }
   const int id = xcd_remap(blockIdx.x, tbig);
   EpiW1Big epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw,
-               (float)a.reg, (float)a.lr, a.xscale, a.b1, a.gb1};
+               (float)a.reg, (float)a.lr, a.xscale, a.b1, a.gb1, ag_err_load(a.ag_err)};
   const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
   lds_gemm_tile<BM, BN, NPZ, uint8_t, EpiW1Big, NT, NKS>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
                                       static_cast<const uint8_t*>(a.XT), a.ldxt, r1, a.P + a.bias_col, a.n,
                                       a.w1_row0 + (id / tn) * BM, (id % tn) * BN, epi, lds_dyn);
+  mark_status(a, epi.perr);
 }
 
 // ---- the same two GEMMs on the direct-to-LDS engine (glds_gemm.h): bf16 copies of X / XT as B.
@@ -687,9 +716,11 @@ __device__ __forceinline__ void st_bf16(__amdgpu_buffer_rsrc_t r, int off, bf16 
 //      D . a1^T (SplitStepArgs::dw2_cols = 128).
 // The hand-off is MI355X_MICROARCH.md's table's first row (sc1 stores drained before one agent add per
 // workgroup, returning-atomic polls, barrier, sc1 loads), one workgroup per CU (the launcher's LDS request
-// and <= 32 workgroups per XCD).  Every workgroup must be resident at once; a wait past kRegaAgSpinLimit sets *err
-// (MlpEngine.kernel_error()) and the workgroup writes nothing more -- the counter still gets both adds, so
-// later launches stay aligned.
+// and <= 32 workgroups per XCD).  Every workgroup must be resident at once; a wait past 2^ag_spin_shift polls
+// sets *err (MlpEngine.kernel_error()) and the workgroup writes nothing more -- the counter still gets both adds,
+// so later launches stay aligned -- and the weight-gradient launch that follows applies nothing (ag_err).
+// Each tiling (128 x 128, 64 x 64) has its own counter array: the wait targets assume that every launch on a
+// counter added 2 tm, and tm differs between the tilings (a partial last batch can switch them).
 struct RegaAgArgs {
   HeadArgs h{};
   unsigned long long* counters = nullptr;  // [column tile * kRegaAgCounterStride], monotonic
@@ -701,7 +732,6 @@ struct RegaAgArgs {
   int xcd_grouped = 0;
 };
 constexpr int kRegaAgCounterStride = 32;  // uint64 words: one 256-byte line per column-tile counter
-constexpr uint32_t kRegaAgSpinLimit = 1u << 22;
 // LDS of the fused head for a BM x BN tile: the D tile [16][BN + 4], the a1 tile [BM][BN + 4] (row pitch BN + 4:
 // conflict-free MFMA-layout reads), z2 [16][17], loss [16], 2 flags
 template <int BM, int BN>
@@ -710,11 +740,12 @@ constexpr int wide_ag_lds_bytes() {
 }
 
 // one lane: 1 when the counter did not reach `target` within the spin bound (and *err is set)
-__device__ __forceinline__ int rega_ag_wait(unsigned long long* cnt, unsigned long long target, int* err) {
+__device__ __forceinline__ int rega_ag_wait(unsigned long long* cnt, unsigned long long target, int* err,
+                                            uint32_t limit) {
   uint32_t spins = 0;
   // polled with a returning atomic (add 0): served where the adds are performed, never a stale L2 copy
   while (__hip_atomic_fetch_add(cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (++spins > kRegaAgSpinLimit) {
+    if (++spins > limit) {
       atomicExch(err, 1);
       return 1;
     }
@@ -760,10 +791,13 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
   __syncthreads();  // (and every read of the z2 reduction scratch in lds is done)
   unsigned long long* cnt = g.counters + (size_t)ct * kRegaAgCounterStride;
   unsigned long long base = 0;
+  const uint32_t limit = 1u << a.ag_spin_shift;
   if (t == 0) {
-    const unsigned long long old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (test hook: one workgroup of column tile 0 leaves its first add out -- that tile's wait times out)
+    const unsigned long long inc = (a.ag_test_skip == rt && ct == 0) ? 0ull : 1ull;
+    const unsigned long long old = __hip_atomic_fetch_add(cnt, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     base = old / (2ull * (unsigned)tm) * (2ull * (unsigned)tm);
-    sflag[0] = rega_ag_wait(cnt, base + (unsigned)tm, g.err);
+    sflag[0] = rega_ag_wait(cnt, base + (unsigned)tm, g.err, limit);
   }
   __syncthreads();
   const bool bad1 = sflag[0] != 0;
@@ -827,7 +861,7 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
   __syncthreads();
   if (t == 0) {
     __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (also after a timeout)
-    sflag[1] = bad1 ? 1 : rega_ag_wait(cnt, base + 2ull * (unsigned)tm, g.err);
+    sflag[1] = bad1 ? 1 : rega_ag_wait(cnt, base + 2ull * (unsigned)tm, g.err, limit);
   }
   __syncthreads();
   if (sflag[1]) return;  // workgroup-uniform
@@ -1044,12 +1078,14 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
         w[mb][nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
       }
     }
+  const int perr = ag_err_load(a.ag_err);  // the step's forward timed out: no update
   f32x4 acc[MB][NB];
   glds_gemm_mainloop<BM, BN, NPZ>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
                                   static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0, n0, lds_dyn,
                                   acc);
   const size_t plane = (size_t)a.H * P;
   const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
+  const bool upd = a.sgd && !poisoned(perr);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
@@ -1062,7 +1098,7 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
         const int idx = row * P + col;
         const float wv = w[mb][nb][i];
         const float g = v * xs + reg * wv;
-        if (a.sgd) {
+        if (upd) {
           const float nw = wv - lr * g;
           st_f32(rW, in ? idx * 4 : kOOB, nw);
           float r = nw;
@@ -1076,10 +1112,11 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
           st_f32(rg, in ? idx * 4 : kOOB, g);
         }
         if (a.bias_col && col == P && row < M) {  // all-ones feature: db1 (no input scale, no regulariser)
-          if (a.sgd) a.b1[row] = bb[mb][i] - lr * v;
+          if (upd) a.b1[row] = bb[mb][i] - lr * v;
           else a.gb1[row] = v;
         }
       }
+  mark_status(a, perr);
 }
 
 // a1 = sigmoid(W1 X + b1) on the A-in-registers engine (rega_gemm.h): W1 read as fp32 and split into the
@@ -1216,12 +1253,14 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
         w[mb][nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
       }
     }
+  const int perr = ag_err_load(a.ag_err);  // the step's forward timed out: no update
   f32x4 acc[MB][NB];
   const AT* A = NP == 3 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
   rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n,
                                        m0, n0, lds_dyn, acc);
   const size_t plane = (size_t)a.H * P;
   const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
+  const bool upd = a.sgd && !poisoned(perr);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
@@ -1234,7 +1273,7 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
         const int idx = row * P + col;
         const float wv = w[mb][nb][i];
         const float g = v * xs + reg * wv;
-        if (a.sgd) {
+        if (upd) {
           const float nw = wv - lr * g;
           st_f32(rW, in ? idx * 4 : kOOB, nw);
           float r = nw;
@@ -1248,10 +1287,11 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
           st_f32(rg, in ? idx * 4 : kOOB, g);
         }
         if (a.bias_col && col == P && row < M) {  // all-ones feature: db1
-          if (a.sgd) a.b1[row] = bb[mb][i] - lr * v;
+          if (upd) a.b1[row] = bb[mb][i] - lr * v;
           else a.gb1[row] = v;
         }
       }
+  mark_status(a, perr);
 }
 
 template <auto Kern>
@@ -1536,7 +1576,8 @@ int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long lo
   CME_REQUIRE(counters && err && cdiv(a.n, bm) <= max_tiles, "fwd1_wide_ag: counter array too small");
   RegaAgArgs g;
   g.h = h;
-  g.counters = counters;
+  // [2][max_tiles][kRegaAgCounterStride]: the 64 x 64 tiling's counters after the 128 x 128 tiling's
+  g.counters = counters + (bm == 64 ? (size_t)max_tiles * kRegaAgCounterStride : 0);
   g.err = err;
   g.store_a1 = store_a1;
   g.tm = cdiv(a.H, bm);
@@ -1681,13 +1722,13 @@ void mlp_split_planes(const float* W, void* planes, int64_t n, int np, hipStream
 }
 
 void mlp_split_sgd(float* params, const float* grads, int64_t count, double lr, void* W1p, int64_t w1_count,
-                   int npw, hipStream_t s) {
+                   int npw, hipStream_t s, const float* status) {
   if (count <= 0) return;
   const int grid = (int)std::min<int64_t>(2048, (count + 255) / 256);
   if (npw == 3)
-    sgd_planes_kernel<3><<<grid, 256, 0, s>>>(params, grads, count, (float)lr, (bf16*)W1p, w1_count);
+    sgd_planes_kernel<3><<<grid, 256, 0, s>>>(params, grads, count, (float)lr, (bf16*)W1p, w1_count, status);
   else
-    sgd_planes_kernel<1><<<grid, 256, 0, s>>>(params, grads, count, (float)lr, (bf16*)W1p, w1_count);
+    sgd_planes_kernel<1><<<grid, 256, 0, s>>>(params, grads, count, (float)lr, (bf16*)W1p, w1_count, status);
   CME_LAUNCH_CHECK(s);
 }
 

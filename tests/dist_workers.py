@@ -354,3 +354,48 @@ def multigpu_dp_main(out_dir, world, modes, scalings, steps, backend):
     from cme213_sp18_amd.parallel.launcher import spawn
 
     spawn(multigpu_dp_worker, world, (out_dir, modes, scalings, steps), backend=backend)
+
+
+def handoff_timeout_dp_worker(rank, world, comm, device, out_dir, allreduce):
+    """A REAL timed-out all-gather forward + head launch on rank 0 only (MlpEngine.inject_handoff_timeout)
+    in data-parallel training, 2 ranks sharing GPU 0: no rank applies that step or any later one (rank 0's
+    weight-gradient launch reads the sticky error word; it marks the gradient bucket's status element, which
+    the all-reduce carries to every rank's SGD, or -- xGMI fused -- stops taking part so rank 1's waits time
+    out), and train() raises KernelHandoffTimeout on BOTH ranks."""
+    from cme213_sp18_amd import NeuralNetwork
+    from cme213_sp18_amd.parallel import DataParallelTrainer
+    from cme213_sp18_amd.parallel.trainer import KernelHandoffTimeout
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    x, y = synthetic_mnist(3200, seed=3)
+    tr = DataParallelTrainer(NeuralNetwork([784, 100, 10]), comm=comm, device=dev, batch_size=1600,
+                             allreduce=allreduce)
+    tr.engine.set_fh_allgather(True)  # (off by default when ranks share a GPU; both launches fit here)
+    tr.load(x, y)
+    res = {"impl": tr.allreduce_impl}
+    tr.train(1, 0.05, 1e-4)  # a clean epoch on both ranks
+    torch.cuda.synchronize()
+    res["clean_err"] = float(tr.engine.kernel_error())
+    comm.barrier()
+    if rank == 0:
+        tr.engine.inject_handoff_timeout(0, 12)
+    before = (tr.engine.params.clone(), tr.engine.W1p.clone())
+    try:
+        tr.train(1, 0.05, 1e-4)
+        res["raised"] = 0.0
+    except KernelHandoffTimeout:
+        res["raised"] = 1.0
+    torch.cuda.synchronize()
+    res["local_err"] = float(tr.engine.kernel_error())
+    res["untouched"] = float(torch.equal(tr.engine.params, before[0]) and torch.equal(tr.engine.W1p, before[1]))
+    tr.close()
+    np.savez(os.path.join(out_dir, f"handoff_{allreduce}_{rank}.npz"),
+             **{k: np.array(v) for k, v in res.items()})
+
+
+def handoff_timeout_dp_main(out_dir, allreduce):
+    from cme213_sp18_amd.parallel.launcher import spawn
+
+    spawn(handoff_timeout_dp_worker, 2, (out_dir, allreduce), backend="gloo")

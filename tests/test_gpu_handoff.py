@@ -1,0 +1,141 @@
+"""Failure semantics of the in-launch hand-offs (the all-gather forward + head launches) on the GPU.
+
+The forward + head launch waits, inside the kernel, for the other workgroups of its column tile (H <= 128:
+csrc/mlp/fha_body.h; wide layers: mlp_split.hip wide_head_ag).  A wait that outlasts its bound sets a sticky
+error word; the weight-gradient launch reads that word and APPLIES NOTHING, and train() raises
+KernelHandoffTimeout -- on every rank (a failing rank must take the job down, not leave it hung
+or let the replicas diverge; the reference only ``exit(1)``s, fpcode/neural_network.cpp:9-15).  Here the
+timeout is REAL: MlpEngine.inject_handoff_timeout makes one workgroup of column tile 0 leave its counter add
+out, so that tile's wait expires.  Also pinned: the wide fused head's counters stay consistent when a partial
+batch switches the launch between its 128 x 128 and 64 x 64 tilings (each tiling has its own counters).
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from cme213_sp18_amd import NeuralNetwork
+from cme213_sp18_amd.parallel import DataParallelTrainer, MlpEngine
+from cme213_sp18_amd.parallel.trainer import KernelHandoffTimeout
+from cme213_sp18_amd.utils.data import synthetic_mnist
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# (dtype, H, n): the H <= 128 form, the 128 x 128 wide form (H = 4096, n = 800), the 64 x 64 wide form
+CASES = [("f32", 100, 800), ("bf16", 100, 800), ("f32", 100, 37), ("f32", 4096, 800), ("bf16", 1024, 800),
+         ("f32", 4096, 200)]
+
+
+def _engine(dt, H, n, N=None):
+    x, y = synthetic_mnist(N or 3 * n + 64, seed=H + n)
+    nn = NeuralNetwork([784, H, 10])
+    e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda")
+    e.set_params(*nn.params)
+    e.load_dataset(x, y)
+    e.set_store_a1(False)  # the trainer's setting: the wide fused head's measured form
+    return e
+
+
+@pytest.mark.parametrize("dt,H,n", CASES)
+def test_forced_handoff_timeout_applies_nothing(dt, H, n):
+    """A step whose forward + head launch really timed out leaves params and the W1 planes bitwise as they
+    were (sgd=1: the fused update is skipped); so does every later step (the error word is sticky); in
+    gradient mode (sgd=0) the bucket's status element is 1 and the separate SGD kernel changes nothing."""
+    e = _engine(dt, H, n)
+    e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=True)  # one good step
+    torch.cuda.synchronize()
+    assert not e.kernel_error()
+    moved = e.params.clone()
+    e.run(n, n, 1.0 / n, 1e-4, 0.05, sgd=False)
+    torch.cuda.synchronize()
+    assert float(e.grads[e.status_index]) == 0.0  # a trusted step's status
+    before = (e.params.clone(), e.W1p.clone())
+    assert torch.equal(before[0], moved)
+    e.inject_handoff_timeout(0, 12)
+    e.run(n, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+    torch.cuda.synchronize()
+    assert e.kernel_error(), "the forced hand-off did not time out"
+    assert torch.equal(e.params, before[0]) and torch.equal(e.W1p, before[1])
+    e.inject_handoff_timeout(-1)
+    e.run(2 * n, n, 1.0 / n, 1e-4, 0.05, sgd=True)  # sticky: nothing after the timeout is applied either
+    e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=False)
+    torch.cuda.synchronize()
+    assert torch.equal(e.params, before[0]) and torch.equal(e.W1p, before[1])
+    assert float(e.grads[e.status_index]) == 1.0
+    e.sgd(0.05)  # the separate SGD kernel honours the status element
+    torch.cuda.synchronize()
+    assert torch.equal(e.params, before[0]) and torch.equal(e.W1p, before[1])
+
+
+@pytest.mark.parametrize("H", [100, 4096])
+def test_real_timeout_raises_in_train_and_freezes_params(H):
+    """train() (native step loop) after a real timed-out hand-off: KernelHandoffTimeout at the end of the
+    epoch, and not one of the epoch's steps changed a parameter."""
+    x, y = synthetic_mnist(3200, seed=2)
+    tr = DataParallelTrainer(NeuralNetwork([784, H, 10]), dtype="f32", batch_size=800)
+    tr.load(x, y)
+    tr.train(1, 0.01, 1e-4)
+    assert tr._allgather_live() and not tr.engine.kernel_error()
+    tr.engine.inject_handoff_timeout(1, 12)
+    before = tr.engine.params.clone()
+    with pytest.raises(KernelHandoffTimeout):
+        tr.train(1, 0.01, 1e-4)
+    assert torch.equal(tr.engine.params, before)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_wide_head_counters_survive_tiling_switch(dt):
+    """One engine alternating per-GPU batches that take the 128 x 128 tiling (n = 800) and the 64 x 64
+    tiling (n = 200) of the wide fused head, H = 4096: every step agrees with the plain forward + head
+    launches (to fp32 rounding of the dW2 partial sums) and no wait timed out -- with ONE shared counter
+    array the 64 x 64 launch after an 800-column launch computed its wait target from the other tiling's
+    count and read unpublished partials."""
+    H, N = 4096, 2400
+    x, y = synthetic_mnist(N, seed=17)
+    nn = NeuralNetwork([784, H, 10])
+    outs = []
+    for ag in (True, False):
+        e = MlpEngine(nn.H, dtype=dt, max_cols=800, device="cuda")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        e.set_store_a1(False)
+        e.set_fh_allgather(ag)
+        e._hip_step().ag_tiles64 = 1
+        for off, n in ((0, 800), (800, 200), (1000, 800), (1800, 200), (0, 200), (200, 800)):
+            e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+        torch.cuda.synchronize()
+        if ag:
+            assert not e.kernel_error()
+            c = e.ag_counters.view(2, -1, 32)[:, :, 0]
+            t128, t64 = (800 + 127) // 128, (800 + 63) // 64
+            assert c[0, :t128].tolist() == [2 * 32 * 3] * t128  # three 800-column launches, tm = 32
+            assert c[1, :(200 + 63) // 64].tolist() == [2 * 64 * 3] * ((200 + 63) // 64)  # tm = 64
+            assert int(c[1, (200 + 63) // 64:t64].sum()) == 0
+        outs.append(e.params.clone())
+    rel = float((outs[0] - outs[1]).abs().max() / outs[1].abs().max())
+    assert rel < (1e-5 if dt == "f32" else 1e-3), rel
+
+
+@pytest.mark.parametrize("allreduce", ["rccl", "xgmi"])
+def test_handoff_timeout_on_one_rank_stops_every_rank(tmp_path, allreduce):
+    """2 data-parallel ranks sharing the GPU, rank 0's hand-off really times out: both ranks raise
+    KernelHandoffTimeout and neither applied a step of that epoch.  rccl here is the gloo all-reduce of the
+    gradient bucket (its status element carries the failure to the other rank's SGD); xgmi is the all-reduce
+    fused into the weight-gradient launch (the failed rank stops taking part, rank 1's waits time out)."""
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); from tests.dist_workers import handoff_timeout_dp_main; "
+            f"handoff_timeout_dp_main({str(tmp_path)!r}, {allreduce!r})")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    z = [dict(np.load(tmp_path / f"handoff_{allreduce}_{rank}.npz")) for rank in range(2)]
+    if allreduce == "xgmi":
+        assert str(z[0]["impl"]).startswith("xgmi"), z[0]["impl"]
+    for rank in range(2):
+        assert float(z[rank]["clean_err"]) == 0.0
+        assert float(z[rank]["raised"]) == 1.0, (rank, z[rank])
+        assert float(z[rank]["untouched"]) == 1.0, (rank, z[rank])
+    assert float(z[0]["local_err"]) == 1.0 and float(z[1]["local_err"]) == 0.0
