@@ -271,7 +271,8 @@ def run_tp(a, comm, device, placement, sync) -> int:
     B = a.batch
     x, y = synthetic_mnist(a.train_size, seed=0)
     nn = NeuralNetwork([784, a.hidden, 10])
-    tr = TensorParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=B, backend=a.backend)
+    tr = TensorParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=B, backend=a.backend,
+                               allreduce="rccl" if a.allreduce in ("rccl", "host") else a.allreduce)
     tr.load(x, y)
     full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == B]
     lr, reg = 1e-3, 1e-4
@@ -302,6 +303,23 @@ def run_tp(a, comm, device, placement, sync) -> int:
     sync()
     dt = comm.allreduce_scalar(time.perf_counter() - t0, op="max")
     ok = comm.allreduce_scalar(0.0 if bool(torch.isfinite(tr.engine.params).all().item()) else 1.0, op="max") == 0
+    comm_failed = tr.comm_failed()
+    ok = ok and not comm_failed
+    ar = {"allreduce_us": None}
+    if R > 1 and ok:  # the step's z2 all-reduce on its own (same implementation and bytes), max over ranks
+        fn = (lambda: tr._xz.allreduce_(tr.z2)) if tr._xz is not None else (lambda: comm.allreduce_(tr.z2))
+        for _ in range(3):
+            fn()
+        sync()
+        comm.barrier()
+        sync()
+        t1 = time.perf_counter()
+        for _ in range(20):
+            fn()
+        sync()
+        us = comm.allreduce_scalar(1e6 * (time.perf_counter() - t1) / 20, op="max")
+        ar = {"allreduce_us": round(us, 2), "allreduce_bytes": int(tr.z2.numel() * 4)}
+    tr.close()
     value = a.steps * B / dt
     if rank == 0:
         print(json.dumps({
@@ -312,7 +330,8 @@ def run_tp(a, comm, device, placement, sync) -> int:
             "data": "synthetic (MNIST-shaped 784-dim uint8 images, random-init weights)",
             "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": B, "seq_len": None,
                        "parallelism": f"tp{R}", "hidden_per_gpu": a.hidden // R, "backend": a.backend,
-                       "hip_graphs": graphs, "params_finite": ok, **placement},
+                       "hip_graphs": graphs, "allreduce": tr.allreduce_impl, "params_finite": ok,
+                       "comm_ok": not comm_failed, **placement, **ar},
         }), flush=True)
     shutdown()
     return 0 if ok else 1

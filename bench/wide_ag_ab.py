@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """A/B of the wide-layer head forms on one GPU: the forward launch + head_wide_kernel ("head") against the
-head fused into the forward launch (mlp_fwd1_wide_ag: "ag", "ag_noa1" without the a1 store, "agx*" on the
-XCD-grouped grid -- 128 x 128 tiles only, else the same launch as "ag*").  Each form: whole training steps (forward + head + wgrad + fused SGD) captured into a HIP graph of
+head fused into the forward launch (mlp_fwd1_wide_ag: "ag", "ag_noa1" without the a1 store).  Each form: whole training steps (forward + head + wgrad + fused SGD) captured into a HIP graph of
 `reps` steps, best of 5 replays, plus the forward + head launch alone (parts=1).  One JSON line per form.
 
     python bench/wide_ag_ab.py [--hidden 4096] [--cols 800] [--cfg f32:split3 bf16:split1]
@@ -55,13 +54,12 @@ def main(argv=None):
         nn = NeuralNetwork([784, H, 10])
         for cfg in a.cfg:
             dt, path = cfg.split(":")
-            for mode in ("head", "ag", "ag_noa1", "agx", "agx_noa1"):
+            for mode in ("head", "ag", "ag_noa1"):
                 e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", path=path)
                 e.set_params(*nn.params)
                 e.load_dataset(x, y)
                 e.set_fh_allgather(mode != "head")
                 e.set_store_a1(not mode.endswith("noa1"))
-                e._hip_step().ag_xcd_grouped = int(mode.startswith("agx"))
                 e._hip_step().ag_tiles64 = 1
                 off = [0]
 

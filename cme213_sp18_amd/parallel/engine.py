@@ -167,7 +167,7 @@ class MlpEngine:
         # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
         # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
         self.fh_counters = None
-        self.ag_counters = self.ag_slabs = self.ag_err = None
+        self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = None
         if self.backend == "hip" and self.np and H <= 128 and C <= 16:
             tiles = (ld + 31) // 32
             self.fh_counters = torch.zeros(tiles, dtype=torch.int32, device=dev)
@@ -183,6 +183,9 @@ class MlpEngine:
             tiles = (ld + 31) // 32
             self.ag_counters = torch.zeros(2 * tiles * 32, dtype=torch.int64, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
+            # its hand-off granules: 8-byte {value, epoch} z2 partials [H/64][16][ld] and D [16][ld] (tags only
+            # grow, so the buffer is never re-zeroed)
+            self.ag_gran = torch.zeros(((H + 63) // 64 * 16 + 16) * ld, dtype=torch.int64, device=dev)
         self._step = None
 
     def load_dataset(self, x, labels, normalize: bool = False):
@@ -343,6 +346,7 @@ class MlpEngine:
                 s.fh_allgather = int(self.fh_allgather)
             elif self.ag_counters is not None:
                 s.fh_tiles = int(self.ag_counters.numel()) // 64  # [2 tilings][tiles][32]
+                s.ag_gran, s.ag_gran_count = self.ag_gran.data_ptr(), int(self.ag_gran.numel())
                 s.ag_counters = self.ag_counters.data_ptr()
                 s.ag_err = self.ag_err.data_ptr()
                 s.fh_allgather = int(self.fh_allgather)

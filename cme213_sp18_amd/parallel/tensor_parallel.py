@@ -13,10 +13,13 @@ SUM of the output pre-activations z2 (C x batch = 32 KB at batch 800), because
     db2  = D 1                                                       (identical on every rank)
 
 so there is no gradient all-reduce at all and every rank processes the FULL global batch.  On MI355X the
-z2 partials come for free out of the forward LDS GEMM's tile epilogue (EpiSigBig::tile, H_r >= 512), the
-32 KB all-reduce rides RCCL over xGMI, and the head / weight-gradient kernels are the data-parallel
-engine's (MlpStep.tp_forward / tp_head / run(parts=2)).  f64 and the torch backend run the same
-algorithm in PyTorch ops (CPU-testable with gloo / LoopbackComm).
+z2 partials come for free out of the forward GEMM's tile epilogue (H_r >= 512), the z2 all-reduce (16 x B
+fp32: 410 KB at B = 6400) goes through the xGMI one-shot kernel (parallel/xgmi.py, one launch that pulls the
+R - 1 peer buffers over the point-to-point links -- latency-bound at this size, where a ring pays R - 1 hops)
+or RCCL, and the head / weight-gradient kernels are the data-parallel engine's (MlpStep.tp_forward / tp_head
+/ run(parts=2)).  f64 and the torch backend run the same algorithm in PyTorch ops (CPU-testable with gloo /
+LoopbackComm).  This is the chosen plan for BASELINE config 4 (784-4096-10, 8 GPUs): one 410 KB all-reduce per
+step instead of data parallelism's 13 MB gradient all-reduce (docs/PERFORMANCE.md, Communication policy).
 """
 from __future__ import annotations
 
@@ -35,7 +38,7 @@ class TensorParallelTrainer:
 
     def __init__(self, nn, comm: Communicator | None = None, device=None, dtype: str = "f32",
                  batch_size: int = 800, backend: str = "hip", shift: bool = True, normalize: bool = False,
-                 path: str = "auto"):
+                 path: str = "auto", allreduce: str = "auto"):
         self.nn = nn
         self.comm = comm or NullComm()
         self.R, self.rank = self.comm.world_size, self.comm.rank
@@ -60,7 +63,53 @@ class TensorParallelTrainer:
         self._graphs: dict = {}
         self.use_graphs = True
         self.profiler = None
-        self.allreduce_impl = f"z2 all-reduce ({self.comm.name})" if self.R > 1 else "none"
+        # the z2 all-reduce: the xGMI one-shot kernel (allreduce auto / xgmi) when every rank is a GPU of this
+        # node, else the communicator's (RCCL / gloo)
+        self._xz = self._setup_xgmi(allreduce)
+        self.allreduce_impl = "none" if self.R == 1 else (
+            "xgmi-z2" if self._xz is not None else f"z2 all-reduce ({self.comm.name})")
+
+    def _setup_xgmi(self, mode: str):
+        from .comm import TorchDistComm
+
+        if mode not in ("auto", "xgmi", "rccl"):
+            raise ValueError("allreduce must be auto, xgmi or rccl")
+        e = self.engine
+        ok = (self.R > 1 and isinstance(self.comm, TorchDistComm) and e.device.type == "cuda" and e.backend == "hip"
+              and e.np and self.z2.dtype == torch.float32)
+        if mode == "rccl" or not ok:
+            if mode == "xgmi" and not ok:
+                raise RuntimeError("the xGMI z2 all-reduce needs >1 GPU ranks on the hip split path")
+            return None
+        from .xgmi import XgmiBucket, same_node
+
+        if mode == "auto" and not same_node(self.R):
+            return None
+        try:
+            xb = XgmiBucket(self.comm.group, self.rank, self.R, self.z2.numel(), torch.float32, e.device)
+        except Exception as ex:  # every rank fails at the same point (collective set-up)
+            if mode == "xgmi":
+                raise
+            print(f"[rank {self.rank}] xgmi z2 all-reduce unavailable ({ex}); using {self.comm.name}", flush=True)
+            return None
+        if not xb.ok:
+            xb.close()
+            if mode == "xgmi":
+                raise RuntimeError("xgmi z2 all-reduce self-test failed")
+            return None
+        return xb
+
+    def comm_failed(self) -> bool:
+        """Collective: True on every rank when any rank's xGMI peer wait timed out."""
+        local = self._xz is not None and self._xz.error() != 0
+        return local if self.R == 1 else self.comm.allreduce_scalar(1.0 if local else 0.0, op="max") > 0
+
+    def close(self) -> None:
+        """Collective: release the xGMI IPC bucket (every rank must call it)."""
+        if self._xz is not None:
+            self._xz.close()
+            self._xz = None
+        self._graphs.clear()
 
     # ------------------------------------------------------------------ params
     def _set_shard(self, W1, b1, W2, b2):
@@ -121,7 +170,9 @@ class TensorParallelTrainer:
             self.z2[:, :n] = zp[:chunks * 16 * ld].view(chunks, 16, ld)[:, :, :n].sum(0)
         else:  # narrow shard (the wave-split-K forward): z2 partial through hipBLAS
             self.z2[:C, :n] = e.W2 @ e.a1[:, :n]
-        if self.R > 1:
+        if self._xz is not None:
+            self._xz.allreduce_(self.z2)
+        elif self.R > 1:
             self.comm.allreduce_(self.z2)
         st.tp_head(int(off), int(n), 1.0 / n, int(bool(with_loss)), self.z2.data_ptr(), stream)
         # local weight gradients + SGD (db1 from the all-ones feature column, dW2 / db2 roles)
@@ -170,7 +221,8 @@ class TensorParallelTrainer:
 
     # ------------------------------------------------------------------ graphs
     def graphs_usable(self, use_graphs: bool = True) -> bool:
-        return bool(use_graphs and self.engine.device.type == "cuda" and (self.R == 1 or self.comm.graph_capturable))
+        return bool(use_graphs and self.engine.device.type == "cuda"
+                    and (self.R == 1 or self.comm.graph_capturable or self._xz is not None))
 
     def capture(self, plan: EpochPlan, lr: float, reg: float) -> torch.cuda.CUDAGraph:
         """Capture every step of ``plan`` into one HIP graph (state-neutral warm-up first); cached."""

@@ -126,7 +126,8 @@ def run(cfg: TrainConfig) -> dict:
                 cfg.debug = False
             tr = TensorParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,
                                        backend=backend, shift=cfg.softmax_shift, normalize=cfg.normalize,
-                                       path=cfg.path)
+                                       path=cfg.path,
+                                       allreduce=cfg.allreduce if cfg.allreduce in ("auto", "xgmi") else "rccl")
             tr.use_graphs = cfg.use_graphs
         else:
             tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,

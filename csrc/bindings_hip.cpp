@@ -67,7 +67,9 @@ struct MlpStep {
   // mlp_fwd1_wide_ag) leaves dW2 partials per 128 / 64 columns (32 from head_wide_kernel): what run_wgrad sums
   int dw2_cols_last = 32;
   int store_a1 = 1;  // the fused wide head: 0 skips the a1 store (nothing in the step reads it)
-  int ag_xcd_grouped = 0;  // the fused wide head's grid: 1 = each column tile on one XCD (RegaAgArgs)
+  // the fused wide head's hand-off granules ([cdiv(H, 64)][16][ld] z2 partials, then [16][ld] D; uint64)
+  uintptr_t ag_gran = 0;
+  int64_t ag_gran_count = 0;
   // the fused wide head on the 64 x 64 tiling (H = 512-1024): -1 = when a1 is not stored (measured faster only
   // then: profiles/wide_fused_head_r2.md), 1 = always, 0 = never
   int ag_tiles64 = -1;
@@ -191,11 +193,11 @@ struct MlpStep {
               h.dw2part = P_<float>(dw2p);
               a.dw2part = h.dw2part;
             }
-            if (fh_allgather && ag_counters && ag_err && h.dw2part && !(parts & 12) &&
+            if (fh_allgather && ag_counters && ag_err && ag_gran && h.dw2part && !(parts & 12) &&
                 cme::mlp_fwd1_wide_ag_ok(f, h, ag64())) {  // one launch: forward GEMM + the all-gather head
               a.dw2_cols = cme::mlp_fwd1_wide_ag(f, h, P_<unsigned long long>(ag_counters), fh_tiles,
-                                                 P_<int>(ag_err), store_a1, ag_xcd_grouped, ag64(),
-                                                 S(stream));
+                                                 P_<unsigned long long>(ag_gran), ag_gran_count, P_<int>(ag_err),
+                                                 store_a1, ag64(), S(stream));
             } else {
               if (!(parts & 8)) cme::mlp_split_fwd1(f, S(stream));
               if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
@@ -435,7 +437,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_spin_shift", &MlpStep::ag_spin_shift)
       .def_readwrite("ag_test_skip", &MlpStep::ag_test_skip)
       .def_readwrite("store_a1", &MlpStep::store_a1)
-      .def_readwrite("ag_xcd_grouped", &MlpStep::ag_xcd_grouped)
+      .def_readwrite("ag_gran", &MlpStep::ag_gran)
+      .def_readwrite("ag_gran_count", &MlpStep::ag_gran_count)
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
       .def_readwrite("a_fp32", &MlpStep::a_fp32)
       .def("w1_planes_read",

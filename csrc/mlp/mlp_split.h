@@ -125,12 +125,15 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s);
 // tiles, fwd1_glds_kernel<64, 64, ..., AG> on 64 x 64): one launch leaves a1 (store_a1), D, the loss partials,
 // dZ1 (fp32 and / or planes) and the dW2 partials per column tile (h.dw2part).  Returns the tile width: the
 // weight-gradient launch then needs a.dw2_cols = it.  Every workgroup must be resident at once (off when
-// processes share a GPU); a timed-out wait sets *err.  counters: [2][max_tiles][32] uint64 (one array per tiling).
+// processes share a GPU); a timed-out poll sets *err.  counters: [2][max_tiles][32] uint64 (one array per tiling);
+// the hand-offs are data-tagged granules (gran) whose epoch comes from those counters.
 struct HeadArgs;
 // allow64: also the 64 x 64 tiling (MlpStep.ag_tiles64: by default only when a1 is not stored)
 bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64);
+// gran: >= (cdiv(H, 64) * 16 + 16) * ld uint64 granules (z2 partials, then D), tags never reused
 int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long long* counters, int max_tiles,
-                     int* err, int store_a1, int xcd_grouped, int allow64, hipStream_t s);
+                     unsigned long long* gran, int64_t gran_count, int* err, int store_a1, int allow64,
+                     hipStream_t s);
 void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s);
 int mlp_split_fwdhead_blocks(int n);
 

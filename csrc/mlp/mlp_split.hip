@@ -702,56 +702,92 @@ __device__ __forceinline__ void st_bf16(__amdgpu_buffer_rsrc_t r, int off, bf16 
   __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, v), r, off, 0, 0);
 }
 
-// ---- wide layers: the head fused into the A-in-registers forward launch (all-gather form, H >= 1024).
-// Every 128 x 128 a1 tile is still in its workgroup's accumulators when the forward GEMM ends, so instead of
+// ---- wide layers: the head fused into the forward launch (all-gather form, H >= 512).
+// Every BM x BN a1 tile is still in its workgroup's accumulators when the forward GEMM ends, so instead of
 // storing z2 partials for head_wide_kernel to reduce (and re-reading all of a1 there), the tm row-tile
-// workgroups of a column tile hand off twice through one monotonic counter per column tile:
-//   1. every workgroup publishes its z2 partial (sc1 stores above, vmcnt(0), barrier, one agent add), then
-//      waits for the tm adds of this launch;
-//   2. row tile rt < 8 reduces columns n0 + 16 rt .. +15 (the tm partials in tile order, + b2), forms
-//      softmax / D / the loss partial of those 16 columns exactly as head_wide_kernel does (same operation
-//      order: bit-identical D, loss and dZ1), stores D sc1, vmcnt(0), barrier, second add;
-//   3. after the 2 tm adds every workgroup reads the tile's 16 x 128 D (sc1 loads) and forms dZ1 = (W2^T D)
-//      .* a1 .* (1 - a1) for its own 128 x 128 tile on the f32 MFMA, plus the tile's dW2 partial
-//      D . a1^T (SplitStepArgs::dw2_cols = 128).
-// The hand-off is MI355X_MICROARCH.md's table's first row (sc1 stores drained before one agent add per
-// workgroup, returning-atomic polls, barrier, sc1 loads), one workgroup per CU (the launcher's LDS request
-// and <= 32 workgroups per XCD).  Every workgroup must be resident at once; a wait past 2^ag_spin_shift polls
-// sets *err (MlpEngine.kernel_error()) and the workgroup writes nothing more -- the counter still gets both adds,
-// so later launches stay aligned -- and the weight-gradient launch that follows applies nothing (ag_err).
-// Each tiling (128 x 128, 64 x 64) has its own counter array: the wait targets assume that every launch on a
-// counter added 2 tm, and tm differs between the tilings (a partial last batch can switch them).
+// workgroups of a column tile hand off twice, both times through DATA-TAGGED GRANULES -- 8 bytes {value,
+// epoch}, each written by ONE sc1 store (MI355X_MICROARCH.md price list 'handoff-1to1'; cdna_hip_programming.md
+// Guideline 16 R2): the data is its own flag, so a hand-off is one poll that returns the payload, with no
+// store drain, no counter add and no separate payload load behind it.
+//   0. before its K loop every workgroup makes ONE agent-scope add to its column tile's monotonic counter.
+//      Each launch adds exactly tm per tile (every workgroup adds, whatever happens later; one counter array
+//      per tiling, so a partial batch switching 128 x 128 <-> 64 x 64 keeps both aligned), hence the launch
+//      epoch is old / tm + 1, never 0 (a kernel argument cannot carry it: graph replays freeze them); the tag
+//      is 2 epoch + tiling, so the two tilings' launches never accept each other's granules;
+//   1. every workgroup stores its z2 partial as granules tagged with the epoch (RegaAgArgs::z2g);
+//   2. row tile rt < BN / 16 polls the tm partials of its 16 columns until every tag is the epoch, sums them in
+//      tile order (+ b2) and forms softmax / D / the loss partial of those columns exactly as head_wide_kernel
+//      does (same operation order: bit-identical D, loss and dZ1); D goes out as tagged granules (dg) and as
+//      plain fp32 for the weight-gradient launch;
+//   3. every workgroup polls the tile's 16 x BN D granules and forms dZ1 = (W2^T D) .* a1 .* (1 - a1) for its
+//      own tile on the f32 MFMA, plus the tile's dW2 partial D . a1^T (SplitStepArgs::dw2_cols = BN).
+// Every workgroup must be resident at once (one per CU: the launcher's LDS request and tm * tn <= CUs).  A poll
+// that outlasts 2^ag_spin_shift passes sets *err (MlpEngine.kernel_error()) and the workgroup writes nothing
+// more; the weight-gradient launch that follows applies nothing (SplitStepArgs::ag_err).
 struct RegaAgArgs {
   HeadArgs h{};
-  unsigned long long* counters = nullptr;  // [column tile * kRegaAgCounterStride], monotonic
+  unsigned long long* counters = nullptr;  // [column tile * kRegaAgCounterStride], monotonic: the launch epoch
+  unsigned long long* z2g = nullptr;       // z2 partial granules [tm][16][ld]
+  unsigned long long* dg = nullptr;        // D granules [16][ld]
   int* err = nullptr;
   int store_a1 = 1;  // 0: a1 is not stored (nothing after the fused head reads it)
   int tm = 0;        // row tiles
-  // 1: XCD-grouped grid (8 * tm * cdiv(tn, 8) workgroups, each column tile on one XCD); 0: the plain forward's
-  // xcd_remap grid (tm * tn workgroups; a column tile's row tiles span XCDs -- the hand-off crosses L2s)
-  int xcd_grouped = 0;
+  int ep_off = 0;    // LDS byte offset of the epoch + 2 flag words (past every other LDS use of the launch)
+  int tiling = 0;    // 0: 128 x 128, 1: 64 x 64 -- the low bit of every tag (both tilings share the granules)
 };
 constexpr int kRegaAgCounterStride = 32;  // uint64 words: one 256-byte line per column-tile counter
 // LDS of the fused head for a BM x BN tile: the D tile [16][BN + 4], the a1 tile [BM][BN + 4] (row pitch BN + 4:
-// conflict-free MFMA-layout reads), z2 [16][17], loss [16], 2 flags
+// conflict-free MFMA-layout reads), z2 [16][17], loss [16]
 template <int BM, int BN>
 constexpr int wide_ag_lds_bytes() {
-  return (16 * (BN + 4) + BM * (BN + 4) + 16 * 17 + 16 + 4) * 4;
+  return (16 * (BN + 4) + BM * (BN + 4) + 16 * 17 + 16) * 4;
+}
+// the launch's dynamic LDS: > 80 KB keeps it at one workgroup per CU (the hand-off's measured form), and the
+// last 16 bytes hold the epoch and the two timeout flags (no other use reaches them)
+constexpr int wide_ag_launch_lds(int used) { return (used + 16 > 84 * 1024 ? used + 16 : 84 * 1024) / 16 * 16; }
+
+using gran_t = unsigned long long;
+__device__ __forceinline__ void gran_store(gran_t* p, float v, unsigned ep) {  // ONE 8-byte sc1 store
+  __hip_atomic_store(p, ((gran_t)ep << 32) | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ gran_t gran_load(const gran_t* p) {  // sc1 load (L2-served, never a stale L1 line)
+  return __hip_atomic_load(const_cast<gran_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one lane: 1 when the counter did not reach `target` within the spin bound (and *err is set)
-__device__ __forceinline__ int rega_ag_wait(unsigned long long* cnt, unsigned long long target, int* err,
-                                            uint32_t limit) {
-  uint32_t spins = 0;
-  // polled with a returning atomic (add 0): served where the adds are performed, never a stale L2 copy
-  while (__hip_atomic_fetch_add(cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (++spins > limit) {
-      atomicExch(err, 1);
-      return 1;
+// Poll the granules base[off + k * stride] (k < cnt <= N; lanes with !need take no part) until every tag is
+// `ep`, then hand the values to f(k, value) in k order.  The base is uniform and the offsets 32-bit, so each
+// poll is one global_load_dwordx2 sc1 with an SGPR base.  Wave-uniform; false when the wave gave up after
+// `limit` passes (f is then not called).
+template <int N, class F>
+__device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsigned stride, int cnt, bool need,
+                                          unsigned ep, uint32_t limit, F&& f) {
+  // the granule addresses, once: k >= cnt re-reads granule 0 (needed anyway, so its tag check is the same)
+  const gran_t* p[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    p[k] = reinterpret_cast<const gran_t*>(reinterpret_cast<const char*>(base) +
+                                           (off + (k < cnt ? (unsigned)k * stride : 0u)) * 8u);
+  bool done = !need;
+  gran_t x[N];
+  for (uint32_t spins = 0;; ++spins) {
+    if (!done) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) x[k] = gran_load(p[k]);
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < N; ++k) ok &= (unsigned)(x[k] >> 32) == ep;
+      done = ok;
     }
+    if (__all(done)) break;
+    if (spins >= limit) return false;
     __builtin_amdgcn_s_sleep(2);
   }
-  return 0;
+  if (need) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) f(k, k < cnt ? __builtin_bit_cast(float, (unsigned)x[k]) : 0.f);
+  }
+  return true;
 }
 
 __device__ __forceinline__ void ag_wave_sync() {
@@ -760,8 +796,31 @@ __device__ __forceinline__ void ag_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// diagnostics (SplitStepArgs::stamps, bench/stamps_wide_ag.py): thread 0 records s_memrealtime (100 MHz) as
+// stamp i of this workgroup's 8: 0 entry, 1 K loop done, 2 z2 granules stored, 3 hand-off 1 done, 4 D stored
+// (reducers), 5 D arrived, 6 end (stores drained)
+__device__ __forceinline__ void ag_stamp(const SplitStepArgs& a, int i, bool drain = false) {
+  if (!a.stamps) return;
+  if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+}
+
+// kernel entry, thread 0 only: this workgroup's epoch add (the returned count is used after the K loop)
+__device__ __forceinline__ gran_t ag_epoch_add(const RegaAgArgs& g, int ct) {
+  return __hip_atomic_fetch_add(g.counters + (size_t)ct * kRegaAgCounterStride, 1ull, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+}
+// after the K loop, before the first barrier that follows it, thread 0: the epoch + zeroed flags into LDS
+__device__ __forceinline__ void ag_epoch_publish(const RegaAgArgs& g, char* lds, gran_t old) {
+  unsigned* w = reinterpret_cast<unsigned*>(lds + g.ep_off);
+  w[0] = (((unsigned)(old / (unsigned)g.tm) + 1u) << 1) | (unsigned)g.tiling;
+  w[1] = 0u;
+  w[2] = 0u;
+}
+
 // BM x BN tile at (m0, n0); this wave holds a1v[nb][j] = a1(row rw + 4 fg + j, column cw + 16 nb + fr) (16 rows x
 // 16 NB columns); tm row tiles; ct = column tile.  BN / 16 row tiles reduce 16 columns each (tm >= BN / 16).
+// Called after the barrier that follows ag_epoch_publish and the z2 granule stores.
 template <int BM, int BN, int NB>
 __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaAgArgs& g, const f32x4 (&a1v)[NB],
                                              char* lds, int m0, int n0, int rw, int cw, int tm, int ct) {
@@ -774,7 +833,9 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
   float* ts = Ds + 16 * LD;                     // [BM][LD] the a1 tile
   float* zs = ts + BM * LD;                     // [16][17] z2 (+ b2) of the reduced 16 columns
   float* ls = zs + 16 * 17;                         // [16] loss of those columns
-  int* sflag = reinterpret_cast<int*>(ls + 16);
+  unsigned* sw = reinterpret_cast<unsigned*>(lds + g.ep_off);  // [0] epoch, [1] [2] timeout flags
+  const unsigned ep = sw[0];
+  const uint32_t limit = 1u << a.ag_spin_shift;
   // independent loads first: the W2^T operand of dZ1 (class 4 fg + i, row rw + fr), the reducer's labels, b2
   float wv[4];
 #pragma unroll
@@ -786,41 +847,26 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
       make_rsrc(h.labels), (red && t < 16 && u0 + t < n) ? (u0 + t) * 4 : kOOB, 0, 0);
   const int zc = t >> 4, zcol = u0 + (t & 15);
   const float b2v = buf_load1<float>(make_rsrc(h.b2), (red && t < 256 && zc < C) ? zc * 4 : kOOB);
-  // ---- hand-off 1: this tile's z2 partial is published
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
-  __syncthreads();  // (and every read of the z2 reduction scratch in lds is done)
-  unsigned long long* cnt = g.counters + (size_t)ct * kRegaAgCounterStride;
-  unsigned long long base = 0;
-  const uint32_t limit = 1u << a.ag_spin_shift;
-  if (t == 0) {
-    // (test hook: one workgroup of column tile 0 leaves its first add out -- that tile's wait times out)
-    const unsigned long long inc = (a.ag_test_skip == rt && ct == 0) ? 0ull : 1ull;
-    const unsigned long long old = __hip_atomic_fetch_add(cnt, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    base = old / (2ull * (unsigned)tm) * (2ull * (unsigned)tm);
-    sflag[0] = rega_ag_wait(cnt, base + (unsigned)tm, g.err, limit);
-  }
-  __syncthreads();
-  const bool bad1 = sflag[0] != 0;
-  // ---- reduce-scatter: softmax / loss / D of columns u0 .. u0 + 15
-  if (red && !bad1) {
-    if (t < 256) {
-      const bool ok = zc < C && zcol < n;
-      const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
-      constexpr int kBurst = 32;
-      float v[kBurst];
-#pragma unroll
-      for (int k = 0; k < kBurst; ++k)
-        v[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                             rz, (ok && k < tm) ? ((k * 16 + zc) * a.ld + zcol) * 4 : kOOB, 0, kSc1));
-      float zsum = 0.f;
-#pragma unroll
-      for (int k = 0; k < kBurst; ++k) zsum += v[k];
-      for (int k = kBurst; k < tm; ++k)
-        zsum += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                              rz, ok ? ((k * 16 + zc) * a.ld + zcol) * 4 : kOOB, 0, kSc1));
-      zs[zc * 17 + (t & 15)] = zsum + (zc < C ? b2v : 0.f);
+  // ---- hand-off 1 (reducers): the tm z2 partials of (class zc, column zcol), in tile order, 32 per poll
+  if (red && t < 256) {
+    const bool need = zc < C && zcol < n;
+    const unsigned stride = 16u * (unsigned)a.ld;
+    float zsum = 0.f;
+    bool good = true;
+    for (int k0 = 0; k0 < tm && good; k0 += 16)  // the partials summed in tile order, 16 per poll
+      good = gran_poll<16>(g.z2g, (unsigned)(k0 * 16 + zc) * a.ld + zcol, stride, min(16, tm - k0), need, ep, limit,
+                           [&](int, float v) { zsum += v; });
+    if (!good && lane == 0) {
+      atomicExch(g.err, 1);
+      sw[1] = 1u;
     }
-    __syncthreads();
+    zs[zc * 17 + (t & 15)] = zsum + (zc < C ? b2v : 0.f);
+  }
+  __syncthreads();  // (also: every wave's reads of the z2 reduction scratch in lds are done)
+  ag_stamp(a, 3);
+  if (sw[1]) return;  // workgroup-uniform: a partial never arrived
+  // ---- softmax / loss / D of columns u0 .. u0 + 15
+  if (red) {
     if (t < 16) {  // head_wide_kernel's softmax arithmetic, in its order
       const int col = u0 + t;
       const bool ok = col < n;
@@ -839,40 +885,44 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
       const float inv = 1.f / sum, sc = (float)h.scale;
       float lp = 0.f;
       const __amdgpu_buffer_rsrc_t rd = make_rsrc(h.D);
+      const bool hooked = a.ag_test_skip == rt && ct == 0;  // test hook: this tile's D never arrives
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const float y = e[c] * inv;
         if (c == lab) lp = -__logf(y);
         const float d = (ok && c < C) ? (y - (c == lab ? 1.f : 0.f)) * sc : 0.f;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, d), rd,
-                                              (ok && c < C) ? (c * h.ldd + col) * 4 : kOOB, 0, kSc1);
+        st_f32(rd, (ok && c < C) ? (c * h.ldd + col) * 4 : kOOB, d);  // for the weight-gradient launch
+        if (ok && c < C && !hooked) gran_store(g.dg + (size_t)c * a.ld + col, d, ep);
       }
       ls[t] = lp;
     }
     __syncthreads();
+    ag_stamp(a, 4, true);
     if (t == 0 && h.loss_partial) {  // the column head's layout: one partial per 16 columns
       float s = 0.f;
       for (int k = 0; k < 16; ++k) s += ls[k];
       h.loss_partial[u0 / 16] = s;
     }
   }
-  // ---- hand-off 2: D of the reduced columns is published; wait for all tm row tiles' D
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (also after a timeout)
-    sflag[1] = bad1 ? 1 : rega_ag_wait(cnt, base + 2ull * (unsigned)tm, g.err, limit);
-  }
-  __syncthreads();
-  if (sflag[1]) return;  // workgroup-uniform
+  // ---- hand-off 2: the tile's 16 x BN D granules.  Lane t's NDS granules are D rows c = t / BN + q * 512 / BN
+  // of column n0 + t % BN: the needed ones (c < C, column < n) are the first `cnt`
   {
-    const __amdgpu_buffer_rsrc_t rd = make_rsrc(h.D);
+    constexpr int kRowsPerQ = 512 / BN;
+    const int c0 = t / BN, j = t % BN;
+    int cnt = 0;
 #pragma unroll
-    for (int q = 0; q < NDS; ++q) {
-      const int e = t + 512 * q, c = e / BN, j = e % BN, col = n0 + j;
-      Ds[c * LD + j] = __builtin_bit_cast(
-          float, __builtin_amdgcn_raw_buffer_load_b32(rd, (c < C && col < n) ? (c * h.ldd + col) * 4 : kOOB, 0, kSc1));
+    for (int q = 0; q < NDS; ++q) cnt += (c0 + kRowsPerQ * q < C && n0 + j < n) ? 1 : 0;
+    float v[NDS];
+#pragma unroll
+    for (int q = 0; q < NDS; ++q) v[q] = 0.f;
+    const bool good = gran_poll<NDS>(g.dg, (unsigned)c0 * a.ld + n0 + j, (unsigned)(kRowsPerQ * a.ld), cnt, cnt > 0,
+                                     ep, limit, [&](int q, float x) { v[q] = x; });
+    if (!good && lane == 0) {
+      atomicExch(g.err, 1);
+      sw[2] = 1u;
     }
+#pragma unroll
+    for (int q = 0; q < NDS; ++q) Ds[(c0 + kRowsPerQ * q) * LD + j] = q < cnt ? v[q] : 0.f;
   }
   // this wave's a1 block into the row-major a1 tile, for the dW2 partial's B operand
 #pragma unroll
@@ -880,6 +930,8 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
 #pragma unroll
     for (int j = 0; j < 4; ++j) ts[(rw - m0 + 4 * fg + j) * LD + cw - n0 + 16 * nb + fr] = a1v[nb][j];
   __syncthreads();
+  ag_stamp(a, 5);
+  if (sw[2]) return;  // workgroup-uniform: the tile's D never arrived
   if (h.dw2part && wave < BM / 16) {
     // P[c][row m0 + 16 wave + fr] = sum over the tile's BN columns of D[c][col] a1[row][col] (head_wide_kernel's
     // chain over BN columns instead of 32): A = D, B = the row-major a1 rows
@@ -956,6 +1008,10 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
       }
     }
   }
+  if (a.stamps) {
+    __syncthreads();
+    ag_stamp(a, 6, true);
+  }
 }
 
 // a1 = sigmoid(W1 X + b1) and (z2p != nullptr) the head's z2 partials of this tile's rows:
@@ -971,7 +1027,10 @@ __global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn,
   const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
   const int rw = m0 + wr * G::WM, cw = n0 + wc * G::WN;  // this wave's first row / column
   const int H = a.H, n = a.n, C = a.C;
-  const bool z2 = a.z2part != nullptr;
+  const bool z2 = a.z2part != nullptr || AG;
+  gran_t ep_old = 0;  // the fused head's launch epoch (wide_head_ag step 0): one add per workgroup, now
+  if (AG && threadIdx.x == 0) ep_old = ag_epoch_add(ag, n0 / BN);
+  if (AG) ag_stamp(a, 0);
   // epilogue operands, issued before the K loop: b1 of this lane's rows, W2[class fr][those rows]
   const __amdgpu_buffer_rsrc_t rb1 = make_rsrc(a.b1), rw2 = make_rsrc(a.W2);
   float bb[MB][4], w2[MB][4];
@@ -986,6 +1045,7 @@ __global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn,
   f32x4 acc[MB][NB];
   glds_gemm_mainloop<BM, BN, NPW>(static_cast<const bf16*>(a.W1p), a.P, H * a.P * (int)sizeof(bf16),
                                   static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
+  if (AG) ag_stamp(a, 1);
   const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
@@ -1012,6 +1072,7 @@ __global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn,
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
         z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2[mb][i], acc[mb][nb][i], z[nb], 0, 0, 0);
+  if (AG && threadIdx.x == 0) ag_epoch_publish(ag, lds_dyn, ep_old);
   __syncthreads();
   f32x4* red = reinterpret_cast<f32x4*>(lds_dyn);  // [4][2][NB][64]
 #pragma unroll
@@ -1020,6 +1081,7 @@ __global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn,
   if (wr == 0) {
     const int tile = m0 / BM;
     const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
+    const unsigned ep = AG ? reinterpret_cast<const unsigned*>(lds_dyn + ag.ep_off)[0] : 0u;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       f32x4 sz = red[(wc * NB + nb) * 64 + lane];
@@ -1029,9 +1091,13 @@ __global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn,
 #pragma unroll
       for (int i = 0; i < 4; ++i) {  // (classes past C are zero: not stored, the head does not read them)
         const float zv = sz[i];      // (a scalar copy: see fwd1_rega_kernel)
-        __builtin_amdgcn_raw_buffer_store_b32(
-            __builtin_bit_cast(unsigned, zv), rz,
-            (col < n && 4 * fg + i < a.C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, 0, AG ? kSc1 : 0);
+        if constexpr (AG) {  // tagged granules for the fused head (hand-off 1)
+          if (col < n && 4 * fg + i < a.C) gran_store(ag.z2g + (size_t)(tile * 16 + 4 * fg + i) * a.ld + col, zv, ep);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b32(
+              __builtin_bit_cast(unsigned, zv), rz,
+              (col < n && 4 * fg + i < a.C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, 0, 0);
+        }
       }
     }
   }
@@ -1040,6 +1106,7 @@ __global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn,
     f32x4 a1v[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) a1v[nb] = acc[0][nb];
+    ag_stamp(a, 2, true);
     wide_head_ag<BM, BN, NB>(a, ag, a1v, lds_dyn, m0, n0, rw, cw, ag.tm, n0 / BN);
   }
 }
@@ -1127,26 +1194,18 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   using G = RegaGeom<128, WC>;
   constexpr int MB = G::MB, NB = G::NB, WR = G::WR, BM = G::BM;
-  int m0, n0;
-  if (AG && ag.xcd_grouped) {
-    // XCD-grouped grid (hardware XCD = blockIdx % 8): the tm row tiles of a column tile share one XCD, so
-    // both hand-offs stay inside one L2 (the form fwd1_head_ag_kernel runs) -- but every XCD then reads all
-    // of W1; padding workgroups leave
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    const int ct = xcd + 8 * (slot / ag.tm), rt = slot % ag.tm;
-    if (ct >= tn) return;
-    m0 = rt * BM;
-    n0 = ct * 128;
-  } else {
-    const int id = xcd_remap(blockIdx.x, gridDim.x);
-    m0 = (id / tn) * BM;
-    n0 = (id % tn) * 128;
-  }
+  // (a column tile's row tiles span XCDs: measured faster than an XCD-grouped grid, where every XCD reads all
+  // of W1 -- profiles/wide_fused_head_r2.md)
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (id / tn) * BM, n0 = (id % tn) * 128;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave / WC, wc = wave % WC, fr = lane & 15, fg = lane >> 4;
   const int rw = m0 + 16 * MB * wr, cw = n0 + 16 * NB * wc;  // this wave's first row / column
   const int H = a.H, n = a.n, C = a.C;
-  const bool z2 = a.z2part != nullptr;
+  const bool z2 = a.z2part != nullptr || AG;
+  gran_t ep_old = 0;  // the fused head's launch epoch (wide_head_ag step 0): one add per workgroup, now
+  if (AG && threadIdx.x == 0) ep_old = ag_epoch_add(ag, n0 / 128);
+  if (AG) ag_stamp(a, 0);
   const __amdgpu_buffer_rsrc_t rb1 = make_rsrc(a.b1), rw2 = make_rsrc(a.W2);
   float bb[MB][4], w2[MB][4];
 #pragma unroll
@@ -1161,6 +1220,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
   const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.W1) : reinterpret_cast<const AT*>(a.W1p);
   rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn,
                                        acc);
+  if (AG) ag_stamp(a, 1);
   const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
@@ -1187,6 +1247,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
       for (int i = 0; i < 4; ++i)
         z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2[mb][i], acc[mb][nb][i], z[nb], 0, 0, 0);
   }
+  if (AG && threadIdx.x == 0) ag_epoch_publish(ag, lds_dyn, ep_old);
   __syncthreads();
   f32x4* red = reinterpret_cast<f32x4*>(lds_dyn);  // [WR][WC][NB][64]
 #pragma unroll
@@ -1200,21 +1261,32 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
   for (int r = 1; r < WR; ++r) sz += red[((r * WC + oc) * NB + onb) * 64 + lane];
   const int col = n0 + 16 * wave + fr;
   const int tile = m0 / BM;
-  const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
+  if constexpr (AG) {  // tagged granules for the fused head (hand-off 1)
+    const unsigned ep = reinterpret_cast<const unsigned*>(lds_dyn + ag.ep_off)[0];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {  // (classes past C are zero: not stored, the head does not read them)
-    // (the element is copied to a scalar first: hipcc (ROCm 7.2) lowered __builtin_bit_cast of the vector
-    // element sz[i] to element 0 for every i -- all four z2 rows stored the same value)
-    const float zv = sz[i];
-    __builtin_amdgcn_raw_buffer_store_b32(
-        __builtin_bit_cast(unsigned, zv), rz,
-        (col < n && 4 * fg + i < C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB, 0, AG ? kSc1 : 0);
+    for (int i = 0; i < 4; ++i)
+      if (col < n && 4 * fg + i < C) {
+        const float zv = sz[i];  // (a scalar copy: see below)
+        gran_store(ag.z2g + (size_t)(tile * 16 + 4 * fg + i) * a.ld + col, zv, ep);
+      }
+  } else {
+    const __amdgpu_buffer_rsrc_t rz = make_rsrc(a.z2part);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // (classes past C are zero: not stored, the head does not read them)
+      // (the element is copied to a scalar first: hipcc (ROCm 7.2) lowered __builtin_bit_cast of the vector
+      // element sz[i] to element 0 for every i -- all four z2 rows stored the same value)
+      const float zv = sz[i];
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, zv), rz,
+                                            (col < n && 4 * fg + i < C) ? ((tile * 16 + 4 * fg + i) * a.ld + col) * 4 : kOOB,
+                                            0, 0);
+    }
   }
   if constexpr (AG) {
     static_assert(MB == 1 && NB == 8, "all-gather head: 8 row waves of 16 rows x 128 columns");
     f32x4 a1v[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) a1v[nb] = acc[0][nb];
+    ag_stamp(a, 2, true);
     wide_head_ag<128, 128, NB>(a, ag, a1v, lds_dyn, m0, n0, rw, cw, ag.tm, n0 / 128);
   }
 }
@@ -1345,11 +1417,13 @@ void launch_fwd1_rega_k(const SplitStepArgs& a, hipStream_t s) {
 
 // the fused all-gather head: > 80 KB of LDS keeps it at one workgroup per CU (the hand-off's measured form)
 template <typename AT, int NKS>
-void launch_fwd1_rega_ag_k(const SplitStepArgs& a, const RegaAgArgs& g, hipStream_t s) {
-  constexpr int L = std::max({ra::lds_bytes<128>(), 8 * 8 * 64 * 16, wide_ag_lds_bytes<128, 128>(), 84 * 1024});
+void launch_fwd1_rega_ag_k(const SplitStepArgs& a, RegaAgArgs g, hipStream_t s) {
+  constexpr int L = wide_ag_launch_lds(std::max({ra::lds_bytes<128>(), 8 * 8 * 64 * 16, wide_ag_lds_bytes<128, 128>()}));
   set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true>>(L);
-  const int tn = cdiv(a.n, 128), grid = g.xcd_grouped ? 8 * g.tm * cdiv(tn, 8) : g.tm * tn;
-  fwd1_rega_kernel<AT, kRegaWC, NKS, true><<<grid, 512, L, s>>>(a, tn, g);
+  g.ep_off = L - 16;
+  g.tiling = 0;
+  const int tn = cdiv(a.n, 128);
+  fwd1_rega_kernel<AT, kRegaWC, NKS, true><<<g.tm * tn, 512, L, s>>>(a, tn, g);
 }
 
 // K = P = 784 (MNIST) is 25 stages of 32: the fully unrolled K loop; anything else the runtime loop
@@ -1559,15 +1633,18 @@ bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64)
 }
 
 template <int NP>
-void launch_fwd1_glds64_ag(const SplitStepArgs& a, const RegaAgArgs& g, hipStream_t s) {
-  constexpr int L = std::max({gl::lds_bytes<64, 64, NP>(), 4 * 2 * 2 * 64 * 16, wide_ag_lds_bytes<64, 64>(), 84 * 1024});
+void launch_fwd1_glds64_ag(const SplitStepArgs& a, RegaAgArgs g, hipStream_t s) {
+  constexpr int L = wide_ag_launch_lds(std::max({gl::lds_bytes<64, 64, NP>(), 4 * 2 * 2 * 64 * 16, wide_ag_lds_bytes<64, 64>()}));
   set_lds_limit<fwd1_glds_kernel<64, 64, NP, true>>(L);
+  g.ep_off = L - 16;
+  g.tiling = 1;
   const int tn = cdiv(a.n, 64);
   fwd1_glds_kernel<64, 64, NP, true><<<g.tm * tn, 512, L, s>>>(a, tn, g);
 }
 
 int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long long* counters, int max_tiles,
-                     int* err, int store_a1, int xcd_grouped, int allow64, hipStream_t s) {
+                     unsigned long long* gran, int64_t gran_count, int* err, int store_a1, int allow64,
+                     hipStream_t s) {
   CME_REQUIRE(mlp_fwd1_wide_ag_ok(a, h, allow64), "fwd1_wide_ag: wide split path (128 x 128 A-in-registers or 64 x 64 "
                                          "direct-to-LDS tiles, grid <= CU count), train-mode head, C <= 16");
   CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
@@ -1581,8 +1658,10 @@ int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long lo
   g.err = err;
   g.store_a1 = store_a1;
   g.tm = cdiv(a.H, bm);
-  // the XCD-grouped grid needs a column tile's tm workgroups on one XCD's 32 CUs (128 x 128 tiles only)
-  g.xcd_grouped = xcd_grouped && bm == 128 && g.tm * cdiv(cdiv(a.n, 128), 8) <= device_cu_count() / 8;
+  // granules: the z2 partials [tm][16][ld], then D [16][ld]
+  CME_REQUIRE(gran && (int64_t)(g.tm * 16 + 16) * a.ld <= gran_count, "fwd1_wide_ag: granule buffer too small");
+  g.z2g = gran;
+  g.dg = gran + (size_t)g.tm * 16 * a.ld;
   if (bm == 128) {
     const bool k25 = cdiv(a.P, ra::kBK) == 25;
     if (a.npw == 3) {

@@ -399,3 +399,40 @@ def handoff_timeout_dp_main(out_dir, allreduce):
     from cme213_sp18_amd.parallel.launcher import spawn
 
     spawn(handoff_timeout_dp_worker, 2, (out_dir, allreduce), backend="gloo")
+
+
+def tp_xgmi_worker(rank, world, comm, device, out_dir, H):
+    """Hidden-sharded training with the z2 all-reduce on the xGMI one-shot kernel (ranks sharing GPU 0),
+    against single-process data-parallel training of the full model (rank 0 computes it)."""
+    import json
+
+    from cme213_sp18_amd import NeuralNetwork
+    from cme213_sp18_amd.parallel import DataParallelTrainer, TensorParallelTrainer
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    N, B, E, lr, reg = 2000, 800, 2, 0.05, 1e-4
+    x, y = synthetic_mnist(N, seed=4)
+    nn = NeuralNetwork([784, H, 10])
+    ref = nn.copy()
+    tr = TensorParallelTrainer(nn, comm=comm, device=dev, dtype="f32", batch_size=B, allreduce="xgmi")
+    tr.load(x, y)
+    impl = tr.allreduce_impl
+    tr.train(E, lr, reg)
+    failed = tr.comm_failed()
+    tr.close()
+    if rank == 0:
+        single = DataParallelTrainer(ref, device=dev, dtype="f32", batch_size=B)
+        single.load(x, y)
+        single.train(E, lr, reg)
+        rel = max(float(np.abs(nn.W[i] - ref.W[i]).max() / np.abs(ref.W[i]).max()) for i in range(2))
+        with open(os.path.join(out_dir, "tp_xgmi.json"), "w") as f:
+            json.dump({"impl": impl, "rel": rel, "failed": bool(failed),
+                       "b_err": max(float(np.abs(nn.b[i] - ref.b[i]).max()) for i in range(2))}, f)
+
+
+def tp_xgmi_main(out_dir, world, H):
+    from cme213_sp18_amd.parallel.launcher import spawn
+
+    spawn(tp_xgmi_worker, world, (out_dir, H), backend="gloo")

@@ -91,9 +91,9 @@ def test_real_timeout_raises_in_train_and_freezes_params(H):
 def test_wide_head_counters_survive_tiling_switch(dt):
     """One engine alternating per-GPU batches that take the 128 x 128 tiling (n = 800) and the 64 x 64
     tiling (n = 200) of the wide fused head, H = 4096: every step agrees with the plain forward + head
-    launches (to fp32 rounding of the dW2 partial sums) and no wait timed out -- with ONE shared counter
-    array the 64 x 64 launch after an 800-column launch computed its wait target from the other tiling's
-    count and read unpublished partials."""
+    launches (to fp32 rounding of the dW2 partial sums) and no poll timed out -- each tiling keeps its own
+    epoch counters (with ONE shared array a round-2 64 x 64 launch after an 800-column launch computed its
+    wait target from the other tiling's count and read unpublished partials: ADVICE r2)."""
     H, N = 4096, 2400
     x, y = synthetic_mnist(N, seed=17)
     nn = NeuralNetwork([784, H, 10])
@@ -112,8 +112,8 @@ def test_wide_head_counters_survive_tiling_switch(dt):
             assert not e.kernel_error()
             c = e.ag_counters.view(2, -1, 32)[:, :, 0]
             t128, t64 = (800 + 127) // 128, (800 + 63) // 64
-            assert c[0, :t128].tolist() == [2 * 32 * 3] * t128  # three 800-column launches, tm = 32
-            assert c[1, :(200 + 63) // 64].tolist() == [2 * 64 * 3] * ((200 + 63) // 64)  # tm = 64
+            assert c[0, :t128].tolist() == [32 * 3] * t128  # three 800-column launches, tm = 32 epoch adds each
+            assert c[1, :(200 + 63) // 64].tolist() == [64 * 3] * ((200 + 63) // 64)  # tm = 64
             assert int(c[1, (200 + 63) // 64:t64].sum()) == 0
         outs.append(e.params.clone())
     rel = float((outs[0] - outs[1]).abs().max() / outs[1].abs().max())

@@ -131,3 +131,19 @@ def test_dp_one_rank_per_gpu(tmp_path, world):
         pytest.skip(f"needs {world} GPUs, {_gpus()} visible")
     modes = ("xgmi-fused", "xgmi", "xgmi-bf16wire", "rccl", "rccl-bucketed", "host")
     _run_multigpu(tmp_path, world, "nccl", modes, ("weak", "strong"), dict(os.environ, OMP_NUM_THREADS="2"))
+
+
+@pytest.mark.parametrize("world,H", [(2, 1024), (4, 4096)])
+def test_tensor_parallel_xgmi_z2_allreduce(tmp_path, world, H):
+    """BASELINE config 4's chosen plan: hidden-sharded training whose only collective, the 16 x B z2 SUM, runs
+    on the xGMI one-shot kernel (ranks sharing the GPU here) == single-process training of the full model."""
+    import json
+
+    code = f"import sys; sys.path.insert(0, {ROOT!r}); from tests.dist_workers import tp_xgmi_main; " \
+           f"tp_xgmi_main({str(tmp_path)!r}, {world}, {H})"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads((tmp_path / "tp_xgmi.json").read_text())
+    assert res["impl"] == "xgmi-z2" and not res["failed"], res
+    assert res["rel"] < 1e-5 and res["b_err"] < 1e-6, res
