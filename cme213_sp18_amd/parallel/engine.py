@@ -171,10 +171,10 @@ class MlpEngine:
         if self.backend == "hip" and self.np and H <= 128 and C <= 16:
             tiles = (ld + 31) // 32
             self.fh_counters = torch.zeros(tiles, dtype=torch.int32, device=dev)
-            # all-gather form (mlp_fwd1_head_ag): monotonic uint64 tile counters, z2 partial slabs
-            # [tile][8 row tiles][16 classes][32 columns], and the timed-out-wait word
+            # all-gather form (mlp_fwd1_head_ag): monotonic uint64 tile counters (the launch epoch), z2 partial
+            # granules {value, epoch} [tile][8 row tiles][16 classes][32 columns], and the timed-out-poll word
             self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)  # one 256-B line each
-            self.ag_slabs = torch.zeros(tiles * 8 * 16 * 32, dtype=torch.float32, device=dev)
+            self.ag_slabs = torch.zeros(tiles * 8 * 16 * 32, dtype=torch.int64, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
         elif self.backend == "hip" and self.np and H >= 512 and C <= 16 and self.dw2buf is not None:
             # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_wide_ag) uses one

@@ -175,7 +175,8 @@ struct MlpStep {
           if (dz32) h.dZ1_planes = nullptr;
           if (fh_allgather && ag_counters && ag_slabs && ag_err && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h) &&
               cme::mlp_fwd1_head_ag_fits(a)) {
-            cme::mlp_fwd1_head_ag(a, h, P_<unsigned long long>(ag_counters), P_<float>(ag_slabs), P_<int>(ag_err),
+            cme::mlp_fwd1_head_ag(a, h, P_<unsigned long long>(ag_counters), P_<unsigned long long>(ag_slabs),
+                                  P_<int>(ag_err),
                                   fh_tiles, S(stream));
           } else if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
             cme::mlp_fwd1_head(a, h, P_<unsigned>(fh_counters), fh_tiles, S(stream));

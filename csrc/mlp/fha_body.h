@@ -1,23 +1,22 @@
 // Forward GEMM + head, all-gather form (H <= 128): the body of fwd1_head_ag_kernel (mlp_kernels.hip).
 //
 // The 16 x 32 a1 tiles of the forward GEMM; each of the tm row-tile workgroups of a 32-column tile
+//   0. makes ONE agent-scope add to the tile's monotonic 64-bit counter at entry: every launch adds exactly tm
+//      per tile (tm = cdiv(H, 16) is fixed for an engine), so old / tm + 1 is this launch's epoch, never 0;
 //   1. forms its z2 partial W2[:, its 16 rows] . a1[its rows, cols] (16 classes x 32 columns) and publishes
-//      it: sc1 (write-through) stores, vmcnt(0), barrier, one agent-scope add to the tile's 64-bit counter;
-//   2. waits (one lane, returning-atomic polls, s_sleep, bounded) until all tm adds of this launch are in --
-//      counters only grow, each launch adds exactly tm per tile (tm = cdiv(H, 16) is fixed for an engine, and a
-//      workgroup whose wait timed out still added), so the target is the next multiple of tm;
-//   3. sums the tm partials in row-tile order (sc1 loads: bit-identical z2 in every workgroup), softmax,
-//      D (row tile 0 stores it and the loss partial);
-//   4. forms dZ1 for ITS OWN 16 rows from the a1 tile it still holds in LDS and stores it (fp32 and / or
+//      it as data-tagged granules {value, epoch} (granule.h: one 8-byte sc1 store each, no drain, no flag);
+//   2. polls the tm partials of its (class, column) until every tag is the epoch (bounded, s_sleep between
+//      passes) and sums them in row-tile order (bit-identical z2 in every workgroup), softmax, D (row tile 0
+//      stores it and the loss partial);
+//   3. forms dZ1 for ITS OWN 16 rows from the a1 tile it still holds in LDS and stores it (fp32 and / or
 //      the bf16 planes, two columns per 4-byte word).
-// The hand-off is MI355X_MICROARCH.md's table's first row (sc1 stores, vmcnt(0) in every storing wave,
-// barrier, one agent add per workgroup, sc1 loads after the poll).  Requires every workgroup of the launch
-// to be resident at once (mlp_fwd1_head_ag_fits); a wait that outlasts 2^ag_spin_shift polls sets *err: the
-// launch's results are not trusted, and the weight-gradient launch that follows reads *err and applies nothing
-// (SplitStepArgs::ag_err; MlpEngine.kernel_error(), KernelHandoffTimeout).
+// Requires every workgroup of the launch to be resident at once (mlp_fwd1_head_ag_fits); a poll that outlasts
+// 2^ag_spin_shift passes sets *err: the launch's results are not trusted, and the weight-gradient launch that
+// follows reads *err and applies nothing (SplitStepArgs::ag_err; MlpEngine.kernel_error(), KernelHandoffTimeout).
 #pragma once
 
 #include "fwd_tile.h"
+#include "granule.h"
 #include "mlp_kernels.h"
 #include "mlp_split.h"
 #include "mma_tile.h"
@@ -50,7 +49,7 @@ struct EpiSigLds {
 // floats of LDS.
 template <int NPW, int VEC, bool AF>
 __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs& h,
-                                         unsigned long long* __restrict__ counters, float* __restrict__ slabs,
+                                         unsigned long long* __restrict__ counters, gran_t* __restrict__ slabs,
                                          int* __restrict__ err, int tm, int tn, int blk, float* red) {
   constexpr int kCols = 32;
   __shared__ float a1s[16][kCols + 1];
@@ -59,6 +58,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   __shared__ float zs[16][kCols + 1];  // z2 (+ b2), then D
   __shared__ float ls[kCols];
   __shared__ int s_bad;
+  __shared__ unsigned s_ep;
   const int xcd = blk & 7, slot = blk >> 3;
   const int ct = xcd + 8 * (slot / tm), rt = slot % tm;
   if (ct >= tn) return;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
@@ -69,6 +69,11 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     if (st && t == 0) st[i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
+  // the launch epoch: one add per workgroup now, its value used after the GEMM
+  unsigned long long ep_old = 0;
+  if (t == 0)
+    ep_old = __hip_atomic_fetch_add(counters + (size_t)ct * kAgCounterStride, 1ull, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
   // the label of this thread's softmax column (t >> 4), fetched now: loaded where the softmax uses it, it was
   // a dependent memory round trip after the all-gather wait
   const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(
@@ -86,61 +91,36 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red);
   // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
   // they are masked below.
-  // ---- 1. z2 partial for (class c, column col), one per thread, published write-through
+  if (t == 0) {
+    s_ep = (unsigned)(ep_old / (unsigned)tm) + 1u;
+    s_bad = 0;
+  }
+  __syncthreads();
+  const unsigned ep = s_ep;
+  // ---- 1. z2 partial for (class c, column col), one per thread, published as a tagged granule
   const int c = t >> 5, col = t & 31;
   {
     float z = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) z += (r0 + r < H && c0 + col < n) ? w2s[c][r] * a1s[r][col] : 0.f;
-    float* slab = slabs + (size_t)(ct * tm + rt) * 16 * kCols;
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, z), make_rsrc(slab), (c * kCols + col) * 4,
-                                          0, kSc1);
+    // (test hook: one workgroup of column tile 0 never publishes, so that tile's polls time out)
+    if (c < C && !(f.ag_test_skip == rt && ct == 0))
+      gran_store(slabs + (size_t)(ct * tm + rt) * 16 * kCols + c * kCols + col, z, ep);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
-  __syncthreads();
   stamp(1);
-  // ---- 2. one add per workgroup, then wait for the tile's tm adds of this launch
-  if (t == 0) {
-    unsigned long long* cnt = counters + (size_t)ct * kAgCounterStride;
-    // (test hook: one workgroup of column tile 0 leaves its add out, so that tile's wait really times out)
-    const unsigned long long inc = (f.ag_test_skip == rt && ct == 0) ? 0ull : 1ull;
-    const unsigned long long old = __hip_atomic_fetch_add(cnt, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long target = (old / (unsigned)tm + 1) * (unsigned)tm;
-    const uint32_t limit = 1u << f.ag_spin_shift;
-    uint32_t spins = 0;
-    int bad = 0;
-    // polled with a returning atomic (add 0): served where the adds are performed, never from a
-    // possibly stale L2 copy of the line (measured: sc1 load polls saw the last adds only ~20 us late)
-    while (old + inc < target &&
-           __hip_atomic_fetch_add(cnt, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++spins > limit) {
-        bad = 1;
-        atomicExch(err, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    s_bad = bad;
-  }
-  __syncthreads();
-  stamp(2);
-  // ---- 3. z2 = sum of the tm partials (row-tile order: the same bits in every workgroup) + b2
+  // ---- 2. z2 = sum of the tm partials (row-tile order: the same bits in every workgroup) + b2
   {
-    // (the descriptor is built from the uniform slab base: a per-lane base makes hipcc waterfall every
-    // load over the 64 distinct descriptors -- measured +21 us)
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(slabs + (size_t)ct * tm * 16 * kCols);
-    const int lo = (c * kCols + col) * 4;
-    float v[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-      v[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                           rs, r < tm ? lo + r * 16 * kCols * 4 : kOOB, 0, kSc1));
     float z = 0.f;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) z += v[r];
+    const bool good = gran_poll<8>(slabs, (unsigned)(ct * tm * 16 * kCols + c * kCols + col), 16u * kCols, tm,
+                                   c < C, ep, 1u << f.ag_spin_shift, [&](int, float v) { z += v; });
+    if (!good && (t & 63) == 0) {
+      atomicExch(err, 1);
+      s_bad = 1;
+    }
     zs[c][col] = z + b2s[c];
   }
   __syncthreads();
+  stamp(2);
   // softmax + cross-entropy gradient: 16 lanes (classes) per column, 4 columns per wave
   {
     const int col2 = t >> 4, cls = t & 15;

@@ -1,0 +1,59 @@
+// Data-tagged granules: the in-launch hand-off form of MI355X_MICROARCH.md's price list row 'handoff-1to1'
+// (cdna_hip_programming.md Guideline 16, R2).  A granule is 8 bytes {value (low 32), tag (high 32)} written by
+// ONE sc1 store; the consumer polls the granules themselves until every tag is the launch's epoch, so the data
+// is its own flag: no store drain, no counter add, no flag poll and no separate payload load.  Tags only grow
+// (the callers derive the epoch from a monotonic per-tile counter), so granule buffers are never re-zeroed.
+// Used by the all-gather forward + head launches: fha_body.h (H <= 128) and mlp_split.hip wide_head_ag.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace cme {
+
+using gran_t = unsigned long long;
+__device__ __forceinline__ void gran_store(gran_t* p, float v, unsigned ep) {  // ONE 8-byte sc1 store
+  __hip_atomic_store(p, ((gran_t)ep << 32) | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ gran_t gran_load(const gran_t* p) {  // sc1 load (L2-served, never a stale L1 line)
+  return __hip_atomic_load(const_cast<gran_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Poll the granules base[off + k * stride] (k < cnt <= N; lanes with !need take no part) until every tag is
+// `ep`, then hand the values to f(k, value) in k order (0 for k >= cnt).  The N addresses are formed once,
+// before the poll loop; a pass is N back-to-back global_load_dwordx2 sc1 and one wait.  Wave-uniform; false
+// when the wave gave up after `limit` passes (f is then not called).
+template <int N, class F>
+__device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsigned stride, int cnt, bool need,
+                                          unsigned ep, uint32_t limit, F&& f) {
+  // the granule addresses, once: k >= cnt re-reads granule 0 (needed anyway, so its tag check is the same)
+  const gran_t* p[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    p[k] = reinterpret_cast<const gran_t*>(reinterpret_cast<const char*>(base) +
+                                           (off + (k < cnt ? (unsigned)k * stride : 0u)) * 8u);
+  bool done = !need;
+  gran_t x[N];
+  for (uint32_t spins = 0;; ++spins) {
+    if (!done) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) x[k] = gran_load(p[k]);
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < N; ++k) ok &= (unsigned)(x[k] >> 32) == ep;
+      done = ok;
+    }
+    if (__all(done)) break;
+    if (spins >= limit) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (need) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) f(k, k < cnt ? __builtin_bit_cast(float, (unsigned)x[k]) : 0.f);
+  }
+  return true;
+}
+
+}  // namespace cme

@@ -68,10 +68,10 @@ bool mlp_fwd1_head_ok(const SplitStepArgs& f, const HeadArgs& h);
 void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters, int max_tiles, hipStream_t s);
 // the same launch in the all-gather form (every row-tile workgroup of a column tile sums the tile's z2
 // partials and forms dZ1 for its own rows): counters >= max_tiles * 32 uint64 (one 256-byte line per tile,
-// only ever incremented), slabs
-// >= max_tiles * 8 * 16 * 32 floats, err: set to 1 if a wait for the tile's workgroups timed out
-void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long long* counters, float* slabs,
-                      int* err, int max_tiles, hipStream_t s);
+// only ever incremented: the launch epoch), slabs >= max_tiles * 8 * 16 * 32 uint64 granules (tags only grow:
+// never re-zeroed), err: set to 1 if a poll for the tile's partials timed out
+void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long long* counters,
+                      unsigned long long* slabs, int* err, int max_tiles, hipStream_t s);
 // the all-gather form's grid fits on the device at once (occupancy x CU count): every workgroup waits for the
 // others of its column tile, so a larger grid (a large per-GPU batch) must take the last-arriver form
 bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f);

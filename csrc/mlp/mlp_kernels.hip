@@ -576,7 +576,7 @@ __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArg
 template <int NPW, int VEC, bool AF>
 __global__ __launch_bounds__(512) void fwd1_head_ag_kernel(SplitStepArgs f, HeadArgs h,
                                                            unsigned long long* __restrict__ counters,
-                                                           float* __restrict__ slabs, int* __restrict__ err, int tm,
+                                                           gran_t* __restrict__ slabs, int* __restrict__ err, int tm,
                                                            int tn) {
   __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];
   fha_body<NPW, VEC, AF>(f, h, counters, slabs, err, tm, tn, blockIdx.x, red);
@@ -1318,8 +1318,8 @@ bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f) {
   return nwg <= occ * cu_count();
 }
 
-void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long long* counters, float* slabs,
-                      int* err, int max_tiles, hipStream_t s) {
+void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long long* counters,
+                      unsigned long long* slabs, int* err, int max_tiles, hipStream_t s) {
   if (f.n <= 0) return;
   CME_REQUIRE(mlp_fwd1_head_ok(f, h), "fwd1_head_ag: H <= 128, C <= 16, train-mode head over the same a1");
   CME_REQUIRE((int64_t)f.H * f.P * 2 * f.npw < (int64_t)kOOB && (int64_t)f.n * f.P < (int64_t)kOOB,

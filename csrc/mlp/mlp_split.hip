@@ -5,6 +5,7 @@
 #include <algorithm>
 
 #include "glds_gemm.h"
+#include "granule.h"
 #include "rega_gemm.h"
 #include "lds_gemm.h"
 #include "mma_tile.h"
@@ -745,50 +746,6 @@ constexpr int wide_ag_lds_bytes() {
 // the launch's dynamic LDS: > 80 KB keeps it at one workgroup per CU (the hand-off's measured form), and the
 // last 16 bytes hold the epoch and the two timeout flags (no other use reaches them)
 constexpr int wide_ag_launch_lds(int used) { return (used + 16 > 84 * 1024 ? used + 16 : 84 * 1024) / 16 * 16; }
-
-using gran_t = unsigned long long;
-__device__ __forceinline__ void gran_store(gran_t* p, float v, unsigned ep) {  // ONE 8-byte sc1 store
-  __hip_atomic_store(p, ((gran_t)ep << 32) | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ gran_t gran_load(const gran_t* p) {  // sc1 load (L2-served, never a stale L1 line)
-  return __hip_atomic_load(const_cast<gran_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Poll the granules base[off + k * stride] (k < cnt <= N; lanes with !need take no part) until every tag is
-// `ep`, then hand the values to f(k, value) in k order.  The base is uniform and the offsets 32-bit, so each
-// poll is one global_load_dwordx2 sc1 with an SGPR base.  Wave-uniform; false when the wave gave up after
-// `limit` passes (f is then not called).
-template <int N, class F>
-__device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsigned stride, int cnt, bool need,
-                                          unsigned ep, uint32_t limit, F&& f) {
-  // the granule addresses, once: k >= cnt re-reads granule 0 (needed anyway, so its tag check is the same)
-  const gran_t* p[N];
-#pragma unroll
-  for (int k = 0; k < N; ++k)
-    p[k] = reinterpret_cast<const gran_t*>(reinterpret_cast<const char*>(base) +
-                                           (off + (k < cnt ? (unsigned)k * stride : 0u)) * 8u);
-  bool done = !need;
-  gran_t x[N];
-  for (uint32_t spins = 0;; ++spins) {
-    if (!done) {
-#pragma unroll
-      for (int k = 0; k < N; ++k) x[k] = gran_load(p[k]);
-      bool ok = true;
-#pragma unroll
-      for (int k = 0; k < N; ++k) ok &= (unsigned)(x[k] >> 32) == ep;
-      done = ok;
-    }
-    if (__all(done)) break;
-    if (spins >= limit) return false;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  if (need) {
-#pragma unroll
-    for (int k = 0; k < N; ++k) f(k, k < cnt ? __builtin_bit_cast(float, (unsigned)x[k]) : 0.f);
-  }
-  return true;
-}
 
 __device__ __forceinline__ void ag_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
