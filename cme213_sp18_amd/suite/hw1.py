@@ -77,6 +77,16 @@ def radix_sort_parallel(keys, num_bits: int = RADIX_NUM_BITS, num_blocks: int = 
     return host().radix_sort_parallel(np.ascontiguousarray(keys, np.uint32), num_bits, num_blocks)
 
 
+def radix_sort_lsd(keys) -> np.ndarray:
+    """The production OpenMP LSD sort (8-bit digits, one parallel region, write-combined scatter)."""
+    return host().radix_sort_lsd(np.ascontiguousarray(keys, np.uint32))
+
+
+def std_sort(keys) -> np.ndarray:
+    """C++ std::sort of the keys: the reference's baseline (hw1code/main_q2.cpp:249-256)."""
+    return host().std_sort(np.ascontiguousarray(keys, np.uint32))
+
+
 def radix_geometry(n: int, num_blocks: int = RADIX_NUM_BLOCKS) -> tuple[int, int]:
     """(block_size, num_blocks) as the stage tests derive them: ``blockSize = n / 8``,
     ``numBlocks = ceil(n / blockSize)`` (tests_q2.cpp:84-85)."""

@@ -97,8 +97,14 @@ class SimParams:
         return math.exp(-2 * self.dt)  # narrowed to float at the kernel call, as BC.h:67
 
     def calc_bytes(self) -> int:
-        """Stencil traffic model: iters * nx * ny * {6,10,18} words (simParams.cpp:79-93)."""
+        """Stencil traffic model: iters * nx * ny * {6,10,18} words (simParams.cpp:79-93).  It counts every
+        stencil tap as a memory read, so it exceeds what any kernel that reuses neighbours moves."""
         return self.iters * self.nx * self.ny * {2: 6, 4: 10, 8: 18}[self.order] * 4
+
+    def compulsory_bytes(self) -> int:
+        """The bytes an ideal kernel moves: per iteration the whole current grid (halo included) read once and
+        the next grid's interior written once."""
+        return self.iters * (self.gx * self.gy + self.nx * self.ny) * 4
 
 
 def init_grid(p: SimParams) -> np.ndarray:

@@ -72,6 +72,25 @@ void bind_suite_cpu(pybind11::module_& m) {
     radix_serial(out.mutable_data(), tmp.data(), keys.size(), num_bits);
     return out;
   }, py::arg("keys"), py::arg("num_bits") = 16);
+  sm.def("radix_sort_lsd", [](u32arr keys) {
+    py::array_t<uint32_t> out(keys.size());
+    std::memcpy(out.mutable_data(), keys.data(), keys.size() * 4);
+    std::vector<uint32_t> tmp(keys.size());
+    {
+      py::gil_scoped_release r;
+      radix_parallel_lsd(out.mutable_data(), tmp.data(), keys.size());
+    }
+    return out;
+  }, py::arg("keys"));
+  sm.def("std_sort", [](u32arr keys) {
+    py::array_t<uint32_t> out(keys.size());
+    std::memcpy(out.mutable_data(), keys.data(), keys.size() * 4);
+    {
+      py::gil_scoped_release r;
+      std_sort(out.mutable_data(), keys.size());
+    }
+    return out;
+  }, py::arg("keys"));
   sm.def("stencil", [](py::array_t<float, py::array::c_style> grid, int order, float xcfl, float ycfl, float scale,
                        int iters) {
     if (grid.ndim() != 2) throw std::invalid_argument("grid must be 2-D [gy][gx]");

@@ -73,6 +73,52 @@ u32vec block_exscan(int num_buckets, int num_blocks, const u32vec& gscan, const 
   return o;
 }
 
+// Software write-combining for the scatter: each bucket's next keys are staged in a 64-byte (one cache
+// line) slot of a per-thread buffer and written out a full line at a time, so the 2^num_bits scattered
+// output streams cost one line write each per 16 keys instead of a read-for-ownership per key.  Used when
+// the slots fit in ~L2 (<= 4096 buckets: 256 KB); larger digits scatter directly.
+namespace {
+constexpr int kWc = 16;  // keys per slot (64 bytes)
+constexpr int kWcMaxBuckets = 4096;
+
+struct WcScatter {
+  std::vector<uint32_t> buf;  // [bucket][kWc]
+  std::vector<uint8_t> fill;  // keys staged per bucket
+  uint32_t* pos;              // next output index per bucket (advanced as lines are written)
+  uint32_t* out;
+  WcScatter(int buckets, uint32_t* pos_, uint32_t* out_)
+      : buf((size_t)buckets * kWc), fill(buckets, 0), pos(pos_), out(out_) {}
+  inline void put(uint32_t b, uint32_t key) {
+    uint32_t* slot = buf.data() + (size_t)b * kWc;
+    slot[fill[b]++] = key;
+    if (fill[b] == kWc) {
+      std::memcpy(out + pos[b], slot, kWc * sizeof(uint32_t));
+      pos[b] += kWc;
+      fill[b] = 0;
+    }
+  }
+  void flush(int buckets) {
+    for (int b = 0; b < buckets; ++b) {
+      std::memcpy(out + pos[b], buf.data() + (size_t)b * kWc, fill[b] * sizeof(uint32_t));
+      pos[b] += fill[b];
+      fill[b] = 0;
+    }
+  }
+};
+
+// stable scatter of keys[lo, hi) by digit (keys >> start_bit) & mask to out[pos[digit]++]
+void scatter_range(const uint32_t* keys, int64_t lo, int64_t hi, int start_bit, uint32_t mask, int buckets,
+                   uint32_t* pos, uint32_t* out) {
+  if (buckets <= kWcMaxBuckets && hi - lo >= 8 * (int64_t)buckets) {
+    WcScatter wc(buckets, pos, out);
+    for (int64_t i = lo; i < hi; ++i) wc.put((keys[i] >> start_bit) & mask, keys[i]);
+    wc.flush(buckets);
+  } else {
+    for (int64_t i = lo; i < hi; ++i) out[pos[(keys[i] >> start_bit) & mask]++] = keys[i];
+  }
+}
+}  // namespace
+
 void populate(const u32vec& bex, int num_blocks, int num_buckets, int start_bit, int64_t block_size,
               const uint32_t* keys, int64_t n, uint32_t* sorted) {
   const uint32_t mask = (uint32_t)num_buckets - 1;
@@ -80,7 +126,7 @@ void populate(const u32vec& bex, int num_blocks, int num_buckets, int start_bit,
   for (int b = 0; b < num_blocks; ++b) {
     std::vector<uint32_t> pos(bex.begin() + (size_t)b * num_buckets, bex.begin() + (size_t)(b + 1) * num_buckets);
     const int64_t lo = (int64_t)b * block_size, hi = std::min<int64_t>(n, lo + block_size);
-    for (int64_t i = lo; i < hi; ++i) sorted[pos[(keys[i] >> start_bit) & mask]++] = keys[i];
+    scatter_range(keys, lo, hi, start_bit, mask, num_buckets, pos.data(), sorted);
   }
 }
 
@@ -103,26 +149,94 @@ void radix_parallel(uint32_t* keys, uint32_t* tmp, int64_t n, int num_bits, int 
   }
 }
 
+// Serial LSD sort: every digit's histogram from ONE read of the keys, passes whose digit is the same for
+// every key skipped, write-combined scatter.  num_bits divides 32 in pairs of passes (ping-pong), as the
+// reference's loop does (hw1code/main_q2.cpp:174-206).
 void radix_serial(uint32_t* keys, uint32_t* tmp, int64_t n, int num_bits) {
   const int buckets = 1 << num_bits;
   const uint32_t mask = (uint32_t)buckets - 1;
-  std::vector<uint32_t> cnt(buckets);
-  auto pass = [&](const uint32_t* in, uint32_t* out, int sb) {
-    std::fill(cnt.begin(), cnt.end(), 0);
-    for (int64_t i = 0; i < n; ++i) ++cnt[(in[i] >> sb) & mask];
+  const int passes = (32 + num_bits - 1) / num_bits;
+  std::vector<uint32_t> hist((size_t)passes * buckets, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t k = keys[i];
+    for (int p = 0; p < passes; ++p) ++hist[(size_t)p * buckets + ((k >> (p * num_bits)) & mask)];
+  }
+  uint32_t* in = keys;
+  uint32_t* out = tmp;
+  for (int p = 0; p < passes; ++p) {
+    uint32_t* h = hist.data() + (size_t)p * buckets;
+    bool trivial = false;
     uint32_t run = 0;
     for (int k = 0; k < buckets; ++k) {
-      const uint32_t c = cnt[k];
-      cnt[k] = run;
+      const uint32_t c = h[k];
+      trivial |= c == (uint32_t)n;
+      h[k] = run;
       run += c;
     }
-    for (int64_t i = 0; i < n; ++i) out[cnt[(in[i] >> sb) & mask]++] = in[i];
-  };
-  for (int sb = 0; sb < 32; sb += 2 * num_bits) {
-    pass(keys, tmp, sb);
-    pass(tmp, keys, sb + num_bits);
+    if (trivial) continue;  // one digit value for every key: the pass is the identity
+    scatter_range(in, 0, n, p * num_bits, mask, buckets, h, out);
+    std::swap(in, out);
   }
+  if (in != keys) std::memcpy(keys, in, (size_t)n * sizeof(uint32_t));
 }
+
+// The production OpenMP LSD sort for 32-bit keys: 8-bit digits, ONE parallel region for the whole sort (per
+// pass: each thread histograms its chunk, one thread forms every (thread, digit) output offset, each thread
+// scatters its chunk stably through write-combining slots), passes whose digit is the same for every key
+// skipped.  radix_parallel keeps the reference's block decomposition for the stage tests and the threads x
+// blocks sweep (hw1code/main_q2.cpp:123-148, :282-309).
+void radix_parallel_lsd(uint32_t* keys, uint32_t* tmp, int64_t n) {
+  constexpr int B = 8, NBK = 1 << B, P = 4;
+  if (n <= 1) return;
+  const int T = std::max(1, std::min<int>(omp_get_max_threads(), (int)std::max<int64_t>(1, n / 65536)));
+  const int64_t chunk = (n + T - 1) / T;
+  std::vector<uint32_t> hist((size_t)T * NBK), pos((size_t)T * NBK);
+  uint32_t* bufs[2] = {keys, tmp};
+  int cur = 0;  // bufs[cur] holds the keys
+  bool skip = false;
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+    for (int p = 0; p < P; ++p) {
+      const uint32_t* in = bufs[cur];
+      // (nt < T only when the runtime refuses threads: thread t then covers chunks t, t + nt, ...)
+      for (int c = t; c < T; c += nt) {
+        uint32_t* h = hist.data() + (size_t)c * NBK;
+        std::fill(h, h + NBK, 0u);
+        const int64_t lo = std::min<int64_t>(n, c * chunk), hi = std::min<int64_t>(n, lo + chunk);
+        for (int64_t i = lo; i < hi; ++i) ++h[(in[i] >> (p * B)) & (NBK - 1)];
+      }
+#pragma omp barrier
+#pragma omp single
+      {
+        uint32_t run = 0;
+        skip = false;
+        for (int d = 0; d < NBK; ++d) {
+          uint32_t tot = 0;
+          for (int c = 0; c < T; ++c) {
+            const uint32_t k = hist[(size_t)c * NBK + d];
+            pos[(size_t)c * NBK + d] = run;
+            run += k;
+            tot += k;
+          }
+          skip |= tot == (uint32_t)n;
+        }
+      }  // (implicit barrier)
+      if (!skip) {
+        for (int c = t; c < T; c += nt) {
+          const int64_t lo = std::min<int64_t>(n, c * chunk), hi = std::min<int64_t>(n, lo + chunk);
+          scatter_range(in, lo, hi, p * B, NBK - 1, NBK, pos.data() + (size_t)c * NBK, bufs[cur ^ 1]);
+        }
+      }
+#pragma omp barrier
+#pragma omp single
+      if (!skip) cur ^= 1;
+    }
+  }
+  if (cur) std::memcpy(keys, tmp, (size_t)n * sizeof(uint32_t));
+}
+
+void std_sort(uint32_t* keys, int64_t n) { std::sort(keys, keys + n); }
 
 // ------------------------------------------------------------- hw3 stencil
 static float stencil_point(const float* c, int64_t gx, int order, float xcfl, float ycfl) {

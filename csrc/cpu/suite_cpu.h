@@ -37,6 +37,10 @@ void radix_parallel_pass(const uint32_t* keys, uint32_t* sorted, int64_t n, int 
 // full sorts: result in keys, tmp is n-element scratch
 void radix_parallel(uint32_t* keys, uint32_t* tmp, int64_t n, int num_bits, int num_blocks);
 void radix_serial(uint32_t* keys, uint32_t* tmp, int64_t n, int num_bits);
+// the production OpenMP sort (8-bit digits, fused histograms, write-combined scatter; see suite_cpu.cpp)
+void radix_parallel_lsd(uint32_t* keys, uint32_t* tmp, int64_t n);
+// std::sort of the same keys (the reference's baseline, hw1code/main_q2.cpp:249-256)
+void std_sort(uint32_t* keys, int64_t n);
 
 // hw3: `iters` steps of next.border = curr.border * bc_scale, next.interior = stencil(curr); grid [gy][gx]
 void stencil_cpu(float* grid, int gx, int gy, int order, float xcfl, float ycfl, float bc_scale, int iters);

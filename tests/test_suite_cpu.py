@@ -77,7 +77,17 @@ def test_radix_sort_parallel(n, bits, blocks):
     assert np.array_equal(hw1.radix_sort_parallel(keys, bits, blocks), np.sort(keys))
 
 
-@pytest.mark.parametrize("bits", [4, 8, 16])
+@pytest.mark.parametrize("n", [0, 1, 7, 65535, 300_001])
+def test_radix_sort_lsd_and_std_sort(n):
+    keys = hw1.glibc_rand(n, seed=n + 5) * np.uint32(3)
+    ref = np.sort(keys)
+    assert np.array_equal(hw1.radix_sort_lsd(keys), ref)
+    assert np.array_equal(hw1.std_sort(keys), ref)
+    same = np.full(n, 7, np.uint32)  # every pass trivial (skipped)
+    assert np.array_equal(hw1.radix_sort_lsd(same), same)
+
+
+@pytest.mark.parametrize("bits", [4, 8, 11, 16])
 def test_radix_sort_serial(bits):
     keys = np.random.default_rng(0).integers(0, 2**32, 100_001, dtype=np.uint64).astype(np.uint32)
     assert np.array_equal(hw1.radix_sort_serial(keys, bits), np.sort(keys))
@@ -204,3 +214,12 @@ def test_synthetic_english_ioc_separates_period():
     m = np.array([np.count_nonzero(x[:-k] == x[k:]) for k in s])
     ioc = hw4.index_of_coincidence(m, len(x), s)
     assert list(s[ioc > hw4.IOC_THRESHOLD]) == [6, 12, 18]
+
+
+def test_stencil_byte_models():
+    """calcBytes (simParams.cpp:79-93) counts every tap; the compulsory model reads the grid and writes the
+    interior once per iteration, so it is the smaller (and the one HBM bandwidth applies to)."""
+    p = hw3.SimParams(256, 128, 1.0, 1.0, 10, 8)
+    assert p.calc_bytes() == 10 * 256 * 128 * 18 * 4
+    assert p.compulsory_bytes() == 10 * (p.gx * p.gy + 256 * 128) * 4
+    assert p.compulsory_bytes() < p.calc_bytes()
