@@ -51,9 +51,12 @@ def parse(argv=None):
     ap.add_argument("--executor", default="auto", choices=["auto", "graph", "eager"],
                     help="auto: the native C++ step loop where a step is pure device work (one process, or the "
                          "xGMI-fused all-reduce), else captured HIP graphs; graph: always graphs")
-    ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl", "host"],
-                    help="gradient sync for N>1: xGMI peer kernel with fused SGD (auto/xgmi), RCCL all-reduce, "
-                         "or host-staged gloo (reference-equivalent)")
+    ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "xgmi2", "rccl", "host"],
+                    help="gradient sync for N>1: auto (by bucket size and ranks), the xGMI one-shot peer kernel "
+                         "with fused SGD (xgmi), the xGMI two-shot kernel with sharded SGD (xgmi2), RCCL, or "
+                         "host-staged gloo (reference-equivalent)")
+    ap.add_argument("--grad-wire", default="auto", choices=["auto", "f32", "bf16"],
+                    help="element type of the gradients on the xGMI one-shot wire (bf16: opt-in, half the bytes)")
     ap.add_argument("--mode", default="optimized", choices=["optimized", "reference"],
                     help="reference: the reference's execution model on MI355X -- unfused PyTorch/hipBLAS ops, "
                          "no graphs, host-staged gradient all-reduce (for comparison only)")
@@ -112,6 +115,7 @@ def main(argv=None) -> int:
         """Trainer + captured graphs + W warm-up steps.  Returns (trainer, timed plans)."""
         tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=global_batch,
                                  backend=a.backend, use_graphs=not a.no_graphs, allreduce=allreduce,
+                                 grad_wire=a.grad_wire,
                                  executor="eager" if a.no_graphs else a.executor)
         tr.load(x, y)
         full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == global_batch]

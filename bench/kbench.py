@@ -68,7 +68,10 @@ def main(argv=None):
         # split3 operand forms (SplitStepArgs.a_fp32): "+a<bits>" bit0 fp32 W1, bit1 fp32 dZ1 (default: engine's)
         m = re.search(r"\+a(\d)", path)
         a32 = int(m.group(1)) if m else None
-        path = re.sub(r"\+a\d", "", path).replace("+fh", "")
+        # "+p<0|1>": the pixel operand's 16-byte chunk-pair loads (SplitStepArgs.u8_pairs; default on)
+        m = re.search(r"\+p(\d)", path)
+        pairs = int(m.group(1)) if m else None
+        path = re.sub(r"\+[ap]\d", "", path).replace("+fh", "")
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -80,12 +83,14 @@ def main(argv=None):
                 step.fused_head = int(fused)
                 if a32 is not None:
                     step.a_fp32 = a32
+                if pairs is not None:
+                    step.u8_pairs = pairs
                 st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
 
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+fh" if fused else "") + (f"+a{a32}" if a32 is not None else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+fh" if fused else "") + (f"+a{a32}" if a32 is not None else "") + (f"+p{pairs}" if pairs is not None else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(

@@ -36,22 +36,30 @@ def main(argv=None):
     assert step.fh_allgather == 1
     st = torch.cuda.current_stream().cuda_stream
     buf = torch.zeros(4096 * 4, dtype=torch.int64, device="cuda")
+    wbuf = torch.zeros(4096 * 8 * 4, dtype=torch.int64, device="cuda")
     pct = lambda v: [round(float(np.percentile(v, q)), 3) for q in (0, 50, 90, 100)]  # noqa: E731
     for rep in range(4):
         for _ in range(20):
             step.run(0, a.n, 1.0 / a.n, 1e-4, 0.0, 1, 0, st, 3)
         torch.cuda.synchronize()
         buf.zero_()
+        wbuf.zero_()
         step.stamps = buf.data_ptr()
+        step.hstamps = wbuf.data_ptr()  # per wave of the GEMM tile (mma_tile.h wsk_tile)
         step.run(0, a.n, 1.0 / a.n, 1e-4, 0.0, 1, 0, st, 1)
-        step.stamps = 0
+        step.stamps = step.hstamps = 0
         torch.cuda.synchronize()
         s = buf.view(-1, 4).cpu().numpy().astype(np.int64)
         s = s[s[:, 0] > 0]
         t0 = s[:, 0].min()
         rel = (s - t0) * 10.0 / 1000.0
+        w = wbuf.view(-1, 4).cpu().numpy().astype(np.int64)
+        w = w[w[:, 0] > 0]
+        wr = (w - t0) * 10.0 / 1000.0
         print(json.dumps({"wgs": int(len(s)), "entry": pct(rel[:, 0]), "published": pct(rel[:, 1]),
-                          "all_arrived": pct(rel[:, 2]), "wait": pct(rel[:, 2] - rel[:, 1]), "end": pct(rel[:, 3])}))
+                          "all_arrived": pct(rel[:, 2]), "wait": pct(rel[:, 2] - rel[:, 1]), "end": pct(rel[:, 3]),
+                          "wave_entry": pct(wr[:, 0]), "wave_kloop": pct(wr[:, 1]), "wave_reduced": pct(wr[:, 2]),
+                          "wave_epilogue": pct(wr[:, 3]), "kloop_dur": pct(wr[:, 1] - wr[:, 0])}))
         if rep == 3:  # per column tile (XCD-grouped grid: block b -> xcd b & 7, slot b >> 3, ct = xcd + 8 (slot // tm))
             tm = (a.hidden + 15) // 16
             allv = buf.view(-1, 4).cpu().numpy().astype(np.int64)

@@ -39,7 +39,7 @@ class TrainConfig:
     use_graphs: bool = True
     softmax_shift: bool = True
     ckpt_precision: int = 12
-    allreduce: str = "auto"     # auto | xgmi (peer kernel, SGD fused) | rccl
+    allreduce: str = "auto"     # auto | xgmi (one-shot peer kernel, SGD fused) | xgmi2 (two-shot, sharded SGD) | rccl
     comm_timeout: float = 300.0  # seconds before a stuck collective fails the job
     fault_inject: str = ""      # "rank:step" -- raise on that rank at that step (failure-detection test hook)
     log_json: str = ""          # rank-0 JSON-lines event log
@@ -103,7 +103,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-graphs", dest="use_graphs", action="store_false", default=None)
     ap.add_argument("--no-softmax-shift", dest="softmax_shift", action="store_false", default=None)
     ap.add_argument("--ckpt-precision", type=int)
-    ap.add_argument("--allreduce", choices=["auto", "xgmi", "rccl", "host"])
+    ap.add_argument("--allreduce", choices=["auto", "xgmi", "xgmi2", "rccl", "host"])
     ap.add_argument("--comm-timeout", type=float)
     ap.add_argument("--fault-inject", help="rank:step")
     ap.add_argument("--log-json")

@@ -344,7 +344,7 @@ class MlpEngine:
                 s.ag_slabs = self.ag_slabs.data_ptr()
                 s.ag_err = self.ag_err.data_ptr()
                 s.fh_allgather = int(self.fh_allgather)
-            elif self.ag_counters is not None:
+            elif self.ag_gran is not None:  # the wide fused head
                 s.fh_tiles = int(self.ag_counters.numel()) // 64  # [2 tilings][tiles][32]
                 s.ag_gran, s.ag_gran_count = self.ag_gran.data_ptr(), int(self.ag_gran.numel())
                 s.ag_counters = self.ag_counters.data_ptr()

@@ -33,6 +33,7 @@ from .engine import MlpEngine
 
 
 XGMI_AUTO_MAX_BYTES = 2 << 20  # allreduce="auto" uses the xGMI one-shot kernel up to this bucket size
+XGMI2_AUTO_MAX_BYTES = 8 << 20  # ... and the two-shot kernel (4+ ranks) up to this one; RCCL beyond
 BUCKET_BYTES = 4 << 20         # dW1 all-reduce chunk of the overlapped RCCL backward
 
 
@@ -79,10 +80,10 @@ class DataParallelTrainer:
         if executor not in ("auto", "graph", "eager"):
             raise ValueError("executor must be auto, graph or eager")
         self.executor = executor
-        # element type of the gradients on the xGMI wire: "f32" (exact), "bf16" (half the bytes, summed in
-        # fp32 after the pull), "auto" = bf16 for the bf16 compute path (its GEMM operands are bf16 already)
-        # when that is what brings the bucket under XGMI_AUTO_MAX_BYTES (784-1024-10: 3.3 -> 1.6 MB), else
-        # the parameter dtype (small buckets keep the exact, wgrad-fused all-reduce)
+        # element type of the gradients on the xGMI wire: "f32" / "auto" (exact), "bf16" (opt-in: half the
+        # bytes of the one-shot kernel, each rank's gradient rounded to bf16 once and summed in fp32 after the
+        # pull -- data-parallel bf16 training then differs from single-GPU bf16 by that rounding; the two-shot
+        # kernel moves 2 S / R bytes per link exactly, which beats it from 4 ranks on)
         if grad_wire not in ("auto", "f32", "bf16"):
             raise ValueError("grad_wire must be auto, f32 or bf16")
         self.grad_wire = grad_wire
@@ -128,7 +129,8 @@ class DataParallelTrainer:
         # bitwise comparison with the separate-kernel step has passed on every rank
         self._xgmi_fused = None
         self.fused_allreduce = False
-        if self.xgmi is not None and fuse_allreduce and self.xgmi.wire == self.engine.params.dtype:
+        if (self.xgmi is not None and fuse_allreduce and self.xgmi.wire == self.engine.params.dtype
+                and self.xgmi.shots == 1):
             slots = self.engine.fused_allreduce_slots()
             if slots and self.engine.params.dtype == torch.float32 and self._fused_fits(slots):
                 from .xgmi import XgmiBucket
@@ -153,7 +155,8 @@ class DataParallelTrainer:
                           and len(self._buckets()) > 1)
         self._comm_stream = torch.cuda.Stream(self.engine.device) if self._bucketed else None
         self.allreduce_impl = "none" if self.R == 1 else (
-            ("xgmi-bf16wire" if self.xgmi.wire == torch.bfloat16 else "xgmi") if self.xgmi is not None
+            ("xgmi-bf16wire" if self.xgmi.wire == torch.bfloat16 else "xgmi-2shot" if self.xgmi.shots == 2
+             else "xgmi") if self.xgmi is not None
             else "host-gloo" if allreduce == "host" else self.comm.name)
 
     def _setup_xgmi(self, mode: str):
@@ -161,8 +164,8 @@ class DataParallelTrainer:
         mode: auto (use it if the self-test passes), xgmi (require it), rccl/off (never)."""
         from .comm import TorchDistComm
 
-        if mode not in ("auto", "xgmi", "rccl", "off", "host"):
-            raise ValueError("allreduce must be auto, xgmi, rccl, host or off")
+        if mode not in ("auto", "xgmi", "xgmi2", "rccl", "off", "host"):
+            raise ValueError("allreduce must be auto, xgmi, xgmi2, rccl, host or off")
         if mode == "host":
             # reference-equivalent sync: gradients staged through host memory and summed over a
             # gloo group, as the reference's MPI_Allreduce on host buffers (neural_network.cpp:496-536)
@@ -176,35 +179,40 @@ class DataParallelTrainer:
         eligible = (self.R > 1 and isinstance(self.comm, TorchDistComm) and e.device.type == "cuda"
                     and e.backend == "hip" and e.params.dtype in (torch.float32, torch.float64))
         if mode in ("rccl", "off") or not eligible:
-            if mode == "xgmi" and not eligible:
+            if mode in ("xgmi", "xgmi2") and not eligible:
                 raise RuntimeError("xgmi all-reduce needs >1 GPU ranks of the hip backend")
             return None
         from .xgmi import XgmiBucket, same_node
 
         if mode == "auto" and (not same_node(self.R) or self.R > 8):
             return None
-        # one-shot: every rank pulls all R-1 peer buckets over its links -- the win for latency-bound
-        # buckets (318 KB at H=100); past a few MB the ring/tree of RCCL moves fewer bytes per link
+        # one-shot: every rank pulls all R-1 peer buckets over its links (S bytes per link) -- the win for
+        # latency-bound buckets (318 KB at H=100); two-shot (R >= 4): 2 S / R bytes per link and one more
+        # round trip -- buckets of a few MB (784-1024-10: 3.3 MB); past that the overlapped RCCL backward
         # (docs/PERFORMANCE.md "Communication policy"); the bytes that count are the WIRE bytes
         fp_bytes = e.params.numel() * e.params.element_size()
-        bf16_wire = e.params.dtype == torch.float32 and (
-            self.grad_wire == "bf16" or (self.grad_wire == "auto" and self.dtype == "bf16"
-                                         and fp_bytes > XGMI_AUTO_MAX_BYTES))
+        bf16_wire = e.params.dtype == torch.float32 and self.grad_wire == "bf16"
         wire = torch.bfloat16 if bf16_wire else e.params.dtype
         wire_bytes = e.params.numel() * torch.tensor([], dtype=wire).element_size()
-        if mode == "auto" and wire_bytes > XGMI_AUTO_MAX_BYTES:
-            return None
+        shots = 2 if mode == "xgmi2" else 1
+        if mode == "auto":
+            if wire_bytes > XGMI_AUTO_MAX_BYTES:
+                if bf16_wire or self.R < 4 or fp_bytes > XGMI2_AUTO_MAX_BYTES:
+                    return None
+                shots = 2
+        if shots == 2 and bf16_wire:
+            raise ValueError("the two-shot xGMI all-reduce moves the exact gradient (grad_wire f32)")
         try:
             xb = XgmiBucket(self.comm.group, self.rank, self.R, e.params.numel(), e.params.dtype, e.device,
-                            wire=wire)
+                            wire=wire, shots=shots)
         except Exception as ex:  # IPC unavailable: every rank sees the same failure at the same point
-            if mode == "xgmi":
+            if mode in ("xgmi", "xgmi2"):
                 raise
             print(f"[rank {self.rank}] xgmi all-reduce unavailable ({ex}); using {self.comm.name}", flush=True)
             return None
         if not xb.ok:
             xb.close()
-            if mode == "xgmi":
+            if mode in ("xgmi", "xgmi2"):
                 raise RuntimeError("xgmi all-reduce self-test failed")
             return None
         return xb

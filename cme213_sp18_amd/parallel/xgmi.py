@@ -32,11 +32,16 @@ def same_node(world: int) -> bool:
 class XgmiBucket:
     MODE_SGD = 0
     MODE_ALLREDUCE = 1
+    MODE_SGD2 = 2
+    MODE_ALLREDUCE2 = 3
 
     def __init__(self, group, rank: int, world: int, numel: int, dtype: torch.dtype, device, self_test: bool = True,
-                 flag_slots: int = 0, wire: torch.dtype | None = None):
+                 flag_slots: int = 0, wire: torch.dtype | None = None, shots: int = 1):
         """wire: the element type in the IPC buffers -- ``dtype`` (default), or torch.bfloat16 for float32
-        gradients (half the bytes over xGMI; every rank sums the R bf16 values in fp32, in rank order)."""
+        gradients (half the bytes over xGMI; every rank sums the R bf16 values in fp32, in rank order).
+        shots: 1 = one-shot (every rank pulls every peer's whole bucket: S bytes per link), 2 = two-shot
+        (reduce-scatter + sharded update + all-gather over peer reads: 2 S / R bytes per link, one more
+        round trip; exact wire only).  A bucket keeps one form: their epochs and flags differ."""
         import torch.distributed as dist
 
         if world > hip().comm.MAX_RANKS:
@@ -46,6 +51,9 @@ class XgmiBucket:
         wire = dtype if wire is None else wire
         if wire not in (dtype, torch.bfloat16) or (wire == torch.bfloat16 and dtype != torch.float32):
             raise TypeError("xGMI bucket: the wire is the gradient dtype, or bf16 for float32 gradients")
+        if shots not in (1, 2) or (shots == 2 and wire != dtype):
+            raise ValueError("xGMI bucket: shots 1, or 2 with the exact wire")
+        self.shots = shots
         self.rank, self.world, self.numel, self.dtype, self.wire = rank, world, int(numel), dtype, wire
         self.group = group
         self.device = torch.device(device)
@@ -108,7 +116,8 @@ class XgmiBucket:
     def allreduce_(self, t: torch.Tensor) -> None:
         """In-place SUM of a contiguous tensor of exactly ``numel`` elements."""
         assert t.numel() == self.numel and t.dtype == self.dtype and t.is_contiguous()
-        self.c.run(self.code, t.data_ptr(), 0, 0.0, 0, 0, 0, self.MODE_ALLREDUCE, self.numel, self._stream())
+        mode = self.MODE_ALLREDUCE2 if self.shots == 2 else self.MODE_ALLREDUCE
+        self.c.run(self.code, t.data_ptr(), 0, 0.0, 0, 0, 0, mode, self.numel, self._stream())
 
     def sgd_(self, grads: torch.Tensor, params: torch.Tensor, lr: float, planes: torch.Tensor | None = None,
              np_: int = 0, w1n: int = 0, status_index: int | None = None) -> None:
@@ -118,8 +127,9 @@ class XgmiBucket:
         assert grads.numel() == self.numel == params.numel()
         pl = planes.data_ptr() if planes is not None else 0
         st = grads[status_index:].data_ptr() if status_index is not None else 0
+        mode = self.MODE_SGD2 if self.shots == 2 else self.MODE_SGD
         self.c.run(self.code, grads.data_ptr(), params.data_ptr(), float(lr), pl, np_ if pl else 0, w1n,
-                   self.MODE_SGD, self.numel, self._stream(), st)
+                   mode, self.numel, self._stream(), st)
 
     def error(self) -> int:
         return int(self.c.error())

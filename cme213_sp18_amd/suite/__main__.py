@@ -129,7 +129,7 @@ def cmd_shift(a):
     from . import hw2, hw4
 
     _cuda()
-    text = open(a.text, "rb").read() if a.text else hw4.synthetic_english(1_235_150, seed=0)
+    text = hw4.read_text(a.text)  # default: the reference's Moby Dick (tests/fixtures)
     print(f"{'bytes':>12} " + " ".join(f"{'w=' + str(w) + ' GB/s':>12}" for w in hw2.SHIFT_WIDTHS))
     rows = []
     for d in range(a.doublings + 1):
@@ -192,7 +192,7 @@ def cmd_create_cipher(a):
     from . import hw4
 
     _cuda()
-    text = open(a.text, "rb").read()
+    text = hw4.read_text(None if a.text == "-" else a.text)
     clean = hw4.sanitize(text)
     print("\nBefore ciphering!\n")
     g = hw4.letter_frequency_gpu(clean)
@@ -255,7 +255,7 @@ def main(argv=None) -> int:
     s.add_argument("--order", type=int, default=8)
     s.add_argument("--json", action="store_true")
     s = sub.add_parser("create_cipher")
-    s.add_argument("text")
+    s.add_argument("text", help="plaintext file (.gz ok); '-' = the shipped Moby Dick")
     s.add_argument("period", type=int)
     s.add_argument("--seed", type=int, default=123)
     s.add_argument("--no-wrap", action="store_true", help="reference byte-add semantics")

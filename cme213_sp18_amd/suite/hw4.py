@@ -16,6 +16,9 @@ reproduces the reference's plain byte add (apply_shift has no mod-26 wrap).
 """
 from __future__ import annotations
 
+import gzip
+import os
+
 import numpy as np
 import torch
 
@@ -42,6 +45,20 @@ def synthetic_english(n: int, seed: int = 0) -> bytes:
     gaps = gaps[gaps < n]
     out[gaps] = rng.choice(np.frombuffer(b"     ,.;\n", np.uint8), gaps.size)
     return out.tobytes()
+
+
+MOBY_DICK = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                         "tests", "fixtures", "mobydick.txt.gz")
+
+
+def read_text(path: str | None = None) -> bytes:
+    """The plaintext of the reference's shift / cipher drivers (hw2code/main_q1.cu:74-141,
+    hw4code/create_cipher.cu:147-195 read ``mobydick.txt``).  ``None`` -> the public-domain Moby Dick shipped
+    gzipped in tests/fixtures (byte-identical to the reference's 1,235,150-byte file once decompressed); a
+    path ending in ``.gz`` is decompressed."""
+    p = path or MOBY_DICK
+    with (gzip.open(p, "rb") if p.endswith(".gz") else open(p, "rb")) as f:
+        return f.read()
 
 
 def _t(a) -> torch.Tensor:

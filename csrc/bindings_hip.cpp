@@ -113,6 +113,7 @@ struct MlpStep {
   // H = 300 -- at H <= 128 the all-gather head stores planes cheaply and the 25-fold re-split of dZ1 in the
   // dW1 tiles costs +0.5 us (VALU: 4 cycles per wave64 op on the 16-lane SIMD)
   int a_fp32 = -1;
+  int u8_pairs = 1;  // SplitStepArgs::u8_pairs (the pixel operand's 16-byte chunk-pair loads; 0 for A/B)
 
   cme::SplitStepArgs split_args(int64_t off, int n, double scale, double reg, double lr, int sgd,
                                 int with_loss) const {
@@ -135,6 +136,7 @@ struct MlpStep {
     a.stamps = reinterpret_cast<unsigned long long*>(stamps);
     a.bias_col = bias_col;
     a.a_fp32 = a_fp32 >= 0 ? a_fp32 : (H <= 128 ? 1 : 3);
+    a.u8_pairs = u8_pairs;
     // a timed-out all-gather forward + head launch (sticky word) makes every later update a no-op
     a.ag_err = P_<const int>(ag_err);
     a.gstatus = P_<float>(gstatus);
@@ -442,6 +444,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_gran_count", &MlpStep::ag_gran_count)
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
       .def_readwrite("a_fp32", &MlpStep::a_fp32)
+      .def_readwrite("u8_pairs", &MlpStep::u8_pairs)
       .def("w1_planes_read",
            [](const MlpStep& st) {  // a forward kernel of this step reads the W1 planes (else: not refreshed)
              return st.split != 0 && cme::mlp_split_w1_planes_read(st.split_args(0, st.ld, 1.0, 0.0, 0.0, 1, 0));

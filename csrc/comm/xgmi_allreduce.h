@@ -13,6 +13,12 @@ namespace cme::comm {
 constexpr int kMaxRanks = 8;  // one xGMI hive
 constexpr int kModeSgd = 0;        // params -= lr * sum(grads)   (+ bf16 plane/shadow refresh)
 constexpr int kModeAllReduce = 1;  // grads  := sum(grads)
+// two-shot forms (reduce-scatter + all-gather over peer reads, exact wire only): chunk c is owned by rank
+// c % world, which sums the R gradient chunks (rank order: the one-shot's bits) and applies the update
+// (sharded SGD) or keeps the sum; every other rank then copies the owner's result.  Each xGMI link carries
+// 2 S / R bytes instead of the one-shot's S: the form for buckets of a few MB at 8 ranks.
+constexpr int kModeSgd2 = 2;
+constexpr int kModeAllReduce2 = 3;
 
 struct XgmiDesc {
   int rank = 0, world = 1;

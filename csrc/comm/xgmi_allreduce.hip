@@ -237,6 +237,157 @@ __device__ __forceinline__ void do_chunk(const Args<T, W>& a, int64_t c, uint32_
   if (t == 0) a.epochs[c] = epoch;
 }
 
+// ---- two-shot: reduce-scatter + (sharded update) + all-gather, over peer reads (kModeSgd2 / kModeAllReduce2)
+// Chunk c (kChunk2 elements) belongs to rank c % world.  Every rank stores its gradient chunk write-through
+// into this step's half of its IPC buffer and signals the owner (flag 2e); the owner waits for all R, sums
+// them in rank order (the one-shot's order: identical bits), applies params -= lr * sum (or keeps the sum),
+// stores the result write-through over its own gradient chunk (only the owner ever reads that chunk) and
+// signals every peer (flag 2e + 1); a non-owner waits for that flag and copies the owner's chunk.  Blocks
+// visit chunks in the same order on every rank and publish before they wait, so no wait is circular.  Double
+// buffering holds as in the one-shot: a rank rewrites half e & 1 of chunk c only after completing step e + 1
+// of it, which needed every reader of its step-e data (the owner; every rank for the owner's result) done.
+constexpr int kVec2 = 16;                  // elements per thread
+constexpr int kChunk2 = kThreads * kVec2;  // 4096 elements per chunk
+
+template <typename T>
+__device__ __forceinline__ void do_chunk2(const Args<T, T>& a, int64_t c, uint32_t* s_sync) {
+  const int t = threadIdx.x;
+  const int owner = (int)(c % a.world);
+  if (t == 0) {
+    s_sync[0] = a.epochs[c] + 1;
+    s_sync[1] = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                (a.status && *a.status != T(0));
+  }
+  __syncthreads();
+  if (s_sync[1]) return;
+  const uint32_t e = s_sync[0];
+  const int64_t half = (int64_t)(e & 1u) * a.npad;
+  const int64_t i0 = c * kChunk2;
+  using V = T __attribute__((ext_vector_type(4)));
+  constexpr int Q = kVec2 / 4;  // 4-element vectors per thread; vector q of thread t: i0 + (q * kThreads + t) * 4
+  const __amdgpu_buffer_rsrc_t rmine = __builtin_amdgcn_make_buffer_rsrc(a.mybuf, (short)0, 0x7FFFFFFF, 0x00020000);
+  auto store_v = [&](int64_t idx, const V& v) {  // 4 elements at idx of this step's half, write-through
+    if (idx + 4 <= a.n) {
+#pragma unroll
+      for (int q = 0; q < (int)(sizeof(V) / 16); ++q) {
+        __attribute__((ext_vector_type(4))) unsigned w;
+        __builtin_memcpy(&w, reinterpret_cast<const char*>(&v) + 16 * q, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(w, rmine, (int)((half + idx) * (int64_t)sizeof(T)) + 16 * q, 0,
+                                               kSysCoherent);
+      }
+    } else {
+      for (int k = 0; k < 4 && idx + k < a.n; ++k) {
+        const T x = v[k];
+        if constexpr (sizeof(T) == 4) {
+          unsigned w;
+          __builtin_memcpy(&w, &x, 4);
+          __builtin_amdgcn_raw_buffer_store_b32(w, rmine, (int)((half + idx + k) * 4), 0, kSysCoherent);
+        } else {
+          __attribute__((ext_vector_type(2))) unsigned w;
+          __builtin_memcpy(&w, &x, 8);
+          __builtin_amdgcn_raw_buffer_store_b64(w, rmine, (int)((half + idx + k) * 8), 0, kSysCoherent);
+        }
+      }
+    }
+  };
+  auto load_v = [&](const void* base, int64_t idx) -> V {  // 4 elements of a peer's half, system coherent
+    V v;
+    if (idx + 4 <= a.n) {
+      v = peer_load<V>(base, (half + idx) * (int64_t)sizeof(T));
+    } else {
+      for (int k = 0; k < 4; ++k) v[k] = idx + k < a.n ? peer_load<T>(base, (half + idx + k) * (int64_t)sizeof(T)) : T(0);
+    }
+    return v;
+  };
+  auto apply = [&](int64_t idx, const V& v, bool from_sum) {  // sum -> update, or the owner's result -> copy
+    for (int k = 0; k < 4 && idx + k < a.n; ++k) {
+      const int64_t i = idx + k;
+      if (a.mode == kModeAllReduce2) {
+        const_cast<T*>(a.grads)[i] = v[k];
+        continue;
+      }
+      const T w = from_sum ? a.params[i] - a.lr * v[k] : v[k];
+      a.params[i] = w;
+      if (a.planes && i < a.w1n) {
+        if (a.np == 3) store_planes<3>((float)w, a.planes, a.w1n, i);
+        else store_planes<1>((float)w, a.planes, a.w1n, i);
+      }
+    }
+  };
+  // 1. my gradient chunk -> my IPC buffer, drained by every wave, then signal the owner
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int64_t idx = i0 + ((int64_t)q * kThreads + t) * 4;
+    if (idx >= a.n) break;
+    V g;
+    if (idx + 4 <= a.n) g = *reinterpret_cast<const V*>(a.grads + idx);
+    else
+      for (int k = 0; k < 4; ++k) g[k] = idx + k < a.n ? a.grads[idx + k] : T(0);
+    store_v(idx, g);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0)
+    __hip_atomic_store(a.peerflags[owner] + c * kMaxRanks + a.rank, 2u * e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  auto wait_flag = [&](int slot, uint32_t target) {  // one lane; sets s_sync[1] on timeout
+    uint32_t spins = 0;
+    const uint32_t* f = a.myflags + c * kMaxRanks + slot;
+    while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+      if (++spins > kSpinLimit) {
+        atomicExch(a.err, 1);
+        s_sync[1] = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  if (owner == a.rank) {
+    // 2a. every rank's chunk, summed in rank order; the update (or the sum) published write-through
+    if (t < a.world) wait_flag(t, 2u * e);
+    __syncthreads();
+    if (s_sync[1]) return;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int64_t idx = i0 + ((int64_t)q * kThreads + t) * 4;
+      if (idx >= a.n) break;
+      V acc = load_v(a.peers[0], idx);
+      for (int r = 1; r < a.world; ++r) acc += load_v(a.peers[r], idx);
+      apply(idx, acc, true);
+      V res;
+      if (a.mode == kModeAllReduce2) res = acc;
+      else
+        for (int k = 0; k < 4; ++k) res[k] = idx + k < a.n ? a.params[idx + k] : T(0);
+      store_v(idx, res);  // (over this rank's own gradient chunk: only the owner reads it)
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t < a.world && t != a.rank)
+      __hip_atomic_store(a.peerflags[t] + c * kMaxRanks + a.rank, 2u * e + 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    // 2b. the owner's result of this chunk
+    if (t == 0) wait_flag(owner, 2u * e + 1u);
+    __syncthreads();
+    if (s_sync[1]) return;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int64_t idx = i0 + ((int64_t)q * kThreads + t) * 4;
+      if (idx >= a.n) break;
+      apply(idx, load_v(a.peers[owner], idx), false);
+    }
+  }
+  if (t == 0) a.epochs[c] = e;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void xgmi_twoshot_kernel(Args<T, T> a, int64_t nchunks) {
+  __shared__ uint32_t s_sync[2];
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    do_chunk2(a, c, s_sync);
+    __syncthreads();
+  }
+}
+
 // Grid-stride over chunks with a capped grid: a block only ever waits on the
 // same chunk of its peers, and the capped grid is always fully resident.
 template <typename T, typename W>
@@ -250,7 +401,10 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(Args<T, W> a, 
 
 }  // namespace
 
-int64_t xgmi_padded_count(int64_t n) { return (n + kChunk - 1) / kChunk * kChunk; }
+int64_t xgmi_padded_count(int64_t n) {
+  const int64_t c = std::max<int64_t>(kChunk, kChunk2);  // both forms' chunks tile the padded halves
+  return (n + c - 1) / c * c;
+}
 int64_t xgmi_num_blocks(int64_t n) { return (n + kChunk - 1) / kChunk; }
 
 void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* params, double lr, void* planes, int np,
@@ -259,7 +413,42 @@ void xgmi_allreduce(const XgmiDesc& d, int dtype, const void* grads, void* param
   CME_REQUIRE(d.rank >= 0 && d.rank < d.world, "xgmi_allreduce: bad rank");
   CME_REQUIRE(d.npad == xgmi_padded_count(d.n), "xgmi_allreduce: descriptor count mismatch");
   CME_REQUIRE(np == 0 || np == 1 || np == 3, "xgmi_allreduce: planes must be 0, 1 or 3");
-  CME_REQUIRE(mode == kModeSgd || mode == kModeAllReduce, "xgmi_allreduce: bad mode");
+  CME_REQUIRE(mode >= kModeSgd && mode <= kModeAllReduce2, "xgmi_allreduce: bad mode");
+  if (mode >= kModeSgd2) {
+    CME_REQUIRE(dtype != 2, "xgmi_allreduce: the two-shot forms move the exact gradient (no bf16 wire)");
+    const int64_t nc2 = (d.n + kChunk2 - 1) / kChunk2;
+    if (nc2 == 0) return;
+    const unsigned grid2 = (unsigned)std::min<int64_t>(nc2, kMaxGrid);
+    auto fill2 = [&](auto* tag) {
+      using T = std::remove_pointer_t<decltype(tag)>;
+      Args<T, T> a{};
+      a.grads = static_cast<const T*>(grads);
+      a.params = static_cast<T*>(params);
+      a.mybuf = static_cast<T*>(d.mybuf);
+      for (int r = 0; r < d.world; ++r) {
+        a.peers[r] = static_cast<const T*>(d.peers[r]);
+        a.peerflags[r] = d.peerflags[r];
+      }
+      a.myflags = d.myflags;
+      a.epochs = d.epochs;
+      a.err = d.err;
+      a.n = d.n;
+      a.npad = d.npad;
+      a.w1n = w1n;
+      a.lr = (T)lr;
+      a.planes = static_cast<__hip_bfloat16*>(planes);
+      a.np = planes ? np : 0;
+      a.rank = d.rank;
+      a.world = d.world;
+      a.mode = mode;
+      a.status = static_cast<const T*>(status);
+      xgmi_twoshot_kernel<T><<<grid2, kThreads, 0, s>>>(a, nc2);
+    };
+    if (dtype == 1) fill2((double*)nullptr);
+    else fill2((float*)nullptr);
+    CME_LAUNCH_CHECK(s);
+    return;
+  }
   const int64_t nchunks = xgmi_num_blocks(d.n);
   if (nchunks == 0) return;
   const unsigned grid = (unsigned)std::min<int64_t>(nchunks, kMaxGrid);

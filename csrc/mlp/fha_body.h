@@ -78,19 +78,20 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   // a dependent memory round trip after the all-gather wait
   const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(
       make_rsrc(h.labels), c0 + (t >> 4) < n ? (c0 + (t >> 4)) * 4 : kOOB, 0, 0);
-  // W2 slice of this tile's rows (read by the z2 partial and by dZ1) and b2; wsk_tile's barrier orders them
-  if (t < 256) {
-    const int c = t >> 4, r = t & 15;
-    w2s[c][r] = buf_load1<float>(make_rsrc(h.W2), (c < C && r0 + r < H) ? (c * H + r0 + r) * 4 : kOOB);
-  } else if (t < 256 + 16) {
-    const int c = t - 256;
-    b2s[c] = buf_load1<float>(make_rsrc(h.b2), c < C ? c * 4 : kOOB);
-  }
+  // W2 slice of this tile's rows (read by the z2 partial and by dZ1) and b2: loaded now, written to LDS after
+  // the GEMM (written here, each wave waited for its W2 load before its K-loop burst: a dependent memory round
+  // trip in front of the GEMM, ~0.5 us of the launch per bench/stamps_fha.py)
+  const int wc = t >> 4, wr = t & 15;
+  const float w2v = buf_load1<float>(
+      make_rsrc(h.W2), (t < 256 && wc < C && r0 + wr < H) ? (wc * H + r0 + wr) * 4 : kOOB);
+  const float b2v = buf_load1<float>(make_rsrc(h.b2), (t >= 256 && t < 256 + 16 && t - 256 < C) ? (t - 256) * 4 : kOOB);
   TileGeom g{H, n, f.P, r0, c0};
   EpiSigLds epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
-  fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red);
+  fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
   // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
-  // they are masked below.
+  // they are masked below.  w2s / b2s are complete after the barrier below.
+  if (t < 256) w2s[wc][wr] = w2v;
+  else if (t < 256 + 16) b2s[t - 256] = b2v;
   if (t == 0) {
     s_ep = (unsigned)(ep_old / (unsigned)tm) + 1u;
     s_bad = 0;

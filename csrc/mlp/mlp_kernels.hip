@@ -6,6 +6,7 @@
 #include "mma_tile.h"
 #include "fwd_tile.h"
 #include "fha_body.h"
+#include "head_math.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -832,9 +833,10 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
     float lp = 0.f;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-      const float y = e[c] * inv;
+      float d;
+      const float y = head_prob_grad(e[c], inv, c == lab, sc, d);  // the fused wide head's arithmetic
       if (c == lab) lp = -__logf(y);
-      const float d = (ok && c < C) ? (y - (c == lab ? 1.f : 0.f)) * sc : 0.f;
+      if (!(ok && c < C)) d = 0.f;
       Ds[c][t] = d;
       if (rb == 0 && ok && c < C) static_cast<float*>(a.D)[(size_t)c * a.ldd + col] = d;
     }
@@ -1305,16 +1307,26 @@ int cu_count() {
 }
 }  // namespace
 
+// the wave-split-K forward's operand form: 3 = 16-byte pixel loads over chunk pairs (16-byte X rows), 1 = 4-byte
+// pixel loads, 0 = element loads (mma_tile.h VEC)
+static int fha_vec(const SplitStepArgs& f) {
+  const bool af = mlp_split_fwd_fp32_w(f);
+  const uintptr_t x = reinterpret_cast<uintptr_t>(f.X);
+  if (x % 4 != 0 || reinterpret_cast<uintptr_t>(af ? (const void*)f.W1 : f.W1p) % 16 != 0 || f.P % 8 != 0) return 0;
+  return f.u8_pairs && x % 16 == 0 && f.P % 16 == 0 ? 3 : 1;
+}
+
 bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f) {
   if (f.n <= 0) return true;
   const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32), nwg = 8 * tm * cdiv(tn, 8);
   const bool af = mlp_split_fwd_fp32_w(f);
-  const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 &&
-                   reinterpret_cast<uintptr_t>(af ? (const void*)f.W1 : f.W1p) % 16 == 0 && f.P % 8 == 0;
-  int occ;
-  if (af) occ = vec ? resident_per_cu<fwd1_head_ag_kernel<3, 1, true>>(512) : resident_per_cu<fwd1_head_ag_kernel<3, 0, true>>(512);
-  else if (f.npw == 3) occ = vec ? resident_per_cu<fwd1_head_ag_kernel<3, 1, false>>(512) : resident_per_cu<fwd1_head_ag_kernel<3, 0, false>>(512);
-  else occ = vec ? resident_per_cu<fwd1_head_ag_kernel<1, 1, false>>(512) : resident_per_cu<fwd1_head_ag_kernel<1, 0, false>>(512);
+  const int vec = fha_vec(f);
+#define CME_OCC(np, af)                                                            \
+  (vec == 3   ? resident_per_cu<fwd1_head_ag_kernel<np, 3, af>>(512)               \
+   : vec == 1 ? resident_per_cu<fwd1_head_ag_kernel<np, 1, af>>(512)               \
+              : resident_per_cu<fwd1_head_ag_kernel<np, 0, af>>(512))
+  const int occ = af ? CME_OCC(3, true) : (f.npw == 3 ? CME_OCC(3, false) : CME_OCC(1, false));
+#undef CME_OCC
   return nwg <= occ * cu_count();
 }
 
@@ -1330,11 +1342,11 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
   CME_REQUIRE(mlp_fwd1_head_ag_fits(f), "fwd1_head_ag: grid larger than the device holds at once (use the "
                                         "last-arriver form, mlp_fwd1_head)");
   const bool af = mlp_split_fwd_fp32_w(f);
-  const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 &&
-                   reinterpret_cast<uintptr_t>(af ? (const void*)f.W1 : f.W1p) % 16 == 0 && f.P % 8 == 0;
+  const int vec = fha_vec(f);
   const int nwg = 8 * tm * cdiv(tn, 8);
-#define CME_FHA(np, af)                                                                             \
-  if (vec) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
+#define CME_FHA(np, af)                                                                                  \
+  if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
+  else if (vec == 1) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn); \
   else fwd1_head_ag_kernel<np, 0, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);
   if (af) { CME_FHA(3, true) } else if (f.npw == 3) { CME_FHA(3, false) } else { CME_FHA(1, false) }
 #undef CME_FHA

@@ -82,6 +82,9 @@ struct SplitStepArgs {
   // GEMM reads fp32 dZ1 (4 B per element, split into the exact bf16 planes in registers; the head then
   // writes no dZ1 planes); clear bits: the stored planes (6 B per element, split once by their writer)
   int a_fp32 = 1;
+  // small layers: the uint8 pixel operand of the wave-split-K GEMMs as ONE 16-byte load per lane per pair of
+  // K chunks (mma_tile.h VEC = 3) where rows are 16-byte aligned and K % 16 == 0; 0: two 4-byte loads per chunk
+  int u8_pairs = 1;
   // wide layers: the head left dW2 partials [cdiv(n, 32)][16][H] (HeadArgs::dw2part); the dW2 role then sums
   // them in column-tile order instead of forming D . a1^T from all of a1
   float* dw2part = nullptr;

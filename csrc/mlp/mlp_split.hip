@@ -6,6 +6,7 @@
 
 #include "glds_gemm.h"
 #include "granule.h"
+#include "head_math.h"
 #include "rega_gemm.h"
 #include "lds_gemm.h"
 #include "mma_tile.h"
@@ -800,8 +801,9 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
     wv[i] = buf_load1<float>(make_rsrc(a.W2), (4 * fg + i < C && rw + fr < H) ? ((4 * fg + i) * H + rw + fr) * 4 : kOOB);
   const int u0 = n0 + 16 * rt;  // the 16 columns row tile rt < NU reduces
   const bool red = rt < NU && u0 < n;
+  // (the label of this thread's softmax column u0 + (t >> 4), fetched now)
   const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(
-      make_rsrc(h.labels), (red && t < 16 && u0 + t < n) ? (u0 + t) * 4 : kOOB, 0, 0);
+      make_rsrc(h.labels), (red && t < 256 && u0 + (t >> 4) < n) ? (u0 + (t >> 4)) * 4 : kOOB, 0, 0);
   const int zc = t >> 4, zcol = u0 + (t & 15);
   const float b2v = buf_load1<float>(make_rsrc(h.b2), (red && t < 256 && zc < C) ? zc * 4 : kOOB);
   // ---- hand-off 1 (reducers): the tm z2 partials of (class zc, column zcol), in tile order, 32 per poll
@@ -824,34 +826,36 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
   if (sw[1]) return;  // workgroup-uniform: a partial never arrived
   // ---- softmax / loss / D of columns u0 .. u0 + 15
   if (red) {
-    if (t < 16) {  // head_wide_kernel's softmax arithmetic, in its order
-      const int col = u0 + t;
+    if (t < 256) {  // softmax / loss / D: 16 lanes (classes) per column, 4 columns per wave
+      const int col2 = t >> 4, cls = t & 15, col = u0 + col2, lb = lane & ~15;
       const bool ok = col < n;
       const int lab = ok ? lab_pre : -1;
+      const float z = zs[cls * 17 + col2];
       float m = 0.f;
-      if (h.shift) {
-        m = zs[t];
-        for (int c = 1; c < C; ++c) m = fmaxf(m, zs[c * 17 + t]);
-      }
-      float e[16], sum = 0.f;
+      if (h.shift) {  // (max is exact: any order gives head_wide_kernel's value)
+        m = cls < C ? z : -3.402823466e38f;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        e[c] = c < C ? __expf(zs[c * 17 + t] - m) : 0.f;
-        sum += e[c];
+        for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
       }
+      const float e = cls < C ? __expf(z - m) : 0.f;
+      // the class sum in class order, as head_wide_kernel adds it: bit-identical D, loss and dZ1
+      float sum = 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) sum += __shfl(e, lb + c, 64);
       const float inv = 1.f / sum, sc = (float)h.scale;
-      float lp = 0.f;
-      const __amdgpu_buffer_rsrc_t rd = make_rsrc(h.D);
-      const bool hooked = a.ag_test_skip == rt && ct == 0;  // test hook: this tile's D never arrives
+      const bool hit = cls == lab;
+      float d;
+      const float y = head_prob_grad(e, inv, hit, sc, d);  // head_wide_kernel's arithmetic (head_math.h)
+      if (!(ok && cls < C)) d = 0.f;
+      float lp = hit ? -__logf(y) : 0.f;  // one non-zero lane per column: any summation order is exact
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const float y = e[c] * inv;
-        if (c == lab) lp = -__logf(y);
-        const float d = (ok && c < C) ? (y - (c == lab ? 1.f : 0.f)) * sc : 0.f;
-        st_f32(rd, (ok && c < C) ? (c * h.ldd + col) * 4 : kOOB, d);  // for the weight-gradient launch
-        if (ok && c < C && !hooked) gran_store(g.dg + (size_t)c * a.ld + col, d, ep);
+      for (int o = 1; o < 16; o <<= 1) lp += __shfl_xor(lp, o, 64);
+      const bool hooked = a.ag_test_skip == rt && ct == 0;  // test hook: this tile's D never arrives
+      if (ok && cls < C) {
+        st_f32(make_rsrc(h.D), (cls * h.ldd + col) * 4, d);  // for the weight-gradient launch
+        if (!hooked) gran_store(g.dg + (size_t)cls * a.ld + col, d, ep);
       }
-      ls[t] = lp;
+      if (cls == 0) ls[col2] = lp;
     }
     __syncthreads();
     ag_stamp(a, 4, true);
@@ -1731,12 +1735,15 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   // (fp32 dZ1: 2 x 16-byte vectors when n % 8 == 0, else element loads -- mma_tile.h VA)
   const bool af = small_wgrad_fp32_ok(a);
   const bool base_ok = al16(af ? (const void*)a.dZ1 : a.dZ1p) && al4(a.XT) && a.ld % 8 == 0 && a.ldxt % 4 == 0;
-  const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? 1 : (a.n % 4 == 0 ? 2 : 0));
+  // (3: the XT bytes as 16-byte loads over chunk pairs, mma_tile.h: 16-byte XT rows, n % 16 == 0)
+  const bool pairs = a.u8_pairs && al16(a.XT) && a.ldxt % 16 == 0 && a.n % 16 == 0;
+  const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? (pairs ? 3 : 1) : (a.n % 4 == 0 ? 2 : 0));
   const dim3 grid(t1 + t2 + tb);
   SplitStepArgs b = a;
   b.w1_planes = mlp_split_w1_planes_read(a) ? 1 : 0;
 #define CME_WG(npz, af)                                                                   \
-  if (vec == 1) wgrad_split_kernel<npz, 1, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);      \
+  if (vec == 3) wgrad_split_kernel<npz, 3, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);      \
+  else if (vec == 1) wgrad_split_kernel<npz, 1, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \
   else if (vec == 2) wgrad_split_kernel<npz, 2, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \
   else wgrad_split_kernel<npz, 0, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
   if (af) { CME_WG(3, true) } else if (a.npz == 3) { CME_WG(3, false) } else { CME_WG(1, false) }

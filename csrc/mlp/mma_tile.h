@@ -354,16 +354,24 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
 
   constexpr bool AF32 = std::is_same_v<TA, float> && !std::is_same_v<T, float>;
   static_assert(!AF32 || (std::is_same_v<T, __hip_bfloat16> && NPA == 3 && AK), "fp32 A: split3 bf16, K-contiguous");
-  constexpr int VA = VEC == 1 ? 1 : 0;  // fp32 A: 2 x 16-byte loads, or element loads
+  constexpr bool BU8 = std::is_same_v<TB, uint8_t>;
+  // VEC == 3 (u8 B only): chunks go in PAIRS.  Lane group grp of chunk pair (u, u + 1) covers the 16 k
+  // kp + 16 grp .. kp + 16 grp + 15 (kp = the pair's first k): chunk u takes the first 8, chunk u + 1 the
+  // last 8 (the MFMA sums over its chunk, so any bijection of k onto (lane group, element) that A and B
+  // share is the same product).  B is then ONE 16-byte load per lane per pair instead of four 4-byte loads
+  // (the u8 rows are 16 B per lane group); A keeps its 16-byte vectors.  Needs kend % 16 == 0 and 16-byte
+  // aligned B rows.
+  static_assert(VEC != 3 || (BU8 && U % 2 == 0 && V == 8), "paired chunks: u8 B, even U");
+  constexpr int VECA = VEC == 3 ? 1 : VEC;  // the A operand's load form
+  constexpr int VA = VECA == 1 ? 1 : 0;     // fp32 A: 2 x 16-byte loads, or element loads
   for (int kc = kbeg; kc < kend; kc += KC * U) {
     T af[U][NPA][MB][V];
     float ar[AF32 ? U : 1][MB][V];
     T bf[U][NB][V];
-    constexpr bool BU8 = std::is_same_v<TB, uint8_t>;
-    U8Raw<VEC> braw[BU8 ? U : 1][NB];
+    U8Raw<VEC == 3 ? 1 : VEC> braw[BU8 ? U : 1][NB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int k = kc + u * KC + V * grp;
+      const int k = VEC == 3 ? kc + (u & ~1) * KC + 2 * V * grp + (u & 1) * V : kc + u * KC + V * grp;
       if constexpr (AF32) {
 #pragma unroll
         for (int i = 0; i < MB; ++i) load_frag<float, V, true, VA>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, ar[u][i]);
@@ -372,15 +380,27 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
         for (int p = 0; p < NPA; ++p)
 #pragma unroll
           for (int i = 0; i < MB; ++i)
-            load_frag<T, V, AK, VEC>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, af[u][p][i], p * plane_bytes);
+            load_frag<T, V, AK, VECA>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, af[u][p][i], p * plane_bytes);
       }
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        if constexpr (std::is_same_v<TB, uint8_t>) {
+        if constexpr (BU8) {
           static_assert(std::is_same_v<T, __hip_bfloat16> && BK, "u8 B operand: bf16 MFMA, K-contiguous");
-          load_u8_raw<VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, braw[u][j]);
+          if constexpr (VEC == 3) {
+            if ((u & 1) == 0) {  // the pair's 16 bytes: words 0-1 -> chunk u, words 2-3 -> chunk u + 1
+              const int r = g.n0 + 16 * j + c;
+              const auto w = __builtin_amdgcn_raw_buffer_load_b128(
+                  rsB, (r < g.N && k + 16 <= kend) ? r * ldb + k : kOOB, 0, 0);
+              braw[u][j].w[0] = w[0];
+              braw[u][j].w[1] = w[1];
+              braw[u + 1][j].w[0] = w[2];
+              braw[u + 1][j].w[1] = w[3];
+            }
+          } else {
+            load_u8_raw<VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, braw[u][j]);
+          }
         } else {
-          load_frag<T, V, BK, VEC>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, bf[u][j]);
+          load_frag<T, V, BK, VECA>(rsB, ldb, g.n0 + 16 * j + c, g.N, k, kend, bf[u][j]);
         }
       }
     }
@@ -393,7 +413,7 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
     for (int u = 0; u < U; ++u) {
       if constexpr (BU8) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) widen_u8<VEC>(braw[u][j], bf[u][j]);
+        for (int j = 0; j < NB; ++j) widen_u8<VEC == 3 ? 1 : VEC>(braw[u][j], bf[u][j]);
       }
       if constexpr (AF32) {
 #pragma unroll

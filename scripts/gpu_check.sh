@@ -20,7 +20,8 @@ for st in "$@"; do
   case "$st" in
     tests=*)
       eval "timeout -k 10 900 python -u -m pytest ${st#tests=} -m gpu -x -q --timeout 240 --timeout-method thread" \
-        > $O/pytest.log 2>&1; rc=$?; tail -4 $O/pytest.log; [ $rc -eq 0 ] || exit $rc ;;
+        > $O/pytest.log 2>&1; rc=$?; tail -4 $O/pytest.log
+      [ $rc -eq 0 ] || { grep -E "^E |^FAILED" $O/pytest.log | tail -30; exit $rc; } ;;
     tests)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
         > $O/pytest_all.log 2>&1; rc=$?; tail -4 $O/pytest_all.log; [ $rc -eq 0 ] || exit $rc ;;

@@ -299,7 +299,10 @@ DP_MODES = (  # (name, H, trainer kwargs)
     ("rccl", 100, dict(allreduce="rccl")),
     ("rccl-bucketed", 4096, dict(allreduce="rccl", overlap_chunks=4)),
     # BASELINE config 5's shape: the bf16 path's 3.3 MB fp32 gradient over a bf16 xGMI wire (1.6 MB)
-    ("xgmi-bf16wire", 1024, dict(allreduce="xgmi", dtype="bf16")),
+    ("xgmi-bf16wire", 1024, dict(allreduce="xgmi", dtype="bf16", grad_wire="bf16")),
+    # ... and exactly, through the two-shot kernel (reduce-scatter + sharded SGD + all-gather)
+    ("xgmi-2shot", 1024, dict(allreduce="xgmi2", dtype="bf16")),
+    ("xgmi-2shot-f32", 300, dict(allreduce="xgmi2")),
     ("host", 100, dict(allreduce="host")),
 )
 

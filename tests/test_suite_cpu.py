@@ -216,6 +216,18 @@ def test_synthetic_english_ioc_separates_period():
     assert list(s[ioc > hw4.IOC_THRESHOLD]) == [6, 12, 18]
 
 
+def test_moby_dick_fixture_and_period():
+    """The shipped plaintext is the reference's mobydick.txt (1,235,150 bytes); the host Vigenere
+    + kappa IoC pipeline on it recovers the period, as hw4code/solve_cipher.cu:75-109 does."""
+    raw = hw4.read_text()
+    assert len(raw) == 1_235_150 and raw.count(b"Ishmael") > 10
+    t = hw4.sanitize_host(raw)
+    x = hw4.vigenere_host(t, hw4.make_shifts(7), 1, True)
+    s = np.arange(4, 16)
+    m = np.array([np.count_nonzero(x[:-k] == x[k:]) for k in s])
+    assert list(s[hw4.index_of_coincidence(m, len(x), s) > hw4.IOC_THRESHOLD]) == [7, 14]
+
+
 def test_stencil_byte_models():
     """calcBytes (simParams.cpp:79-93) counts every tap; the compulsory model reads the grid and writes the
     interior once per iteration, so it is the smaller (and the one HBM bandwidth applies to)."""

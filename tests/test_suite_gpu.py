@@ -7,14 +7,8 @@ from cme213_sp18_amd.suite import hw1, hw2, hw3, hw4
 
 pytestmark = pytest.mark.gpu
 
-MOBY = "/root/reference/hw4code/mobydick.txt"
-
-
 def _text(n=300_000):
-    try:
-        return open(MOBY, "rb").read()[:n]
-    except OSError:
-        return hw4.synthetic_english(n, seed=5)  # the reference text is not on the GPU box
+    return hw4.read_text()[:n]  # the reference's Moby Dick, shipped as tests/fixtures/mobydick.txt.gz
 
 
 # ------------------------------------------------------------------ hw1
