@@ -336,6 +336,29 @@ def test_training_is_deterministic(dtype, H):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("H,n", [(100, 800), (4096, 800), (4096, 160)])
+def test_step_is_deterministic_on_fresh_engines(H, n):
+    """The same gradient step on 6 freshly created engines (cold caches, reused allocator blocks): a1, D, dZ1
+    and every gradient bitwise equal each time -- a missed wait on an operand load (the in-register and
+    direct-to-LDS engines manage their own vmcnt waits) or a stale hand-off read shows up here as a few
+    scattered wrong elements (bench/diag_repeat.py prints where)."""
+    x, y = synthetic_mnist(2 * n + 64, seed=3)
+    nn = NeuralNetwork([784, H, 10])
+    ref = None
+    for _ in range(6):
+        e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        e.run(64, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
+        torch.cuda.synchronize()
+        got = [e.a1[:, :n].clone(), e.D[:, :n].clone(), e.dZ1[:, :n].clone(), e.grads.clone()]
+        if ref is None:
+            ref = got
+        for name, a, b in zip(("a1", "D", "dZ1", "grads"), got, ref):
+            assert torch.equal(a, b), (name, int((a != b).sum()))
+        del e
+
+
 @pytest.mark.parametrize("H,R", [(1024, 2), (256, 2), (512, 1)])
 def test_tensor_parallel_gpu_matches_data_parallel(H, R):
     """Hidden-sharded training on the HIP kernels (tp_forward with the GEMM-epilogue z2 partials when the
