@@ -265,7 +265,9 @@ class MlpEngine:
 
     def set_store_a1(self, on: bool) -> None:
         """Wide split layers with the head fused into the forward launch: False skips the a1 store (no kernel
-        of the training step reads a1 there: dZ1 and the dW2 partials come out of the same launch)."""
+        of the training step reads a1 there: dZ1 and the dW2 partials come out of the same launch).  (At
+        H <= 128 the all-gather head leaving dW2 partials so that a1 need not be stored measured 0.2-0.3 us
+        per step SLOWER, profiles/kbench_dw2_partials_r3.jsonl: the dW2 roles are not the critical path.)"""
         self.store_a1 = bool(on)
         if self._step is not None:
             self._step.store_a1 = int(self.store_a1)
@@ -335,8 +337,8 @@ class MlpEngine:
                 s.dZ1p = self.dZ1p.data_ptr()
             if self.z2buf is not None:
                 s.z2p = self.z2buf.data_ptr()
-                if self.dw2buf is not None:
-                    s.dw2p = self.dw2buf.data_ptr()
+            if self.dw2buf is not None:
+                s.dw2p = self.dw2buf.data_ptr()
             if self.fh_counters is not None:
                 s.fh_counters = self.fh_counters.data_ptr()
                 s.fh_tiles = int(self.fh_counters.numel())

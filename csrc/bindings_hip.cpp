@@ -66,6 +66,7 @@ struct MlpStep {
   // wide split layers: the all-gather head fused into the forward launch (fh_allgather, ag_counters, ag_err;
   // mlp_fwd1_wide_ag) leaves dW2 partials per 128 / 64 columns (32 from head_wide_kernel): what run_wgrad sums
   int dw2_cols_last = 32;
+  int dw2_left = 0;  // the last run(parts & 1) left dW2 partials in dw2p (the H <= 128 all-gather head or wide)
   int store_a1 = 1;  // the fused wide head: 0 skips the a1 store (nothing in the step reads it)
   // the fused wide head's hand-off granules ([cdiv(H, 64)][16][ld] z2 partials, then [16][ld] D; uint64)
   uintptr_t ag_gran = 0;
@@ -178,8 +179,7 @@ struct MlpStep {
           if (fh_allgather && ag_counters && ag_slabs && ag_err && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h) &&
               cme::mlp_fwd1_head_ag_fits(a)) {
             cme::mlp_fwd1_head_ag(a, h, P_<unsigned long long>(ag_counters), P_<unsigned long long>(ag_slabs),
-                                  P_<int>(ag_err),
-                                  fh_tiles, S(stream));
+                                  P_<int>(ag_err), fh_tiles, S(stream));
           } else if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
             cme::mlp_fwd1_head(a, h, P_<unsigned>(fh_counters), fh_tiles, S(stream));
           } else {
@@ -205,9 +205,14 @@ struct MlpStep {
               if (!(parts & 8)) cme::mlp_split_fwd1(f, S(stream));
               if (!(parts & 4)) cme::mlp_head(DType::F32, h, S(stream));
             }
-            dw2_cols_last = a.dw2_cols;
           }
         }
+        // what run_wgrad (the rest of this step's backward) reads: did this forward leave dW2 partials
+        dw2_left = a.dw2part != nullptr;
+        dw2_cols_last = a.dw2_cols;
+      } else if (dw2p && dw2_left) {  // the backward half alone (profiling): the partials of the last forward
+        a.dw2part = P_<float>(dw2p);
+        a.dw2_cols = dw2_cols_last;
       }
       if (parts & 2) cme::mlp_split_wgrad(a, S(stream));
       return;
@@ -278,13 +283,9 @@ struct MlpStep {
     a.wg_parts = parts;
     a.w1_row0 = row0;
     a.w1_rows = rows;
-    if (dw2p && z2p) {  // the forward + head half (run(parts=1)) of this step left dW2 partials: same test as run()
-      cme::SplitStepArgs f = a;
-      f.z2part = P_<float>(z2p);
-      if (cme::mlp_split_fwd1_z2_chunks(f) > 0) {
-        a.dw2part = P_<float>(dw2p);
-        a.dw2_cols = dw2_cols_last;
-      }
+    if (dw2p && dw2_left) {  // the forward + head half (run(parts=1)) of this step left dW2 partials
+      a.dw2part = P_<float>(dw2p);
+      a.dw2_cols = dw2_cols_last;
     }
     cme::mlp_split_wgrad(a, S(stream));
   }
