@@ -134,8 +134,8 @@ __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int
     abase[mb] = arow < M ? (arow * lda + 8 * fg) * (int)sizeof(AT) : -1;
   }
   // B DMA: chunk c = wave + 8 j of 16 rows; lane -> row lane >> 2, physical slot lane & 3 holding logical
-  // k-chunk slot ^ ((row >> 2) & 3)
-  const int dr = lane >> 2, dkc = (lane & 3) ^ ((dr >> 2) & 3);
+  // k-chunk slot ^ gl::swz(row)
+  const int dr = lane >> 2, dkc = (lane & 3) ^ gl::swz(dr);
   int bsrc[LB], blds[LB];
 #pragma unroll
   for (int j = 0; j < LB; ++j) {
@@ -169,7 +169,7 @@ __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int frag = (wc * 16 * NB + fr) * kRowB + ((fg ^ ((fr >> 2) & 3)) << 4);
+  const int frag = (wc * 16 * NB + fr) * kRowB + ((fg ^ gl::swz(fr)) << 4);
   // one stage's MFMA operands in registers: NB B fragments (LDS) and the A planes (split of the A ring slot)
   constexpr int NPL = F32 ? 3 : 1;
   struct Frags {
