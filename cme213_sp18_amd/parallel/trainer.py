@@ -37,6 +37,25 @@ XGMI2_AUTO_MAX_BYTES = 8 << 20  # ... and the two-shot kernel (4+ ranks) up to t
 BUCKET_BYTES = 4 << 20         # dW1 all-reduce chunk of the overlapped RCCL backward
 
 
+def auto_allreduce_shots(R: int, wire_bytes: int, fp_bytes: int, bf16_wire: bool) -> int:
+    """allreduce="auto" on one node: 1 = the xGMI one-shot kernel, 2 = the two-shot kernel, 0 = RCCL.
+
+    Cost model (docs/PERFORMANCE.md "Communication policy"; B = one xGMI link, L = one kernel's fixed cost):
+    one-shot L + S / B (every rank pulls the R - 1 peer buckets over R - 1 links in parallel), two-shot
+    2 L + 2 S / (R B) (reduce-scatter + all-gather, 2 S / R per link), an RCCL ring L_rccl + 2 S / (R B) at best
+    but overlappable with the dW1 GEMM.  Latency-bound buckets (<= 2 MB: 318 KB at H = 100) take the one-shot.
+    At R = 2 the two-shot and the ring move S per link too, so the one-shot stays up to 8 MB (784-1024-10's
+    3.3 MB at N = 2).  From R = 3 the two-shot cuts the bytes per link to 2 S / R, up to 8 MB of fp32.  Past
+    that (784-4096-10: 13 MB) the bucketed RCCL backward, whose ring hides behind the dW1 GEMM."""
+    if wire_bytes <= XGMI_AUTO_MAX_BYTES:
+        return 1
+    if R == 2 and wire_bytes <= XGMI2_AUTO_MAX_BYTES:
+        return 1
+    if R >= 3 and not bf16_wire and fp_bytes <= XGMI2_AUTO_MAX_BYTES:
+        return 2
+    return 0
+
+
 class FaultInjected(RuntimeError):
     """Raised by ``train(fault=(rank, step))`` -- the failure-detection test hook."""
 
@@ -186,20 +205,17 @@ class DataParallelTrainer:
 
         if mode == "auto" and (not same_node(self.R) or self.R > 8):
             return None
-        # one-shot: every rank pulls all R-1 peer buckets over its links (S bytes per link) -- the win for
-        # latency-bound buckets (318 KB at H=100); two-shot (R >= 4): 2 S / R bytes per link and one more
-        # round trip -- buckets of a few MB (784-1024-10: 3.3 MB); past that the overlapped RCCL backward
-        # (docs/PERFORMANCE.md "Communication policy"); the bytes that count are the WIRE bytes
+        # one-shot / two-shot / RCCL by the cost model of auto_allreduce_shots (the bytes that count are the
+        # WIRE bytes)
         fp_bytes = e.params.numel() * e.params.element_size()
         bf16_wire = e.params.dtype == torch.float32 and self.grad_wire == "bf16"
         wire = torch.bfloat16 if bf16_wire else e.params.dtype
         wire_bytes = e.params.numel() * torch.tensor([], dtype=wire).element_size()
         shots = 2 if mode == "xgmi2" else 1
         if mode == "auto":
-            if wire_bytes > XGMI_AUTO_MAX_BYTES:
-                if bf16_wire or self.R < 4 or fp_bytes > XGMI2_AUTO_MAX_BYTES:
-                    return None
-                shots = 2
+            shots = auto_allreduce_shots(self.R, wire_bytes, fp_bytes, bf16_wire)
+            if shots == 0:
+                return None
         if shots == 2 and bf16_wire:
             raise ValueError("the two-shot xGMI all-reduce moves the exact gradient (grad_wire f32)")
         try:

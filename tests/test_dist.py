@@ -132,3 +132,20 @@ def test_shard_math():
            for c in comms]
     assert [t.shard(800, 800) for t in trs] == [(800, 266), (1066, 266), (1332, 266)]
     assert [t.shard(0, 2) for t in trs] == [(0, 0), (0, 0), (0, 0)]
+
+
+def test_auto_allreduce_policy_follows_the_cost_model():
+    """allreduce="auto": one-shot for latency-bound buckets at any R, and up to 8 MB at R = 2 (where the
+    two-shot and the ring also move S per link); two-shot from R = 3 up to 8 MB of fp32; RCCL past that and
+    for the bf16 wire's big buckets (the two-shot moves the exact gradient only)."""
+    from cme213_sp18_amd.parallel.trainer import auto_allreduce_shots as pick
+
+    h100, h1024, h4096 = 79_552 * 4, 814_208 * 4, 3_256_448 * 4  # the three BASELINE models' fp32 buckets
+    for R in (2, 4, 8):
+        assert pick(R, h100, h100, False) == 1
+        assert pick(R, h4096, h4096, False) == 0
+    assert pick(2, h1024, h1024, False) == 1
+    assert pick(4, h1024, h1024, False) == 2 and pick(8, h1024, h1024, False) == 2
+    assert pick(3, h1024, h1024, False) == 2
+    assert pick(8, h1024 // 2, h1024, True) == 1  # the opt-in bf16 wire brings 3.3 MB under the one-shot bound
+    assert pick(8, h4096 // 2, h4096, True) == 0
