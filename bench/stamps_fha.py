@@ -38,6 +38,13 @@ def main(argv=None):
     buf = torch.zeros(4096 * 4, dtype=torch.int64, device="cuda")
     wbuf = torch.zeros(4096 * 8 * 4, dtype=torch.int64, device="cuda")
     pct = lambda v: [round(float(np.percentile(v, q)), 3) for q in (0, 50, 90, 100)]  # noqa: E731
+
+    def per_wg(wb, t0):
+        g = wb.view(-1, 8, 4).cpu().numpy().astype(np.int64)
+        g = g[(g[:, :, 0] > 0).all(axis=1)]
+        r = (g - t0) * 10.0 / 1000.0
+        return {"wg_entry_spread": pct(r[:, :, 0].max(1) - r[:, :, 0].min(1)),
+                "wg_first_entry_to_last_kloop": pct(r[:, :, 1].max(1) - r[:, :, 0].min(1))}
     for rep in range(4):
         for _ in range(20):
             step.run(0, a.n, 1.0 / a.n, 1e-4, 0.0, 1, 0, st, 3)
@@ -59,7 +66,9 @@ def main(argv=None):
         print(json.dumps({"wgs": int(len(s)), "entry": pct(rel[:, 0]), "published": pct(rel[:, 1]),
                           "all_arrived": pct(rel[:, 2]), "wait": pct(rel[:, 2] - rel[:, 1]), "end": pct(rel[:, 3]),
                           "wave_entry": pct(wr[:, 0]), "wave_kloop": pct(wr[:, 1]), "wave_reduced": pct(wr[:, 2]),
-                          "wave_epilogue": pct(wr[:, 3]), "kloop_dur": pct(wr[:, 1] - wr[:, 0])}))
+                          "wave_epilogue": pct(wr[:, 3]), "kloop_dur": pct(wr[:, 1] - wr[:, 0]),
+                          # per workgroup (8 waves): first -> last wave entry, and first wave entry -> last K-loop end
+                          **per_wg(wbuf, t0)}))
         if rep == 3:  # per column tile (XCD-grouped grid: block b -> xcd b & 7, slot b >> 3, ct = xcd + 8 (slot // tm))
             tm = (a.hidden + 15) // 16
             allv = buf.view(-1, 4).cpu().numpy().astype(np.int64)

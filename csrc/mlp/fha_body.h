@@ -98,15 +98,25 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   }
   __syncthreads();
   const unsigned ep = s_ep;
-  // ---- 1. z2 partial for (class c, column col), one per thread, published as a tagged granule
+  // ---- 1. z2 partial W2[:, tile rows] . a1[tile rows, 32 columns] on MFMA (waves 0 and 1: 16 columns each,
+  // 4 x v_mfma_f32_16x16x4_f32 over the 16 rows), published as tagged granules (lane: classes 4 g + i of
+  // column 16 w + (lane & 15)).  Rows past H and columns past n read 0 (a1s holds stale LDS there).
   const int c = t >> 5, col = t & 31;
-  {
-    float z = 0.f;
+  if (t < 128) {
+    const int w = t >> 6, l16 = t & 15, kg = (t & 63) >> 4, zc = 16 * w + l16;
+    const bool colok = c0 + zc < n;
+    f32x4 p = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) z += (r0 + r < H && c0 + col < n) ? w2s[c][r] * a1s[r][col] : 0.f;
+    for (int s = 0; s < 4; ++s) {
+      const int r = 4 * s + kg;
+      p = __builtin_amdgcn_mfma_f32_16x16x4f32(w2s[l16][r], (colok && r0 + r < H) ? a1s[r][zc] : 0.f, p, 0, 0, 0);
+    }
     // (test hook: one workgroup of column tile 0 never publishes, so that tile's polls time out)
-    if (c < C && !(f.ag_test_skip == rt && ct == 0))
-      gran_store(slabs + (size_t)(ct * tm + rt) * 16 * kCols + c * kCols + col, z, ep);
+    if (!(f.ag_test_skip == rt && ct == 0)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (4 * kg + i < C) gran_store(slabs + (size_t)(ct * tm + rt) * 16 * kCols + (4 * kg + i) * kCols + zc, p[i], ep);
+    }
   }
   stamp(1);
   // ---- 2. z2 = sum of the tm partials (row-tile order: the same bits in every workgroup) + b2
