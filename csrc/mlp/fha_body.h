@@ -17,6 +17,7 @@
 
 #include "fwd_tile.h"
 #include "granule.h"
+#include "head_math.h"
 #include "mlp_kernels.h"
 #include "mlp_split.h"
 #include "mma_tile.h"
@@ -26,7 +27,7 @@ namespace cme {
 constexpr int kAgCounterStride = 32;  // uint64 words: one 256-byte line per tile counter (polls and adds of
                                       // different tiles must not share a line)
 
-__device__ __forceinline__ float ag_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float ag_sigmoid(float x) { return sigmoid_f32(x); }  // (head_math.h)
 
 struct EpiSigLds {
   const float* b1;
@@ -69,11 +70,11 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     if (st && t == 0) st[i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  // the launch epoch: one add per workgroup now, its value used after the GEMM
-  unsigned long long ep_old = 0;
-  if (t == 0)
-    ep_old = __hip_atomic_fetch_add(counters + (size_t)ct * kAgCounterStride, 1ull, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
+  // the launch epoch: one add per workgroup now (by wave 7, which has no K range at K = 784 or 800: its wait
+  // for the add never delays a GEMM wave), its value used after the GEMM
+  constexpr int kEpochThread = 448;
+  gran_t ep_old = 0;
+  if (t == kEpochThread) ep_old = gran_epoch_add(counters + (size_t)ct * kAgCounterStride);
   // the label of this thread's softmax column (t >> 4), fetched now: loaded where the softmax uses it, it was
   // a dependent memory round trip after the all-gather wait
   const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(
@@ -92,7 +93,8 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   // they are masked below.  w2s / b2s are complete after the barrier below.
   if (t < 256) w2s[wc][wr] = w2v;
   else if (t < 256 + 16) b2s[t - 256] = b2v;
-  if (t == 0) {
+  if (t == kEpochThread) {
+    gran_epoch_wait(ep_old);
     s_ep = (unsigned)(ep_old / (unsigned)tm) + 1u;
     s_bad = 0;
   }

@@ -13,6 +13,20 @@
 namespace cme {
 
 using gran_t = unsigned long long;
+
+// The launch-epoch add (one per workgroup at kernel entry; old / tm + 1 is the epoch), issued WITHOUT a wait.
+// Written as __hip_atomic_fetch_add, hipcc's atomic optimizer turns the one-lane returning atomic into a wave
+// reduction and waits for its result at once (s_waitcnt vmcnt(0) right after it): an L2 atomic round trip on
+// the counter line that every workgroup of the column tile hits, before the wave issues a single K-loop load --
+// and in the per-stage-barrier GEMM engines, on the critical path of every wave.  As inline asm the add is
+// counted by the hardware in issue order like any load, so every later vmcnt wait covers it (waits only get
+// stricter), and gran_epoch_wait names the result register so no use of it is scheduled above the wait.
+__device__ __forceinline__ gran_t gran_epoch_add(gran_t* p) {
+  gran_t old;
+  asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0" : "=v"(old) : "v"(p), "v"((gran_t)1) : "memory");
+  return old;
+}
+__device__ __forceinline__ void gran_epoch_wait(gran_t& old) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(old)::"memory"); }
 __device__ __forceinline__ void gran_store(gran_t* p, float v, unsigned ep) {  // ONE 8-byte sc1 store
   __hip_atomic_store(p, ((gran_t)ep << 32) | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);

@@ -32,6 +32,8 @@ __device__ __forceinline__ double dev_log<double>(double x) { return log(x); }
 
 template <typename T>
 __device__ __forceinline__ T sigmoid_(T x) { return T(1) / (T(1) + dev_exp<T>(-x)); }
+template <>
+__device__ __forceinline__ float sigmoid_<float>(float x) { return sigmoid_f32(x); }  // (head_math.h)
 
 // ---------------------------------------------------------------- K1: forward
 template <typename P>  // param / activation type

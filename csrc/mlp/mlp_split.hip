@@ -18,7 +18,7 @@ namespace {
 
 using bf16 = __hip_bfloat16;
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float sigm(float x) { return sigmoid_f32(x); }  // (head_math.h)
 
 // exact np-way split of an fp32 value into bf16 planes (np = 1: plain rounding)
 template <int NP>
@@ -765,11 +765,11 @@ __device__ __forceinline__ void ag_stamp(const SplitStepArgs& a, int i, bool dra
 
 // kernel entry, thread 0 only: this workgroup's epoch add (the returned count is used after the K loop)
 __device__ __forceinline__ gran_t ag_epoch_add(const RegaAgArgs& g, int ct) {
-  return __hip_atomic_fetch_add(g.counters + (size_t)ct * kRegaAgCounterStride, 1ull, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
+  return gran_epoch_add(g.counters + (size_t)ct * kRegaAgCounterStride);  // (no wait: granule.h)
 }
 // after the K loop, before the first barrier that follows it, thread 0: the epoch + zeroed flags into LDS
 __device__ __forceinline__ void ag_epoch_publish(const RegaAgArgs& g, char* lds, gran_t old) {
+  gran_epoch_wait(old);
   unsigned* w = reinterpret_cast<unsigned*>(lds + g.ep_off);
   w[0] = (((unsigned)(old / (unsigned)g.tm) + 1u) << 1) | (unsigned)g.tiling;
   w[1] = 0u;

@@ -5,8 +5,8 @@ csrc/mlp/fha_body.h; wide layers: mlp_split.hip wide_head_ag).  A wait that outl
 error word; the weight-gradient launch reads that word and APPLIES NOTHING, and train() raises
 KernelHandoffTimeout -- on every rank (a failing rank must take the job down, not leave it hung
 or let the replicas diverge; the reference only ``exit(1)``s, fpcode/neural_network.cpp:9-15).  Here the
-timeout is REAL: MlpEngine.inject_handoff_timeout makes one workgroup of column tile 0 leave its counter add
-out, so that tile's wait expires.  Also pinned: the wide fused head's counters stay consistent when a partial
+timeout is REAL: MlpEngine.inject_handoff_timeout makes one workgroup of column tile 0 withhold its hand-off
+granules (the z2 partial at H <= 128, the column tile's D in the wide fused head), so that tile's polls expire.  Also pinned: the wide fused head's counters stay consistent when a partial
 batch switches the launch between its 128 x 128 and 64 x 64 tilings (each tiling has its own counters).
 """
 import os
@@ -117,7 +117,9 @@ def test_wide_head_counters_survive_tiling_switch(dt):
             assert int(c[1, (200 + 63) // 64:t64].sum()) == 0
         outs.append(e.params.clone())
     rel = float((outs[0] - outs[1]).abs().max() / outs[1].abs().max())
-    assert rel < (1e-5 if dt == "f32" else 1e-3), rel
+    # (bf16: the two heads' dW2 partial sums round differently in fp32, and over 6 steps the bf16 rounding of
+    # D / dZ1 turns some of those last-bit differences into bf16-ulp ones: 4e-4 .. 1.5e-3 measured)
+    assert rel < (1e-5 if dt == "f32" else 3e-3), rel
 
 
 @pytest.mark.parametrize("allreduce", ["rccl", "xgmi"])
