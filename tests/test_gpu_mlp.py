@@ -484,6 +484,27 @@ def test_fwd1_head_allgather_matches_last_arriver(dtype, H, n):
     assert abs(a[-1] - b[-1]) / abs(b[-1]) < 1e-5
 
 
+@pytest.mark.parametrize("dt,path", [("f32", "split3"), ("bf16", "split1")])
+@pytest.mark.parametrize("H,n,off", [(100, 800, 0), (100, 800, 64), (300, 160, 16), (100, 48, 7)])
+def test_pixel_chunk_pair_loads_match_torch(dt, path, H, n, off):
+    """The wave-split-K GEMMs' uint8 pixel operand as one 16-byte load per pair of K chunks (u8_pairs = 1, the
+    default where rows are 16-byte aligned and K % 16 == 0) and as two 4-byte loads per chunk (u8_pairs = 0):
+    both within fp32 reassociation of the PyTorch step (the pairs permute k inside each 64-deep pair, so the
+    fp32 sums round differently); offsets that break the 16-byte alignment of the feature-major copy fall
+    back to the 4-byte form on their own."""
+    hipe, te = _engine_pair(dt, H=H, n=n, N=2 * n + 64, path=path)
+    te.run(off, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
+    torch.cuda.synchronize()
+    tol = TOL[(dt, path)]
+    for pairs in (1, 0):
+        hipe._hip_step().u8_pairs = pairs
+        hipe.run(off, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
+        torch.cuda.synchronize()
+        for name in ("gW1", "gb1", "gW2", "gb2"):
+            assert _rel(getattr(hipe, name), getattr(te, name)) < tol, (pairs, name)
+        assert _rel(hipe.a1[:, :n], te.a1[:, :n]) < max(tol, 1e-5), pairs
+
+
 @pytest.mark.parametrize("H,n", [(100, 800), (100, 37), (128, 513), (300, 100)])
 def test_fp32_operands_split_in_registers_match_stored_planes(H, n):
     """split3 small layers: the GEMMs reading fp32 W1 / dZ1 and splitting them into their exact bf16 planes
