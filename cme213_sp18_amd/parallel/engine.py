@@ -129,6 +129,7 @@ class MlpEngine:
         self.fh_allgather = True
         self.store_a1 = True
         self._ag_test_skip, self._ag_spin_shift = -1, 22  # inject_handoff_timeout (tests)
+        self.kpart = None  # split-K dW1 slabs (enable_splitk)
 
     def _configure_path(self):
         dev = self.device
@@ -263,6 +264,16 @@ class MlpEngine:
         if self._step is not None:
             self._step.fh_allgather = int(self.fh_allgather)
 
+    def enable_splitk(self, max_split: int = 8) -> None:
+        """Let the wide weight-gradient launch split K (the batch) over up to ``max_split`` slices when its output
+        tiles alone cannot fill the chip and K is long -- the tensor-parallel shard at a large global batch
+        (784-4096-10 at global batch 6400 on 8 GPUs: 512 x 785 outputs, K = 6400).  Allocates the fp32 partial
+        slabs [max_split][H][P + 1]; a second kernel sums them in slab order and applies the update."""
+        if self.backend != "hip" or not self.np or max_split < 2:
+            return
+        self.kpart = torch.zeros(int(max_split) * self.H * (self.P + 1), dtype=torch.float32, device=self.device)
+        self._step = None
+
     def set_store_a1(self, on: bool) -> None:
         """Wide split layers with the head fused into the forward launch: False skips the a1 store (no kernel
         of the training step reads a1 there: dZ1 and the dW2 partials come out of the same launch).  (At
@@ -354,6 +365,8 @@ class MlpEngine:
                 s.fh_allgather = int(self.fh_allgather)
             s.store_a1 = int(self.store_a1)
             s.ag_test_skip, s.ag_spin_shift = self._ag_test_skip, self._ag_spin_shift
+            if self.kpart is not None:
+                s.kpart, s.kpart_cap = self.kpart.data_ptr(), int(self.kpart.numel())
             if self.np and self.XT is not None and self.XT.shape[0] == self.P + 1:
                 s.bias_col = 1
             if self._xgmi_fuse is not None and s.bias_col:

@@ -54,6 +54,9 @@ class TensorParallelTrainer:
                                 shift=shift, path=path)
         self._set_shard(*nn.params)
         e = self.engine
+        # the shard's dW1 has few output tiles and K = the whole global batch (512 x 785 outputs, K = 6400 for
+        # 784-4096-10 on 8 ranks): the weight-gradient launch may split K (mlp_split.hip splitk_sgd_kernel)
+        e.enable_splitk(8)
         # all-reduced pre-activation z2 (without b2), [16][ld] fp32 -- the layout head_wide_kernel reads
         self.z2 = torch.zeros(16, e.ld, dtype=e.pdt if not e.np else torch.float32, device=e.device)
         self._z2part = None

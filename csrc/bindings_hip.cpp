@@ -115,6 +115,8 @@ struct MlpStep {
   // dW1 tiles costs +0.5 us (VALU: 4 cycles per wave64 op on the 16-lane SIMD)
   int a_fp32 = -1;
   int u8_pairs = 1;  // SplitStepArgs::u8_pairs (the pixel operand's 16-byte chunk-pair loads; 0 for A/B)
+  uintptr_t kpart = 0;  // split-K dW1 partial slabs (SplitStepArgs::kpart), kpart_cap floats; 0: no split-K
+  int64_t kpart_cap = 0;
 
   cme::SplitStepArgs split_args(int64_t off, int n, double scale, double reg, double lr, int sgd,
                                 int with_loss) const {
@@ -138,6 +140,8 @@ struct MlpStep {
     a.bias_col = bias_col;
     a.a_fp32 = a_fp32 >= 0 ? a_fp32 : (H <= 128 ? 1 : 3);
     a.u8_pairs = u8_pairs;
+    a.kpart = P_<float>(kpart);
+    a.kpart_cap = kpart_cap;
     // a timed-out all-gather forward + head launch (sticky word) makes every later update a no-op
     a.ag_err = P_<const int>(ag_err);
     a.gstatus = P_<float>(gstatus);
@@ -446,6 +450,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
       .def_readwrite("a_fp32", &MlpStep::a_fp32)
       .def_readwrite("u8_pairs", &MlpStep::u8_pairs)
+      .def_readwrite("kpart", &MlpStep::kpart)
+      .def_readwrite("kpart_cap", &MlpStep::kpart_cap)
       .def("w1_planes_read",
            [](const MlpStep& st) {  // a forward kernel of this step reads the W1 planes (else: not refreshed)
              return st.split != 0 && cme::mlp_split_w1_planes_read(st.split_args(0, st.ld, 1.0, 0.0, 0.0, 1, 0));

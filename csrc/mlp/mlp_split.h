@@ -66,6 +66,13 @@ struct SplitStepArgs {
   // weight-gradient launch selection (bucketed all-reduce overlap): wg_parts bit0 = dW1 rows
   // [w1_row0, w1_row0 + w1_rows) (w1_rows < 0: all), bit1 = dW2 + bias gradients
   int wg_parts = 3, w1_row0 = 0, w1_rows = -1;
+  // split-K dW1 (wide layers, few output tiles and a long K: the tensor-parallel shard at a large global batch,
+  // e.g. 512 hidden rows x 6400 columns): fp32 partial slabs [ksplit][rows][P + 1] of kpart_cap floats; the
+  // launcher takes it when the tiles alone cannot fill the chip, and a second kernel sums the slabs in slab order
+  // and applies the update.  nullptr: never split.
+  float* kpart = nullptr;
+  int64_t kpart_cap = 0;
+  int wg_ksplit = 1, wg_kchunk = 0;  // (set by the launcher)
   // XT carries an extra all-ones feature row P: the dW1 GEMM's column P is then sum_b dZ1[h][b] = db1[h]
   // (exact, same planes), so db1 / b1 come out of the dW1 launch and the role kernel only does dW2 / db2
   int bias_col = 0;

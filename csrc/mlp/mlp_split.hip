@@ -1084,13 +1084,35 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
   }
   using G = GldsGeom<BM, BN>;
   constexpr int MB = G::MB, NB = G::NB;
-  const int id = xcd_remap(blockIdx.x, tbig);
+  // split-K (a.wg_ksplit > 1): workgroup -> (tile, K slice ks); the slice's columns [ks kc, ks kc + kc) of dZ1 and
+  // XT are the GEMM's whole K, and the raw partial goes to slab ks (splitk_sgd_kernel applies the update)
+  const int ksplit = a.wg_ksplit, tiles = tbig / ksplit;
+  const int id0 = xcd_remap(blockIdx.x, tbig), id = id0 % tiles, ks = id0 / tiles;
+  const int k0 = ks * a.wg_kchunk, klen = ksplit > 1 ? min(a.n - k0, a.wg_kchunk) : a.n;
   const int m0 = a.w1_row0 + (id / tn) * BM, n0 = (id % tn) * BN;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
   const int rw = m0 + wr * G::WM, cw = n0 + wc * G::WN;
   const int M = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows, P = a.P;
   const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
+  if (ksplit > 1) {
+    f32x4 acc[MB][NB];
+    glds_gemm_mainloop<BM, BN, NPZ>(static_cast<const bf16*>(a.dZ1p) + k0, a.ld, a.H * a.ld * (int)sizeof(bf16),
+                                    static_cast<const bf16*>(a.XTw) + k0, a.ldxt, M, P + a.bias_col, klen, m0, n0,
+                                    lds_dyn, acc);
+    const int W = P + a.bias_col;
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(a.kpart + (size_t)ks * (M - a.w1_row0) * W);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
+          st_f32(rk, (row < M && col < W) ? ((row - a.w1_row0) * W + col) * 4 : kOOB, acc[mb][nb][i]);
+        }
+    return;
+  }
   // the weights this lane updates (and b1 of its rows, for the all-ones column), before the K loop
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
   float w[MB][NB][4], bb[MB][4];
@@ -1433,22 +1455,78 @@ void launch_wgrad_rega(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
   else launch_wgrad_rega_k<AT, 0>(a, t2, tb, s);
 }
 
+// split-K dW1, second half: sum the ksplit partial slabs in slab order (deterministic), then the fused
+// epilogue of wgrad_glds_kernel: reg + SGD + the W1 planes (or the gradient), db1 from the all-ones column.
+template <int NPZ>
+__global__ __launch_bounds__(256) void splitk_sgd_kernel(SplitStepArgs a) {
+  const int M = a.w1_rows < 0 ? a.H - a.w1_row0 : a.w1_rows, P = a.P, W = P + a.bias_col;
+  const int64_t total = (int64_t)M * W, slab = total;
+  const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
+  const int perr = ag_err_load(a.ag_err);  // the step's forward timed out: no update
+  const bool upd = a.sgd && !poisoned(perr);
+  const size_t plane = (size_t)a.H * P;
+  mark_status(a, perr);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    float v = a.kpart[e];
+    for (int k = 1; k < a.wg_ksplit; ++k) v += a.kpart[k * slab + e];
+    const int row = a.w1_row0 + (int)(e / W), col = (int)(e % W);
+    if (col == P) {  // all-ones feature: db1 (no input scale, no regulariser)
+      if (upd) a.b1[row] -= lr * v;
+      else a.gb1[row] = v;
+      continue;
+    }
+    const size_t idx = (size_t)row * P + col;
+    const float wv = a.W1[idx], g = v * xs + reg * wv;
+    if (upd) {
+      const float nw = wv - lr * g;
+      a.W1[idx] = nw;
+      split_store<NPZ>(nw, static_cast<bf16*>(a.W1p), plane, idx);
+    } else {
+      a.gW1[idx] = g;
+    }
+  }
+}
+
 template <int NP>
 void launch_wgrad_glds(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int NW = a.P + a.bias_col;
   const int t128 = cdiv(rows, 128) * cdiv(NW, 128);
+  const int tn64 = cdiv(NW, 64), t64 = cdiv(rows, 64) * tn64;
   constexpr int kRoleLds = kWKS * 4 * 64 * (int)sizeof(float) + 16;
+  constexpr int L128 = std::max(gl::lds_bytes<128, 128, NP>(), kRoleLds);
+  constexpr int L64 = std::max(gl::lds_bytes<64, 64, NP>(), kRoleLds);
+  // split-K when the output tiles cannot fill the chip and K is long (the tensor-parallel shard at a large
+  // global batch): K slices of whole 32-deep stages, the 128 x 128 tiles first (the data-parallel launch's
+  // per-workgroup shape when 8 slices of K = 6400 give 200+ workgroups), else the 64 x 64 ones
+  auto slices = [&](int tiles, int& kc) {
+    if (!a.kpart || a.sgd == 2 || a.n < 2048) return 1;
+    int ks = std::min(8, 256 / tiles);
+    kc = cdiv(cdiv(a.n, ks), 32) * 32;
+    ks = cdiv(a.n, kc);
+    return (int64_t)ks * rows * NW <= a.kpart_cap ? ks : 1;
+  };
+  auto split_launch = [&](auto kern, int L, int tn, int tiles, int ks, int kc) {
+    SplitStepArgs b = a;
+    b.wg_ksplit = ks;
+    b.wg_kchunk = kc;
+    kern<<<tiles * ks + t2 + tb, 512, L, s>>>(b, tn, tiles * ks, t2);
+    const int64_t total = (int64_t)rows * NW;
+    splitk_sgd_kernel<NP><<<(unsigned)std::min<int64_t>(2048, (total + 255) / 256), 256, 0, s>>>(b);
+  };
+  int kc = a.n;
   if (t128 >= 192) {
-    constexpr int L = std::max(gl::lds_bytes<128, 128, NP>(), kRoleLds);
-    set_lds_limit<wgrad_glds_kernel<128, 128, NP>>(L);
-    wgrad_glds_kernel<128, 128, NP><<<t128 + t2 + tb, 512, L, s>>>(a, cdiv(NW, 128), t128, t2);
+    set_lds_limit<wgrad_glds_kernel<128, 128, NP>>(L128);
+    wgrad_glds_kernel<128, 128, NP><<<t128 + t2 + tb, 512, L128, s>>>(a, cdiv(NW, 128), t128, t2);
+  } else if (int ks = slices(t128, kc); ks > 1 && t128 * ks >= 192) {
+    set_lds_limit<wgrad_glds_kernel<128, 128, NP>>(L128);
+    split_launch(wgrad_glds_kernel<128, 128, NP>, L128, cdiv(NW, 128), t128, ks, kc);
+  } else if (int ks64 = t64 < 128 ? slices(t64, kc) : 1; ks64 > 1) {
+    set_lds_limit<wgrad_glds_kernel<64, 64, NP>>(L64);
+    split_launch(wgrad_glds_kernel<64, 64, NP>, L64, tn64, t64, ks64, kc);
   } else {
-    constexpr int L = std::max(gl::lds_bytes<64, 64, NP>(), kRoleLds);
-    set_lds_limit<wgrad_glds_kernel<64, 64, NP>>(L);
-    const int tn = cdiv(NW, 64);
-    const int t64 = cdiv(rows, 64) * tn;
-    wgrad_glds_kernel<64, 64, NP><<<t64 + t2 + tb, 512, L, s>>>(a, tn, t64, t2);
+    set_lds_limit<wgrad_glds_kernel<64, 64, NP>>(L64);
+    wgrad_glds_kernel<64, 64, NP><<<t64 + t2 + tb, 512, L64, s>>>(a, tn64, t64, t2);
   }
 }
 

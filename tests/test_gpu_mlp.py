@@ -505,6 +505,38 @@ def test_pixel_chunk_pair_loads_match_torch(dt, path, H, n, off):
         assert _rel(hipe.a1[:, :n], te.a1[:, :n]) < max(tol, 1e-5), pairs
 
 
+@pytest.mark.parametrize("dt,path", [("f32", "split3"), ("bf16", "split1")])
+@pytest.mark.parametrize("H,n", [(512, 3200), (512, 6400), (512, 2048)])
+def test_splitk_weight_gradient_matches_torch(dt, path, H, n):
+    """The tensor-parallel shard's weight gradient (few 64 x 64 output tiles, K = a large global batch): the
+    launch splits K over up to 8 slices into fp32 slabs and a second kernel sums them in slab order and applies
+    reg + SGD + the W1 planes (csrc/mlp/mlp_split.hip splitk_sgd_kernel).  Gradients (sgd = 0) and the updated
+    parameters (sgd = 1) against the PyTorch step and against the unsplit launch."""
+    outs = []
+    for split in (True, False):
+        hipe, te = _engine_pair(dt, H=H, n=n, N=n + 64, path=path)
+        if split:
+            hipe.enable_splitk(8)
+        for e in (hipe, te):
+            e.run(64, n, 1.0 / n, 1e-4, 0.0, sgd=False)
+        torch.cuda.synchronize()
+        if split:  # the split launch really ran: its slabs hold the partial sums
+            assert float(hipe.kpart.abs().sum()) > 0
+        tol = TOL[(dt, path)]
+        for name in ("gW1", "gb1", "gW2", "gb2"):
+            assert _rel(getattr(hipe, name), getattr(te, name)) < tol, (split, name)
+        for e in (hipe, te):
+            e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+        torch.cuda.synchronize()
+        assert _rel(hipe.params, te.params) < (1e-5 if dt == "f32" else 1e-2), split
+        if path == "split3":
+            if not hipe.w1_planes_maintained():
+                hipe.refresh_w1_planes()
+            assert torch.equal(hipe.W1p.float().sum(0), hipe.W1), split
+        outs.append(hipe.params.clone())
+    assert _rel(outs[0], outs[1]) < (1e-5 if dt == "f32" else 1e-2)
+
+
 @pytest.mark.parametrize("H,n", [(100, 800), (100, 37), (128, 513), (300, 100)])
 def test_fp32_operands_split_in_registers_match_stored_planes(H, n):
     """split3 small layers: the GEMMs reading fp32 W1 / dZ1 and splitting them into their exact bf16 planes
