@@ -71,9 +71,12 @@ def main(argv=None):
         # "+p<0|1>": the pixel operand's 16-byte chunk-pair loads (SplitStepArgs.u8_pairs; default on)
         m = re.search(r"\+p(\d)", path)
         pairs = int(m.group(1)) if m else None
+        # "+q<0|1>": the hand-off polls re-load only the granules still missing (SplitStepArgs.poll_skip; default on)
+        m = re.search(r"\+q(\d)", path)
+        pskip = int(m.group(1)) if m else None
         # "+s0": no a1 store (the trainer's setting); "+d0": no dW2 partials from the head (dw2p = 0)
         no_a1, no_dw2 = "+s0" in path, "+d0" in path
-        path = re.sub(r"\+[apsd]\d", "", path).replace("+fh", "")
+        path = re.sub(r"\+[apsdq]\d", "", path).replace("+fh", "")
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -87,6 +90,8 @@ def main(argv=None):
                     step.a_fp32 = a32
                 if pairs is not None:
                     step.u8_pairs = pairs
+                if pskip is not None:
+                    step.poll_skip = pskip
                 if no_a1:
                     e.set_store_a1(False)
                 if no_dw2:
@@ -96,7 +101,7 @@ def main(argv=None):
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+fh" if fused else "") + (f"+a{a32}" if a32 is not None else "") + (f"+p{pairs}" if pairs is not None else "") + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+fh" if fused else "") + (f"+a{a32}" if a32 is not None else "") + (f"+p{pairs}" if pairs is not None else "") + (f"+q{pskip}" if pskip is not None else "") + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(

@@ -61,7 +61,7 @@ def main(argv=None):
         return best * 1e6
 
     for k in a.ks:
-        plan = EpochPlan([(i * n, n) for i in range(k)])
+        plan = EpochPlan([((i * n) % (e.num_samples - e.num_samples % n), n) for i in range(k)])
         g = tr.capture(plan, lr, reg)
         g.replay()
         t_graph = wall(lambda: g.replay())

@@ -21,6 +21,9 @@ def main(argv=None):
     ap.add_argument("--cols", type=int, default=800)
     ap.add_argument("--cfg", nargs="*", default=["f32:split3", "bf16:split1"])
     ap.add_argument("--reps", type=int, default=100)
+    ap.add_argument("--modes", nargs="*", default=["head", "ag", "ag_noa1"],
+                    help="head | ag | ag_noa1, each optionally +q0 (SplitStepArgs.poll_skip = 0: the hand-off polls "
+                         "re-load every granule every pass); a mode may repeat (A/B alternation)")
     a = ap.parse_args(argv)
     import torch
 
@@ -54,13 +57,16 @@ def main(argv=None):
         nn = NeuralNetwork([784, H, 10])
         for cfg in a.cfg:
             dt, path = cfg.split(":")
-            for mode in ("head", "ag", "ag_noa1"):
+            ref = ref_ag = None
+            for mode_q in a.modes:
+                mode, _, q = mode_q.partition("+")
                 e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", path=path)
                 e.set_params(*nn.params)
                 e.load_dataset(x, y)
                 e.set_fh_allgather(mode != "head")
                 e.set_store_a1(not mode.endswith("noa1"))
                 e._hip_step().ag_tiles64 = 1
+                e._hip_step().poll_skip = 0 if q == "q0" else 1
                 off = [0]
 
                 def step():
@@ -70,14 +76,15 @@ def main(argv=None):
                 def fwd_head():
                     e.run(0, n, 1.0 / n, 1e-4, 0.0, sgd=False, parts=1)
 
-                r = {"H": H, "n": n, "cfg": cfg, "mode": mode, "step_us": round(timeit(step, a.reps), 3)}
+                r = {"H": H, "n": n, "cfg": cfg, "mode": mode_q, "step_us": round(timeit(step, a.reps), 3)}
                 # every form runs the same 6 * reps + 2 steps: the fused forms must leave BITWISE equal params
                 # (a stale hand-off read would show here), the head form equal to fp32 rounding
                 p = e.params.clone()
-                if mode == "head":
+                if mode == "head" and ref is None:
                     ref = p
-                r["params_rel_vs_head"] = float((p - ref).abs().max() / ref.abs().max())
-                if mode == "ag":
+                if ref is not None:
+                    r["params_rel_vs_head"] = float((p - ref).abs().max() / ref.abs().max())
+                if mode != "head" and ref_ag is None:
                     ref_ag = p
                 if mode != "head":
                     r["params_bitwise_eq_ag"] = bool(torch.equal(p, ref_ag))

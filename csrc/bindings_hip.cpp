@@ -114,6 +114,7 @@ struct MlpStep {
   // H = 300 -- at H <= 128 the all-gather head stores planes cheaply and the 25-fold re-split of dZ1 in the
   // dW1 tiles costs +0.5 us (VALU: 4 cycles per wave64 op on the 16-lane SIMD)
   int a_fp32 = -1;
+  int poll_skip = 1;  // SplitStepArgs::poll_skip (hand-off polls re-load only missing granules; 0 for A/B)
   int u8_pairs = 1;  // SplitStepArgs::u8_pairs (the pixel operand's 16-byte chunk-pair loads; 0 for A/B)
   uintptr_t kpart = 0;  // split-K dW1 partial slabs (SplitStepArgs::kpart), kpart_cap floats; 0: no split-K
   int64_t kpart_cap = 0;
@@ -140,6 +141,7 @@ struct MlpStep {
     a.bias_col = bias_col;
     a.a_fp32 = a_fp32 >= 0 ? a_fp32 : (H <= 128 ? 1 : 3);
     a.u8_pairs = u8_pairs;
+    a.poll_skip = poll_skip;
     a.kpart = P_<float>(kpart);
     a.kpart_cap = kpart_cap;
     // a timed-out all-gather forward + head launch (sticky word) makes every later update a no-op
@@ -450,6 +452,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
       .def_readwrite("a_fp32", &MlpStep::a_fp32)
       .def_readwrite("u8_pairs", &MlpStep::u8_pairs)
+      .def_readwrite("poll_skip", &MlpStep::poll_skip)
       .def_readwrite("kpart", &MlpStep::kpart)
       .def_readwrite("kpart_cap", &MlpStep::kpart_cap)
       .def("w1_planes_read",

@@ -125,7 +125,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   {
     float z = 0.f;
     const bool good = gran_poll<8>(slabs, (unsigned)(ct * tm * 16 * kCols + c * kCols + col), 16u * kCols, tm,
-                                   c < C, ep, 1u << f.ag_spin_shift, [&](int, float v) { z += v; });
+                                   c < C, ep, 1u << f.ag_spin_shift, [&](int, float v) { z += v; }, f.poll_skip != 0);
     if (!good && (t & 63) == 0) {
       atomicExch(err, 1);
       s_bad = 1;

@@ -39,25 +39,32 @@ __device__ __forceinline__ gran_t gran_load(const gran_t* p) {  // sc1 load (L2-
 // `ep`, then hand the values to f(k, value) in k order (0 for k >= cnt).  The N addresses are formed once,
 // before the poll loop; a pass is N back-to-back global_load_dwordx2 sc1 and one wait.  Wave-uniform; false
 // when the wave gave up after `limit` passes (f is then not called).
+// A granule seen with the epoch is final for this launch (tags only grow), so later passes re-load only the
+// granules still missing (the others' loads are masked off): every workgroup of the launch polls at once,
+// and re-reading the already-arrived granules made the waiting workgroups' sc1 traffic compete with the
+// stores and polls of the workgroups they wait for.  The first pass is unchanged: no added latency.
 template <int N, class F>
 __device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsigned stride, int cnt, bool need,
-                                          unsigned ep, uint32_t limit, F&& f) {
+                                          unsigned ep, uint32_t limit, F&& f, bool skip = true) {
+  static_assert(N <= 32, "ready mask");
   // the granule addresses, once: k >= cnt re-reads granule 0 (needed anyway, so its tag check is the same)
   const gran_t* p[N];
 #pragma unroll
   for (int k = 0; k < N; ++k)
     p[k] = reinterpret_cast<const gran_t*>(reinterpret_cast<const char*>(base) +
                                            (off + (k < cnt ? (unsigned)k * stride : 0u)) * 8u);
+  constexpr unsigned kAll = N == 32 ? ~0u : (1u << N) - 1u;
   bool done = !need;
+  unsigned rdy = 0u;  // bit k: granule k carried the epoch in an earlier pass (x[k] is final)
   gran_t x[N];
   for (uint32_t spins = 0;; ++spins) {
     if (!done) {
 #pragma unroll
-      for (int k = 0; k < N; ++k) x[k] = gran_load(p[k]);
-      bool ok = true;
+      for (int k = 0; k < N; ++k)
+        if (!(skip && (rdy & (1u << k)))) x[k] = gran_load(p[k]);
 #pragma unroll
-      for (int k = 0; k < N; ++k) ok &= (unsigned)(x[k] >> 32) == ep;
-      done = ok;
+      for (int k = 0; k < N; ++k) rdy |= (unsigned)((unsigned)(x[k] >> 32) == ep) << k;
+      done = rdy == kAll;
     }
     if (__all(done)) break;
     if (spins >= limit) return false;

@@ -108,6 +108,8 @@ struct SplitStepArgs {
   // the all-gather hand-off's wait bound (2^ag_spin_shift polls) and a TEST hook: row tile ag_test_skip of
   // column tile 0 leaves out its (first) counter add, so that tile's wait really times out (-1: off)
   int ag_spin_shift = 22;
+  // the hand-off polls re-load only the granules still missing (granule.h gran_poll; 0: every granule every pass, A/B)
+  int poll_skip = 1;
   int ag_test_skip = -1;
 };
 

@@ -814,7 +814,7 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
     bool good = true;
     for (int k0 = 0; k0 < tm && good; k0 += 16)  // the partials summed in tile order, 16 per poll
       good = gran_poll<16>(g.z2g, (unsigned)(k0 * 16 + zc) * a.ld + zcol, stride, min(16, tm - k0), need, ep, limit,
-                           [&](int, float v) { zsum += v; });
+                           [&](int, float v) { zsum += v; }, a.poll_skip != 0);
     if (!good && lane == 0) {
       atomicExch(g.err, 1);
       sw[1] = 1u;
@@ -877,7 +877,7 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
 #pragma unroll
     for (int q = 0; q < NDS; ++q) v[q] = 0.f;
     const bool good = gran_poll<NDS>(g.dg, (unsigned)c0 * a.ld + n0 + j, (unsigned)(kRowsPerQ * a.ld), cnt, cnt > 0,
-                                     ep, limit, [&](int q, float x) { v[q] = x; });
+                                     ep, limit, [&](int q, float x) { v[q] = x; }, a.poll_skip != 0);
     if (!good && lane == 0) {
       atomicExch(g.err, 1);
       sw[2] = 1u;
