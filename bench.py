@@ -64,6 +64,10 @@ def parse(argv=None):
                     help="dp: data parallel (the reference's scheme); tp: hidden-dimension tensor parallel "
                          "(one z2 all-reduce per step, every rank runs the whole global batch --batch; strong "
                          "scaling of a fixed model, meant for the wide configs)")
+    ap.add_argument("--tune-allreduce", default="on", choices=["on", "off"],
+                    help="N > 1 with --allreduce auto: time the policy's xGMI pick and RCCL for --tune-steps steps "
+                         "each before the timed region and run the faster (the record lists both)")
+    ap.add_argument("--tune-steps", type=int, default=100)
     ap.add_argument("--train-size", type=int, default=54000)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -111,8 +115,8 @@ def main(argv=None) -> int:
     nn = NeuralNetwork([784, a.hidden, 10])
     lr, reg = 1e-3, 1e-4  # reference defaults (fpcode/main.cpp:58-60)
 
-    def prepare(allreduce: str):
-        """Trainer + captured graphs + W warm-up steps.  Returns (trainer, timed plans)."""
+    def prepare(allreduce: str, probe_steps: int = 0):
+        """Trainer + captured graphs + W warm-up steps.  Returns (trainer, timed plans, probe plans)."""
         tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=global_batch,
                                  backend=a.backend, use_graphs=not a.no_graphs, allreduce=allreduce,
                                  grad_wire=a.grad_wire,
@@ -130,11 +134,11 @@ def main(argv=None) -> int:
                 i += m
             return out
 
-        warm_plans, timed_plans = plans_for(a.warmup), plans_for(a.steps)
-        native = all(tr.native_plan(p) is not None for p in warm_plans + timed_plans)
+        warm_plans, timed_plans, probe_plans = plans_for(a.warmup), plans_for(a.steps), plans_for(probe_steps)
+        native = all(tr.native_plan(p) is not None for p in warm_plans + timed_plans + probe_plans)
         if tr.use_graphs and not native:  # capture outside the timed region (graphs are cached by plan)
             try:
-                for p in {tuple(p.steps): p for p in warm_plans + timed_plans}.values():
+                for p in {tuple(p.steps): p for p in warm_plans + timed_plans + probe_plans}.values():
                     tr.capture(p, lr, reg)
             except Exception as ex:  # pragma: no cover - depends on the collective backend
                 print(f"warning: HIP graph capture failed ({ex!r}); running eager steps", file=sys.stderr)
@@ -146,9 +150,32 @@ def main(argv=None) -> int:
         comm.barrier()
         for p in warm_plans:
             tr.run_plan(p, lr, reg)
-        return tr, timed_plans
+        return tr, timed_plans, probe_plans
 
-    tr, timed_plans = prepare(a.allreduce)
+    def probe(tr, plans) -> float:
+        """us/step of the probe plans on this trainer, max over ranks (inf if an xGMI wait timed out or the
+        replicas diverged): the same runners and bracketing as the timed region."""
+        runners = [tr.plan_runner(p, lr, reg) for p in plans]
+        sync()
+        comm.barrier()
+        sync()
+        t = time.perf_counter()
+        for run in runners:
+            run()
+        sync()
+        comm.barrier()
+        sync()
+        us = comm.allreduce_scalar(1e6 * (time.perf_counter() - t) / a.tune_steps, op="max")
+        bad = tr.comm_failed()
+        bad = bad or not tr.replicas_agree()
+        return float("inf") if bad else round(us, 3)
+
+    # --tune-allreduce: with N > 1 and --allreduce auto, the gradient sync is CHOSEN BY MEASUREMENT on this
+    # node before anything is timed -- the policy's xGMI pick (cost model, docs/PERFORMANCE.md) and RCCL each
+    # run --tune-steps steps, the faster one (max over ranks, agreed by every rank) runs the timed region
+    tuning = R > 1 and a.allreduce == "auto" and a.backend == "hip" and a.tune_allreduce == "on"
+    tune = {}
+    tr, timed_plans, probe_plans = prepare(a.allreduce, a.tune_steps if tuning else 0)
     sync()
     comm.barrier()
     if tr.allreduce_impl.startswith("xgmi") and a.allreduce == "auto":
@@ -162,7 +189,20 @@ def main(argv=None) -> int:
                 why = "replicas diverged" if diverged else "peer wait timed out" if failed else "forced"
                 print(f"warning: xGMI all-reduce failed in warm-up ({why}); re-running on RCCL", file=sys.stderr)
             tr.close()
-            tr, timed_plans = prepare("rccl")
+            tr, timed_plans, probe_plans = prepare("rccl", a.tune_steps if tuning else 0)
+            tune["xgmi"] = "failed in warm-up"
+    if tuning and tr.allreduce_impl.startswith("xgmi"):
+        first = tr.allreduce_impl
+        tune[first] = probe(tr, probe_plans)
+        tr.close()  # (collective) the RCCL candidate starts from the initial weights like every prepare
+        tr, timed_plans, probe_plans = prepare("rccl", a.tune_steps)
+        tune[tr.allreduce_impl] = probe(tr, probe_plans)
+        if tune[first] <= tune[tr.allreduce_impl]:  # identical floats on every rank: one decision
+            tr.close()
+            tr, timed_plans, _ = prepare(a.allreduce)  # (a failure from here on invalidates the record below)
+        tune = {k: (v if v != float("inf") else "failed") for k, v in tune.items()}
+        if rank == 0:
+            print(f"allreduce tuned on this node: {tune} -> {tr.allreduce_impl}", file=sys.stderr, flush=True)
     native_exec = all(tr.native_plan(p) is not None for p in timed_plans)
     runners = [tr.plan_runner(p, lr, reg) for p in timed_plans]  # resolved before the clock starts
     sync()
@@ -210,7 +250,8 @@ def main(argv=None) -> int:
                        "hip_graphs": tr.use_graphs and not native_exec,
                        "executor": "native" if native_exec else ("graph" if tr.use_graphs else "eager"),
                        "allreduce": tr.allreduce_impl, "params_finite": not bad,
-                       "comm_ok": not comm_failed, "replicas_bitwise_equal": agree, **placement, **ar},
+                       "comm_ok": not comm_failed, "replicas_bitwise_equal": agree, **placement, **ar,
+                       "allreduce_tuning_us_per_step": tune or None},
         }
         if not ok:
             rec["invalid"] = ("non-finite parameters" if bad else "an xGMI peer wait timed out" if comm_failed

@@ -83,6 +83,11 @@ class TorchDistComm(Communicator):
         self._dist.all_reduce(x, op=rop, group=self.group)
         return float(x.item())
 
+    @property
+    def name(self) -> str:
+        """"rccl" (the nccl backend on ROCm) or the gloo backend's name: what the record's allreduce reports."""
+        return "rccl" if self.backend == "nccl" else str(self.backend)
+
     def barrier(self):
         if self.backend == "nccl":
             self._dist.barrier(device_ids=[torch.cuda.current_device()])

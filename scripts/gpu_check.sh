@@ -6,6 +6,7 @@
 #   configs              the other BASELINE configs at N=1 (H=4096 f32, H=1024 bf16, H=100 bf16)
 #   launch               bench.py --gpus 2 on a 1-GPU box: refused without CME_SHARED_GPU, 2 ranks with it
 #   prof                 rocprofv3 --kernel-trace --stats of the headline bench
+#   probes               launch fixed cost (default and spin-wait device flags) and batch-locality probes
 #   wideab               bench/wide_ag_ab.py: the wide fused head vs forward + head kernel (H = 4096, 1024)
 # Usage (from the repo root on the GPU box): scripts/gpu_check.sh tests smoke bench
 # Every GPU step has its own time limit; outputs go to gpurun_out/check/.
@@ -46,6 +47,10 @@ for st in "$@"; do
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" -o run \
         --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2000 --warmup 200) > $O/prof.log 2>&1
       echo "rocprof rc=$?"; find $O/prof -name "*kernel_stats*" ;;
+    probes)
+      timeout -k 10 240 python bench/launch_overhead.py > $O/launch_overhead.jsonl 2>&1 && grep fit $O/launch_overhead.jsonl &&
+      timeout -k 10 240 python bench/launch_overhead.py --spin > $O/launch_overhead_spin.jsonl 2>&1 && grep -E "fit|spin" $O/launch_overhead_spin.jsonl &&
+      timeout -k 10 240 python bench/batch_locality.py > $O/batch_locality.jsonl 2>&1 && grep '^{' $O/batch_locality.jsonl || exit 1 ;;
     wideab)
       timeout -k 10 300 python bench/wide_ag_ab.py --hidden 4096 1024 > $O/wide_ab.jsonl 2>&1 || { tail -20 $O/wide_ab.jsonl; exit 1; }
       grep '^{' $O/wide_ab.jsonl ;;

@@ -1,0 +1,10 @@
+#!/bin/bash
+# bf16 wide-layer PMC (config 5 at H=1024 and the H=4096 bf16 step) + the headline's hand-off poll A/B.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/ab
+mkdir -p $O
+timeout -k 10 300 python bench/kbench.py --hidden 100 --cols 800 --cfg f32:split3+q0 f32:split3+q1 f32:split3+q0 f32:split3+q1 > $O/kbench_pollskip_h100.jsonl 2>&1 && grep '^{' $O/kbench_pollskip_h100.jsonl | cut -c1-330 &&
+H=4096 CFG=bf16:split1+s0 TAG=pmc_bf4096 bash scripts/gpu_pmc_wide.sh &&
+H=1024 CFG=bf16:split1+s0 TAG=pmc_bf1024 bash scripts/gpu_pmc_wide.sh &&
+python scripts/pmc_table.py gpurun_out/pmc_bf4096 --min-us 5 && python scripts/pmc_table.py gpurun_out/pmc_bf1024 --min-us 5
