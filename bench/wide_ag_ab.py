@@ -23,7 +23,8 @@ def main(argv=None):
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--modes", nargs="*", default=["head", "ag", "ag_noa1"],
                     help="head | ag | ag_noa1, each optionally +q0 (SplitStepArgs.poll_skip = 0: the hand-off polls "
-                         "re-load every granule every pass); a mode may repeat (A/B alternation)")
+                         "re-load every granule every pass) and / or +l1 (MlpStep.lazy_planes: the in-place W1 update "
+                         "skips the W1-plane refresh); a mode may repeat (A/B alternation)")
     a = ap.parse_args(argv)
     import torch
 
@@ -59,14 +60,15 @@ def main(argv=None):
             dt, path = cfg.split(":")
             ref = ref_ag = None
             for mode_q in a.modes:
-                mode, _, q = mode_q.partition("+")
+                mode, *opts = mode_q.split("+")
                 e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", path=path)
                 e.set_params(*nn.params)
                 e.load_dataset(x, y)
                 e.set_fh_allgather(mode != "head")
                 e.set_store_a1(not mode.endswith("noa1"))
                 e._hip_step().ag_tiles64 = 1
-                e._hip_step().poll_skip = 0 if q == "q0" else 1
+                e._hip_step().poll_skip = 0 if "q0" in opts else 1
+                e._hip_step().lazy_planes = 1 if "l1" in opts else 0
                 off = [0]
 
                 def step():

@@ -128,6 +128,10 @@ class MlpEngine:
         # launch must be resident at once; DataParallelTrainer turns it off when processes share a GPU)
         self.fh_allgather = True
         self.store_a1 = True
+        # wide split3 layers: the in-place W1 update skips the W1-plane refresh when no forward reads the planes
+        # (MlpStep.lazy_planes; they are re-split before one that does)
+        # (measured at 784-4096-10 fp32: step 58.0 -> 55.2 us, profiles/wide_ag_ab_lazy_planes_r3.jsonl)
+        self.lazy_planes = True
         self._ag_test_skip, self._ag_spin_shift = -1, 22  # inject_handoff_timeout (tests)
         self.kpart = None  # split-K dW1 slabs (enable_splitk)
 
@@ -286,14 +290,21 @@ class MlpEngine:
     def w1_planes_maintained(self) -> bool:
         """True when the W1 bf16 planes track the fp32 master after every update.  Below H = 512 the split3
         forward kernels read fp32 W1 and split it in registers, so the update stops refreshing the planes
-        (csrc/mlp/mlp_split.hip mlp_split_w1_planes_read); refresh_w1_planes() rebuilds them on demand."""
-        return bool(self.np) and self.backend == "hip" and bool(self._hip_step().w1_planes_read())
+        (csrc/mlp/mlp_split.hip mlp_split_w1_planes_read); at H = 4096 the 128 x 128 forward does too, and with
+        lazy_planes the in-place update leaves them stale until a forward that reads them (MlpStep.planes_stale).
+        refresh_w1_planes() rebuilds them on demand."""
+        if not (self.np and self.backend == "hip"):
+            return False
+        s = self._hip_step()
+        return bool(s.w1_planes_read()) and not s.lazy_planes_apply()
 
     def refresh_w1_planes(self) -> None:
         """Rebuild the W1 planes from the fp32 master (exact split3 / rounded split1)."""
         if self.np and self.backend == "hip":
             hip().split_planes(self.W1.data_ptr(), self.W1p.data_ptr(), self.W1.numel(), self.np,
                                torch.cuda.current_stream(self.device).cuda_stream)
+            if self._step is not None:
+                self._step.planes_stale = False
 
     def inject_handoff_timeout(self, row_tile: int = 0, spin_shift: int = 14) -> None:
         """TEST HOOK: from the next step on, row tile ``row_tile`` of column tile 0 leaves its counter add out
@@ -319,6 +330,17 @@ class MlpEngine:
                      for t in (self.W1, self.b1, self.W2, self.b2))
 
     # -------------------------------------------------------------- one step
+    def set_lazy_planes(self, on: bool) -> None:
+        self.lazy_planes = bool(on)
+        if self._step is not None:
+            self._step.lazy_planes = int(self.lazy_planes)
+
+    def mark_planes_stale(self) -> None:
+        """W1 / the W1 planes were overwritten from outside the step (a snapshot restore): the next forward that
+        reads the planes re-splits W1 first (MlpStep.lazy_planes: the wide in-place update skips the refresh)."""
+        if self._step is not None and self.W1p is not None:
+            self._step.planes_stale = True
+
     def _hip_step(self):
         if self._step is None:
             m = hip()
@@ -346,6 +368,9 @@ class MlpEngine:
                 s.npw = s.npz = self.np
                 s.W1p = self.W1p.data_ptr()
                 s.dZ1p = self.dZ1p.data_ptr()
+                # a new step cannot know whether an earlier one left the planes stale: re-split once
+                s.planes_stale = True
+                s.lazy_planes = int(self.lazy_planes)
             if self.z2buf is not None:
                 s.z2p = self.z2buf.data_ptr()
             if self.dw2buf is not None:

@@ -249,6 +249,7 @@ class TensorParallelTrainer:
             e.W1p.copy_(snap[1])
         if snap[2] is not None:
             e.W1g.copy_(snap[2])
+        e.mark_planes_stale()
         torch.cuda.synchronize(e.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):

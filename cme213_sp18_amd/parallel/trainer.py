@@ -538,6 +538,7 @@ class DataParallelTrainer:
             e.W1g.copy_(snap[1])
         if snap[2] is not None:
             e.W1p.copy_(snap[2])
+        e.mark_planes_stale()
 
     def capture(self, plan: EpochPlan, lr: float, reg: float) -> torch.cuda.CUDAGraph:
         """Capture every step of ``plan`` into one HIP graph (state-neutral warm-up first)."""

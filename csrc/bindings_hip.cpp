@@ -114,6 +114,15 @@ struct MlpStep {
   // H = 300 -- at H <= 128 the all-gather head stores planes cheaply and the 25-fold re-split of dZ1 in the
   // dW1 tiles costs +0.5 us (VALU: 4 cycles per wave64 op on the 16-lane SIMD)
   int a_fp32 = -1;
+  // wide split3 layers: the in-place dW1 update skips the W1-plane refresh (SplitStepArgs::w1_planes_lazy) and
+  // planes_stale records it; refresh_planes() re-splits W1 before any forward that reads the planes
+  int lazy_planes = 0;
+  bool planes_stale = false;
+  void refresh_planes(uintptr_t stream) {
+    if (!planes_stale) return;
+    cme::mlp_split_planes(P_<float>(W1), reinterpret_cast<void*>(W1p), (int64_t)H * P, npw, S(stream));
+    planes_stale = false;
+  }
   int poll_skip = 1;  // SplitStepArgs::poll_skip (hand-off polls re-load only missing granules; 0 for A/B)
   int u8_pairs = 1;  // SplitStepArgs::u8_pairs (the pixel operand's 16-byte chunk-pair loads; 0 for A/B)
   uintptr_t kpart = 0;  // split-K dW1 partial slabs (SplitStepArgs::kpart), kpart_cap floats; 0: no split-K
@@ -170,6 +179,7 @@ struct MlpStep {
       }
       if (parts & 1) {
         if (fused_head) {
+          if (!cme::mlp_split_fwd_fp32_w(a)) refresh_planes(stream);
           cme::mlp_split_fwdhead(a, S(stream));
         } else {  // tiled forward + the per-column head kernel (fp32 head)
           cme::HeadArgs h{};
@@ -182,6 +192,9 @@ struct MlpStep {
           // the dW1 GEMM splits fp32 dZ1 in registers: the head writes fp32 dZ1 and no planes
           const bool dz32 = cme::mlp_split_wgrad_fp32_dz(a);
           if (dz32) h.dZ1_planes = nullptr;
+          // (the small forms read the planes unless they split fp32 W1 in registers; the wide forms below decide
+          // by their kernel)
+          if (H < 512 && !cme::mlp_split_fwd_fp32_w(a)) refresh_planes(stream);
           if (fh_allgather && ag_counters && ag_slabs && ag_err && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h) &&
               cme::mlp_fwd1_head_ag_fits(a)) {
             cme::mlp_fwd1_head_ag(a, h, P_<unsigned long long>(ag_counters), P_<unsigned long long>(ag_slabs),
@@ -202,8 +215,10 @@ struct MlpStep {
               h.dw2part = P_<float>(dw2p);
               a.dw2part = h.dw2part;
             }
-            if (fh_allgather && ag_counters && ag_err && ag_gran && h.dw2part && !(parts & 12) &&
-                cme::mlp_fwd1_wide_ag_ok(f, h, ag64())) {  // one launch: forward GEMM + the all-gather head
+            const bool ag = fh_allgather && ag_counters && ag_err && ag_gran && h.dw2part && !(parts & 12) &&
+                            cme::mlp_fwd1_wide_ag_ok(f, h, ag64());
+            if (!(parts & 8) && cme::mlp_split_wide_fwd_reads_planes(f, ag, ag64())) refresh_planes(stream);
+            if (ag) {  // one launch: forward GEMM + the all-gather head
               a.dw2_cols = cme::mlp_fwd1_wide_ag(f, h, P_<unsigned long long>(ag_counters), fh_tiles,
                                                  P_<unsigned long long>(ag_gran), ag_gran_count, P_<int>(ag_err),
                                                  store_a1, ag64(), S(stream));
@@ -220,7 +235,11 @@ struct MlpStep {
         a.dw2part = P_<float>(dw2p);
         a.dw2_cols = dw2_cols_last;
       }
-      if (parts & 2) cme::mlp_split_wgrad(a, S(stream));
+      if (parts & 2) {
+        a.w1_planes_lazy = lazy_planes;
+        cme::mlp_split_wgrad(a, S(stream));
+        if (cme::mlp_split_wgrad_leaves_planes_stale(a)) planes_stale = true;
+      }
       return;
     }
     CME_REQUIRE(sgd != 2, "MlpStep.run(sgd=2): split paths only");
@@ -303,6 +322,7 @@ struct MlpStep {
     CME_REQUIRE(split && n > 0 && n <= ld, "MlpStep.tp_forward: split path, 0 < n <= ld");
     cme::SplitStepArgs a = split_args(off, n, 1.0, 0.0, 0.0, 1, 0);
     a.z2part = z2p_ ? P_<float>(z2p_) : nullptr;
+    refresh_planes(stream);
     cme::mlp_split_fwd1(a, S(stream));
     return a.z2part ? cme::mlp_split_fwd1_z2_chunks(a) : 0;
   }
@@ -453,11 +473,21 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("a_fp32", &MlpStep::a_fp32)
       .def_readwrite("u8_pairs", &MlpStep::u8_pairs)
       .def_readwrite("poll_skip", &MlpStep::poll_skip)
+      .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
+      .def_readwrite("planes_stale", &MlpStep::planes_stale)
+      .def("refresh_planes", &MlpStep::refresh_planes, py::arg("stream"))
       .def_readwrite("kpart", &MlpStep::kpart)
       .def_readwrite("kpart_cap", &MlpStep::kpart_cap)
       .def("w1_planes_read",
            [](const MlpStep& st) {  // a forward kernel of this step reads the W1 planes (else: not refreshed)
              return st.split != 0 && cme::mlp_split_w1_planes_read(st.split_args(0, st.ld, 1.0, 0.0, 0.0, 1, 0));
+           })
+      .def("lazy_planes_apply",
+           [](const MlpStep& st) {  // this step's in-place W1 update leaves the planes stale (lazy_planes on)
+             if (!st.split || !st.lazy_planes) return false;
+             cme::SplitStepArgs a = st.split_args(0, st.ld, 1.0, 0.0, 0.0, 1, 0);
+             a.w1_planes_lazy = 1;
+             return cme::mlp_split_wgrad_leaves_planes_stale(a);
            })
       .def("tp_forward", &MlpStep::tp_forward)
       .def("tp_head", &MlpStep::tp_head)
@@ -484,8 +514,9 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("W1p", &MlpStep::W1p)
       .def_readwrite("dZ1p", &MlpStep::dZ1p)
       .def("predict",
-           [](const MlpStep& st, uintptr_t x, int n, uintptr_t a1buf, int lda, uintptr_t pred, uintptr_t s) {
+           [](MlpStep& st, uintptr_t x, int n, uintptr_t a1buf, int lda, uintptr_t pred, uintptr_t s) {
              // split path forward + argmax for n samples at x (bf16 [n][P]); a1buf: [H][lda] scratch
+             st.refresh_planes(s);
              cme::SplitStepArgs a = st.split_args(0, n, 1.0, 0.0, 0.0, 0, 0);
              a.X = reinterpret_cast<const void*>(x);
              a.a1 = reinterpret_cast<float*>(a1buf);

@@ -97,6 +97,9 @@ struct SplitStepArgs {
   float* dw2part = nullptr;
   int dw2_cols = 32;  // columns per dW2 partial: 32 (head_wide_kernel), 128 (the fused all-gather head)
   int w1_planes = 1;  // (set by mlp_split_wgrad) the small-layer W1 update refreshes the W1 planes
+  // wide split3 layers: the A-in-registers dW1 launch's in-place update (sgd = 1) leaves the W1 planes alone (the
+  // 128 x 128 forward reads fp32 W1); the caller marks them stale and refreshes them before a forward that reads them
+  int w1_planes_lazy = 0;
   // The all-gather forward + head launches' timed-out-wait word (MlpEngine.ag_err).  The weight-gradient
   // launch reads it and, when set, APPLIES NOTHING: no SGD / plane refresh (sgd = 1), no xGMI exchange (the
   // fused all-reduce: this rank stops taking part, its peers time out), and the gradient status word below
@@ -125,6 +128,11 @@ int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a);
 // true when the weight-gradient launch of this (whole-layer) step reads dZ1 in fp32 and splits it in
 // registers (rega_gemm.h): the head then writes fp32 dZ1 and no dZ1 planes
 bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a);
+// true when mlp_split_wgrad(a) leaves the W1 planes stale (a.w1_planes_lazy on the A-in-registers dW1 update)
+bool mlp_split_wgrad_leaves_planes_stale(const SplitStepArgs& a);
+// true when the wide forward launch of `a` (ag: the fused all-gather head form, allow64 as for it) reads the W1
+// planes; false when it reads fp32 W1 only (the split3 128 x 128 A-in-registers engine)
+bool mlp_split_wide_fwd_reads_planes(const SplitStepArgs& a, int ag, int allow64);
 
 // flag slots (workgroup tiles) of the fused-all-reduce wgrad launch for a P-H layer with the all-ones
 // feature; -1 when above `cap`

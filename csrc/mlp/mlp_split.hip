@@ -1333,7 +1333,8 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
           st_f32(rW, in ? idx * 4 : kOOB, nw);
           float r = nw;
 #pragma unroll
-          for (int p = 0; p < NP; ++p) {  // the W1 planes (npw == npz)
+          for (int p = 0; p < NP; ++p) {  // the W1 planes (npw == npz); split3 w1_planes_lazy: none
+            if (NP == 3 && a.w1_planes_lazy) break;
             const bf16 hb = __float2bfloat16(r);
             st_bf16(rp, in ? (int)((p * plane + idx) * 2) : kOOB, hb);
             r -= __bfloat162float(hb);
@@ -1657,6 +1658,20 @@ static int wide_ag_bm(const SplitStepArgs& a, int allow64) {
   if (rega_fwd_ok(a)) return 128;
   if (allow64 && glds_fwd_ok(a) && cdiv(a.H, 128) * cdiv(a.n, 128) < 192) return 64;
   return 0;
+}
+
+bool mlp_split_wide_fwd_reads_planes(const SplitStepArgs& a, int ag, int allow64) {
+  if (a.npw != 3) return true;
+  if (ag) return wide_ag_bm(a, allow64) != 128;  // 128: fwd1_rega_kernel<float>; 64: the glds planes
+  // mirrors mlp_split_fwd1's dispatch: rega (fp32 W1), glds / big (planes), the small kernels (fp32 W1 or planes)
+  if (rega_fwd_ok(a)) return false;
+  if (glds_fwd_ok(a) || big_fwd_ok(a)) return true;
+  return !mlp_split_fwd_fp32_w(a);
+}
+
+bool mlp_split_wgrad_leaves_planes_stale(const SplitStepArgs& a) {
+  return a.w1_planes_lazy && a.npw == 3 && a.npz == 3 && a.sgd && (a.wg_parts & 1) && a.w1_rows != 0 &&
+         a.xf.world == 0 && big_wgrad_ok(a) && rega_wgrad_ok(a);
 }
 
 bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64) {
