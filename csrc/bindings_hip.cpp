@@ -197,7 +197,11 @@ struct MlpStep {
           if (H < 512 && !cme::mlp_split_fwd_fp32_w(a)) refresh_planes(stream);
           if (fh_allgather && ag_counters && ag_slabs && ag_err && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h) &&
               cme::mlp_fwd1_head_ag_fits(a)) {
-            cme::mlp_fwd1_head_ag(a, h, P_<unsigned long long>(ag_counters), P_<unsigned long long>(ag_slabs),
+            // training (store_a1 off): with the all-ones XT feature the dW1 launch reads only the dZ1 planes (db1 is
+            // its column P) unless it splits fp32 dZ1 itself -- the fp32 dZ1 store is then skipped
+            cme::HeadArgs hg = h;
+            if (!store_a1 && bias_col && !dz32 && hg.dZ1_planes) hg.dZ1 = nullptr;
+            cme::mlp_fwd1_head_ag(a, hg, P_<unsigned long long>(ag_counters), P_<unsigned long long>(ag_slabs),
                                   P_<int>(ag_err), fh_tiles, S(stream));
           } else if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
             cme::mlp_fwd1_head(a, h, P_<unsigned>(fh_counters), fh_tiles, S(stream));
