@@ -1295,58 +1295,80 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
   const int M = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows, P = a.P;
   const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
-  float w[MB][NB][4], bb[MB][4];
+  // Epilogue in ROW-CONTIGUOUS 4-column chunks (the accumulators go through an LDS transpose after the K loop):
+  // 16-byte W1 / gradient accesses and 8-byte plane stores instead of a 4-byte (2-byte) scatter in the MFMA
+  // layout -- 8 instead of 32 (+ 8 instead of 32 per plane) memory instructions per lane.  Chunk q = t + 512 k
+  // of the 128 x 128 tile: row q / 32, columns 4 (q % 32) .. + 3.  P % 4 == 0 (rega_wgrad_ok), so a chunk is all
+  // weights, or (the chunk at column P) the all-ones feature's db1 in its first element.
+  constexpr int kCh = 128 * 128 / 4 / 512;  // chunks per thread
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  f32x4v wq[kCh];
+  float bq[kCh];
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = rw + 16 * mb + 4 * fg + i;
-      bb[mb][i] = buf_load1<float>(rb1, row < M ? row * 4 : kOOB);
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        const int col = cw + 16 * nb + fr;
-        w[mb][nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
-      }
-    }
+  for (int k = 0; k < kCh; ++k) {
+    const int q = (int)threadIdx.x + 512 * k, row = m0 + q / 32, col = n0 + 4 * (q % 32);
+    const bool rok = row < M;
+    wq[k] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rW, (rok && col + 4 <= P) ? (row * P + col) * 4 : kOOB, 0, 0));
+    bq[k] = buf_load1<float>(rb1, (rok && a.bias_col && col == P) ? row * 4 : kOOB);
+  }
   const int perr = ag_err_load(a.ag_err);  // the step's forward timed out: no update
   f32x4 acc[MB][NB];
   const AT* A = NP == 3 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
   rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n,
                                        m0, n0, lds_dyn, acc);
-  const size_t plane = (size_t)a.H * P;
-  const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
-  const bool upd = a.sgd && !poisoned(perr);
+  constexpr int LDT = 128 + 4;  // row pitch of the transposed tile (floats)
+  float* T = reinterpret_cast<float*>(lds_dyn);
+  __syncthreads();  // every wave's K-loop reads of lds_dyn are done
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
-        const float v = acc[mb][nb][i];
-        const bool in = row < M && col < P;
-        const int idx = row * P + col;
-        const float wv = w[mb][nb][i];
-        const float g = v * xs + reg * wv;
-        if (upd) {
-          const float nw = wv - lr * g;
-          st_f32(rW, in ? idx * 4 : kOOB, nw);
-          float r = nw;
+      for (int i = 0; i < 4; ++i) T[(rw - m0 + 16 * mb + 4 * fg + i) * LDT + cw - n0 + 16 * nb + fr] = acc[mb][nb][i];
+  __syncthreads();
+  const size_t plane = (size_t)a.H * P;
+  const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
+  const bool upd = a.sgd && !poisoned(perr);
+  const int nps = (NP == 3 && a.w1_planes_lazy) ? 0 : NP;  // the W1 planes refreshed (npw == npz)
 #pragma unroll
-          for (int p = 0; p < NP; ++p) {  // the W1 planes (npw == npz); split3 w1_planes_lazy: none
-            if (NP == 3 && a.w1_planes_lazy) break;
-            const bf16 hb = __float2bfloat16(r);
-            st_bf16(rp, in ? (int)((p * plane + idx) * 2) : kOOB, hb);
-            r -= __bfloat162float(hb);
-          }
-        } else {
-          st_f32(rg, in ? idx * 4 : kOOB, g);
-        }
-        if (a.bias_col && col == P && row < M) {  // all-ones feature: db1
-          if (upd) a.b1[row] = bb[mb][i] - lr * v;
-          else a.gb1[row] = v;
-        }
+  for (int k = 0; k < kCh; ++k) {
+    const int q = (int)threadIdx.x + 512 * k, r = q / 32, c4 = 4 * (q % 32);
+    const int row = m0 + r, col = n0 + c4;
+    if (row >= M) continue;
+    const f32x4v v = *reinterpret_cast<const f32x4v*>(T + r * LDT + c4);
+    if (col + 4 <= P) {
+      const int idx = row * P + col;
+      f32x4v g, nw;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        g[e] = v[e] * xs + reg * wq[k][e];
+        nw[e] = wq[k][e] - lr * g[e];
       }
+      if (upd) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ra::u32x4, nw), rW, idx * 4, 0, 0);
+        float rem[4] = {nw[0], nw[1], nw[2], nw[3]};
+        for (int pl = 0; pl < nps; ++pl) {
+          unsigned short qb[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bf16 hb = __float2bfloat16(rem[e]);
+            qb[e] = __builtin_bit_cast(unsigned short, hb);
+            rem[e] -= __bfloat162float(hb);
+          }
+          __attribute__((ext_vector_type(2))) unsigned w2;
+          w2.x = (unsigned)qb[0] | ((unsigned)qb[1] << 16);
+          w2.y = (unsigned)qb[2] | ((unsigned)qb[3] << 16);
+          __builtin_amdgcn_raw_buffer_store_b64(w2, rp, (int)((pl * plane + idx) * 2), 0, 0);
+        }
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ra::u32x4, g), rg, idx * 4, 0, 0);
+      }
+    } else if (a.bias_col && col == P) {  // all-ones feature: db1 (no input scale, no regulariser)
+      if (upd) a.b1[row] = bq[k] - lr * v[0];
+      else a.gb1[row] = v[0];
+    }
+  }
   mark_status(a, perr);
 }
 
@@ -1437,6 +1459,7 @@ void launch_fwd1_glds(const SplitStepArgs& a, hipStream_t s) {
 // bucketed call) so the head and every wgrad call of a step agree on what dZ1 form exists.
 bool rega_wgrad_ok(const SplitStepArgs& a) {
   return a.H >= kBigMinH && a.npw == a.npz && a.XTw && cdiv(a.H, 128) * cdiv(a.P + a.bias_col, 128) >= 192 &&
+         a.P % 4 == 0 &&
          a.n % 8 == 0 && a.ld % 8 == 0 && a.ldxt % 8 == 0 && al16(a.XTw) && al16(a.W1) &&
          (a.npz == 3 ? (a.dZ1 != nullptr && al16(a.dZ1)) : al16(a.dZ1p));
 }
@@ -1445,7 +1468,8 @@ template <typename AT, int NKS>
 void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int tn = cdiv(a.P + a.bias_col, 128), tbig = cdiv(rows, 128) * tn;
-  constexpr int L = std::max(ra::lds_bytes<128>(), kWKS * 4 * 64 * (int)sizeof(float) + 16);
+  // (the K-loop ring, the epilogue's transposed 128 x (128 + 4) fp32 tile, the role workgroups' scratch)
+  constexpr int L = std::max({ra::lds_bytes<128>(), 128 * (128 + 4) * 4, kWKS * 4 * 64 * (int)sizeof(float) + 16});
   set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS>>(L);
   wgrad_rega_kernel<AT, kRegaWC, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
 }
