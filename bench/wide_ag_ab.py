@@ -23,8 +23,8 @@ def main(argv=None):
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--modes", nargs="*", default=["head", "ag", "ag_noa1"],
                     help="head | ag | ag_noa1, each optionally +q0 (SplitStepArgs.poll_skip = 0: the hand-off polls "
-                         "re-load every granule every pass) and / or +l1 (MlpStep.lazy_planes: the in-place W1 update "
-                         "skips the W1-plane refresh); a mode may repeat (A/B alternation)")
+                         "re-load every granule every pass) and / or +l0 / +l1 (MlpStep.lazy_planes off / on: the in-place "
+                         "W1 update skips the W1-plane refresh; default: the engine's); a mode may repeat (A/B alternation)")
     a = ap.parse_args(argv)
     import torch
 
@@ -68,7 +68,8 @@ def main(argv=None):
                 e.set_store_a1(not mode.endswith("noa1"))
                 e._hip_step().ag_tiles64 = 1
                 e._hip_step().poll_skip = 0 if "q0" in opts else 1
-                e._hip_step().lazy_planes = 1 if "l1" in opts else 0
+                if "l0" in opts or "l1" in opts:  # (else the engine's default, MlpEngine.lazy_planes)
+                    e.set_lazy_planes("l1" in opts)
                 off = [0]
 
                 def step():

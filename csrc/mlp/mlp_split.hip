@@ -1072,6 +1072,96 @@ __global__ __launch_bounds__(512) void fwd1_glds_kernel(SplitStepArgs a, int tn,
   }
 }
 
+// The wide dW1 launches' epilogue in ROW-CONTIGUOUS 4-column chunks: the BM x BN accumulator tile goes through
+// an LDS transpose after the K loop, so W1 and the gradient move as 16-byte vectors and the planes as 8-byte
+// vectors instead of a 4-byte (2-byte) scatter in the MFMA layout (at 128 x 128: 8 instead of 32 memory
+// instructions per lane per array; 784-4096-10 step -1.1 us fp32, -0.8 us bf16).  Chunk q = t + 512 k: row
+// q / (BN / 4), columns 4 (q % (BN / 4)) .. + 3.  P % 4 == 0 (the launchers check it), so a chunk is all weights,
+// or -- the chunk at column P -- the all-ones feature's db1 in its first element.
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+template <int BM, int BN>
+struct W1Chunks {
+  static constexpr int kCh = BM * BN / 4 / 512, CPR = BN / 4, LDT = BN + 4;
+  static constexpr int kLdsBytes = BM * LDT * 4;
+  static_assert(kCh * 512 * 4 == BM * BN, "tile of whole chunks per thread");
+  f32x4v wq[kCh];
+  float bq[kCh];
+  // the weights (and b1 for the all-ones column) of this thread's chunks: issue BEFORE the K loop
+  __device__ __forceinline__ void prefetch(const SplitStepArgs& a, int m0, int n0, int M) {
+    const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
+#pragma unroll
+    for (int k = 0; k < kCh; ++k) {
+      const int q = (int)threadIdx.x + 512 * k, row = m0 + q / CPR, col = n0 + 4 * (q % CPR);
+      const bool rok = row < M;
+      wq[k] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rW, (rok && col + 4 <= a.P) ? (row * a.P + col) * 4 : kOOB, 0, 0));
+      bq[k] = buf_load1<float>(rb1, (rok && a.bias_col && col == a.P) ? row * 4 : kOOB);
+    }
+  }
+  // the MFMA-layout accumulators (this wave: rows rw + 16 mb + 4 fg + i, columns cw + 16 nb + fr) into the
+  // transposed tile; call after the K loop (its LDS reads are then done once the first barrier passes)
+  template <int MB, int NB>
+  __device__ __forceinline__ void stage(char* lds, const f32x4 (&acc)[MB][NB], int rw, int cw, int m0, int n0, int fg,
+                                        int fr) const {
+    float* T = reinterpret_cast<float*>(lds);
+    __syncthreads();
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) T[(rw - m0 + 16 * mb + 4 * fg + i) * LDT + cw - n0 + 16 * nb + fr] = acc[mb][nb][i];
+    __syncthreads();
+  }
+  // reg + SGD (+ nps planes) in place (upd), or the pre-scaled gradient into gW1 / gb1
+  __device__ __forceinline__ void apply(const SplitStepArgs& a, const char* lds, int m0, int n0, int M, bool upd,
+                                        int nps) const {
+    const float* T = reinterpret_cast<const float*>(lds);
+    const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
+    const int P = a.P;
+    const size_t plane = (size_t)a.H * P;
+    const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
+#pragma unroll
+    for (int k = 0; k < kCh; ++k) {
+      const int q = (int)threadIdx.x + 512 * k, r = q / CPR, c4 = 4 * (q % CPR);
+      const int row = m0 + r, col = n0 + c4;
+      if (row >= M) continue;
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(T + r * LDT + c4);
+      if (col + 4 <= P) {
+        const int idx = row * P + col;
+        f32x4v g, nw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          g[e] = v[e] * xs + reg * wq[k][e];
+          nw[e] = wq[k][e] - lr * g[e];
+        }
+        if (upd) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ra::u32x4, nw), rW, idx * 4, 0, 0);
+          float rem[4] = {nw[0], nw[1], nw[2], nw[3]};
+          for (int pl = 0; pl < nps; ++pl) {
+            unsigned short qb[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const bf16 hb = __float2bfloat16(rem[e]);
+              qb[e] = __builtin_bit_cast(unsigned short, hb);
+              rem[e] -= __bfloat162float(hb);
+            }
+            __attribute__((ext_vector_type(2))) unsigned w2;
+            w2.x = (unsigned)qb[0] | ((unsigned)qb[1] << 16);
+            w2.y = (unsigned)qb[2] | ((unsigned)qb[3] << 16);
+            __builtin_amdgcn_raw_buffer_store_b64(w2, rp, (int)((pl * plane + idx) * 2), 0, 0);
+          }
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ra::u32x4, g), rg, idx * 4, 0, 0);
+        }
+      } else if (a.bias_col && col == P) {  // all-ones feature: db1 (no input scale, no regulariser)
+        if (upd) a.b1[row] = bq[k] - lr * v[0];
+        else a.gb1[row] = v[0];
+      }
+    }
+  }
+};
+
 // dW1 = dZ1 XT (+ the all-ones feature column P = db1) with the fused reg + SGD + bf16-plane refresh (sgd)
 // or the pre-scaled gradient (sgd == 0); the dW2 / db2 role workgroups ride in the same launch
 template <int BM, int BN, int NPZ>
@@ -1113,59 +1203,16 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
         }
     return;
   }
-  // the weights this lane updates (and b1 of its rows, for the all-ones column), before the K loop
-  const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
-  float w[MB][NB][4], bb[MB][4];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = rw + 16 * mb + 4 * fg + i;
-      bb[mb][i] = buf_load1<float>(rb1, row < M ? row * 4 : kOOB);
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        const int col = cw + 16 * nb + fr;
-        w[mb][nb][i] = buf_load1<float>(rW, (row < M && col < P) ? (row * P + col) * 4 : kOOB);
-      }
-    }
+  // the weights this thread updates (and b1 for the all-ones column), before the K loop
+  W1Chunks<BM, BN> wc1;
+  wc1.prefetch(a, m0, n0, M);
   const int perr = ag_err_load(a.ag_err);  // the step's forward timed out: no update
   f32x4 acc[MB][NB];
   glds_gemm_mainloop<BM, BN, NPZ>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
                                   static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0, n0, lds_dyn,
                                   acc);
-  const size_t plane = (size_t)a.H * P;
-  const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
-  const bool upd = a.sgd && !poisoned(perr);
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = rw + 16 * mb + 4 * fg + i, col = cw + 16 * nb + fr;
-        const float v = acc[mb][nb][i];
-        const bool in = row < M && col < P;
-        const int idx = row * P + col;
-        const float wv = w[mb][nb][i];
-        const float g = v * xs + reg * wv;
-        if (upd) {
-          const float nw = wv - lr * g;
-          st_f32(rW, in ? idx * 4 : kOOB, nw);
-          float r = nw;
-#pragma unroll
-          for (int p = 0; p < NPZ; ++p) {  // the W1 planes have the dZ1 planes' count (npw == npz)
-            const bf16 hb = __float2bfloat16(r);
-            st_bf16(rp, in ? (int)((p * plane + idx) * 2) : kOOB, hb);
-            r -= __bfloat162float(hb);
-          }
-        } else {
-          st_f32(rg, in ? idx * 4 : kOOB, g);
-        }
-        if (a.bias_col && col == P && row < M) {  // all-ones feature: db1 (no input scale, no regulariser)
-          if (upd) a.b1[row] = bb[mb][i] - lr * v;
-          else a.gb1[row] = v;
-        }
-      }
+  wc1.stage(lds_dyn, acc, rw, cw, m0, n0, fg, fr);
+  wc1.apply(a, lds_dyn, m0, n0, M, a.sgd && !poisoned(perr), NPZ);  // (the W1 planes: npw == npz)
   mark_status(a, perr);
 }
 
@@ -1295,80 +1342,16 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
   const int M = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows, P = a.P;
   const float reg = (float)a.reg, lr = (float)a.lr, xs = a.xscale;
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(a.W1), rb1 = make_rsrc(a.b1);
-  // Epilogue in ROW-CONTIGUOUS 4-column chunks (the accumulators go through an LDS transpose after the K loop):
-  // 16-byte W1 / gradient accesses and 8-byte plane stores instead of a 4-byte (2-byte) scatter in the MFMA
-  // layout -- 8 instead of 32 (+ 8 instead of 32 per plane) memory instructions per lane.  Chunk q = t + 512 k
-  // of the 128 x 128 tile: row q / 32, columns 4 (q % 32) .. + 3.  P % 4 == 0 (rega_wgrad_ok), so a chunk is all
-  // weights, or (the chunk at column P) the all-ones feature's db1 in its first element.
-  constexpr int kCh = 128 * 128 / 4 / 512;  // chunks per thread
-  typedef float f32x4v __attribute__((ext_vector_type(4)));
-  f32x4v wq[kCh];
-  float bq[kCh];
-#pragma unroll
-  for (int k = 0; k < kCh; ++k) {
-    const int q = (int)threadIdx.x + 512 * k, row = m0 + q / 32, col = n0 + 4 * (q % 32);
-    const bool rok = row < M;
-    wq[k] = __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                           rW, (rok && col + 4 <= P) ? (row * P + col) * 4 : kOOB, 0, 0));
-    bq[k] = buf_load1<float>(rb1, (rok && a.bias_col && col == P) ? row * 4 : kOOB);
-  }
+  W1Chunks<128, 128> wc1;  // (the epilogue: row-contiguous chunks through an LDS transpose)
+  wc1.prefetch(a, m0, n0, M);
   const int perr = ag_err_load(a.ag_err);  // the step's forward timed out: no update
   f32x4 acc[MB][NB];
   const AT* A = NP == 3 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
   rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n,
                                        m0, n0, lds_dyn, acc);
-  constexpr int LDT = 128 + 4;  // row pitch of the transposed tile (floats)
-  float* T = reinterpret_cast<float*>(lds_dyn);
-  __syncthreads();  // every wave's K-loop reads of lds_dyn are done
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) T[(rw - m0 + 16 * mb + 4 * fg + i) * LDT + cw - n0 + 16 * nb + fr] = acc[mb][nb][i];
-  __syncthreads();
-  const size_t plane = (size_t)a.H * P;
-  const __amdgpu_buffer_rsrc_t rg = make_rsrc(a.gW1), rp = make_rsrc(a.W1p);
-  const bool upd = a.sgd && !poisoned(perr);
-  const int nps = (NP == 3 && a.w1_planes_lazy) ? 0 : NP;  // the W1 planes refreshed (npw == npz)
-#pragma unroll
-  for (int k = 0; k < kCh; ++k) {
-    const int q = (int)threadIdx.x + 512 * k, r = q / 32, c4 = 4 * (q % 32);
-    const int row = m0 + r, col = n0 + c4;
-    if (row >= M) continue;
-    const f32x4v v = *reinterpret_cast<const f32x4v*>(T + r * LDT + c4);
-    if (col + 4 <= P) {
-      const int idx = row * P + col;
-      f32x4v g, nw;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        g[e] = v[e] * xs + reg * wq[k][e];
-        nw[e] = wq[k][e] - lr * g[e];
-      }
-      if (upd) {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ra::u32x4, nw), rW, idx * 4, 0, 0);
-        float rem[4] = {nw[0], nw[1], nw[2], nw[3]};
-        for (int pl = 0; pl < nps; ++pl) {
-          unsigned short qb[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bf16 hb = __float2bfloat16(rem[e]);
-            qb[e] = __builtin_bit_cast(unsigned short, hb);
-            rem[e] -= __bfloat162float(hb);
-          }
-          __attribute__((ext_vector_type(2))) unsigned w2;
-          w2.x = (unsigned)qb[0] | ((unsigned)qb[1] << 16);
-          w2.y = (unsigned)qb[2] | ((unsigned)qb[3] << 16);
-          __builtin_amdgcn_raw_buffer_store_b64(w2, rp, (int)((pl * plane + idx) * 2), 0, 0);
-        }
-      } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ra::u32x4, g), rg, idx * 4, 0, 0);
-      }
-    } else if (a.bias_col && col == P) {  // all-ones feature: db1 (no input scale, no regulariser)
-      if (upd) a.b1[row] = bq[k] - lr * v[0];
-      else a.gb1[row] = v[0];
-    }
-  }
+  wc1.stage(lds_dyn, acc, rw, cw, m0, n0, fg, fr);
+  // the W1 planes (npw == npz); split3 w1_planes_lazy: none (the 128 x 128 forward reads fp32 W1)
+  wc1.apply(a, lds_dyn, m0, n0, M, a.sgd && !poisoned(perr), (NP == 3 && a.w1_planes_lazy) ? 0 : NP);
   mark_status(a, perr);
 }
 
@@ -1402,7 +1385,7 @@ bool glds_fwd_ok(const SplitStepArgs& a) {
 }
 bool glds_wgrad_ok(const SplitStepArgs& a) {
   return a.H >= kBigMinH && a.npw == a.npz && a.XTw && a.n % 8 == 0 && a.ld % 8 == 0 && a.ldxt % 8 == 0 && al16(a.dZ1p) &&
-         al16(a.XTw);
+         al16(a.XTw) && a.P % 4 == 0 && al16(a.W1);  // (W1Chunks: 16-byte W1 rows chunks)
 }
 
 // 128x128 tiles when that still gives ~200+ workgroups, else 64x64 (same choice as the register-staged
@@ -1469,7 +1452,7 @@ void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) 
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int tn = cdiv(a.P + a.bias_col, 128), tbig = cdiv(rows, 128) * tn;
   // (the K-loop ring, the epilogue's transposed 128 x (128 + 4) fp32 tile, the role workgroups' scratch)
-  constexpr int L = std::max({ra::lds_bytes<128>(), 128 * (128 + 4) * 4, kWKS * 4 * 64 * (int)sizeof(float) + 16});
+  constexpr int L = std::max({ra::lds_bytes<128>(), W1Chunks<128, 128>::kLdsBytes, kWKS * 4 * 64 * (int)sizeof(float) + 16});
   set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS>>(L);
   wgrad_rega_kernel<AT, kRegaWC, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
 }
@@ -1519,8 +1502,8 @@ void launch_wgrad_glds(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
   const int t128 = cdiv(rows, 128) * cdiv(NW, 128);
   const int tn64 = cdiv(NW, 64), t64 = cdiv(rows, 64) * tn64;
   constexpr int kRoleLds = kWKS * 4 * 64 * (int)sizeof(float) + 16;
-  constexpr int L128 = std::max(gl::lds_bytes<128, 128, NP>(), kRoleLds);
-  constexpr int L64 = std::max(gl::lds_bytes<64, 64, NP>(), kRoleLds);
+  constexpr int L128 = std::max({gl::lds_bytes<128, 128, NP>(), W1Chunks<128, 128>::kLdsBytes, kRoleLds});
+  constexpr int L64 = std::max({gl::lds_bytes<64, 64, NP>(), W1Chunks<64, 64>::kLdsBytes, kRoleLds});
   // split-K when the output tiles cannot fill the chip and K is long (the tensor-parallel shard at a large
   // global batch): K slices of whole 32-deep stages, the 128 x 128 tiles first (the data-parallel launch's
   // per-workgroup shape when 8 slices of K = 6400 give 200+ workgroups), else the 64 x 64 ones
