@@ -65,8 +65,9 @@ def parse(argv=None):
                          "(one z2 all-reduce per step, every rank runs the whole global batch --batch; strong "
                          "scaling of a fixed model, meant for the wide configs)")
     ap.add_argument("--tune-allreduce", default="on", choices=["on", "off"],
-                    help="N > 1 with --allreduce auto: time the policy's xGMI pick and RCCL for --tune-steps steps "
-                         "each before the timed region and run the faster (the record lists both)")
+                    help="N > 1 with --allreduce auto: time the policy's xGMI pick, the xGMI two-shot (N >= 3) and RCCL "
+                         "for --tune-steps steps each before the timed region and run the fastest (the record lists "
+                         "every candidate)")
     ap.add_argument("--tune-steps", type=int, default=100)
     ap.add_argument("--train-size", type=int, default=54000)
     ap.add_argument("--verbose", action="store_true")
@@ -171,8 +172,9 @@ def main(argv=None) -> int:
         return float("inf") if bad else round(us, 3)
 
     # --tune-allreduce: with N > 1 and --allreduce auto, the gradient sync is CHOSEN BY MEASUREMENT on this
-    # node before anything is timed -- the policy's xGMI pick (cost model, docs/PERFORMANCE.md) and RCCL each
-    # run --tune-steps steps, the faster one (max over ranks, agreed by every rank) runs the timed region
+    # node before anything is timed -- the policy's xGMI pick (cost model, docs/PERFORMANCE.md), the two-shot
+    # (N >= 3) and RCCL each run --tune-steps steps, the fastest (max over ranks, agreed by every rank) runs
+    # the timed region
     tuning = R > 1 and a.allreduce == "auto" and a.backend == "hip" and a.tune_allreduce == "on"
     tune = {}
     tr, timed_plans, probe_plans = prepare(a.allreduce, a.tune_steps if tuning else 0)
@@ -192,14 +194,31 @@ def main(argv=None) -> int:
             tr, timed_plans, probe_plans = prepare("rccl", a.tune_steps if tuning else 0)
             tune["xgmi"] = "failed in warm-up"
     if tuning and tr.allreduce_impl.startswith("xgmi"):
-        first = tr.allreduce_impl
-        tune[first] = probe(tr, probe_plans)
-        tr.close()  # (collective) the RCCL candidate starts from the initial weights like every prepare
-        tr, timed_plans, probe_plans = prepare("rccl", a.tune_steps)
+        # candidates: the policy's pick (already prepared), the xGMI two-shot from 3 ranks on (when the pick is the
+        # one-shot: 2 S / R bytes per link against S, one more round trip), RCCL
+        modes = {tr.allreduce_impl: a.allreduce}
         tune[tr.allreduce_impl] = probe(tr, probe_plans)
-        if tune[first] <= tune[tr.allreduce_impl]:  # identical floats on every rank: one decision
-            tr.close()
-            tr, timed_plans, _ = prepare(a.allreduce)  # (a failure from here on invalidates the record below)
+        last = tr.allreduce_impl
+        for mode in (["xgmi2"] if R >= 3 and tr.allreduce_impl != "xgmi-2shot" else []) + ["rccl"]:
+            if tr is not None:
+                tr.close()  # (collective) every candidate starts from the initial weights, like every prepare
+            try:
+                tr, timed_plans, probe_plans = prepare(mode, a.tune_steps)
+            except Exception as ex:  # noqa: BLE001 - a candidate the node cannot run (raised on every rank)
+                tr, last = None, None
+                tune[mode] = "unavailable"
+                if rank == 0:
+                    print(f"allreduce candidate {mode} unavailable: {ex}", file=sys.stderr, flush=True)
+                continue
+            modes[tr.allreduce_impl] = mode
+            tune[tr.allreduce_impl] = probe(tr, probe_plans)
+            last = tr.allreduce_impl
+        nums = {k: v for k, v in tune.items() if isinstance(v, float)}
+        best = min(nums, key=lambda k: (nums[k], k))  # identical floats on every rank: one decision
+        if best != last:
+            if tr is not None:
+                tr.close()
+            tr, timed_plans, _ = prepare(modes[best])  # (a failure from here on invalidates the record below)
         tune = {k: (v if v != float("inf") else "failed") for k, v in tune.items()}
         if rank == 0:
             print(f"allreduce tuned on this node: {tune} -> {tr.allreduce_impl}", file=sys.stderr, flush=True)

@@ -8,6 +8,7 @@
 #   prof                 rocprofv3 --kernel-trace --stats of the headline bench
 #   probes               launch fixed cost (default and spin-wait device flags) and batch-locality probes
 #   wideab               bench/wide_ag_ab.py: the wide fused head vs forward + head kernel (H = 4096, 1024)
+#   wideab_lazy          bench/wide_ag_ab.py: lazy W1 planes off / on, alternated (784-4096-10 fp32)
 # Usage (from the repo root on the GPU box): scripts/gpu_check.sh tests smoke bench
 # Every GPU step has its own time limit; outputs go to gpurun_out/check/.
 set -o pipefail
@@ -51,6 +52,10 @@ for st in "$@"; do
       timeout -k 10 240 python bench/launch_overhead.py > $O/launch_overhead.jsonl 2>&1 && grep fit $O/launch_overhead.jsonl &&
       timeout -k 10 240 python bench/launch_overhead.py --spin > $O/launch_overhead_spin.jsonl 2>&1 && grep -E "fit|spin" $O/launch_overhead_spin.jsonl &&
       timeout -k 10 240 python bench/batch_locality.py > $O/batch_locality.jsonl 2>&1 && grep '^{' $O/batch_locality.jsonl || exit 1 ;;
+    wideab_lazy)
+      timeout -k 10 300 python bench/wide_ag_ab.py --hidden 4096 --cfg f32:split3 --modes ag_noa1+l0 ag_noa1+l1 ag_noa1+l0 ag_noa1+l1 \
+        > $O/wide_lazy.jsonl 2>&1 || { tail -20 $O/wide_lazy.jsonl; exit 1; }
+      grep '^{' $O/wide_lazy.jsonl ;;
     wideab)
       timeout -k 10 300 python bench/wide_ag_ab.py --hidden 4096 1024 > $O/wide_ab.jsonl 2>&1 || { tail -20 $O/wide_ab.jsonl; exit 1; }
       grep '^{' $O/wide_ab.jsonl ;;

@@ -159,20 +159,22 @@ def test_tensor_parallel_xgmi_z2_allreduce(tmp_path, world, H):
     assert res["rel"] < 1e-5 and res["b_err"] < 1e-6, res
 
 
-def test_bench_tunes_allreduce_two_ranks_shared_gpu():
-    """bench.py --gpus 2 (self-launched, 2 ranks on GPU 0): the gradient sync is chosen by measurement --
-    the policy's xGMI pick and the communicator's all-reduce each run the probe, both timings are in the
-    record, the faster one ran the timed region, and the record is valid (replicas bitwise equal)."""
+@pytest.mark.parametrize("gpus", [2, 4])
+def test_bench_tunes_allreduce_shared_gpu(gpus):
+    """bench.py --gpus N (self-launched, N ranks on GPU 0): the gradient sync is chosen by measurement -- the
+    policy's xGMI pick, the xGMI two-shot (N >= 3) and the communicator's all-reduce each run the probe, every
+    timing is in the record, the fastest ran the timed region, and the record is valid (replicas bitwise equal)."""
     import json
 
     env = dict(os.environ, CME_SHARED_GPU="1", OMP_NUM_THREADS="2")
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup",
-                        "5", "--tune-steps", "20"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "20",
+                        "--warmup", "5", "--tune-steps", "20"], capture_output=True, text=True, timeout=600, env=env,
+                       cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     cfg = rec["config"]
     tune = cfg["allreduce_tuning_us_per_step"]
-    assert rec["n_gpus"] == 2 and cfg["ranks_seen"] == 2 and cfg["replicas_bitwise_equal"], rec
-    assert len(tune) == 2 and any(k.startswith("xgmi") for k in tune), tune
+    assert rec["n_gpus"] == gpus and cfg["ranks_seen"] == gpus and cfg["replicas_bitwise_equal"], rec
+    assert len(tune) == (2 if gpus == 2 else 3) and any(k.startswith("xgmi") for k in tune), tune
     nums = {k: v for k, v in tune.items() if isinstance(v, (int, float))}
     assert nums and cfg["allreduce"] == min(nums, key=nums.get), (cfg["allreduce"], tune)
