@@ -534,6 +534,10 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("sgd"), py::arg("with_loss"), py::arg("stream"), py::arg("parts") = 3);
 
   m.def(
+      "occupy_cus",
+      [](int wgs, int lds_bytes, int64_t ns, uintptr_t s) { cme::occupy_cus(wgs, lds_bytes, ns, S(s)); },
+      py::arg("wgs"), py::arg("lds_bytes"), py::arg("ns"), py::arg("stream"));
+  m.def(
       "split_planes",
       [](uintptr_t W, uintptr_t planes, int64_t n, int np, uintptr_t s) {
         cme::mlp_split_planes(P<const float>(W), P<void>(planes), n, np, S(s));

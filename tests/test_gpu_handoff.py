@@ -141,3 +141,30 @@ def test_handoff_timeout_on_one_rank_stops_every_rank(tmp_path, allreduce):
         assert float(z[rank]["raised"]) == 1.0, (rank, z[rank])
         assert float(z[rank]["untouched"]) == 1.0, (rank, z[rank])
     assert float(z[0]["local_err"]) == 1.0 and float(z[1]["local_err"]) == 0.0
+
+
+@pytest.mark.parametrize("H", [100, 4096])
+def test_partial_residency_times_out_and_applies_nothing(H):
+    """The hazard the bounded polls exist for, forced for real: a side stream holds all but 8 CUs (one
+    160 KB-LDS workgroup per CU, sleeping ~30 ms, csrc/mlp/occupy.hip) while the step's all-gather forward + head
+    launch starts, so most of its column tiles' workgroups are NOT resident.  The resident ones' polls must time out
+    (no hang), the error word must be set, and the weight-gradient launch must apply nothing."""
+    import time
+
+    from cme213_sp18_amd._native import hip
+
+    n = 800
+    e = _engine("f32", H, n)
+    e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+    torch.cuda.synchronize()
+    assert not e.kernel_error()
+    before = e.params.clone()
+    e.inject_handoff_timeout(-1, 10)  # no withheld granules: only a short poll bound (2^10 passes)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    side = torch.cuda.Stream()
+    hip().occupy_cus(cus - 8, 160 * 1024, 30_000_000, side.cuda_stream)
+    time.sleep(0.003)  # the holder is running before the step is queued
+    e.run(n, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+    torch.cuda.synchronize()
+    assert e.kernel_error(), "most of the grid was not resident: the hand-off polls should have timed out"
+    assert torch.equal(e.params, before)
