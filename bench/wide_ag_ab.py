@@ -68,6 +68,8 @@ def main(argv=None):
                 e.set_store_a1(not mode.endswith("noa1"))
                 e._hip_step().ag_tiles64 = 1
                 e._hip_step().poll_skip = 0 if "q0" in opts else 1
+                if "w2" in opts or "w1" in opts:  # wide bf16 dW1 wave layout (MlpStep.rega_wc)
+                    e._hip_step().rega_wc = 2 if "w2" in opts else 1
                 if "l0" in opts or "l1" in opts:  # (else the engine's default, MlpEngine.lazy_planes)
                     e.set_lazy_planes("l1" in opts)
                 off = [0]

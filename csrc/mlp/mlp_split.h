@@ -100,6 +100,9 @@ struct SplitStepArgs {
   // wide split3 layers: the A-in-registers dW1 launch's in-place update (sgd = 1) leaves the W1 planes alone (the
   // 128 x 128 forward reads fp32 W1); the caller marks them stale and refreshes them before a forward that reads them
   int w1_planes_lazy = 0;
+  // wide bf16 (split1) layers: the A-in-registers dW1 launch's wave layout, 8 x 1 (1: each wave 16 rows x 128
+  // columns) or 4 x 2 (2: 32 rows x 64 columns, half the B-fragment LDS reads; A rows loaded by two waves)
+  int rega_wc = 1;
   // The all-gather forward + head launches' timed-out-wait word (MlpEngine.ag_err).  The weight-gradient
   // launch reads it and, when set, APPLIES NOTHING: no SGD / plane refresh (sgd = 1), no xGMI exchange (the
   // fused all-reduce: this rank stops taking part, its peers time out), and the gradient status word below

@@ -1453,6 +1453,11 @@ void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) 
   const int tn = cdiv(a.P + a.bias_col, 128), tbig = cdiv(rows, 128) * tn;
   // (the K-loop ring, the epilogue's transposed 128 x (128 + 4) fp32 tile, the role workgroups' scratch)
   constexpr int L = std::max({ra::lds_bytes<128>(), W1Chunks<128, 128>::kLdsBytes, kWKS * 4 * 64 * (int)sizeof(float) + 16});
+  if constexpr (sizeof(AT) == 2) if (a.rega_wc == 2) {  // (bf16 only: for split3 the 4 x 2 layout splits every A value twice)
+    set_lds_limit<wgrad_rega_kernel<AT, 2, NKS>>(L);
+    wgrad_rega_kernel<AT, 2, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
+    return;
+  }
   set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS>>(L);
   wgrad_rega_kernel<AT, kRegaWC, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
 }
