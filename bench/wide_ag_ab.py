@@ -68,6 +68,9 @@ def main(argv=None):
                 e.set_store_a1(not mode.endswith("noa1"))
                 e._hip_step().ag_tiles64 = 1
                 e._hip_step().poll_skip = 0 if "q0" in opts else 1
+                for o in opts:  # "+a<bits>": split3 operand forms (SplitStepArgs.a_fp32: bit0 fp32 W1, bit1 fp32 dZ1)
+                    if o[:1] == "a" and o[1:].isdigit():
+                        e._hip_step().a_fp32 = int(o[1:])
                 if "w2" in opts or "w1" in opts:  # wide bf16 dW1 wave layout (MlpStep.rega_wc)
                     e._hip_step().rega_wc = 2 if "w2" in opts else 1
                 if "l0" in opts or "l1" in opts:  # (else the engine's default, MlpEngine.lazy_planes)

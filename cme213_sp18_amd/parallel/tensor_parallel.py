@@ -264,6 +264,7 @@ class TensorParallelTrainer:
         (RCCL / one rank) -- the z2 all-reduce is then a graph node like the kernels around it."""
         if self.graphs_usable(use_graphs):
             self.capture(plan, lr, reg).replay()
+            self.engine.mark_planes_stale()  # (a host-free replay: the lazily refreshed planes may be stale)
         else:
             for s, ln in plan.steps:
                 self.step(s, ln, lr, reg)

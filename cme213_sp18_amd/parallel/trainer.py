@@ -594,7 +594,13 @@ class DataParallelTrainer:
             fn = e._hip_step().run_steps
             return lambda: fn(*args)
         if self.use_graphs and self.executor != "eager":
-            return self.capture(plan, lr, reg).replay
+            g = self.capture(plan, lr, reg)
+
+            def replay():
+                g.replay()
+                # a replay runs host-free: the lazily refreshed W1 planes (MlpStep.planes_stale) may be stale again
+                self.engine.mark_planes_stale()
+            return replay
         return lambda: self._enqueue_plan(plan, lr, reg)
 
     def run_plan(self, plan: EpochPlan, lr: float, reg: float) -> None:
@@ -607,6 +613,7 @@ class DataParallelTrainer:
                                     sgd, torch.cuda.current_stream(e.device).cuda_stream)
         elif self.use_graphs and self.executor != "eager":
             self.capture(plan, lr, reg).replay()
+            self.engine.mark_planes_stale()  # (the replay's in-place updates skipped the plane refresh)
         else:
             self._enqueue_plan(plan, lr, reg)
 

@@ -243,8 +243,9 @@ struct MlpStep {
       }
       if (parts & 2) {
         a.w1_planes_lazy = lazy_planes;
+        a.w1_planes_lazy = cme::mlp_split_wgrad_leaves_planes_stale(a) ? 1 : 0;  // (only where nothing reads them)
         cme::mlp_split_wgrad(a, S(stream));
-        if (cme::mlp_split_wgrad_leaves_planes_stale(a)) planes_stale = true;
+        if (a.w1_planes_lazy) planes_stale = true;
       }
       return;
     }
@@ -538,8 +539,10 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def(
       "occupy_cus",
-      [](int wgs, int lds_bytes, int64_t ns, uintptr_t s) { cme::occupy_cus(wgs, lds_bytes, ns, S(s)); },
-      py::arg("wgs"), py::arg("lds_bytes"), py::arg("ns"), py::arg("stream"));
+      [](int wgs, int lds_bytes, int64_t ns, uintptr_t s, uintptr_t running) {
+        cme::occupy_cus(wgs, lds_bytes, ns, S(s), reinterpret_cast<int*>(running));
+      },
+      py::arg("wgs"), py::arg("lds_bytes"), py::arg("ns"), py::arg("stream"), py::arg("running") = 0);
   m.def(
       "split_planes",
       [](uintptr_t W, uintptr_t planes, int64_t n, int np, uintptr_t s) {

@@ -1219,7 +1219,7 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
 // a1 = sigmoid(W1 X + b1) on the A-in-registers engine (rega_gemm.h): W1 read as fp32 and split into the
 // exact bf16 planes in registers (AT = float), or the bf16 plane 0 (AT = bf16, split1); z2 partials of
 // this 128-row tile as in fwd1_glds_kernel
-template <typename AT, int WC, int NKS, bool AG = false>
+template <typename AT, int WC, int NKS, bool AG = false, int APL = 1>
 __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn, RegaAgArgs ag = {}) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   using G = RegaGeom<128, WC>;
@@ -1248,8 +1248,8 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
     }
   f32x4 acc[MB][NB];
   const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.W1) : reinterpret_cast<const AT*>(a.W1p);
-  rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn,
-                                       acc);
+  rega_gemm_mainloop<AT, 128, WC, NKS, 0, APL>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0,
+                                               lds_dyn, acc, APL == 3 ? H * a.P * 2 : 0);
   if (AG) ag_stamp(a, 1);
   const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
 #pragma unroll
@@ -1324,7 +1324,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
 // dW1 = dZ1 XT on the A-in-registers engine: dZ1 read as fp32 (AT = float; the head writes it instead of
 // the three bf16 planes: 4 B per element stored and loaded instead of 6) or as its one bf16 plane (split1),
 // with wgrad_glds_kernel's fused reg + SGD + plane-refresh epilogue; the dW2 / db2 roles ride along
-template <typename AT, int WC, int NKS>
+template <typename AT, int WC, int NKS, int APL = 1>
 __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {
@@ -1333,7 +1333,7 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
     return;
   }
   using G = RegaGeom<128, WC>;
-  constexpr int MB = G::MB, NB = G::NB, BM = G::BM, NP = sizeof(AT) == 4 ? 3 : 1;
+  constexpr int MB = G::MB, NB = G::NB, BM = G::BM, NP = (sizeof(AT) == 4 || APL == 3) ? 3 : 1;
   const int id = xcd_remap(blockIdx.x, tbig);
   const int m0 = a.w1_row0 + (id / tn) * BM, n0 = (id % tn) * 128;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1346,9 +1346,10 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
   wc1.prefetch(a, m0, n0, M);
   const int perr = ag_err_load(a.ag_err);  // the step's forward timed out: no update
   f32x4 acc[MB][NB];
-  const AT* A = NP == 3 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
-  rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n,
-                                       m0, n0, lds_dyn, acc);
+  // fp32 dZ1 split in registers (AT = float), or its stored planes (bf16: one, APL = 3: three)
+  const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
+  rega_gemm_mainloop<AT, 128, WC, NKS, 0, APL>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col,
+                                               a.n, m0, n0, lds_dyn, acc, APL == 3 ? a.H * a.ld * 2 : 0);
   wc1.stage(lds_dyn, acc, rw, cw, m0, n0, fg, fr);
   // the W1 planes (npw == npz); split3 w1_planes_lazy: none (the 128 x 128 forward reads fp32 W1)
   wc1.apply(a, lds_dyn, m0, n0, M, a.sgd && !poisoned(perr), (NP == 3 && a.w1_planes_lazy) ? 0 : NP);
@@ -1397,29 +1398,29 @@ bool rega_fwd_ok(const SplitStepArgs& a) {
 
 constexpr int kRegaWC = 1;  // wave layout of the A-in-registers kernels: 8 (rows) x 1 (bench/micro/rega_ablate.hip: WC = 2 splits every A value twice, +25 % at H = 4096)
 
-template <typename AT, int NKS>
+template <typename AT, int NKS, int APL = 1>
 void launch_fwd1_rega_k(const SplitStepArgs& a, hipStream_t s) {
   constexpr int L = std::max(ra::lds_bytes<128>(), 8 * 8 * 64 * 16);  // (z2 reduction scratch)
-  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS>>(L);
-  fwd1_rega_kernel<AT, kRegaWC, NKS><<<cdiv(a.H, 128) * cdiv(a.n, 128), 512, L, s>>>(a, cdiv(a.n, 128));
+  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, false, APL>>(L);
+  fwd1_rega_kernel<AT, kRegaWC, NKS, false, APL><<<cdiv(a.H, 128) * cdiv(a.n, 128), 512, L, s>>>(a, cdiv(a.n, 128));
 }
 
 // the fused all-gather head: > 80 KB of LDS keeps it at one workgroup per CU (the hand-off's measured form)
-template <typename AT, int NKS>
+template <typename AT, int NKS, int APL = 1>
 void launch_fwd1_rega_ag_k(const SplitStepArgs& a, RegaAgArgs g, hipStream_t s) {
   constexpr int L = wide_ag_launch_lds(std::max({ra::lds_bytes<128>(), 8 * 8 * 64 * 16, wide_ag_lds_bytes<128, 128>()}));
-  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true>>(L);
+  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true, APL>>(L);
   g.ep_off = L - 16;
   g.tiling = 0;
   const int tn = cdiv(a.n, 128);
-  fwd1_rega_kernel<AT, kRegaWC, NKS, true><<<g.tm * tn, 512, L, s>>>(a, tn, g);
+  fwd1_rega_kernel<AT, kRegaWC, NKS, true, APL><<<g.tm * tn, 512, L, s>>>(a, tn, g);
 }
 
 // K = P = 784 (MNIST) is 25 stages of 32: the fully unrolled K loop; anything else the runtime loop
-template <typename AT>
+template <typename AT, int APL = 1>
 void launch_fwd1_rega(const SplitStepArgs& a, hipStream_t s) {
-  if (cdiv(a.P, ra::kBK) == 25) launch_fwd1_rega_k<AT, 25>(a, s);
-  else launch_fwd1_rega_k<AT, 0>(a, s);
+  if (cdiv(a.P, ra::kBK) == 25) launch_fwd1_rega_k<AT, 25, APL>(a, s);
+  else launch_fwd1_rega_k<AT, 0, APL>(a, s);
 }
 
 template <int NP>
@@ -1447,25 +1448,25 @@ bool rega_wgrad_ok(const SplitStepArgs& a) {
          (a.npz == 3 ? (a.dZ1 != nullptr && al16(a.dZ1)) : al16(a.dZ1p));
 }
 
-template <typename AT, int NKS>
+template <typename AT, int NKS, int APL = 1>
 void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int tn = cdiv(a.P + a.bias_col, 128), tbig = cdiv(rows, 128) * tn;
   // (the K-loop ring, the epilogue's transposed 128 x (128 + 4) fp32 tile, the role workgroups' scratch)
   constexpr int L = std::max({ra::lds_bytes<128>(), W1Chunks<128, 128>::kLdsBytes, kWKS * 4 * 64 * (int)sizeof(float) + 16});
-  if constexpr (sizeof(AT) == 2) if (a.rega_wc == 2) {  // (bf16 only: for split3 the 4 x 2 layout splits every A value twice)
+  if constexpr (sizeof(AT) == 2 && APL == 1) if (a.rega_wc == 2) {  // (split1 only: for split3 the 4 x 2 layout splits every A value twice)
     set_lds_limit<wgrad_rega_kernel<AT, 2, NKS>>(L);
     wgrad_rega_kernel<AT, 2, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
     return;
   }
-  set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS>>(L);
-  wgrad_rega_kernel<AT, kRegaWC, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
+  set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS, APL>>(L);
+  wgrad_rega_kernel<AT, kRegaWC, NKS, APL><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
 }
 
-template <typename AT>
+template <typename AT, int APL = 1>
 void launch_wgrad_rega(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
-  if (cdiv(a.n, ra::kBK) == 25) launch_wgrad_rega_k<AT, 25>(a, t2, tb, s);
-  else launch_wgrad_rega_k<AT, 0>(a, t2, tb, s);
+  if (cdiv(a.n, ra::kBK) == 25) launch_wgrad_rega_k<AT, 25, APL>(a, t2, tb, s);
+  else launch_wgrad_rega_k<AT, 0, APL>(a, t2, tb, s);
 }
 
 // split-K dW1, second half: sum the ksplit partial slabs in slab order (deterministic), then the fused
@@ -1637,7 +1638,8 @@ bool small_wgrad_fp32_ok(const SplitStepArgs& a) {
 bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a) {
   if (a.npz != 3) return false;
   const bool big = big_wgrad_ok(a) && a.xf.world == 0;
-  return big ? rega_wgrad_ok(a) : small_wgrad_fp32_ok(a);
+  // (wide: fp32 dZ1 unless a_fp32 bit1 is clear -- then the head writes the planes and the dW1 reads them)
+  return big ? (rega_wgrad_ok(a) && (a.a_fp32 & 2) && a.dZ1 != nullptr) : small_wgrad_fp32_ok(a);
 }
 
 bool mlp_split_fwd_fp32_w(const SplitStepArgs& a) { return a.npw == 3 && (a.a_fp32 & 1) && a.W1 != nullptr && al16(a.W1); }
@@ -1674,16 +1676,17 @@ static int wide_ag_bm(const SplitStepArgs& a, int allow64) {
 
 bool mlp_split_wide_fwd_reads_planes(const SplitStepArgs& a, int ag, int allow64) {
   if (a.npw != 3) return true;
-  if (ag) return wide_ag_bm(a, allow64) != 128;  // 128: fwd1_rega_kernel<float>; 64: the glds planes
-  // mirrors mlp_split_fwd1's dispatch: rega (fp32 W1), glds / big (planes), the small kernels (fp32 W1 or planes)
-  if (rega_fwd_ok(a)) return false;
+  if (ag) return wide_ag_bm(a, allow64) != 128 || !mlp_split_fwd_fp32_w(a);  // 128: fwd1_rega_kernel; 64: glds
+  // mirrors mlp_split_fwd1's dispatch: rega (fp32 W1 or the planes), glds / big (planes), the small kernels (fp32
+  // W1 or planes)
+  if (rega_fwd_ok(a)) return !mlp_split_fwd_fp32_w(a);
   if (glds_fwd_ok(a) || big_fwd_ok(a)) return true;
   return !mlp_split_fwd_fp32_w(a);
 }
 
 bool mlp_split_wgrad_leaves_planes_stale(const SplitStepArgs& a) {
   return a.w1_planes_lazy && a.npw == 3 && a.npz == 3 && a.sgd && (a.wg_parts & 1) && a.w1_rows != 0 &&
-         a.xf.world == 0 && big_wgrad_ok(a) && rega_wgrad_ok(a);
+         a.xf.world == 0 && big_wgrad_ok(a) && rega_wgrad_ok(a) && mlp_split_fwd_fp32_w(a);
 }
 
 bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64) {
@@ -1730,7 +1733,10 @@ int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long lo
   g.dg = gran + (size_t)g.tm * 16 * a.ld;
   if (bm == 128) {
     const bool k25 = cdiv(a.P, ra::kBK) == 25;
-    if (a.npw == 3) {
+    if (a.npw == 3 && !mlp_split_fwd_fp32_w(a)) {  // the stored W1 planes (a_fp32 bit0 clear)
+      if (k25) launch_fwd1_rega_ag_k<bf16, 25, 3>(a, g, s);
+      else launch_fwd1_rega_ag_k<bf16, 0, 3>(a, g, s);
+    } else if (a.npw == 3) {
       if (k25) launch_fwd1_rega_ag_k<float, 25>(a, g, s);
       else launch_fwd1_rega_ag_k<float, 0>(a, g, s);
     } else {
@@ -1752,7 +1758,8 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
               "split path: operand too large for 32-bit buffer offsets");
   CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
   if (rega_fwd_ok(a)) {
-    if (a.npw == 3) launch_fwd1_rega<float>(a, s);
+    if (a.npw == 3 && !mlp_split_fwd_fp32_w(a)) launch_fwd1_rega<bf16, 3>(a, s);  // the stored W1 planes
+    else if (a.npw == 3) launch_fwd1_rega<float>(a, s);
     else launch_fwd1_rega<bf16>(a, s);
     CME_LAUNCH_CHECK(s);
     return;
@@ -1807,7 +1814,8 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
     const int t2f = do_roles ? cdiv(a.H, 16) : 0;
     const int tbf = do_roles ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
     if (rega_wgrad_ok(a)) {
-      if (a.npz == 3) launch_wgrad_rega<float>(a, t2f, tbf, s);
+      if (a.npz == 3 && !mlp_split_wgrad_fp32_dz(a)) launch_wgrad_rega<bf16, 3>(a, t2f, tbf, s);  // dZ1 planes
+      else if (a.npz == 3) launch_wgrad_rega<float>(a, t2f, tbf, s);
       else launch_wgrad_rega<bf16>(a, t2f, tbf, s);
       CME_LAUNCH_CHECK(s);
       return;

@@ -161,10 +161,24 @@ def test_partial_residency_times_out_and_applies_nothing(H):
     before = e.params.clone()
     e.inject_handoff_timeout(-1, 10)  # no withheld granules: only a short poll bound (2^10 passes)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    side = torch.cuda.Stream()
-    hip().occupy_cus(cus - 8, 160 * 1024, 30_000_000, side.cuda_stream)
-    time.sleep(0.003)  # the holder is running before the step is queued
-    e.run(n, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+    # two streams created back to back land on different hardware queues (HIP assigns them round robin), so the
+    # step runs BESIDE the holder (on one queue it would simply wait for it and find the whole device free)
+    side, work = torch.cuda.Stream(), torch.cuda.Stream()
+    work.wait_stream(torch.cuda.current_stream())
+    running = torch.zeros(1, dtype=torch.int32).pin_memory()  # set by the holder's first workgroup
+    hip().occupy_cus(cus - 8, 160 * 1024, 50_000_000, side.cuda_stream, running.data_ptr())
+    t0 = time.time()
+    while int(running[0]) == 0:  # the holder is running before the step is queued
+        assert time.time() - t0 < 5.0, "the CU holder never started"
+        time.sleep(1e-4)
+    time.sleep(0.002)  # (every holder workgroup dispatched)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(work):
+        ev0.record()
+        e.run(n, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+        ev1.record()
     torch.cuda.synchronize()
+    # (a step that ran beside the holder lasts about as long as the holder: its non-resident workgroups waited)
+    assert ev0.elapsed_time(ev1) > 10.0, ("the step did not overlap the CU holder", ev0.elapsed_time(ev1))
     assert e.kernel_error(), "most of the grid was not resident: the hand-off polls should have timed out"
     assert torch.equal(e.params, before)
