@@ -193,13 +193,15 @@ def main(argv=None) -> int:
             tr.close()
             tr, timed_plans, probe_plans = prepare("rccl", a.tune_steps if tuning else 0)
             tune["xgmi"] = "failed in warm-up"
-    if tuning and tr.allreduce_impl.startswith("xgmi"):
-        # candidates: the policy's pick (already prepared), the xGMI two-shot from 3 ranks on (when the pick is the
-        # one-shot: 2 S / R bytes per link against S, one more round trip), RCCL
-        modes = {tr.allreduce_impl: a.allreduce}
+    # candidates besides the policy's pick (already prepared): the xGMI two-shot from 3 ranks on (2 S / R bytes per
+    # link against the one-shot's S, one more round trip), RCCL
+    others = ((["xgmi2"] if R >= 3 and tr.allreduce_impl != "xgmi-2shot" else [])
+              + (["rccl"] if tr.allreduce_impl.startswith("xgmi") else []))
+    if tuning and others:
+        modes = {tr.allreduce_impl: a.allreduce if tr.allreduce_impl.startswith("xgmi") else "rccl"}
         tune[tr.allreduce_impl] = probe(tr, probe_plans)
         last = tr.allreduce_impl
-        for mode in (["xgmi2"] if R >= 3 and tr.allreduce_impl != "xgmi-2shot" else []) + ["rccl"]:
+        for mode in others:
             if tr is not None:
                 tr.close()  # (collective) every candidate starts from the initial weights, like every prepare
             try:
