@@ -71,8 +71,6 @@ def main(argv=None):
                 for o in opts:  # "+a<bits>": split3 operand forms (SplitStepArgs.a_fp32: bit0 fp32 W1, bit1 fp32 dZ1)
                     if o[:1] == "a" and o[1:].isdigit():
                         e._hip_step().a_fp32 = int(o[1:])
-                if "t1" in opts or "t0" in opts:  # wide split3 dW1: truncation split (MlpStep.split_trunc)
-                    e._hip_step().split_trunc = 1 if "t1" in opts else 0
                 if "w2" in opts or "w1" in opts:  # wide bf16 dW1 wave layout (MlpStep.rega_wc)
                     e._hip_step().rega_wc = 2 if "w2" in opts else 1
                 if "l0" in opts or "l1" in opts:  # (else the engine's default, MlpEngine.lazy_planes)

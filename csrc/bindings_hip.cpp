@@ -124,7 +124,6 @@ struct MlpStep {
     planes_stale = false;
   }
   int rega_wc = 1;    // SplitStepArgs::rega_wc (wide bf16 dW1 wave layout; 2 for A/B)
-  int split_trunc = 0;  // SplitStepArgs::split_trunc (wide split3 dW1: truncation split of fp32 dZ1)
   int poll_skip = 1;  // SplitStepArgs::poll_skip (hand-off polls re-load only missing granules; 0 for A/B)
   int u8_pairs = 1;  // SplitStepArgs::u8_pairs (the pixel operand's 16-byte chunk-pair loads; 0 for A/B)
   uintptr_t kpart = 0;  // split-K dW1 partial slabs (SplitStepArgs::kpart), kpart_cap floats; 0: no split-K
@@ -154,7 +153,6 @@ struct MlpStep {
     a.u8_pairs = u8_pairs;
     a.poll_skip = poll_skip;
     a.rega_wc = rega_wc;
-    a.split_trunc = split_trunc;
     a.kpart = P_<float>(kpart);
     a.kpart_cap = kpart_cap;
     // a timed-out all-gather forward + head launch (sticky word) makes every later update a no-op
@@ -483,7 +481,6 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("u8_pairs", &MlpStep::u8_pairs)
       .def_readwrite("poll_skip", &MlpStep::poll_skip)
       .def_readwrite("rega_wc", &MlpStep::rega_wc)
-      .def_readwrite("split_trunc", &MlpStep::split_trunc)
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
       .def_readwrite("planes_stale", &MlpStep::planes_stale)
       .def("refresh_planes", &MlpStep::refresh_planes, py::arg("stream"))

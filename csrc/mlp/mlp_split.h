@@ -103,8 +103,6 @@ struct SplitStepArgs {
   // wide bf16 (split1) layers: the A-in-registers dW1 launch's wave layout, 8 x 1 (1: each wave 16 rows x 128
   // columns) or 4 x 2 (2: 32 rows x 64 columns, half the B-fragment LDS reads; A rows loaded by two waves)
   int rega_wc = 1;
-  // wide split3 dW1 on the A-in-registers engine: split fp32 dZ1 by truncation (1) instead of round-to-nearest (0)
-  int split_trunc = 0;
   // The all-gather forward + head launches' timed-out-wait word (MlpEngine.ag_err).  The weight-gradient
   // launch reads it and, when set, APPLIES NOTHING: no SGD / plane refresh (sgd = 1), no xGMI exchange (the
   // fused all-reduce: this rank stops taking part, its peers time out), and the gradient status word below

@@ -1324,7 +1324,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
 // dW1 = dZ1 XT on the A-in-registers engine: dZ1 read as fp32 (AT = float; the head writes it instead of
 // the three bf16 planes: 4 B per element stored and loaded instead of 6) or as its one bf16 plane (split1),
 // with wgrad_glds_kernel's fused reg + SGD + plane-refresh epilogue; the dW2 / db2 roles ride along
-template <typename AT, int WC, int NKS, int APL = 1, bool TRUNC = false>
+template <typename AT, int WC, int NKS, int APL = 1>
 __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {
@@ -1348,9 +1348,8 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
   f32x4 acc[MB][NB];
   // fp32 dZ1 split in registers (AT = float), or its stored planes (bf16: one, APL = 3: three)
   const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
-  rega_gemm_mainloop<AT, 128, WC, NKS, 0, APL, TRUNC>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M,
-                                                      P + a.bias_col, a.n, m0, n0, lds_dyn, acc,
-                                                      APL == 3 ? a.H * a.ld * 2 : 0);
+  rega_gemm_mainloop<AT, 128, WC, NKS, 0, APL>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col,
+                                               a.n, m0, n0, lds_dyn, acc, APL == 3 ? a.H * a.ld * 2 : 0);
   wc1.stage(lds_dyn, acc, rw, cw, m0, n0, fg, fr);
   // the W1 planes (npw == npz); split3 w1_planes_lazy: none (the 128 x 128 forward reads fp32 W1)
   wc1.apply(a, lds_dyn, m0, n0, M, a.sgd && !poisoned(perr), (NP == 3 && a.w1_planes_lazy) ? 0 : NP);
@@ -1458,11 +1457,6 @@ void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) 
   if constexpr (sizeof(AT) == 2 && APL == 1) if (a.rega_wc == 2) {  // (split1 only: for split3 the 4 x 2 layout splits every A value twice)
     set_lds_limit<wgrad_rega_kernel<AT, 2, NKS>>(L);
     wgrad_rega_kernel<AT, 2, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
-    return;
-  }
-  if constexpr (sizeof(AT) == 4) if (a.split_trunc) {  // (A/B: the truncation split of fp32 dZ1)
-    set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS, APL, true>>(L);
-    wgrad_rega_kernel<AT, kRegaWC, NKS, APL, true><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
     return;
   }
   set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS, APL>>(L);

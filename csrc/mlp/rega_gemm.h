@@ -83,21 +83,6 @@ __device__ __forceinline__ void split3(const u32x4& w0, const u32x4& w1, bf16x8_
   }
 }
 
-// the same three exact planes by TRUNCATION (mma_tile.h split_trunc: an AND and a SUB per plane, the packing takes
-// the upper halves): fewer VALU than the round-to-nearest split, equally exact (hi + mid + lo == x), but other plane
-// values -- so only where nothing has to match stored round-to-nearest planes bit for bit (the dW1 launch's dZ1)
-__device__ __forceinline__ void split3_trunc(const u32x4& w0, const u32x4& w1, bf16x8_t& hi, bf16x8_t& mid,
-                                             bf16x8_t& lo) {
-  float x[8];
-  __builtin_memcpy(x, &w0, 16);
-  __builtin_memcpy(x + 4, &w1, 16);
-  __hip_bfloat16 p[3][8];
-  split_trunc<3, 8>(x, p);
-  __builtin_memcpy(&hi, p[0], 16);
-  __builtin_memcpy(&mid, p[1], 16);
-  __builtin_memcpy(&lo, p[2], 16);
-}
-
 }  // namespace ra
 
 // 8 waves as WR (rows) x WC (columns): wave (wr, wc) owns rows m0 + wr * 16 * MB + [0, 16 * MB) and
@@ -122,8 +107,7 @@ struct RegaGeom {
 // 2 = no loads after the prologue (the MFMAs run on whatever the ring holds)
 // APL = 3 (AT = bf16): A is three stored exact bf16 planes `aplane` bytes apart (the split made once by their
 // writer instead of by every column tile's waves: 6 B per element pulled instead of 4, no split VALU)
-// TRUNC (fp32 A): split by truncation (ra::split3_trunc) instead of round-to-nearest
-template <typename AT, int BN, int WC = 1, int NKS = 0, int ABLATE = 0, int APL = 1, bool TRUNC = false>
+template <typename AT, int BN, int WC = 1, int NKS = 0, int ABLATE = 0, int APL = 1>
 __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int lda,
                                                    const __hip_bfloat16* __restrict__ B, int ldb, int M, int N,
                                                    int K, int m0, int n0, char* __restrict__ lds,
@@ -205,8 +189,7 @@ __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       if constexpr (F32) {
-        if constexpr (TRUNC) split3_trunc(fa.v[2 * mb], fa.v[2 * mb + 1], F.a[mb][0], F.a[mb][1], F.a[mb][2]);
-        else split3(fa.v[2 * mb], fa.v[2 * mb + 1], F.a[mb][0], F.a[mb][1], F.a[mb][2]);
+        split3(fa.v[2 * mb], fa.v[2 * mb + 1], F.a[mb][0], F.a[mb][1], F.a[mb][2]);
       } else {
 #pragma unroll
         for (int p = 0; p < APL; ++p) __builtin_memcpy(&F.a[mb][p], &fa.v[APL * mb + p], 16);
