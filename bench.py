@@ -18,12 +18,22 @@ does) on every rank, gradient all-reduce (xGMI peer kernel with the SGD
 fused in, or RCCL with ``--allreduce rccl``), SGD update -- on
 synthetic MNIST-shaped images resident on every GPU.  Nothing is skipped
 inside the timed region.  Steps cycle over the full batches of the 54,000-image
-training split and are replayed from a captured HIP graph.
+training split.
 
-Scaling (default ``weak``): every GPU processes 800 images per step, so the
-global batch is 800*N (N=8 -> 6400, the BASELINE's 8-GPU batch); at N=1 this
-is exactly batch=800.  ``--scaling strong`` instead splits a global batch of
-800 across the N ranks (n = 800/N each), the reference's ``-b 800`` semantics.
+Scaling (default ``strong``: the metric's own config).  A global batch of 800
+is split over the N ranks, n = 800/N columns each -- the reference's ``-b 800``
+run (fpcode/run.sh:39, ``in_proc = min(batch, N - start) / num_procs``,
+fpcode/neural_network.cpp:458); ``value`` is that run's images/s.  At N > 1 the
+record also carries the weak-scaling run (800 images per GPU per step, global
+batch 800*N) as the labelled secondary ``weak`` sub-record (``--secondary off``
+skips it).  ``--scaling weak`` swaps the two.  At N = 1 both are batch 800.
+
+N > 1 choices made by measurement on the node, inside a wall-time budget
+(``--tune-budget-s``): the gradient all-reduce (the cost model's xGMI pick, the
+two-shot, RCCL) and, for the wide configs (H >= 512), data vs tensor parallel.
+Every probe's us/step is in the record next to the cost model's predicted
+all-reduce time (``allreduce_pred_us``); candidates the budget did not reach are
+recorded as ``"skipped: budget"``.
 """
 from __future__ import annotations
 
@@ -35,6 +45,9 @@ import time
 
 METRIC = "MNIST images/sec, 784-100-10 MLP batch=800 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # BASELINE.json "published": {} -- no reference number exists
+DATA = "synthetic (MNIST-shaped 784-dim uint8 images, random-init weights)"
+DTYPES = {"f32": "fp32", "f64": "fp64", "bf16": "bf16"}
+LR, REG = 1e-3, 1e-4  # reference defaults (fpcode/main.cpp:58-60)
 
 
 def parse(argv=None):
@@ -45,7 +58,11 @@ def parse(argv=None):
     ap.add_argument("--hidden", type=int, default=100)
     ap.add_argument("--batch", type=int, default=800, help="global batch (strong) or per-GPU batch (weak)")
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
-    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"])
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default, the metric's config): --batch is the global batch, split over the "
+                         "ranks; weak: --batch images per GPU")
+    ap.add_argument("--secondary", default="auto", choices=["auto", "off"],
+                    help="auto: with N > 1 also time the other scaling mode into a labelled sub-record")
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--executor", default="auto", choices=["auto", "graph", "eager"],
@@ -54,233 +71,235 @@ def parse(argv=None):
     ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "xgmi2", "rccl", "host"],
                     help="gradient sync for N>1: auto (by bucket size and ranks), the xGMI one-shot peer kernel "
                          "with fused SGD (xgmi), the xGMI two-shot kernel with sharded SGD (xgmi2), RCCL, or "
-                         "host-staged gloo (reference-equivalent)")
+                         "host-staged gloo (reference-equivalent).  Tensor parallel maps it onto its z2 "
+                         "all-reduce (tensor_parallel.tp_allreduce_mode: xgmi2 -> xgmi, host -> rccl)")
     ap.add_argument("--grad-wire", default="auto", choices=["auto", "f32", "bf16"],
                     help="element type of the gradients on the xGMI one-shot wire (bf16: opt-in, half the bytes)")
     ap.add_argument("--mode", default="optimized", choices=["optimized", "reference"],
                     help="reference: the reference's execution model on MI355X -- unfused PyTorch/hipBLAS ops, "
                          "no graphs, host-staged gradient all-reduce (for comparison only)")
-    ap.add_argument("--parallel", default="dp", choices=["dp", "tp"],
+    ap.add_argument("--parallel", default="auto", choices=["auto", "dp", "tp"],
                     help="dp: data parallel (the reference's scheme); tp: hidden-dimension tensor parallel "
-                         "(one z2 all-reduce per step, every rank runs the whole global batch --batch; strong "
-                         "scaling of a fixed model, meant for the wide configs)")
+                         "(one z2 all-reduce per step, every rank runs the whole global batch); auto: dp, except "
+                         "for the wide layers (H >= 512) at N > 1, where both are probed and the faster is timed")
     ap.add_argument("--tune-allreduce", default="on", choices=["on", "off"],
-                    help="N > 1 with --allreduce auto: time the policy's xGMI pick, the xGMI two-shot (N >= 3) and RCCL "
-                         "for --tune-steps steps each before the timed region and run the fastest (the record lists "
-                         "every candidate)")
+                    help="N > 1 with --allreduce auto: time the policy's xGMI pick, the xGMI two-shot (N >= 3) and "
+                         "RCCL for --tune-steps steps each before the timed region and run the fastest (the record "
+                         "lists every candidate)")
     ap.add_argument("--tune-steps", type=int, default=100)
+    ap.add_argument("--tune-budget-s", type=float, default=90.0,
+                    help="wall-time cap on all probing (all-reduce and parallelism candidates); candidates past it "
+                         "are recorded as 'skipped: budget'")
     ap.add_argument("--train-size", type=int, default=54000)
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
 
-def main(argv=None) -> int:
-    argv = sys.argv[1:] if argv is None else list(argv)
-    a = parse(argv)
-    if a.mode == "reference":
-        a.backend, a.no_graphs, a.allreduce = "torch", True, "host"
-    from cme213_sp18_amd.parallel.launcher import PlacementError, self_launch
+class Ctx:
+    """What every measurement shares: arguments, communicator, device, data, the probe budget."""
 
-    # --gpus N without a launcher: start the N ranks here (a child torch.distributed.run, before any GPU
-    # call in this process) and pass their exit code through; rank 0 of the child job prints the record
-    try:
-        rc = self_launch(a.gpus, argv, script=os.path.abspath(__file__), need_gpus=a.backend == "hip")
-    except PlacementError as ex:
-        print(f"error: {ex}; no record", file=sys.stderr, flush=True)
-        return 2
-    if rc is not None:
-        return rc
+    def __init__(self, a, comm, device, placement):
+        import torch
 
-    import numpy as np
-    import torch
+        from cme213_sp18_amd.utils.data import synthetic_mnist
 
-    from cme213_sp18_amd.models.mlp import NeuralNetwork
-    from cme213_sp18_amd.parallel.launcher import init_distributed, shutdown, verify_placement
-    from cme213_sp18_amd.parallel.trainer import DataParallelTrainer, EpochPlan
-    from cme213_sp18_amd.utils.data import synthetic_mnist
+        self.a, self.comm, self.device, self.placement = a, comm, device, placement
+        self.R, self.rank = comm.world_size, comm.rank
+        self.sync = (lambda: torch.cuda.synchronize(device)) if device.type == "cuda" else (lambda: None)
+        self.x, self.y = synthetic_mnist(a.train_size, seed=0)  # identical on every rank, no broadcast
+        self.t_budget0 = time.perf_counter()
 
-    comm, device = init_distributed()
-    R, rank = comm.world_size, comm.rank
-    try:  # the job must be exactly --gpus ranks on --gpus distinct GPUs, or it measures nothing
-        placement = verify_placement(comm, device, a.gpus)
-    except PlacementError as ex:
-        print(f"[rank {rank}] error: {ex}; no record", file=sys.stderr, flush=True)
-        shutdown()
-        return 2
-    sync = (lambda: torch.cuda.synchronize(device)) if device.type == "cuda" else (lambda: None)
-    if a.parallel == "tp":
-        return run_tp(a, comm, device, placement, sync)
-    global_batch = a.batch * R if a.scaling == "weak" else a.batch
+    def budget_left(self) -> bool:
+        """Collective: True while probing may go on (every rank gets the same answer)."""
+        el = self.comm.allreduce_scalar(time.perf_counter() - self.t_budget0, op="max")
+        return el < self.a.tune_budget_s
 
-    x, y = synthetic_mnist(a.train_size, seed=0)  # identical on every rank, no broadcast
-    nn = NeuralNetwork([784, a.hidden, 10])
-    lr, reg = 1e-3, 1e-4  # reference defaults (fpcode/main.cpp:58-60)
+    def barrier_sync(self):
+        self.sync()
+        self.comm.barrier()
+        self.sync()
 
-    def prepare(allreduce: str, probe_steps: int = 0):
-        """Trainer + captured graphs + W warm-up steps.  Returns (trainer, timed plans, probe plans)."""
-        tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=global_batch,
-                                 backend=a.backend, use_graphs=not a.no_graphs, allreduce=allreduce,
-                                 grad_wire=a.grad_wire,
-                                 executor="eager" if a.no_graphs else a.executor)
-        tr.load(x, y)
-        full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == global_batch]
-        if not full:
-            raise SystemExit("training split smaller than one global batch")
 
-        def plans_for(k: int):
-            out, i = [], 0
-            while i < k:
-                m = min(len(full), k - i)
-                out.append(EpochPlan(full[:m]))
-                i += m
-            return out
+def plans_for(full, k: int):
+    from cme213_sp18_amd.parallel.trainer import EpochPlan
 
-        warm_plans, timed_plans, probe_plans = plans_for(a.warmup), plans_for(a.steps), plans_for(probe_steps)
-        native = all(tr.native_plan(p) is not None for p in warm_plans + timed_plans + probe_plans)
-        if tr.use_graphs and not native:  # capture outside the timed region (graphs are cached by plan)
-            try:
-                for p in {tuple(p.steps): p for p in warm_plans + timed_plans + probe_plans}.values():
-                    tr.capture(p, lr, reg)
-            except Exception as ex:  # pragma: no cover - depends on the collective backend
-                print(f"warning: HIP graph capture failed ({ex!r}); running eager steps", file=sys.stderr)
-                tr.use_graphs = False
-                tr._graphs.clear()
-        # every rank done capturing before the first warm-up step: with the xGMI all-reduce a step waits
-        # (bounded) for its peers' same step, so a rank still capturing would count against that bound
-        sync()
-        comm.barrier()
-        for p in warm_plans:
-            tr.run_plan(p, lr, reg)
-        return tr, timed_plans, probe_plans
+    out, i = [], 0
+    while i < k:
+        m = min(len(full), k - i)
+        out.append(EpochPlan(full[:m]))
+        i += m
+    return out
 
-    def probe(tr, plans) -> float:
-        """us/step of the probe plans on this trainer, max over ranks (inf if an xGMI wait timed out or the
-        replicas diverged): the same runners and bracketing as the timed region."""
-        runners = [tr.plan_runner(p, lr, reg) for p in plans]
-        sync()
-        comm.barrier()
-        sync()
-        t = time.perf_counter()
-        for run in runners:
-            run()
-        sync()
-        comm.barrier()
-        sync()
-        us = comm.allreduce_scalar(1e6 * (time.perf_counter() - t) / a.tune_steps, op="max")
-        bad = tr.comm_failed()
-        bad = bad or not tr.replicas_agree()
-        return float("inf") if bad else round(us, 3)
 
-    # --tune-allreduce: with N > 1 and --allreduce auto, the gradient sync is CHOSEN BY MEASUREMENT on this
-    # node before anything is timed -- the policy's xGMI pick (cost model, docs/PERFORMANCE.md), the two-shot
-    # (N >= 3) and RCCL each run --tune-steps steps, the fastest (max over ranks, agreed by every rank) runs
-    # the timed region
-    tuning = R > 1 and a.allreduce == "auto" and a.backend == "hip" and a.tune_allreduce == "on"
-    tune = {}
-    tr, timed_plans, probe_plans = prepare(a.allreduce, a.tune_steps if tuning else 0)
-    sync()
-    comm.barrier()
-    if tr.allreduce_impl.startswith("xgmi") and a.allreduce == "auto":
-        # a bounded peer wait that timed out during the warm-up (the xGMI protocol misbehaving on this
-        # node) -> every rank drops to RCCL together, from the initial weights, before anything is timed
-        forced = os.environ.get("CME_BENCH_TEST_FALLBACK") == "1"  # test hook: take the fallback
-        failed = tr.comm_failed()
-        diverged = not failed and not tr.replicas_agree()  # a stale peer read would show up here
-        if failed or diverged or comm.allreduce_scalar(float(forced), op="max") > 0:
-            if rank == 0:
-                why = "replicas diverged" if diverged else "peer wait timed out" if failed else "forced"
-                print(f"warning: xGMI all-reduce failed in warm-up ({why}); re-running on RCCL", file=sys.stderr)
-            tr.close()
-            tr, timed_plans, probe_plans = prepare("rccl", a.tune_steps if tuning else 0)
-            tune["xgmi"] = "failed in warm-up"
-    # candidates besides the policy's pick (already prepared): the xGMI two-shot from 3 ranks on (2 S / R bytes per
-    # link against the one-shot's S, one more round trip), RCCL
-    others = ((["xgmi2"] if R >= 3 and tr.allreduce_impl != "xgmi-2shot" else [])
-              + (["rccl"] if tr.allreduce_impl.startswith("xgmi") else []))
-    if tuning and others:
-        modes = {tr.allreduce_impl: a.allreduce if tr.allreduce_impl.startswith("xgmi") else "rccl"}
-        tune[tr.allreduce_impl] = probe(tr, probe_plans)
-        last = tr.allreduce_impl
-        for mode in others:
-            if tr is not None:
-                tr.close()  # (collective) every candidate starts from the initial weights, like every prepare
-            try:
-                tr, timed_plans, probe_plans = prepare(mode, a.tune_steps)
-            except Exception as ex:  # noqa: BLE001 - a candidate the node cannot run (raised on every rank)
-                tr, last = None, None
-                tune[mode] = "unavailable"
-                if rank == 0:
-                    print(f"allreduce candidate {mode} unavailable: {ex}", file=sys.stderr, flush=True)
-                continue
-            modes[tr.allreduce_impl] = mode
-            tune[tr.allreduce_impl] = probe(tr, probe_plans)
-            last = tr.allreduce_impl
-        nums = {k: v for k, v in tune.items() if isinstance(v, float)}
-        best = min(nums, key=lambda k: (nums[k], k))  # identical floats on every rank: one decision
-        if best != last:
-            if tr is not None:
-                tr.close()
-            tr, timed_plans, _ = prepare(modes[best])  # (a failure from here on invalidates the record below)
-        tune = {k: (v if v != float("inf") else "failed") for k, v in tune.items()}
-        if rank == 0:
-            print(f"allreduce tuned on this node: {tune} -> {tr.allreduce_impl}", file=sys.stderr, flush=True)
-    native_exec = all(tr.native_plan(p) is not None for p in timed_plans)
-    runners = [tr.plan_runner(p, lr, reg) for p in timed_plans]  # resolved before the clock starts
-    sync()
-    comm.barrier()
-    sync()
+def timed(ctx, runners) -> float:
+    """Seconds for the runners, bracketed by barrier + synchronize on both sides, max over ranks."""
+    ctx.barrier_sync()
     t0 = time.perf_counter()
     for run in runners:
         run()
-    sync()
-    comm.barrier()
-    if R > 1:  # an RCCL barrier is GPU work; one process has nothing left to wait for
-        sync()
-    dt = time.perf_counter() - t0
-    dt = comm.allreduce_scalar(dt, op="max")
+    ctx.sync()
+    ctx.comm.barrier()
+    if ctx.R > 1:  # an RCCL barrier is GPU work; one process has nothing left to wait for
+        ctx.sync()
+    return ctx.comm.allreduce_scalar(time.perf_counter() - t0, op="max")
 
-    # sanity, agreed by every rank: parameters finite everywhere and no xGMI peer wait timed out anywhere;
-    # otherwise the record is marked invalid and every rank exits non-zero
+
+# ------------------------------------------------------------------------------------------ data parallel
+def dp_prepare(ctx, global_batch: int, allreduce: str, warmup: int, extra_plans: int = 0):
+    """Trainer + captured graphs + ``warmup`` warm-up steps.  Returns (trainer, full-batch list)."""
+    from cme213_sp18_amd.models.mlp import NeuralNetwork
+    from cme213_sp18_amd.parallel.trainer import DataParallelTrainer
+
+    a = ctx.a
+    nn = NeuralNetwork([784, a.hidden, 10])
+    tr = DataParallelTrainer(nn, comm=ctx.comm, device=ctx.device, dtype=a.dtype, batch_size=global_batch,
+                             backend=a.backend, use_graphs=not a.no_graphs, allreduce=allreduce,
+                             grad_wire=a.grad_wire, executor="eager" if a.no_graphs else a.executor)
+    tr.load(ctx.x, ctx.y)
+    full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == global_batch]
+    if not full:
+        raise SystemExit("training split smaller than one global batch")
+    warm = plans_for(full, warmup)
+    every = warm + plans_for(full, a.steps) + plans_for(full, extra_plans)
+    native = all(tr.native_plan(p) is not None for p in every)
+    if tr.use_graphs and not native:  # capture outside the timed region (graphs are cached by plan)
+        try:
+            for p in {tuple(p.steps): p for p in every}.values():
+                tr.capture(p, LR, REG)
+        except Exception as ex:  # pragma: no cover - depends on the collective backend
+            print(f"warning: HIP graph capture failed ({ex!r}); running eager steps", file=sys.stderr)
+            tr.use_graphs = False
+            tr._graphs.clear()
+    # every rank done capturing before the first warm-up step: with the xGMI all-reduce a step waits
+    # (bounded) for its peers' same step, so a rank still capturing would count against that bound
+    ctx.sync()
+    ctx.comm.barrier()
+    for p in warm:
+        tr.run_plan(p, LR, REG)
+    return tr, full
+
+
+def dp_healthy(tr) -> bool:
+    """Collective: no xGMI wait timed out and the replicas agree bitwise."""
+    return not tr.comm_failed() and tr.replicas_agree()
+
+
+def dp_probe(ctx, tr, full, steps: int) -> float:
+    """us/step of ``steps`` steps on this trainer, max over ranks (inf if a wait timed out or replicas differ)."""
+    runners = [tr.plan_runner(p, LR, REG) for p in plans_for(full, steps)]
+    us = 1e6 * timed(ctx, runners) / steps
+    return round(us, 3) if dp_healthy(tr) else float("inf")
+
+
+def dp_tune_allreduce(ctx, global_batch: int, tune: dict) -> str:
+    """The gradient sync mode to time (an --allreduce value), chosen by measurement when N > 1 and
+    --allreduce auto: the cost model's pick, the xGMI two-shot (N >= 3) and RCCL each run --tune-steps steps
+    from the initial weights (the fastest wins; identical floats on every rank: one decision).  Results go into
+    ``tune`` (impl name -> us/step, 'failed', 'unavailable' or 'skipped: budget')."""
+    a = ctx.a
+    if not (ctx.R > 1 and a.allreduce == "auto" and a.backend == "hip" and a.tune_allreduce == "on"):
+        return a.allreduce
+    # the policy's own pick first (its trainer tells which implementation "auto" resolves to)
+    tr, full = dp_prepare(ctx, global_batch, "auto", a.warmup, a.tune_steps)
+    pick = tr.allreduce_impl
+    modes = {pick: "auto"}
+    if pick.startswith("xgmi") and (tr.comm_failed() or not tr.replicas_agree()):
+        # a bounded peer wait timed out (or a stale read) during the warm-up: the xGMI protocol misbehaves on
+        # this node -- every rank drops it together
+        tune[pick] = "failed in warm-up"
+    else:
+        tune[pick] = dp_probe(ctx, tr, full, a.tune_steps)
+    tr.close()
+    others = (["xgmi2"] if ctx.R >= 3 and pick != "xgmi-2shot" else []) + (["rccl"] if pick.startswith("xgmi") else [])
+    for mode in others:
+        if not ctx.budget_left():
+            tune[{"xgmi2": "xgmi-2shot", "rccl": ctx.comm.name}[mode]] = "skipped: budget"
+            continue
+        try:
+            tr, full = dp_prepare(ctx, global_batch, mode, a.warmup, a.tune_steps)
+        except Exception as ex:  # noqa: BLE001 - a candidate the node cannot run (raised on every rank)
+            tune[mode] = "unavailable"
+            if ctx.rank == 0:
+                print(f"allreduce candidate {mode} unavailable: {ex}", file=sys.stderr, flush=True)
+            continue
+        modes[tr.allreduce_impl] = mode
+        tune[tr.allreduce_impl] = dp_probe(ctx, tr, full, a.tune_steps)
+        tr.close()
+    nums = {k: v for k, v in tune.items() if isinstance(v, float) and v != float("inf")}
+    for k, v in list(tune.items()):
+        if v == float("inf"):
+            tune[k] = "failed"
+    if not nums:
+        return "rccl"
+    best = min(nums, key=lambda k: (nums[k], k))
+    if ctx.rank == 0:
+        print(f"allreduce tuned on this node: {tune} -> {best}", file=sys.stderr, flush=True)
+    return modes[best]
+
+
+def run_dp(ctx, global_batch: int, allreduce: str | None = None, tune: dict | None = None) -> dict:
+    """One data-parallel measurement: K timed steps of global batch ``global_batch`` (n = global_batch / R per
+    rank).  The trainer is always prepared afresh for the timed region (from the initial weights, after W
+    warm-up steps), whichever candidate won the tuning."""
+    from cme213_sp18_amd.parallel.trainer import allreduce_cost_us
+
+    a = ctx.a
+    tune = {} if tune is None else tune
+    mode = allreduce if allreduce is not None else dp_tune_allreduce(ctx, global_batch, tune)
+    tr, full = dp_prepare(ctx, global_batch, mode, a.warmup)
+    if tr.allreduce_impl.startswith("xgmi") and mode in ("auto",) and not dp_healthy(tr):
+        # a bounded peer wait timed out during the warm-up: every rank drops to RCCL together, from the
+        # initial weights, before anything is timed
+        if ctx.rank == 0:
+            print("warning: xGMI all-reduce failed in warm-up; re-running on RCCL", file=sys.stderr)
+        tr.close()
+        tune["xgmi"] = "failed in warm-up"
+        tr, full = dp_prepare(ctx, global_batch, "rccl", a.warmup)
+    forced = os.environ.get("CME_BENCH_TEST_FALLBACK") == "1" and a.allreduce == "auto"
+    if ctx.comm.allreduce_scalar(float(forced), op="max") > 0 and tr.allreduce_impl.startswith("xgmi"):
+        # test hook: take the fallback as if the warm-up had failed
+        tr.close()
+        tune["xgmi"] = "failed in warm-up"
+        tr, full = dp_prepare(ctx, global_batch, "rccl", a.warmup)
+    timed_plans = plans_for(full, a.steps)
+    native_exec = all(tr.native_plan(p) is not None for p in timed_plans)
+    runners = [tr.plan_runner(p, LR, REG) for p in timed_plans]  # resolved before the clock starts
+    dt = timed(ctx, runners)
+    res = _dp_checks(ctx, tr)
+    ar = measure_allreduce(tr, ctx.comm, ctx.sync) if res["ok"] else {}
+    e = tr.engine
+    wire = e.params.numel() * (2 if tr.xgmi is not None and tr.xgmi.wire != e.params.dtype else e.params.element_size())
+    shots = 0 if tr.xgmi is None else tr.xgmi.shots
+    # strong scaling drops the remainder columns when R does not divide the batch (trainer.shard)
+    images = a.steps * (global_batch // ctx.R) * ctx.R
+    res.update(dt=dt, images=images, global_batch=global_batch, per_gpu_batch=global_batch // ctx.R,
+               parallelism=f"dp{ctx.R}",
+               config={"hip_graphs": tr.use_graphs and not native_exec,
+                       "executor": "native" if native_exec else ("graph" if tr.use_graphs else "eager"),
+                       "allreduce": tr.allreduce_impl, **ar,
+                       "allreduce_pred_us": round(allreduce_cost_us(ctx.R, wire, shots), 2) if ctx.R > 1 else None,
+                       "allreduce_tuning_us_per_step": tune or None})
+    tr.close()
+    return res
+
+
+def _dp_checks(ctx, tr) -> dict:
+    """Sanity, agreed by every rank: parameters finite everywhere, no xGMI peer wait or in-launch hand-off
+    timed out anywhere, replicas bitwise equal; otherwise the record is marked invalid."""
+    import torch
+
+    comm = ctx.comm
     finite = bool(torch.isfinite(tr.engine.params).all().item())
     bad = comm.allreduce_scalar(0.0 if finite else 1.0, op="max") > 0
     comm_failed = tr.comm_failed()
     kerr = comm.allreduce_scalar(1.0 if tr.engine.kernel_error() else 0.0, op="max") > 0
     agree = tr.replicas_agree()
     ok = not bad and not comm_failed and not kerr and agree
-    ar = measure_allreduce(tr, comm, sync) if ok else {}
-    # strong scaling drops the remainder columns when R does not divide the batch (trainer.shard)
-    images = a.steps * (global_batch // R) * R
-    value = images / dt
-    if rank == 0:
-        rec = {
-            "metric": METRIC,
-            "value": round(value, 1),
-            "unit": "images/s",
-            "n_gpus": R,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(1e3 * dt / a.steps, 6),
-            "higher_is_better": True,
-            "scaling": a.scaling,
-            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": {"f32": "fp32", "f64": "fp64", "bf16": "bf16"}[a.dtype],
-            "data": "synthetic (MNIST-shaped 784-dim uint8 images, random-init weights)",
-            "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": global_batch, "seq_len": None,
-                       "parallelism": f"dp{R}", "per_gpu_batch": global_batch // R, "backend": a.backend,
-                       "mode": a.mode,
-                       "hip_graphs": tr.use_graphs and not native_exec,
-                       "executor": "native" if native_exec else ("graph" if tr.use_graphs else "eager"),
-                       "allreduce": tr.allreduce_impl, "params_finite": not bad,
-                       "comm_ok": not comm_failed, "replicas_bitwise_equal": agree, **placement, **ar,
-                       "allreduce_tuning_us_per_step": tune or None},
-        }
-        if not ok:
-            rec["invalid"] = ("non-finite parameters" if bad else "an xGMI peer wait timed out" if comm_failed
-                              else "a forward+head workgroup wait timed out" if kerr
-                              else "replicas diverged across ranks")
-        print(json.dumps(rec), flush=True)
-    shutdown()
-    return 0 if ok else 1
+    out = {"ok": ok, "checks": {"params_finite": not bad, "comm_ok": not comm_failed, "replicas_bitwise_equal": agree}}
+    if not ok:
+        out["invalid"] = ("non-finite parameters" if bad else "an xGMI peer wait timed out" if comm_failed
+                          else "a forward+head workgroup wait timed out" if kerr else "replicas diverged across ranks")
+    return out
 
 
 def measure_allreduce(tr, comm, sync, iters: int = 20) -> dict:
@@ -322,53 +341,35 @@ def measure_allreduce(tr, comm, sync, iters: int = 20) -> dict:
             "allreduce_busbw_GBps": round(2 * (R - 1) / R * nbytes / (us * 1e-6) / 1e9, 2)}
 
 
-def run_tp(a, comm, device, placement, sync) -> int:
-    """Hidden-sharded tensor-parallel step (parallel/tensor_parallel.py): fixed model and global batch
-    (strong scaling), K timed steps bracketed by barrier + synchronize, max over ranks."""
+# ---------------------------------------------------------------------------------------- tensor parallel
+def run_tp(ctx, B: int, steps: int | None = None) -> dict:
+    """Hidden-sharded tensor-parallel step (parallel/tensor_parallel.py): every rank runs the whole global
+    batch B on its H / R hidden units; ``steps`` timed steps (default --steps) bracketed like the DP run."""
     import torch
 
     from cme213_sp18_amd.models.mlp import NeuralNetwork
-    from cme213_sp18_amd.parallel.launcher import shutdown
-    from cme213_sp18_amd.parallel.tensor_parallel import TensorParallelTrainer
-    from cme213_sp18_amd.parallel.trainer import EpochPlan
-    from cme213_sp18_amd.utils.data import synthetic_mnist
+    from cme213_sp18_amd.parallel.tensor_parallel import TensorParallelTrainer, tp_allreduce_mode
+    from cme213_sp18_amd.parallel.trainer import allreduce_cost_us
 
-    R, rank = comm.world_size, comm.rank
-    B = a.batch
-    x, y = synthetic_mnist(a.train_size, seed=0)
+    a, comm, R = ctx.a, ctx.comm, ctx.R
+    steps = a.steps if steps is None else steps
     nn = NeuralNetwork([784, a.hidden, 10])
-    tr = TensorParallelTrainer(nn, comm=comm, device=device, dtype=a.dtype, batch_size=B, backend=a.backend,
-                               allreduce="rccl" if a.allreduce in ("rccl", "host") else a.allreduce)
-    tr.load(x, y)
+    tr = TensorParallelTrainer(nn, comm=comm, device=ctx.device, dtype=a.dtype, batch_size=B, backend=a.backend,
+                               allreduce=tp_allreduce_mode(a.allreduce))
+    tr.load(ctx.x, ctx.y)
     full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == B]
-    lr, reg = 1e-3, 1e-4
-
-    def plans_for(k):
-        out, i = [], 0
-        while i < k:
-            m = min(len(full), k - i)
-            out.append(EpochPlan(full[:m]))
-            i += m
-        return out
-
-    warm, timed = plans_for(a.warmup), plans_for(a.steps)
+    if not full:
+        raise SystemExit("training split smaller than one global batch")
+    warm, tplans = plans_for(full, a.warmup), plans_for(full, steps)
     graphs = tr.graphs_usable(not a.no_graphs)
     if graphs:  # every distinct plan captured outside the timed region
-        for p in {tuple(p.steps): p for p in warm + timed}.values():
-            tr.capture(p, lr, reg)
+        for p in {tuple(p.steps): p for p in warm + tplans}.values():
+            tr.capture(p, LR, REG)
     for p in warm:
-        tr.run_plan(p, lr, reg, use_graphs=graphs)
-    sync()
-    comm.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for p in timed:
-        tr.run_plan(p, lr, reg, use_graphs=graphs)
-    sync()
-    comm.barrier()
-    sync()
-    dt = comm.allreduce_scalar(time.perf_counter() - t0, op="max")
-    ok = comm.allreduce_scalar(0.0 if bool(torch.isfinite(tr.engine.params).all().item()) else 1.0, op="max") == 0
+        tr.run_plan(p, LR, REG, use_graphs=graphs)
+    dt = timed(ctx, [lambda p=p: tr.run_plan(p, LR, REG, use_graphs=graphs) for p in tplans])
+    finite = bool(torch.isfinite(tr.engine.params).all().item())
+    ok = comm.allreduce_scalar(0.0 if finite else 1.0, op="max") == 0
     comm_failed = tr.comm_failed()
     ok = ok and not comm_failed
     ar = {"allreduce_us": None}
@@ -376,29 +377,152 @@ def run_tp(a, comm, device, placement, sync) -> int:
         fn = (lambda: tr._xz.allreduce_(tr.z2)) if tr._xz is not None else (lambda: comm.allreduce_(tr.z2))
         for _ in range(3):
             fn()
-        sync()
-        comm.barrier()
-        sync()
+        ctx.barrier_sync()
         t1 = time.perf_counter()
         for _ in range(20):
             fn()
-        sync()
+        ctx.sync()
         us = comm.allreduce_scalar(1e6 * (time.perf_counter() - t1) / 20, op="max")
         ar = {"allreduce_us": round(us, 2), "allreduce_bytes": int(tr.z2.numel() * 4)}
+    impl = tr.allreduce_impl
     tr.close()
-    value = a.steps * B / dt
-    if rank == 0:
-        print(json.dumps({
-            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": R, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(1e3 * dt / a.steps, 6), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None,
-            "dtype": {"f32": "fp32", "f64": "fp64", "bf16": "bf16"}[a.dtype],
-            "data": "synthetic (MNIST-shaped 784-dim uint8 images, random-init weights)",
-            "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": B, "seq_len": None,
-                       "parallelism": f"tp{R}", "hidden_per_gpu": a.hidden // R, "backend": a.backend,
-                       "hip_graphs": graphs, "allreduce": tr.allreduce_impl, "params_finite": ok,
-                       "comm_ok": not comm_failed, **placement, **ar},
-        }), flush=True)
+    res = {"ok": ok, "dt": dt, "images": steps * B, "global_batch": B, "per_gpu_batch": B, "parallelism": f"tp{R}",
+           "checks": {"params_finite": finite, "comm_ok": not comm_failed},
+           "config": {"hidden_per_gpu": a.hidden // R, "hip_graphs": graphs, "allreduce": impl, **ar,
+                      "allreduce_pred_us": round(allreduce_cost_us(R, int(tr.z2.numel() * 4), 1 if "xgmi" in impl
+                                                                   else 0), 2) if R > 1 else None}}
+    if not ok:
+        res["invalid"] = "an xGMI peer wait timed out" if comm_failed else "non-finite parameters"
+    return res
+
+
+# --------------------------------------------------------------------------------------------- measuring
+def choose_parallel(ctx, gb_dp: int, gb_tp: int, ptune: dict) -> str:
+    """--parallel auto: dp, except for the wide layers at N > 1 on the hip backend, where DP (the all-reduce
+    policy's pick) and TP each run --tune-steps steps and the faster is timed (inside the probe budget)."""
+    a = ctx.a
+    if a.parallel != "auto":
+        return a.parallel
+    if not (ctx.R > 1 and a.hidden >= 512 and a.backend == "hip" and a.hidden % ctx.R == 0):
+        return "dp"
+    tp = run_tp(ctx, gb_tp, steps=a.tune_steps)
+    ptune[tp["parallelism"]] = round(1e6 * tp["dt"] / a.tune_steps, 3) if tp["ok"] else "failed"
+    if ctx.budget_left():
+        tr, full = dp_prepare(ctx, gb_dp, "auto", a.warmup, a.tune_steps)
+        ptune[f"dp{ctx.R}"] = dp_probe(ctx, tr, full, a.tune_steps)
+        if ptune[f"dp{ctx.R}"] == float("inf"):
+            ptune[f"dp{ctx.R}"] = "failed"
+        tr.close()
+    else:
+        ptune[f"dp{ctx.R}"] = "skipped: budget"
+    nums = {k: v for k, v in ptune.items() if isinstance(v, float)}
+    best = min(nums, key=lambda k: (nums[k], k)) if nums else f"dp{ctx.R}"
+    if ctx.rank == 0:
+        print(f"parallelism tuned on this node: {ptune} -> {best}", file=sys.stderr, flush=True)
+    return "tp" if best.startswith("tp") else "dp"
+
+
+def measure(ctx, scaling: str, parallel: str | None = None, allreduce: str | None = None) -> dict:
+    """One timed run of the given scaling mode.  Returns the run's summary (``parallel`` and the all-reduce mode
+    chosen, so a secondary run can reuse them instead of probing again)."""
+    a = ctx.a
+    gb = a.batch if scaling == "strong" else a.batch * ctx.R
+    ptune: dict = {}
+    if parallel is None:
+        parallel = choose_parallel(ctx, gb, gb, ptune)
+    if parallel == "tp":
+        res = run_tp(ctx, gb)
+    else:
+        tune: dict = {}
+        res = run_dp(ctx, gb, allreduce=allreduce, tune=tune)
+        res["allreduce_mode"] = allreduce if allreduce is not None else _mode_of(res["config"]["allreduce"], ctx)
+    res["parallel"] = parallel
+    res["scaling"] = scaling
+    if ptune:
+        res["config"]["parallel_tuning_us_per_step"] = ptune
+    return res
+
+
+def _mode_of(impl: str, ctx) -> str:
+    """The --allreduce value that reproduces an implementation name (for the secondary run)."""
+    if ctx.R == 1:
+        return "auto"
+    return {"xgmi": "xgmi", "xgmi-fused": "xgmi", "xgmi-2shot": "xgmi2", "xgmi-bf16wire": "xgmi",
+            "host-gloo": "host"}.get(impl, "rccl")
+
+
+def summary(ctx, res: dict) -> dict:
+    a = ctx.a
+    value = res["images"] / res["dt"]
+    return {"value": round(value, 1), "ms_per_step": round(1e3 * res["dt"] / a.steps, 6),
+            "global_batch": res["global_batch"], "per_gpu_batch": res["per_gpu_batch"],
+            "parallelism": res["parallelism"]}
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
+    a = parse(argv)
+    if a.mode == "reference":
+        a.backend, a.no_graphs, a.allreduce = "torch", True, "host"
+    from cme213_sp18_amd.parallel.launcher import PlacementError, self_launch
+
+    # --gpus N without a launcher: start the N ranks here (a child torch.distributed.run, before any GPU
+    # call in this process) and pass their exit code through; rank 0 of the child job prints the record
+    try:
+        rc = self_launch(a.gpus, argv, script=os.path.abspath(__file__), need_gpus=a.backend == "hip")
+    except PlacementError as ex:
+        print(f"error: {ex}; no record", file=sys.stderr, flush=True)
+        return 2
+    if rc is not None:
+        return rc
+
+    from cme213_sp18_amd.parallel.launcher import init_distributed, shutdown, verify_placement
+
+    comm, device = init_distributed()
+    try:  # the job must be exactly --gpus ranks on --gpus distinct GPUs, or it measures nothing
+        placement = verify_placement(comm, device, a.gpus)
+    except PlacementError as ex:
+        print(f"[rank {comm.rank}] error: {ex}; no record", file=sys.stderr, flush=True)
+        shutdown()
+        return 2
+    ctx = Ctx(a, comm, device, placement)
+    res = measure(ctx, a.scaling)
+    sec = None
+    if ctx.R > 1 and a.secondary == "auto":
+        other = "weak" if a.scaling == "strong" else "strong"
+        # the secondary reuses the primary's choices (same bucket bytes; no second round of probes)
+        sec = measure(ctx, other, parallel=res["parallel"], allreduce=res.get("allreduce_mode"))
+    ok = res["ok"] and (sec is None or sec["ok"])
+    if ctx.rank == 0:
+        s = summary(ctx, res)
+        rec = {
+            "metric": METRIC,
+            "value": s["value"],
+            "unit": "images/s",
+            "n_gpus": ctx.R,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": s["ms_per_step"],
+            "higher_is_better": True,
+            "scaling": a.scaling,
+            "vs_baseline": (s["value"] / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": DTYPES[a.dtype],
+            "data": DATA,
+            "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": s["global_batch"], "seq_len": None,
+                       "parallelism": s["parallelism"], "per_gpu_batch": s["per_gpu_batch"],
+                       "backend": a.backend, "mode": a.mode, **res["config"], **res["checks"], **ctx.placement},
+        }
+        if sec is not None:
+            ss = summary(ctx, sec)
+            rec[sec["scaling"]] = {"value": ss["value"], "unit": "images/s", "ms_per_step": ss["ms_per_step"],
+                                   "global_batch": ss["global_batch"], "per_gpu_batch": ss["per_gpu_batch"],
+                                   "parallelism": ss["parallelism"], "allreduce": sec["config"].get("allreduce"),
+                                   "allreduce_us": sec["config"].get("allreduce_us"),
+                                   "note": f"secondary: {sec['scaling']} scaling ({'800 images per GPU' if sec['scaling'] == 'weak' else 'global batch split over the ranks'})",
+                                   **({"invalid": sec["invalid"]} if not sec["ok"] else {})}
+        if not res["ok"]:
+            rec["invalid"] = res["invalid"]
+        print(json.dumps(rec), flush=True)
     shutdown()
     return 0 if ok else 1
 

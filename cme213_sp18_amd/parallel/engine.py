@@ -132,7 +132,7 @@ class MlpEngine:
         # (MlpStep.lazy_planes; they are re-split before one that does)
         # (measured at 784-4096-10 fp32: step 58.0 -> 55.2 us, profiles/wide_ag_ab_lazy_planes_r3.jsonl)
         self.lazy_planes = True
-        self._ag_test_skip, self._ag_spin_shift = -1, 22  # inject_handoff_timeout (tests)
+        self._ag_test_skip, self._ag_wait_us = -1, 50_000  # inject_handoff_timeout (tests); 50 ms default
         self.kpart = None  # split-K dW1 slabs (enable_splitk)
 
     def _configure_path(self):
@@ -306,14 +306,15 @@ class MlpEngine:
             if self._step is not None:
                 self._step.planes_stale = False
 
-    def inject_handoff_timeout(self, row_tile: int = 0, spin_shift: int = 14) -> None:
-        """TEST HOOK: from the next step on, row tile ``row_tile`` of column tile 0 leaves its counter add out
-        of every all-gather forward + head launch, so that tile's wait really times out (after 2^spin_shift
-        polls).  ``row_tile=-1`` turns it off.  A timed-out launch sets the sticky error word: this engine then
+    def inject_handoff_timeout(self, row_tile: int = 0, wait_us: int = 2000) -> None:
+        """TEST HOOK: from the next step on, row tile ``row_tile`` of column tile 0 withholds its hand-off
+        granules in every all-gather forward + head launch, so that tile's wait really times out (after
+        ``wait_us`` microseconds of wall time; the production bound is 50 ms).  ``row_tile=-1`` turns the
+        withholding off (the bound stays).  A timed-out launch sets the sticky error word: this engine then
         applies no further update (kernel_error(), KernelHandoffTimeout) -- make a new engine afterwards."""
-        self._ag_test_skip, self._ag_spin_shift = int(row_tile), int(spin_shift)
+        self._ag_test_skip, self._ag_wait_us = int(row_tile), int(wait_us)
         if self._step is not None:
-            self._step.ag_test_skip, self._step.ag_spin_shift = self._ag_test_skip, self._ag_spin_shift
+            self._step.ag_test_skip, self._step.ag_wait_us = self._ag_test_skip, self._ag_wait_us
 
     def kernel_error(self) -> bool:
         """True if a forward + head launch's wait for the workgroups of its column tile timed out (the
@@ -389,7 +390,7 @@ class MlpEngine:
                 s.ag_err = self.ag_err.data_ptr()
                 s.fh_allgather = int(self.fh_allgather)
             s.store_a1 = int(self.store_a1)
-            s.ag_test_skip, s.ag_spin_shift = self._ag_test_skip, self._ag_spin_shift
+            s.ag_test_skip, s.ag_wait_us = self._ag_test_skip, self._ag_wait_us
             if self.kpart is not None:
                 s.kpart, s.kpart_cap = self.kpart.data_ptr(), int(self.kpart.numel())
             if self.np and self.XT is not None and self.XT.shape[0] == self.P + 1:

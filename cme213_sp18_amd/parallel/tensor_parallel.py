@@ -33,6 +33,13 @@ from .engine import MlpEngine
 from .trainer import EpochPlan, TrainStats
 
 
+def tp_allreduce_mode(mode: str) -> str:
+    """The z2 all-reduce for a data-parallel ``--allreduce`` choice, the same in every entry point (bench.py,
+    train.py): the z2 sum is latency-bound (16 x batch fp32), so the xGMI two-shot form maps to the one-shot
+    kernel (xgmi2 -> xgmi) and the host-staged reference form to the communicator (host -> rccl)."""
+    return {"auto": "auto", "xgmi": "xgmi", "xgmi2": "xgmi", "rccl": "rccl", "host": "rccl", "off": "rccl"}[mode]
+
+
 class TensorParallelTrainer:
     """Hidden-sharded training: rank r owns hidden units [r*H/R, (r+1)*H/R)."""
 
@@ -75,8 +82,9 @@ class TensorParallelTrainer:
     def _setup_xgmi(self, mode: str):
         from .comm import TorchDistComm
 
-        if mode not in ("auto", "xgmi", "rccl"):
-            raise ValueError("allreduce must be auto, xgmi or rccl")
+        if mode not in ("auto", "xgmi", "xgmi2", "rccl", "host", "off"):
+            raise ValueError("allreduce must be auto, xgmi, xgmi2, rccl, host or off")
+        mode = tp_allreduce_mode(mode)
         e = self.engine
         ok = (self.R > 1 and isinstance(self.comm, TorchDistComm) and e.device.type == "cuda" and e.backend == "hip"
               and e.np and self.z2.dtype == torch.float32)
@@ -165,6 +173,11 @@ class TensorParallelTrainer:
     def _step_hip(self, off, n, lr, reg, with_loss):
         e = self.engine
         st = e._hip_step()
+        if self._xz is not None:
+            # the weight-gradient launch applies nothing once a z2 peer wait of this rank timed out (the bucket's
+            # sticky error word, read like the all-gather head's: SplitStepArgs::ag_err) -- a timed-out chunk
+            # leaves this rank's unreduced partial in z2, which must never reach the weights
+            st.ag_err = int(self._xz.c.err_address)
         stream = torch.cuda.current_stream(e.device).cuda_stream
         zp = self._z2part
         chunks = st.tp_forward(int(off), int(n), zp.data_ptr() if zp is not None else 0, stream)
@@ -275,7 +288,7 @@ class TensorParallelTrainer:
         """Training loop with the data-parallel trainer's interface (loss every ``print_every`` steps,
         JSON-lines epoch events, ``fault=(rank, step)`` injection); graph-replayed epochs when no loss is
         printed.  ``debug`` (the reference's per-iteration CPU diff) is data-parallel only."""
-        from .trainer import FaultInjected
+        from .trainer import CommFailure, FaultInjected
 
         stats = TrainStats()
         plan = self.epoch_plan()
@@ -309,6 +322,11 @@ class TensorParallelTrainer:
                     self.iter += 1
                     stats.steps += 1
                     stats.images += ln
+            if self._xz is not None and self.comm_failed():
+                # (collective) a z2 peer wait timed out on some rank: that rank's weight-gradient launches applied
+                # nothing from then on, so the shards no longer belong to one model -- every rank stops together
+                raise CommFailure(f"rank {self.rank}: an xGMI z2 all-reduce peer wait timed out on some rank; "
+                                  "no rank applied the affected update")
             if on_event is not None:
                 if dev.type == "cuda":
                     torch.cuda.synchronize(dev)

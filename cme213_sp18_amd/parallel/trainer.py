@@ -36,6 +36,28 @@ XGMI_AUTO_MAX_BYTES = 2 << 20  # allreduce="auto" uses the xGMI one-shot kernel 
 XGMI2_AUTO_MAX_BYTES = 8 << 20  # ... and the two-shot kernel (4+ ranks) up to this one; RCCL beyond
 BUCKET_BYTES = 4 << 20         # dW1 all-reduce chunk of the overlapped RCCL backward
 
+# The cost model's planning constants (docs/PERFORMANCE.md "Communication policy"): one xGMI link per direction,
+# the fixed cost of one peer-kernel launch + hand-off (7.5 us measured with 2 ranks on one GPU), and RCCL's launch
+# + protocol cost.  Only the first multi-GPU run measures them: bench.py records the prediction
+# (allreduce_pred_us) beside the measured all-reduce (allreduce_us) so that run confirms or refutes them.
+XGMI_LINK_GBPS = 64.0
+XGMI_KERNEL_US = 7.5
+RCCL_FIXED_US = 25.0
+
+
+def allreduce_cost_us(R: int, wire_bytes: int, shots: int) -> float:
+    """Predicted time of one gradient all-reduce of ``wire_bytes`` over R ranks of one node: shots 1 = the xGMI
+    one-shot kernel (L + S / B: every rank pulls the R - 1 peer buckets over R - 1 links at once), 2 = the
+    two-shot kernel (2 L + 2 S / (R B)), 0 = an RCCL ring (L_rccl + 2 S / (R B), before any overlap)."""
+    if R <= 1:
+        return 0.0
+    bw = XGMI_LINK_GBPS * 1e3  # bytes per us
+    if shots == 1:
+        return XGMI_KERNEL_US + wire_bytes / bw
+    if shots == 2:
+        return 2 * XGMI_KERNEL_US + 2 * wire_bytes / (R * bw)
+    return RCCL_FIXED_US + 2 * wire_bytes / (R * bw)
+
 
 def auto_allreduce_shots(R: int, wire_bytes: int, fp_bytes: int, bf16_wire: bool) -> int:
     """allreduce="auto" on one node: 1 = the xGMI one-shot kernel, 2 = the two-shot kernel, 0 = RCCL.

@@ -119,7 +119,7 @@ def run(cfg: TrainConfig) -> dict:
         comm.barrier()  # the parallel run's debug diff reads the CPU snapshots
         log0(rank, "\nStart Parallel Training")
         if cfg.parallel == "tp":
-            from .parallel.tensor_parallel import TensorParallelTrainer
+            from .parallel.tensor_parallel import TensorParallelTrainer, tp_allreduce_mode
 
             if cfg.debug:
                 log0(rank, "note: -d (per-iteration CPU diff) is data-parallel only; ignored with --parallel tp")
@@ -127,7 +127,7 @@ def run(cfg: TrainConfig) -> dict:
             tr = TensorParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,
                                        backend=backend, shift=cfg.softmax_shift, normalize=cfg.normalize,
                                        path=cfg.path,
-                                       allreduce=cfg.allreduce if cfg.allreduce in ("auto", "xgmi") else "rccl")
+                                       allreduce=tp_allreduce_mode(cfg.allreduce))
             tr.use_graphs = cfg.use_graphs
         else:
             tr = DataParallelTrainer(nn, comm=comm, device=device, dtype=cfg.dtype, batch_size=cfg.batch_size,

@@ -60,9 +60,9 @@ struct MlpStep {
   int fh_allgather = 0;
   // the gradient bucket's status element (float, after b2): written by the wgrad launch in gradient mode
   uintptr_t gstatus = 0;
-  // the all-gather hand-offs' wait bound (2^ag_spin_shift polls) and the forced-timeout test hook
+  // the all-gather hand-offs' wait bound (microseconds of wall time) and the forced-timeout test hook
   // (SplitStepArgs::ag_test_skip; -1 off)
-  int ag_spin_shift = 22, ag_test_skip = -1;
+  int ag_wait_us = (int)cme::kHandoffWaitUs, ag_test_skip = -1;
   // wide split layers: the all-gather head fused into the forward launch (fh_allgather, ag_counters, ag_err;
   // mlp_fwd1_wide_ag) leaves dW2 partials per 128 / 64 columns (32 from head_wide_kernel): what run_wgrad sums
   int dw2_cols_last = 32;
@@ -158,7 +158,7 @@ struct MlpStep {
     // a timed-out all-gather forward + head launch (sticky word) makes every later update a no-op
     a.ag_err = P_<const int>(ag_err);
     a.gstatus = P_<float>(gstatus);
-    a.ag_spin_shift = ag_spin_shift;
+    a.ag_wait_us = ag_wait_us;
     a.ag_test_skip = ag_test_skip;
     return a;
   }
@@ -471,7 +471,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_err", &MlpStep::ag_err)
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
       .def_readwrite("gstatus", &MlpStep::gstatus)
-      .def_readwrite("ag_spin_shift", &MlpStep::ag_spin_shift)
+      .def_readwrite("ag_wait_us", &MlpStep::ag_wait_us)
       .def_readwrite("ag_test_skip", &MlpStep::ag_test_skip)
       .def_readwrite("store_a1", &MlpStep::store_a1)
       .def_readwrite("ag_gran", &MlpStep::ag_gran)

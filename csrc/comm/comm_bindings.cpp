@@ -197,6 +197,9 @@ class XgmiComm {
   // address of the descriptor, for a kernel that fuses this all-reduce in (MlpStep.set_xgmi); valid
   // while this object is open
   uintptr_t desc_address() const { return reinterpret_cast<uintptr_t>(&d_); }
+  // address of the sticky timed-out-wait word (int, device): a launch that must apply nothing once a peer
+  // wait of this bucket timed out reads it (the tensor-parallel weight-gradient launch, SplitStepArgs::ag_err)
+  uintptr_t err_address() const { return reinterpret_cast<uintptr_t>(d_.err); }
 
  private:
   size_t flag_bytes() const { return (size_t)nblocks_ * kMaxRanks * sizeof(uint32_t); }
@@ -229,7 +232,8 @@ void bind_comm(py::module_& m) {
       .def("close_peers", &XgmiComm::close_peers)
       .def_property_readonly("nblocks", &XgmiComm::nblocks)
       .def_property_readonly("npad", &XgmiComm::npad)
-      .def_property_readonly("desc_address", &XgmiComm::desc_address);
+      .def_property_readonly("desc_address", &XgmiComm::desc_address)
+      .def_property_readonly("err_address", &XgmiComm::err_address);
   sm.attr("MODE_SGD") = cme::comm::kModeSgd;
   sm.attr("MODE_ALLREDUCE") = cme::comm::kModeAllReduce;
   sm.attr("MAX_RANKS") = cme::comm::kMaxRanks;

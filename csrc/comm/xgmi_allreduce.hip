@@ -8,7 +8,7 @@
 //   1. copies the local gradient chunk into this step's half of a
 //      double-buffered IPC buffer and releases it at system scope,
 //   2. signals every peer (per-block flag in the peer's uncached flag page),
-//   3. waits for every peer's flag (bounded spin -> error flag, never a hang;
+//   3. waits for every peer's flag (bounded by 2 s of wall time -> error flag, never a hang;
 //      a block whose wait timed out -- or that starts after ANY block of this
 //      rank has flagged an error -- applies NOTHING: params and planes stay as
 //      they were, so a stalled peer can never make this rank step on stale or
@@ -35,7 +35,7 @@ constexpr int kThreads = 256;
 constexpr int kVec = 4;                       // elements per thread
 constexpr int kChunk = kThreads * kVec;       // elements per block
 constexpr int64_t kMaxGrid = 256;             // one block per CU: always resident, even with several ranks per GPU
-constexpr uint32_t kSpinLimit = 1u << 22;     // ~seconds, then flag an error instead of hanging
+constexpr uint64_t kWaitTicks = kPeerWaitUs * kTicksPerUs;  // 2 s of wall time, then an error instead of a hang
 
 // T: gradient / parameter type; W: the wire type in the IPC buffers (T, or bf16 for fp32 gradients:
 // half the bytes over xGMI, summed in fp32 after the pull)
@@ -193,10 +193,10 @@ __device__ __forceinline__ void do_chunk(const Args<T, W>& a, int64_t c, uint32_
     __hip_atomic_store(a.peerflags[t] + c * kMaxRanks + a.rank, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // 3. wait for every peer's chunk c (bounded)
   if (t < a.world) {
-    uint32_t spins = 0;
+    const uint64_t t0 = wall_ticks();
     const uint32_t* f = a.myflags + c * kMaxRanks + t;
     while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      if (++spins > kSpinLimit) {
+      if (wall_ticks() - t0 > kWaitTicks) {
         atomicExch(a.err, 1);
         s_sync[1] = 1;  // (benign race between the waiting lanes: they all store 1)
         break;
@@ -330,10 +330,10 @@ __device__ __forceinline__ void do_chunk2(const Args<T, T>& a, int64_t c, uint32
   if (t == 0)
     __hip_atomic_store(a.peerflags[owner] + c * kMaxRanks + a.rank, 2u * e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   auto wait_flag = [&](int slot, uint32_t target) {  // one lane; sets s_sync[1] on timeout
-    uint32_t spins = 0;
+    const uint64_t t0 = wall_ticks();
     const uint32_t* f = a.myflags + c * kMaxRanks + slot;
     while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
-      if (++spins > kSpinLimit) {
+      if (wall_ticks() - t0 > kWaitTicks) {
         atomicExch(a.err, 1);
         s_sync[1] = 1;
         break;

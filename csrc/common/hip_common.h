@@ -72,6 +72,15 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Wall-clock bounds for every wait on another workgroup or another GPU (a peer's flag, an in-launch hand-off):
+// s_memrealtime is the constant 100 MHz counter, so a bound is a duration, not a poll count whose real length
+// depends on the sleep, the poll's memory latency and how loaded the fabric is.  A wait that outlasts its bound
+// sets an error word and the kernel applies nothing (never a hang).
+constexpr uint64_t kTicksPerUs = 100;
+constexpr uint64_t kPeerWaitUs = 2'000'000;  // xGMI peer waits: 2 s (a stalled or dead rank)
+constexpr uint64_t kHandoffWaitUs = 50'000;  // in-launch hand-offs between co-resident workgroups: 50 ms
+__device__ __forceinline__ uint64_t wall_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md
 // §5 "XCD swizzle must be bijective"): consecutive logical tiles land on the
 // same XCD so neighbouring tiles share that XCD's L2.  Speed only.

@@ -11,7 +11,7 @@
 //   3. forms dZ1 for ITS OWN 16 rows from the a1 tile it still holds in LDS and stores it (fp32 and / or
 //      the bf16 planes, two columns per 4-byte word).
 // Requires every workgroup of the launch to be resident at once (mlp_fwd1_head_ag_fits); a poll that outlasts
-// 2^ag_spin_shift passes sets *err: the launch's results are not trusted, and the weight-gradient launch that
+// ag_wait_us of wall time sets *err: the launch's results are not trusted, and the weight-gradient launch that
 // follows reads *err and applies nothing (SplitStepArgs::ag_err; MlpEngine.kernel_error(), KernelHandoffTimeout).
 #pragma once
 
@@ -125,7 +125,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   {
     float z = 0.f;
     const bool good = gran_poll<8>(slabs, (unsigned)(ct * tm * 16 * kCols + c * kCols + col), 16u * kCols, tm,
-                                   c < C, ep, 1u << f.ag_spin_shift, [&](int, float v) { z += v; }, f.poll_skip != 0);
+                                   c < C, ep, (uint32_t)f.ag_wait_us, [&](int, float v) { z += v; }, f.poll_skip != 0);
     if (!good && (t & 63) == 0) {
       atomicExch(err, 1);
       s_bad = 1;

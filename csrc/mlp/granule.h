@@ -10,6 +10,8 @@
 
 #include <cstdint>
 
+#include "../common/hip_common.h"
+
 namespace cme {
 
 using gran_t = unsigned long long;
@@ -38,14 +40,14 @@ __device__ __forceinline__ gran_t gran_load(const gran_t* p) {  // sc1 load (L2-
 // Poll the granules base[off + k * stride] (k < cnt <= N; lanes with !need take no part) until every tag is
 // `ep`, then hand the values to f(k, value) in k order (0 for k >= cnt).  The N addresses are formed once,
 // before the poll loop; a pass is N back-to-back global_load_dwordx2 sc1 and one wait.  Wave-uniform; false
-// when the wave gave up after `limit` passes (f is then not called).
+// when the wave gave up after `limit_us` microseconds of wall time (s_memrealtime; f is then not called).
 // A granule seen with the epoch is final for this launch (tags only grow), so later passes re-load only the
 // granules still missing (the others' loads are masked off): every workgroup of the launch polls at once,
 // and re-reading the already-arrived granules made the waiting workgroups' sc1 traffic compete with the
 // stores and polls of the workgroups they wait for.  The first pass is unchanged: no added latency.
 template <int N, class F>
 __device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsigned stride, int cnt, bool need,
-                                          unsigned ep, uint32_t limit, F&& f, bool skip = true) {
+                                          unsigned ep, uint32_t limit_us, F&& f, bool skip = true) {
   static_assert(N <= 32, "ready mask");
   // the granule addresses, once: k >= cnt re-reads granule 0 (needed anyway, so its tag check is the same)
   const gran_t* p[N];
@@ -57,7 +59,8 @@ __device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsi
   bool done = !need;
   unsigned rdy = 0u;  // bit k: granule k carried the epoch in an earlier pass (x[k] is final)
   gran_t x[N];
-  for (uint32_t spins = 0;; ++spins) {
+  const uint64_t t0 = wall_ticks(), limit = (uint64_t)limit_us * kTicksPerUs;
+  for (;;) {
     if (!done) {
 #pragma unroll
       for (int k = 0; k < N; ++k)
@@ -67,7 +70,7 @@ __device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsi
       done = rdy == kAll;
     }
     if (__all(done)) break;
-    if (spins >= limit) return false;
+    if (wall_ticks() - t0 > limit) return false;
     __builtin_amdgcn_s_sleep(2);
   }
   if (need) {

@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "../common/hip_common.h"
+
 namespace cme {
 
 // Gradient all-reduce fused into the weight-gradient launch (data parallel over xGMI, one process per
@@ -111,9 +113,10 @@ struct SplitStepArgs {
   // sgd = 0: the flat gradient bucket's status element (after b2): 0.f good, 1.f = this rank's step is
   // untrusted.  Summed by the all-reduce with the gradients; the SGD kernels skip the update when non-zero.
   float* gstatus = nullptr;
-  // the all-gather hand-off's wait bound (2^ag_spin_shift polls) and a TEST hook: row tile ag_test_skip of
-  // column tile 0 leaves out its (first) counter add, so that tile's wait really times out (-1: off)
-  int ag_spin_shift = 22;
+  // the all-gather hand-off's wait bound in microseconds of wall time (hip_common.h kHandoffWaitUs) and a TEST
+  // hook: row tile ag_test_skip of column tile 0 withholds its granules, so that tile's wait really times out
+  // (-1: off)
+  int ag_wait_us = (int)kHandoffWaitUs;
   // the hand-off polls re-load only the granules still missing (granule.h gran_poll; 0: every granule every pass, A/B)
   int poll_skip = 1;
   int ag_test_skip = -1;

@@ -244,7 +244,7 @@ __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a,
 // flag; rank-order sum with system-coherent loads (bit-identical on every rank).  Double
 // buffering + per-tile epochs: half e&1 of a tile is rewritten only after every peer passed e-1.
 constexpr int kXfSys = 1 | 16;  // cache policy sc0 | sc1: system coherent
-constexpr uint32_t kXfSpinLimit = 1u << 22;
+constexpr uint64_t kXfWaitTicks = kPeerWaitUs * kTicksPerUs;  // 2 s of wall time (hip_common.h)
 
 // The forward + head launch of this step timed out (SplitStepArgs::ag_err): the word is loaded (a vector
 // atomic load from L2) BEFORE the K loop, like the epilogue's other operands, and tested only by the epilogue
@@ -295,10 +295,10 @@ __device__ __forceinline__ bool xf_exchange(const XgmiFuse& x, int tile, uint32_
     // and drained by every wave above, so a release would only write back the L2's OTHER dirty lines
     // (W1/plane updates no peer reads) once per tile.  bench.py checks the replicas bitwise after warm-up.
     __hip_atomic_store(x.peerflags[t] + tile * 8 + x.rank, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t spins = 0;
+    const uint64_t t0 = wall_ticks();
     const uint32_t* f = x.myflags + tile * 8 + t;
     while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) < 0) {
-      if (++spins > kXfSpinLimit) {
+      if (wall_ticks() - t0 > kXfWaitTicks) {
         atomicExch(x.err, 1);
         s_xf[1] = 1;  // (the waiting lanes may race here: they all store 1)
         break;
@@ -724,7 +724,7 @@ __device__ __forceinline__ void st_bf16(__amdgpu_buffer_rsrc_t r, int off, bf16 
 //   3. every workgroup polls the tile's 16 x BN D granules and forms dZ1 = (W2^T D) .* a1 .* (1 - a1) for its
 //      own tile on the f32 MFMA, plus the tile's dW2 partial D . a1^T (SplitStepArgs::dw2_cols = BN).
 // Every workgroup must be resident at once (one per CU: the launcher's LDS request and tm * tn <= CUs).  A poll
-// that outlasts 2^ag_spin_shift passes sets *err (MlpEngine.kernel_error()) and the workgroup writes nothing
+// that outlasts ag_wait_us of wall time sets *err (MlpEngine.kernel_error()) and the workgroup writes nothing
 // more; the weight-gradient launch that follows applies nothing (SplitStepArgs::ag_err).
 struct RegaAgArgs {
   HeadArgs h{};
@@ -793,7 +793,7 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
   float* ls = zs + 16 * 17;                         // [16] loss of those columns
   unsigned* sw = reinterpret_cast<unsigned*>(lds + g.ep_off);  // [0] epoch, [1] [2] timeout flags
   const unsigned ep = sw[0];
-  const uint32_t limit = 1u << a.ag_spin_shift;
+  const uint32_t limit = (uint32_t)a.ag_wait_us;
   // independent loads first: the W2^T operand of dZ1 (class 4 fg + i, row rw + fr), the reducer's labels, b2
   float wv[4];
 #pragma unroll

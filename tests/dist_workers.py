@@ -383,7 +383,7 @@ def handoff_timeout_dp_worker(rank, world, comm, device, out_dir, allreduce):
     res["clean_err"] = float(tr.engine.kernel_error())
     comm.barrier()
     if rank == 0:
-        tr.engine.inject_handoff_timeout(0, 12)
+        tr.engine.inject_handoff_timeout(0, 2000)
     before = (tr.engine.params.clone(), tr.engine.W1p.clone())
     try:
         tr.train(1, 0.05, 1e-4)

@@ -55,7 +55,7 @@ def test_forced_handoff_timeout_applies_nothing(dt, H, n):
     assert float(e.grads[e.status_index]) == 0.0  # a trusted step's status
     before = (e.params.clone(), e.W1p.clone())
     assert torch.equal(before[0], moved)
-    e.inject_handoff_timeout(0, 12)
+    e.inject_handoff_timeout(0, 2000)
     e.run(n, n, 1.0 / n, 1e-4, 0.05, sgd=True)
     torch.cuda.synchronize()
     assert e.kernel_error(), "the forced hand-off did not time out"
@@ -80,7 +80,7 @@ def test_real_timeout_raises_in_train_and_freezes_params(H):
     tr.load(x, y)
     tr.train(1, 0.01, 1e-4)
     assert tr._allgather_live() and not tr.engine.kernel_error()
-    tr.engine.inject_handoff_timeout(1, 12)
+    tr.engine.inject_handoff_timeout(1, 2000)
     before = tr.engine.params.clone()
     with pytest.raises(KernelHandoffTimeout):
         tr.train(1, 0.01, 1e-4)
@@ -158,7 +158,7 @@ def test_partial_residency_times_out_and_applies_nothing(H):
     e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=True)
     torch.cuda.synchronize()
     assert not e.kernel_error()
-    e.inject_handoff_timeout(-1, 10)  # no withheld granules: only a short poll bound (2^10 passes)
+    e.inject_handoff_timeout(-1, 500)  # no withheld granules: only a short wall-time bound (500 us)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     # The step must run BESIDE the holder, i.e. on another hardware queue.  HIP spreads streams over its few
     # hardware queues, so a new stream may share the holder's queue; then the step simply runs after the holder (and

@@ -40,9 +40,26 @@ def test_bench_self_launches_n_ranks(tmp_path):
     assert len(recs) == 1, r.stdout  # rank 0 only
     rec = recs[0]
     assert rec["n_gpus"] == 2 and rec["config"]["ranks_seen"] == 2 and rec["config"]["parallelism"] == "dp2"
-    assert rec["config"]["devices_distinct"] is True and rec["config"]["global_batch"] == 1600
+    # no --scaling flag: the metric's own config -- global batch 800 split over the ranks (fpcode/run.sh:39,
+    # neural_network.cpp:458) -- and the weak-scaling run as a labelled secondary sub-record
+    assert rec["scaling"] == "strong" and rec["config"]["global_batch"] == 800, rec
+    assert rec["config"]["per_gpu_batch"] == 400
+    weak = rec["weak"]
+    assert weak["global_batch"] == 1600 and weak["per_gpu_batch"] == 800 and weak["value"] > 0, weak
+    assert rec["config"]["devices_distinct"] is True
     assert rec["config"]["allreduce_us"] > 0 and rec["config"]["allreduce_bytes"] > 300_000
+    assert rec["config"]["allreduce_pred_us"] > 0  # the cost model's prediction beside the measurement
     assert rec["steps"] == 3 and rec["value"] > 0
+
+
+def test_bench_weak_primary_with_strong_secondary(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "torch",
+                        "--scaling", "weak", "--steps", "2", "--warmup", "1", "--train-size", "3200"],
+                       cwd=tmp_path, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = _records(r.stdout)[0]
+    assert rec["scaling"] == "weak" and rec["config"]["global_batch"] == 1600
+    assert rec["strong"]["global_batch"] == 800 and rec["strong"]["per_gpu_batch"] == 400
 
 
 def test_bench_refuses_more_gpus_than_visible(tmp_path):
