@@ -23,8 +23,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--hidden", type=int, nargs="*", default=[100])
     ap.add_argument("--cols", type=int, nargs="*", default=[800, 100])
-    ap.add_argument("--cfg", nargs="*", default=["f32:split3", "f32:split3+fh", "f32:mfma", "bf16:split1",
-                                                   "f64:mfma"])
+    ap.add_argument("--cfg", nargs="*", default=["f32:split3", "f32:mfma", "bf16:split1", "f64:mfma"])
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--json", default=None)
     a = ap.parse_args(argv)
@@ -64,19 +63,9 @@ def main(argv=None):
 
     for cfg in a.cfg:
         dt, path = cfg.split(":")
-        fused = "+fh" in path
-        # split3 operand forms (SplitStepArgs.a_fp32): "+a<bits>" bit0 fp32 W1, bit1 fp32 dZ1 (default: engine's)
-        m = re.search(r"\+a(\d)", path)
-        a32 = int(m.group(1)) if m else None
-        # "+p<0|1>": the pixel operand's 16-byte chunk-pair loads (SplitStepArgs.u8_pairs; default on)
-        m = re.search(r"\+p(\d)", path)
-        pairs = int(m.group(1)) if m else None
-        # "+q<0|1>": the hand-off polls re-load only the granules still missing (SplitStepArgs.poll_skip; default on)
-        m = re.search(r"\+q(\d)", path)
-        pskip = int(m.group(1)) if m else None
         # "+s0": no a1 store (the trainer's setting); "+d0": no dW2 partials from the head (dw2p = 0)
         no_a1, no_dw2 = "+s0" in path, "+d0" in path
-        path = re.sub(r"\+[apsdq]\d", "", path).replace("+fh", "")
+        path = re.sub(r"\+[sd]\d", "", path)
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -85,13 +74,6 @@ def main(argv=None):
                 e.load_dataset(x, y)
                 step = e._hip_step()
                 join = e.join
-                step.fused_head = int(fused)
-                if a32 is not None:
-                    step.a_fp32 = a32
-                if pairs is not None:
-                    step.u8_pairs = pairs
-                if pskip is not None:
-                    step.poll_skip = pskip
                 if no_a1:
                     e.set_store_a1(False)
                 if no_dw2:
@@ -101,7 +83,7 @@ def main(argv=None):
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+fh" if fused else "") + (f"+a{a32}" if a32 is not None else "") + (f"+p{pairs}" if pairs is not None else "") + (f"+q{pskip}" if pskip is not None else "") + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(

@@ -22,8 +22,7 @@ def main(argv=None):
     ap.add_argument("--cfg", nargs="*", default=["f32:split3", "bf16:split1"])
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--modes", nargs="*", default=["head", "ag", "ag_noa1"],
-                    help="head | ag | ag_noa1, each optionally +q0 (SplitStepArgs.poll_skip = 0: the hand-off polls "
-                         "re-load every granule every pass) and / or +l0 / +l1 (MlpStep.lazy_planes off / on: the in-place "
+                    help="head | ag | ag_noa1, each optionally +l0 / +l1 (MlpStep.lazy_planes off / on: the in-place "
                          "W1 update skips the W1-plane refresh; default: the engine's); a mode may repeat (A/B alternation)")
     a = ap.parse_args(argv)
     import torch
@@ -67,12 +66,6 @@ def main(argv=None):
                 e.set_fh_allgather(mode != "head")
                 e.set_store_a1(not mode.endswith("noa1"))
                 e._hip_step().ag_tiles64 = 1
-                e._hip_step().poll_skip = 0 if "q0" in opts else 1
-                for o in opts:  # "+a<bits>": split3 operand forms (SplitStepArgs.a_fp32: bit0 fp32 W1, bit1 fp32 dZ1)
-                    if o[:1] == "a" and o[1:].isdigit():
-                        e._hip_step().a_fp32 = int(o[1:])
-                if "w2" in opts or "w1" in opts:  # wide bf16 dW1 wave layout (MlpStep.rega_wc)
-                    e._hip_step().rega_wc = 2 if "w2" in opts else 1
                 if "l0" in opts or "l1" in opts:  # (else the engine's default, MlpEngine.lazy_planes)
                     e.set_lazy_planes("l1" in opts)
                 off = [0]

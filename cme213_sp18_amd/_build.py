@@ -105,7 +105,11 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         so = PKG / f"{name}{EXT}"
         objs = [o for _, o in pairs]
         if force or not so.exists() or any(o.stat().st_mtime > so.stat().st_mtime for o in objs):
-            _run(link(objs, so))
+            # linked to a temporary name and renamed into place (atomic): a snapshot of the tree taken meanwhile
+            # (a GPU run's upload) sees the old library or the new one, never a half-written file
+            tmp = so.with_name(so.name + ".tmp")
+            _run(link(objs, tmp))
+            os.replace(tmp, so)
             if verbose:
                 print(f"[cme-build] linked {so.relative_to(ROOT)}", flush=True)
         out[name] = so

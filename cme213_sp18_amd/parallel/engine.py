@@ -346,56 +346,43 @@ class MlpEngine:
         if self._step is None:
             m = hip()
             s = m.MlpStep()
-            s.dt = DTYPE_CODES[self.dtype]
-            s.P, s.H, s.C, s.ld = self.P, self.H, self.C, self.ld
             loaded = self.X is not None
-            s.X = self.X.data_ptr() if loaded else 0
-            s.labels = self.labels.data_ptr() if loaded else 0
-            s.XT = self.XT.data_ptr() if loaded and self.XT is not None else 0
-            s.Xw = self.Xw.data_ptr() if loaded and self.Xw is not None else 0
-            s.XTw = self.XTw.data_ptr() if loaded and self.XTw is not None else 0
-            s.N = self.num_samples if loaded else 0
-            s.W1, s.b1, s.W2, s.b2 = (t.data_ptr() for t in (self.W1, self.b1, self.W2, self.b2))
-            s.gstatus = self.grads[self.status_index:].data_ptr()
-            s.W1g = self.W1g.data_ptr()
-            s.gW1, s.gb1, s.gW2, s.gb2 = (t.data_ptr() for t in (self.gW1, self.gb1, self.gW2, self.gb2))
-            s.a1, s.D, s.dZ1, s.dZ1g = (t.data_ptr() for t in (self.a1, self.D, self.dZ1, self.dZ1g))
-            s.loss = self.loss_buf.data_ptr()
-            s.shift = int(self.shift)
-            s.act = 1
+            ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+            b = dict(dt=DTYPE_CODES[self.dtype], P=self.P, H=self.H, C=self.C, ld=self.ld,
+                     X=ptr(self.X), labels=ptr(self.labels), XT=ptr(self.XT), Xw=ptr(self.Xw), XTw=ptr(self.XTw),
+                     N=self.num_samples if loaded else 0,
+                     W1=ptr(self.W1), b1=ptr(self.b1), W2=ptr(self.W2), b2=ptr(self.b2), W1g=ptr(self.W1g),
+                     gW1=ptr(self.gW1), gb1=ptr(self.gb1), gW2=ptr(self.gW2), gb2=ptr(self.gb2),
+                     gstatus=self.grads[self.status_index:].data_ptr(),
+                     a1=ptr(self.a1), D=ptr(self.D), dZ1=ptr(self.dZ1), dZ1g=ptr(self.dZ1g), loss=ptr(self.loss_buf),
+                     act=1, z2p=ptr(self.z2buf))
             if self.np:
-                s.split = 1
-                s.xscale = float(self.xscale)
-                s.npw = s.npz = self.np
-                s.W1p = self.W1p.data_ptr()
-                s.dZ1p = self.dZ1p.data_ptr()
+                b.update(split=1, xscale=float(self.xscale), npw=self.np, npz=self.np, W1p=ptr(self.W1p),
+                         dZ1p=ptr(self.dZ1p))
+            if self.fh_counters is not None:
+                b.update(fh_counters=ptr(self.fh_counters), fh_tiles=int(self.fh_counters.numel()),
+                         ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs))
+            elif self.ag_gran is not None:  # the wide fused head
+                b.update(fh_tiles=int(self.ag_counters.numel()) // 64,  # [2 tilings][tiles][32]
+                         ag_gran=ptr(self.ag_gran), ag_gran_count=int(self.ag_gran.numel()),
+                         ag_counters=ptr(self.ag_counters))
+            if self.kpart is not None:
+                b.update(kpart=ptr(self.kpart), kpart_cap=int(self.kpart.numel()))
+            bias_col = bool(self.np and self.XT is not None and self.XT.shape[0] == self.P + 1)
+            b.update(bias_col=int(bias_col))
+            s.bind(b)
+            s.shift = int(self.shift)
+            s.dw2p = ptr(self.dw2buf)
+            if self.ag_err is not None and (self.fh_counters is not None or self.ag_gran is not None):
+                s.ag_err = self.ag_err.data_ptr()
+                s.fh_allgather = int(self.fh_allgather)
+            if self.np:
                 # a new step cannot know whether an earlier one left the planes stale: re-split once
                 s.planes_stale = True
                 s.lazy_planes = int(self.lazy_planes)
-            if self.z2buf is not None:
-                s.z2p = self.z2buf.data_ptr()
-            if self.dw2buf is not None:
-                s.dw2p = self.dw2buf.data_ptr()
-            if self.fh_counters is not None:
-                s.fh_counters = self.fh_counters.data_ptr()
-                s.fh_tiles = int(self.fh_counters.numel())
-                s.ag_counters = self.ag_counters.data_ptr()
-                s.ag_slabs = self.ag_slabs.data_ptr()
-                s.ag_err = self.ag_err.data_ptr()
-                s.fh_allgather = int(self.fh_allgather)
-            elif self.ag_gran is not None:  # the wide fused head
-                s.fh_tiles = int(self.ag_counters.numel()) // 64  # [2 tilings][tiles][32]
-                s.ag_gran, s.ag_gran_count = self.ag_gran.data_ptr(), int(self.ag_gran.numel())
-                s.ag_counters = self.ag_counters.data_ptr()
-                s.ag_err = self.ag_err.data_ptr()
-                s.fh_allgather = int(self.fh_allgather)
             s.store_a1 = int(self.store_a1)
             s.ag_test_skip, s.ag_wait_us = self._ag_test_skip, self._ag_wait_us
-            if self.kpart is not None:
-                s.kpart, s.kpart_cap = self.kpart.data_ptr(), int(self.kpart.numel())
-            if self.np and self.XT is not None and self.XT.shape[0] == self.P + 1:
-                s.bias_col = 1
-            if self._xgmi_fuse is not None and s.bias_col:
+            if self._xgmi_fuse is not None and bias_col:
                 s.set_xgmi(*self._xgmi_fuse)
             self._step = s
         return self._step

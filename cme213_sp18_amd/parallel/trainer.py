@@ -199,6 +199,10 @@ class DataParallelTrainer:
             ("xgmi-bf16wire" if self.xgmi.wire == torch.bfloat16 else "xgmi-2shot" if self.xgmi.shots == 2
              else "xgmi") if self.xgmi is not None
             else "host-gloo" if allreduce == "host" else self.comm.name)
+        # train(): one in-process recovery from a timed-out hand-off or peer wait (the snapshot taken at the start
+        # of every epoch is restored and the epoch re-run on the co-residency-free / RCCL path); False: raise
+        self.recover = True
+        self.recovered: str | None = None
 
     def _setup_xgmi(self, mode: str):
         """Peer-to-peer fused all-reduce+SGD (parallel/xgmi.py) when every rank is a GPU on this node.
@@ -639,6 +643,54 @@ class DataParallelTrainer:
         else:
             self._enqueue_plan(plan, lr, reg)
 
+    # ------------------------------------------------------------- recovery
+    def _fall_back_to_comm(self) -> None:
+        """Collective: drop the xGMI all-reduce (its sticky error word and per-tile epochs can no longer be trusted
+        after a timed-out peer wait) and use the communicator's all-reduce (RCCL on GPUs), bucketed and overlapped
+        where the gradient spans several buckets -- the same choice __init__ makes with allreduce="rccl"."""
+        self.engine.attach_xgmi(None)
+        for name in ("_xgmi_fused", "xgmi"):
+            b = getattr(self, name)
+            if b is not None:
+                b.close()
+                setattr(self, name, None)
+        self.fused_allreduce = False
+        self.allreduce_mode = "rccl"
+        self._bucketed = (self.R > 1 and self.engine.supports_bucketed_wgrad and self.engine.device.type == "cuda"
+                          and len(self._buckets()) > 1)
+        self._comm_stream = torch.cuda.Stream(self.engine.device) if self._bucketed else None
+        self.use_graphs = self.use_graphs and (self.R == 1 or self.comm.graph_capturable)
+        self.allreduce_impl = self.comm.name if self.R > 1 else "none"
+
+    def _recover_epoch(self, ex: Exception, snap) -> bool:
+        """Collective (every rank raised ``ex`` together from assert_comm_ok): restore the epoch-start snapshot and
+        switch to the path that cannot hit the same failure -- a timed-out all-gather forward + head launch ->
+        the last-arriver form (no workgroup waits for another, mlp_fwd1_head); a timed-out xGMI peer wait -> the
+        communicator's all-reduce.  Once per trainer; returns False when the failure must propagate."""
+        if not self.recover or self.recovered is not None or snap is None:
+            return False
+        e = self.engine
+        if e.device.type == "cuda":
+            torch.cuda.synchronize(e.device)
+        what = "hand-off" if isinstance(ex, KernelHandoffTimeout) else "peer wait"
+        if isinstance(ex, KernelHandoffTimeout):
+            e.set_fh_allgather(False)
+            e.ag_err.zero_()
+        # a rank whose forward timed out stops taking part in the xGMI exchange, so its peers' waits time out
+        # too: the buckets are poisoned whichever failure was raised
+        if (self.xgmi is not None or self._xgmi_fused is not None) and (isinstance(ex, CommFailure)
+                                                                         or self.comm_failed()):
+            self._fall_back_to_comm()
+        self._restore(snap[0])
+        self.iter = snap[1]
+        self._graphs.clear()
+        self.recovered = f"{what} timed out at epoch-start iter {snap[1]}; re-ran on " + (
+            "the last-arriver forward + head" if isinstance(ex, KernelHandoffTimeout) else self.allreduce_impl)
+        if self.rank == 0:
+            print(f"warning: {ex} -- restored the epoch-start snapshot and continuing "
+                  f"({self.recovered})", flush=True)
+        return True
+
     # ---------------------------------------------------------------- train
     def train(self, epochs: int, lr: float, reg: float, print_every: int = 0, debug: bool = False,
               outdir: str = "Outputs", log=print, on_event=None, fault: tuple[int, int] | None = None,
@@ -678,45 +730,61 @@ class DataParallelTrainer:
             if fault is not None and fault[0] == self.rank and first <= fault[1] < first + count:
                 raise FaultInjected(f"injected fault on rank {self.rank} at step {fault[1]}")
 
+        def run_epoch(epoch: int) -> None:
+            if not host_needed:
+                maybe_fault(self.iter, len(plan.steps))
+                with self.roctx.range(f"epoch {epoch}"):
+                    self.run_plan(plan, lr, reg)
+                if xgmi_live or ag_live:
+                    self.assert_comm_ok()  # syncs; every rank raises together
+                self.iter += len(plan.steps)
+                stats.steps += len(plan.steps)
+                stats.images += sum((ln // self.R) * self.R for _, ln in plan.steps)
+                if on_event is not None:
+                    if dev.type == "cuda":
+                        torch.cuda.synchronize(dev)
+                    el = time.perf_counter() - t0
+                    on_event({"event": "epoch", "epoch": epoch, "iter": self.iter, "seconds": el,
+                              "images_per_s": stats.images / el if el > 0 else None})
+                return
+            for bi, (s, ln) in enumerate(plan.steps):
+                it = self.iter
+                maybe_fault(it, 1)
+                if print_every > 0 and it % print_every == 0:
+                    l = self.step_loss(s, ln, lr, reg)
+                    stats.losses.append(l)
+                    if self.rank == 0:
+                        log(f"Loss at iteration {it} of epoch {epoch}/{epochs} = {l:.10g}")
+                    if on_event is not None:
+                        on_event({"event": "loss", "iter": it, "epoch": epoch, "loss": l})
+                else:
+                    self.step(s, ln, lr, reg)
+                print_flag = (bi == 0) if print_every <= 0 else (it % print_every == 0)
+                if debug and print_flag and self.rank == 0:
+                    self.sync_to(self.nn)
+                    write_diff_gpu_cpu(self.nn, it, err_file, outdir)
+                self.iter += 1
+                stats.steps += 1
+                stats.images += (ln // self.R) * self.R
+            if xgmi_live or ag_live:
+                self.assert_comm_ok()
+
         try:
             for epoch in range(epochs):
-                if not host_needed:
-                    maybe_fault(self.iter, len(plan.steps))
-                    with self.roctx.range(f"epoch {epoch}"):
-                        self.run_plan(plan, lr, reg)
-                    if xgmi_live or ag_live:
-                        self.assert_comm_ok()  # syncs; every rank raises together
-                    self.iter += len(plan.steps)
-                    stats.steps += len(plan.steps)
-                    stats.images += sum((ln // self.R) * self.R for _, ln in plan.steps)
-                    if on_event is not None:
-                        if dev.type == "cuda":
-                            torch.cuda.synchronize(dev)
-                        el = time.perf_counter() - t0
-                        on_event({"event": "epoch", "epoch": epoch, "iter": self.iter, "seconds": el,
-                                  "images_per_s": stats.images / el if el > 0 else None})
-                    continue
-                for bi, (s, ln) in enumerate(plan.steps):
-                    it = self.iter
-                    maybe_fault(it, 1)
-                    if print_every > 0 and it % print_every == 0:
-                        l = self.step_loss(s, ln, lr, reg)
-                        stats.losses.append(l)
-                        if self.rank == 0:
-                            log(f"Loss at iteration {it} of epoch {epoch}/{epochs} = {l:.10g}")
-                        if on_event is not None:
-                            on_event({"event": "loss", "iter": it, "epoch": epoch, "loss": l})
-                    else:
-                        self.step(s, ln, lr, reg)
-                    print_flag = (bi == 0) if print_every <= 0 else (it % print_every == 0)
-                    if debug and print_flag and self.rank == 0:
-                        self.sync_to(self.nn)
-                        write_diff_gpu_cpu(self.nn, it, err_file, outdir)
-                    self.iter += 1
-                    stats.steps += 1
-                    stats.images += (ln // self.R) * self.R
-                if xgmi_live or ag_live:
-                    self.assert_comm_ok()
+                # the recovery point: parameters (+ derived planes) and the step counter at the epoch start
+                can_recover = (self.recover and self.recovered is None and (xgmi_live or ag_live))
+                snap = (self._snapshot(), self.iter, stats.steps, stats.images, len(stats.losses)) \
+                    if can_recover else None
+                try:
+                    run_epoch(epoch)
+                except (KernelHandoffTimeout, CommFailure) as ex:
+                    if not self._recover_epoch(ex, snap):
+                        raise
+                    stats.steps, stats.images = snap[2], snap[3]
+                    del stats.losses[snap[4]:]
+                    xgmi_live = self.xgmi is not None or self._xgmi_fused is not None
+                    ag_live = self._allgather_live()
+                    run_epoch(epoch)  # the same epoch again on the fallback path (a second failure raises)
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
             if xgmi_live and not self.replicas_agree():

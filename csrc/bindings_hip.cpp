@@ -44,7 +44,7 @@ struct MlpStep {
   uintptr_t loss = 0;                                 // float partials, >= head blocks
   int shift = 1, act = 1;
   // split-bf16 path (mlp_split.h): X/XT are bf16, W1p/dZ1p hold npw/npz bf16 planes
-  int split = 0, npw = 3, npz = 3, fused_head = 0;
+  int split = 0, npw = 3, npz = 3;
   uintptr_t stamps = 0;  // diagnostics only
   uintptr_t hstamps = 0;  // diagnostics only: head-block stamps
   uintptr_t z2p = 0;     // wide-layer head scratch (head_big_scratch_floats), 0: column head
@@ -108,12 +108,6 @@ struct MlpStep {
   }
   float xscale = 1.f;    // split path: inputs are uint8 * xscale
   uintptr_t W1p = 0, dZ1p = 0;
-  // split3 small layers: bit0 fp32 W1, bit1 fp32 dZ1 split in registers (SplitStepArgs.a_fp32).  -1 = by
-  // measurement (bench/kbench.py +a<bits>): fp32 W1 always (one split per weight per column tile is cheaper
-  // than pulling 6 B); fp32 dZ1 only above H = 128, where the separate head's plane stores cost ~2 us at
-  // H = 300 -- at H <= 128 the all-gather head stores planes cheaply and the 25-fold re-split of dZ1 in the
-  // dW1 tiles costs +0.5 us (VALU: 4 cycles per wave64 op on the 16-lane SIMD)
-  int a_fp32 = -1;
   // wide split3 layers: the in-place dW1 update skips the W1-plane refresh (SplitStepArgs::w1_planes_lazy) and
   // planes_stale records it; refresh_planes() re-splits W1 before any forward that reads the planes
   int lazy_planes = 0;
@@ -123,11 +117,39 @@ struct MlpStep {
     cme::mlp_split_planes(P_<float>(W1), reinterpret_cast<void*>(W1p), (int64_t)H * P, npw, S(stream));
     planes_stale = false;
   }
-  int rega_wc = 1;    // SplitStepArgs::rega_wc (wide bf16 dW1 wave layout; 2 for A/B)
-  int poll_skip = 1;  // SplitStepArgs::poll_skip (hand-off polls re-load only missing granules; 0 for A/B)
-  int u8_pairs = 1;  // SplitStepArgs::u8_pairs (the pixel operand's 16-byte chunk-pair loads; 0 for A/B)
   uintptr_t kpart = 0;  // split-K dW1 partial slabs (SplitStepArgs::kpart), kpart_cap floats; 0: no split-K
   int64_t kpart_cap = 0;
+
+  // Binds the engine's buffers and shapes in ONE call (MlpEngine._hip_step): every device pointer, count and
+  // layout flag the step reads, by name; an unknown name is an error.  The runtime switches stay plain fields
+  // (fh_allgather, store_a1, lazy_planes, ag_*, diagnostics).
+  void bind(const py::dict& d) {
+    for (const auto& kv : d) {
+      const std::string k = py::str(kv.first);
+      const py::handle v = kv.second;
+      auto u = [&] { return v.cast<uintptr_t>(); };
+      auto i = [&] { return v.cast<int>(); };
+      if (k == "dt") dt = i(); else if (k == "P") P = i(); else if (k == "H") H = i(); else if (k == "C") C = i();
+      else if (k == "ld") ld = i(); else if (k == "N") N = v.cast<int64_t>();
+      else if (k == "X") X = u(); else if (k == "labels") labels = u(); else if (k == "XT") XT = u();
+      else if (k == "Xw") Xw = u(); else if (k == "XTw") XTw = u();
+      else if (k == "W1") W1 = u(); else if (k == "b1") b1 = u(); else if (k == "W2") W2 = u();
+      else if (k == "b2") b2 = u(); else if (k == "W1g") W1g = u();
+      else if (k == "gW1") gW1 = u(); else if (k == "gb1") gb1 = u(); else if (k == "gW2") gW2 = u();
+      else if (k == "gb2") gb2 = u(); else if (k == "gstatus") gstatus = u();
+      else if (k == "a1") a1 = u(); else if (k == "D") D = u(); else if (k == "dZ1") dZ1 = u();
+      else if (k == "dZ1g") dZ1g = u(); else if (k == "loss") loss = u();
+      else if (k == "act") act = i(); else if (k == "split") split = i(); else if (k == "npw") npw = i();
+      else if (k == "npz") npz = i(); else if (k == "xscale") xscale = v.cast<float>();
+      else if (k == "W1p") W1p = u(); else if (k == "dZ1p") dZ1p = u();
+      else if (k == "z2p") z2p = u(); else if (k == "bias_col") bias_col = i();
+      else if (k == "fh_counters") fh_counters = u(); else if (k == "fh_tiles") fh_tiles = i();
+      else if (k == "ag_counters") ag_counters = u(); else if (k == "ag_slabs") ag_slabs = u();
+      else if (k == "ag_gran") ag_gran = u(); else if (k == "ag_gran_count") ag_gran_count = v.cast<int64_t>();
+      else if (k == "kpart") kpart = u(); else if (k == "kpart_cap") kpart_cap = v.cast<int64_t>();
+      else throw std::invalid_argument("MlpStep.bind: unknown name '" + k + "'");
+    }
+  }
 
   cme::SplitStepArgs split_args(int64_t off, int n, double scale, double reg, double lr, int sgd,
                                 int with_loss) const {
@@ -149,10 +171,11 @@ struct MlpStep {
     a.scale = scale; a.reg = reg; a.lr = lr; a.sgd = sgd; a.shift = shift; a.mode = 0;
     a.stamps = reinterpret_cast<unsigned long long*>(stamps);
     a.bias_col = bias_col;
-    a.a_fp32 = a_fp32 >= 0 ? a_fp32 : (H <= 128 ? 1 : 3);
-    a.u8_pairs = u8_pairs;
-    a.poll_skip = poll_skip;
-    a.rega_wc = rega_wc;
+    // split3 small layers, measured (bench/kbench.py): fp32 W1 split in registers always (one split per weight
+    // per column tile is cheaper than pulling 6 B); fp32 dZ1 only above H = 128, where the separate head's plane
+    // stores cost ~2 us at H = 300 -- at H <= 128 the all-gather head stores planes cheaply and the 25-fold
+    // re-split of dZ1 in the dW1 tiles costs +0.5 us.  (The wide engines always split fp32 operands.)
+    a.a_fp32 = H <= 128 ? 1 : 3;
     a.kpart = P_<float>(kpart);
     a.kpart_cap = kpart_cap;
     // a timed-out all-gather forward + head launch (sticky word) makes every later update a no-op
@@ -180,10 +203,7 @@ struct MlpStep {
         a.xf = xf;
       }
       if (parts & 1) {
-        if (fused_head) {
-          if (!cme::mlp_split_fwd_fp32_w(a)) refresh_planes(stream);
-          cme::mlp_split_fwdhead(a, S(stream));
-        } else {  // tiled forward + the per-column head kernel (fp32 head)
+        {  // the forward GEMM + the head (fused into one launch where the shapes allow)
           cme::HeadArgs h{};
           h.a1 = a.a1; h.lda = ld; h.W2 = a.W2; h.b2 = a.b2; h.labels = a.labels; h.H = H; h.C = C; h.n = n;
           h.scale = scale; h.D = a.D; h.ldd = ld; h.dZ1 = a.dZ1; h.ldz = ld; h.dZ1_bf16 = nullptr;
@@ -439,53 +459,26 @@ PYBIND11_MODULE(_hip, m) {
 
   py::class_<MlpStep>(m, "MlpStep")
       .def(py::init<>())
-      .def_readwrite("dt", &MlpStep::dt)
-      .def_readwrite("P", &MlpStep::P)
-      .def_readwrite("H", &MlpStep::H)
-      .def_readwrite("C", &MlpStep::C)
-      .def_readwrite("ld", &MlpStep::ld)
-      .def_readwrite("X", &MlpStep::X)
-      .def_readwrite("labels", &MlpStep::labels)
-      .def_readwrite("XT", &MlpStep::XT)
-      .def_readwrite("Xw", &MlpStep::Xw)
-      .def_readwrite("XTw", &MlpStep::XTw)
-      .def_readwrite("N", &MlpStep::N)
-      .def_readwrite("W1", &MlpStep::W1)
-      .def_readwrite("b1", &MlpStep::b1)
-      .def_readwrite("W2", &MlpStep::W2)
-      .def_readwrite("b2", &MlpStep::b2)
-      .def_readwrite("W1g", &MlpStep::W1g)
-      .def_readwrite("gW1", &MlpStep::gW1)
-      .def_readwrite("gb1", &MlpStep::gb1)
-      .def_readwrite("gW2", &MlpStep::gW2)
-      .def_readwrite("gb2", &MlpStep::gb2)
-      .def_readwrite("a1", &MlpStep::a1)
-      .def_readwrite("D", &MlpStep::D)
-      .def_readwrite("dZ1", &MlpStep::dZ1)
-      .def_readwrite("dZ1g", &MlpStep::dZ1g)
-      .def_readwrite("loss", &MlpStep::loss)
-      .def_readwrite("fh_counters", &MlpStep::fh_counters)
-      .def_readwrite("fh_tiles", &MlpStep::fh_tiles)
-      .def_readwrite("ag_counters", &MlpStep::ag_counters)
-      .def_readwrite("ag_slabs", &MlpStep::ag_slabs)
+      .def("bind", &MlpStep::bind, py::arg("buffers"))
+      .def_readonly("dt", &MlpStep::dt)
+      .def_readonly("P", &MlpStep::P)
+      .def_readonly("H", &MlpStep::H)
+      .def_readonly("C", &MlpStep::C)
+      .def_readonly("ld", &MlpStep::ld)
+      .def_readonly("split", &MlpStep::split)
+      .def_readwrite("shift", &MlpStep::shift)
       .def_readwrite("ag_err", &MlpStep::ag_err)
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
-      .def_readwrite("gstatus", &MlpStep::gstatus)
       .def_readwrite("ag_wait_us", &MlpStep::ag_wait_us)
       .def_readwrite("ag_test_skip", &MlpStep::ag_test_skip)
       .def_readwrite("store_a1", &MlpStep::store_a1)
-      .def_readwrite("ag_gran", &MlpStep::ag_gran)
-      .def_readwrite("ag_gran_count", &MlpStep::ag_gran_count)
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
-      .def_readwrite("a_fp32", &MlpStep::a_fp32)
-      .def_readwrite("u8_pairs", &MlpStep::u8_pairs)
-      .def_readwrite("poll_skip", &MlpStep::poll_skip)
-      .def_readwrite("rega_wc", &MlpStep::rega_wc)
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
       .def_readwrite("planes_stale", &MlpStep::planes_stale)
+      .def_readwrite("dw2p", &MlpStep::dw2p)
+      .def_readwrite("stamps", &MlpStep::stamps)
+      .def_readwrite("hstamps", &MlpStep::hstamps)
       .def("refresh_planes", &MlpStep::refresh_planes, py::arg("stream"))
-      .def_readwrite("kpart", &MlpStep::kpart)
-      .def_readwrite("kpart_cap", &MlpStep::kpart_cap)
       .def("w1_planes_read",
            [](const MlpStep& st) {  // a forward kernel of this step reads the W1 planes (else: not refreshed)
              return st.split != 0 && cme::mlp_split_w1_planes_read(st.split_args(0, st.ld, 1.0, 0.0, 0.0, 1, 0));
@@ -499,16 +492,6 @@ PYBIND11_MODULE(_hip, m) {
            })
       .def("tp_forward", &MlpStep::tp_forward)
       .def("tp_head", &MlpStep::tp_head)
-      .def_readwrite("shift", &MlpStep::shift)
-      .def_readwrite("act", &MlpStep::act)
-      .def_readwrite("split", &MlpStep::split)
-      .def_readwrite("fused_head", &MlpStep::fused_head)
-      .def_readwrite("stamps", &MlpStep::stamps)
-      .def_readwrite("hstamps", &MlpStep::hstamps)
-      .def_readwrite("xscale", &MlpStep::xscale)
-      .def_readwrite("z2p", &MlpStep::z2p)
-      .def_readwrite("dw2p", &MlpStep::dw2p)
-      .def_readwrite("bias_col", &MlpStep::bias_col)
       .def("set_xgmi", &MlpStep::set_xgmi, py::arg("desc"), py::arg("slots"), py::arg("off_b1"), py::arg("off_W2"),
            py::arg("off_b2"))
       .def("run_steps", &MlpStep::run_steps, py::arg("gstart0"), py::arg("count"), py::arg("B"), py::arg("shard_off"),
@@ -517,21 +500,22 @@ PYBIND11_MODULE(_hip, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("run_wgrad", &MlpStep::run_wgrad, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"),
            py::arg("lr"), py::arg("sgd"), py::arg("parts"), py::arg("row0"), py::arg("rows"), py::arg("stream"))
-      .def_readwrite("npw", &MlpStep::npw)
-      .def_readwrite("npz", &MlpStep::npz)
-      .def_readwrite("W1p", &MlpStep::W1p)
-      .def_readwrite("dZ1p", &MlpStep::dZ1p)
       .def("predict",
            [](MlpStep& st, uintptr_t x, int n, uintptr_t a1buf, int lda, uintptr_t pred, uintptr_t s) {
-             // split path forward + argmax for n samples at x (bf16 [n][P]); a1buf: [H][lda] scratch
+             // split path forward + argmax for n samples at x (uint8 [n][P]); a1buf: [H][lda] scratch.  The
+             // tiled forward (wave-split-K: the wide engines' bf16 copies are of the training set, not of x)
+             // into a1buf, then the column head in predict mode
              st.refresh_planes(s);
              cme::SplitStepArgs a = st.split_args(0, n, 1.0, 0.0, 0.0, 0, 0);
              a.X = reinterpret_cast<const void*>(x);
+             a.Xw = nullptr;
              a.a1 = reinterpret_cast<float*>(a1buf);
              a.ld = lda;
-             a.mode = cme::HEAD_PREDICT;
-             a.pred = reinterpret_cast<int*>(pred);
-             cme::mlp_split_fwdhead(a, S(s));
+             cme::mlp_split_fwd1(a, S(s));
+             cme::HeadArgs h{};
+             h.a1 = a.a1; h.lda = lda; h.W2 = a.W2; h.b2 = a.b2; h.H = st.H; h.C = st.C; h.n = n;
+             h.shift = st.shift; h.mode = cme::HEAD_PREDICT; h.pred = reinterpret_cast<int*>(pred);
+             cme::mlp_head(DType::F32, h, S(s));
            },
            py::arg("x"), py::arg("n"), py::arg("a1buf"), py::arg("lda"), py::arg("pred"), py::arg("stream"))
       .def("run", &MlpStep::run, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"), py::arg("lr"),
@@ -558,7 +542,6 @@ PYBIND11_MODULE(_hip, m) {
       },
       py::arg("params"), py::arg("grads"), py::arg("count"), py::arg("lr"), py::arg("W1p"), py::arg("w1n"),
       py::arg("npw"), py::arg("stream") = 0, py::arg("status") = 0);
-  m.def("split_fwdhead_blocks", &cme::mlp_split_fwdhead_blocks);
   m.def("mlp_split_fused_tiles", &cme::mlp_split_fused_tiles, py::arg("P"), py::arg("H"), py::arg("cap"));
 
   bind_suite(m);

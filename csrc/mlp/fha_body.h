@@ -125,7 +125,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   {
     float z = 0.f;
     const bool good = gran_poll<8>(slabs, (unsigned)(ct * tm * 16 * kCols + c * kCols + col), 16u * kCols, tm,
-                                   c < C, ep, (uint32_t)f.ag_wait_us, [&](int, float v) { z += v; }, f.poll_skip != 0);
+                                   c < C, ep, (uint32_t)f.ag_wait_us, [&](int, float v) { z += v; });
     if (!good && (t & 63) == 0) {
       atomicExch(err, 1);
       s_bad = 1;

@@ -1,7 +1,8 @@
 // Direct-to-LDS (buffer_load ... lds) MFMA tile engine for the WIDE MLP GEMMs (H >= 512: BASELINE
-// configs 4 and 5, 784-4096-10 and 784-1024-10) -- the successor of lds_gemm.h's register-staged engine.
+// configs 4 and 5, 784-4096-10 and 784-1024-10) -- the successor of round 1's register-staged engine (removed
+// in round 4: never selected once the bf16 copies of X existed).
 //
-// What limited lds_gemm.h (profiles/wide4096_pmc.md): global -> VGPR -> LDS staging with two LDS buffers
+// What limited that engine (profiles/wide4096_pmc.md): global -> VGPR -> LDS staging with two LDS buffers
 // leaves ONE stage of loads in flight behind each barrier, the waves spend ~45 % parked at the per-stage
 // barrier / vmcnt wait and MFMA is busy ~20-30 %.  Here (cdna_hip_programming.md §5 "Pipelining across
 // barriers", the glds row of its staging table):
@@ -24,12 +25,14 @@
 //
 // Operands: C[m][n] = sum_k A[m][k] B[n][k], both K-contiguous ("NT"); A = NPA exact bf16 planes of an
 // fp32 matrix stored plane_bytes apart (split-fp32, mlp_split.h) or one bf16 plane; B bf16.  The
-// accumulator layout and wave layout (8 waves as 4 x 2) are lds_gemm.h's; the epilogue is the caller's, with
+// accumulator layout is the 16x16x32 MFMA's (8 waves as 4 x 2); the epilogue is the caller's, with
 // its operand loads issued before the K loop and branch-free buffer stores (an element functor that loads
 // b1[row] / W1[i] behind a bounds branch serialises one dependent L2 round trip per output element).
 #pragma once
 
-#include "lds_gemm.h"
+#include "mma_tile.h"
+
+#include <type_traits>
 
 namespace cme {
 

@@ -47,7 +47,7 @@ __device__ __forceinline__ gran_t gran_load(const gran_t* p) {  // sc1 load (L2-
 // stores and polls of the workgroups they wait for.  The first pass is unchanged: no added latency.
 template <int N, class F>
 __device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsigned stride, int cnt, bool need,
-                                          unsigned ep, uint32_t limit_us, F&& f, bool skip = true) {
+                                          unsigned ep, uint32_t limit_us, F&& f) {
   static_assert(N <= 32, "ready mask");
   // the granule addresses, once: k >= cnt re-reads granule 0 (needed anyway, so its tag check is the same)
   const gran_t* p[N];
@@ -64,7 +64,7 @@ __device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsi
     if (!done) {
 #pragma unroll
       for (int k = 0; k < N; ++k)
-        if (!(skip && (rdy & (1u << k)))) x[k] = gran_load(p[k]);
+        if (!(rdy & (1u << k))) x[k] = gran_load(p[k]);
 #pragma unroll
       for (int k = 0; k < N; ++k) rdy |= (unsigned)((unsigned)(x[k] >> 32) == ep) << k;
       done = rdy == kAll;

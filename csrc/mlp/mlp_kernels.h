@@ -43,9 +43,8 @@ struct HeadArgs {
   void* probs; int ldp;           // probs mode: [C][ldp]
   int shift;                      // 1: max-shifted softmax; 0: reference form (common.cpp:13-18)
   int mode;
-  // wide layers (H >= 512, fp32 params, train mode): scratch of head_big_scratch_floats(H, n) floats for
-  // the split-H z2 partial sums; when set, the head runs as two grid-wide kernels instead of one
-  // column-parallel kernel whose per-thread loop over H is serial
+  // wide layers (H >= 512, fp32 params, train mode): scratch of head_big_scratch_floats(H, n) floats for the
+  // z2 row-tile partial sums the forward GEMM leaves (z2_chunks below)
   float* z2part = nullptr;
   // > 0: z2part already holds z2_chunks row-tile partials [chunk][16][lda] left by the forward GEMM
   // (SplitStepArgs::z2part); the head then only reduces them and never re-reads a1 for z2

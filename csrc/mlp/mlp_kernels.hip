@@ -108,7 +108,7 @@ __device__ __forceinline__ void head_stage(const HeadArgs& a, int t, int nthr, P
   if (t < NC) ws[tot + t] = buf_load1<P>(rb, t < C ? t * (int)sizeof(P) : kOOB);
 }
 
-template <typename P, int NC, bool LDSW, int HPT, bool SC1 = false, bool STAGED = false>
+template <typename P, int NC, bool LDSW, int HPT>
 __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, const int t, char* head_dyn,
                                            P (*zred)[NC][kHeadCols], float* lred) {
   // One head block (kHeadCols columns, 256 threads) -- vb: the block index, t: thread in [0, 256);
@@ -116,8 +116,6 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
   // HPT > 0: every thread owns at most HPT hidden units (H <= HPT * NPART); their
   // a1 values are loaded ONCE (one burst, before the W2 staging barrier) and
   // reused by both passes.  HPT == 0: generic loop for large H.
-  // SC1: a1 was written earlier in the SAME launch by other workgroups with write-through (sc1)
-  // stores; it is read with sc1 loads (L1 bypass), the hand-off form of fwd1_head_kernel.
   constexpr int COLS = kHeadCols;
   constexpr int NPART = 256 / COLS;
   const P* __restrict__ a1 = static_cast<const P*>(a.a1);
@@ -138,27 +136,10 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
 #pragma unroll
     for (int u = 0; u < HPT; ++u) {
       const int h = part + u * NPART;
-      const int off = h < H ? (h * a.lda + b) * (int)sizeof(P) : kOOB;
-      if constexpr (SC1) {
-        static_assert(std::is_same_v<P, float>, "sc1 hand-off: fp32 a1");
-        xa[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, kSc1));
-      } else {
-        xa[u] = buf_load1<P>(rs, off);
-      }
+      xa[u] = buf_load1<P>(rs, h < H ? (h * a.lda + b) * (int)sizeof(P) : kOOB);
     }
   }
-  // STAGED: the caller ran head_stage into head_dyn and a barrier already
-  static_assert(!STAGED || LDSW, "staged head needs the LDS copy of W2");
-  auto hstamp = [&](int i, bool drain) {  // diagnostics (HeadArgs::stamps): wave 0 lane 0 of the block
-    if (a.stamps) {
-      if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned long long tt = __builtin_amdgcn_s_memrealtime();
-      if (t == 0) a.stamps[(size_t)vb * 8 + i] = tt;
-    }
-  };
-  hstamp(0, false);
-  hstamp(1, true);
-  if constexpr (LDSW && !STAGED) {
+  if constexpr (LDSW) {
     head_stage<P, NC>(a, t, 256, ws);
     __syncthreads();
   }
@@ -222,7 +203,6 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
     return;
   }
 
-  hstamp(2, false);
   // ---- softmax over the C classes of this column (registers only)
   P m = P(0);
   if (a.shift) {
@@ -274,7 +254,6 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
     if (t == 0 && vb * COLS < a.n) a.loss_partial[vb] = lred[0] + lred[1] + lred[2] + lred[3];
   }
   // ---- pass 2: dZ1 = (W2^T D) .* a1 .* (1 - a1)
-  hstamp(3, false);
   if (!valid) return;
   P* dZ1 = static_cast<P*>(a.dZ1);
   __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
@@ -303,8 +282,6 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
       const int h = part + u * NPART;
       if (h < H) emit(h, xa[u]);
     }
-    hstamp(4, false);
-    hstamp(5, true);
   } else {
     for (int h = part; h < H; h += NPART) emit(h, a1[(size_t)h * a.lda + bcol]);
   }
@@ -599,155 +576,10 @@ void launch_head(const HeadArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------ K2 for wide layers (H >= 512)
-// z2 = W2 a1 split over H-chunks (partial sums, deterministic), then one pass
-// that finishes softmax / D / loss per column and writes dZ1 (+ planes) for
-// its (H-chunk x 64-column) block: the whole chip works on both phases.
-constexpr int kHBCols = 64, kHBRows = 256, kHBMinH = 512;
+// scratch for the forward GEMM's z2 row-tile partials: [chunk][16][ld], 64-row chunks at most
+constexpr int kHBCols = 64;
 inline int hb_cdiv(int a, int b) { return (a + b - 1) / b; }
-
 inline int hb_cols_pad(int n) { return hb_cdiv(n, kHBCols) * kHBCols; }
-
-template <int NC>
-__device__ __forceinline__ void hb_stage_w2(const float* __restrict__ W2, int C, int H, int h0,
-                                            float (*w2s)[kHBRows]) {
-  for (int i = threadIdx.x; i < NC * kHBRows; i += 256) {
-    const int c = i / kHBRows, hh = i - c * kHBRows;
-    w2s[c][hh] = (c < C && h0 + hh < H) ? W2[(size_t)c * H + h0 + hh] : 0.f;
-  }
-}
-
-template <int NC>
-__global__ __launch_bounds__(256) void head_big_z2_kernel(HeadArgs a, int ncb) {
-  __shared__ float w2s[NC][kHBRows];
-  __shared__ float red[4][NC][kHBCols];
-  const int cb = blockIdx.x % ncb, ch = blockIdx.x / ncb;
-  const int t = threadIdx.x, col = t & 63, hq = t >> 6;
-  const int h0 = ch * kHBRows;
-  hb_stage_w2<NC>(static_cast<const float*>(a.W2), a.C, a.H, h0, w2s);
-  __syncthreads();
-  const int bcol = cb * kHBCols + col;
-  const bool ok = bcol < a.n;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.a1);
-  float z[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) z[c] = 0.f;
-#pragma unroll 2
-  for (int j0 = 0; j0 < 64; j0 += 16) {
-    float x[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int h = h0 + hq * 64 + j0 + u;
-      x[u] = buf_load1<float>(ra, (ok && h < a.H) ? (h * a.lda + bcol) * 4 : kOOB);
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-#pragma unroll
-      for (int c = 0; c < NC; ++c) z[c] += w2s[c][hq * 64 + j0 + u] * x[u];
-  }
-#pragma unroll
-  for (int c = 0; c < NC; ++c) red[hq][c][col] = z[c];
-  __syncthreads();
-  const int ldz = ncb * kHBCols;
-  for (int i = t; i < NC * kHBCols; i += 256) {
-    const int c = i / kHBCols, cc = i - c * kHBCols;
-    a.z2part[((size_t)ch * NC + c) * ldz + cb * kHBCols + cc] = red[0][c][cc] + red[1][c][cc] + red[2][c][cc] + red[3][c][cc];
-  }
-}
-
-template <int NC>
-__global__ __launch_bounds__(256) void head_big_dz_kernel(HeadArgs a, int ncb, int nch) {
-  __shared__ float w2s[NC][kHBRows];
-  __shared__ float ds[NC][kHBCols];
-  __shared__ float lsum[kHBCols];
-  const int cb = blockIdx.x % ncb, ch = blockIdx.x / ncb;
-  const int t = threadIdx.x, col = t & 63, hq = t >> 6;
-  const int h0 = ch * kHBRows;
-  hb_stage_w2<NC>(static_cast<const float*>(a.W2), a.C, a.H, h0, w2s);
-  const int bcol = cb * kHBCols + col;
-  const bool ok = bcol < a.n;
-  if (t < kHBCols) {  // finish z2 -> softmax -> D for this column (every H-chunk block recomputes it)
-    const int ldz = ncb * kHBCols;
-    const float* b2 = static_cast<const float*>(a.b2);
-    float z[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) z[c] = c < a.C ? b2[c] : 0.f;
-    for (int k = 0; k < nch; ++k)
-#pragma unroll
-      for (int c = 0; c < NC; ++c) z[c] += a.z2part[((size_t)k * NC + c) * ldz + bcol];
-    float m = 0.f;
-    if (a.shift) {
-      m = z[0];
-#pragma unroll
-      for (int c = 1; c < NC; ++c) m = (c < a.C && z[c] > m) ? z[c] : m;
-    }
-    float sum = 0.f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      z[c] = c < a.C ? __expf(z[c] - m) : 0.f;
-      sum += z[c];
-    }
-    const float inv = 1.f / sum;
-    const int lab = ok ? a.labels[bcol] : 0;
-    float pl = 1.f;
-    const float sc = (float)a.scale;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const float y = z[c] * inv;
-      pl = c == lab ? y : pl;
-      const float d = (y - (c == lab ? 1.f : 0.f)) * sc;
-      ds[c][col] = (ok && c < a.C) ? d : 0.f;
-      if (ch == 0 && ok && c < a.C) static_cast<float*>(a.D)[(size_t)c * a.ldd + bcol] = d;
-    }
-    lsum[col] = ok ? -__logf(pl) : 0.f;
-  }
-  __syncthreads();
-  if (ch == 0 && a.loss_partial && t < kHBCols / 16) {  // the column head's partial layout: one per 16 columns
-    const int g = cb * (kHBCols / 16) + t;
-    if (g * 16 < a.n) {
-      float s = 0.f;
-      for (int k = 0; k < 16; ++k) s += lsum[t * 16 + k];
-      a.loss_partial[g] = s;
-    }
-  }
-  if (!ok) return;
-  // dZ1 = (W2^T D) .* a1 .* (1 - a1) for rows [h0, h0 + 256) of this column
-  float dcol[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) dcol[c] = ds[c][col];
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(a.a1);
-  float* dZ1 = static_cast<float*>(a.dZ1);
-  __hip_bfloat16* dZlo = static_cast<__hip_bfloat16*>(a.dZ1_bf16);
-  __hip_bfloat16* dZp = static_cast<__hip_bfloat16*>(a.dZ1_planes);
-  const size_t pstride = (size_t)a.H * a.ldz;
-  for (int j0 = 0; j0 < 64; j0 += 16) {
-    float x[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int h = h0 + hq * 64 + j0 + u;
-      x[u] = buf_load1<float>(ra, h < a.H ? (h * a.lda + bcol) * 4 : kOOB);
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int hl = hq * 64 + j0 + u, h = h0 + hl;
-      if (h >= a.H) break;
-      float da = 0.f;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) da += w2s[c][hl] * dcol[c];
-      const float dz = da * x[u] * (1.f - x[u]);
-      const size_t zi = (size_t)h * a.ldz + bcol;
-      dZ1[zi] = dz;
-      if (dZlo) dZlo[zi] = __float2bfloat16(dz);
-      if (dZp) {
-        float r = dz;
-        for (int p = 0; p < a.npz; ++p) {
-          const __hip_bfloat16 q = __float2bfloat16(r);
-          dZp[p * pstride + zi] = q;
-          r -= __bfloat162float(q);
-        }
-      }
-    }
-  }
-}
 
 // ----------------------------------- K2 for wide layers when the forward GEMM left z2 partials
 // (HeadArgs::z2_chunks > 0, see EpiSigBig::tile in mlp_split.hip).  One 512-thread workgroup per
@@ -974,13 +806,6 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     hstamp(3);
   }
-}
-
-template <int NC>
-void launch_head_big(const HeadArgs& a, hipStream_t s) {
-  const int ncb = hb_cdiv(a.n, kHBCols), nch = hb_cdiv(a.H, kHBRows);
-  head_big_z2_kernel<NC><<<ncb * nch, 256, 0, s>>>(a, ncb);
-  head_big_dz_kernel<NC><<<ncb * nch, 256, 0, s>>>(a, ncb, nch);
 }
 
 // ----------------------------------------------------------------- K3: wgrad
@@ -1315,7 +1140,7 @@ static int fha_vec(const SplitStepArgs& f) {
   const bool af = mlp_split_fwd_fp32_w(f);
   const uintptr_t x = reinterpret_cast<uintptr_t>(f.X);
   if (x % 4 != 0 || reinterpret_cast<uintptr_t>(af ? (const void*)f.W1 : f.W1p) % 16 != 0 || f.P % 8 != 0) return 0;
-  return f.u8_pairs && x % 16 == 0 && f.P % 16 == 0 ? 3 : 1;
+  return x % 16 == 0 && f.P % 16 == 0 ? 3 : 1;
 }
 
 bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f) {
@@ -1355,8 +1180,8 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
   CME_LAUNCH_CHECK(s);
 }
 
-// covers both the two-kernel head's split-H partials and the forward GEMM's row-tile partials
-// (64-row tiles at most, pitch = the activation ld <= hb_cols_pad(n) for ld = n rounded to 16)
+// the forward GEMM's row-tile partials (64-row tiles at most, pitch = the activation ld <= hb_cols_pad(n) for
+// ld = n rounded to 16)
 int64_t head_big_scratch_floats(int H, int n) { return (int64_t)cdiv(H, 64) * kCMax * hb_cols_pad(n); }
 
 void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
@@ -1376,13 +1201,8 @@ void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
     CME_LAUNCH_CHECK(s);
     return;
   }
-  if (a.z2part && dt != DType::F64 && a.mode == HEAD_TRAIN && a.H >= kHBMinH) {
-    CME_REQUIRE((int64_t)a.H * a.lda < (int64_t)kOOB / 4, "mlp_head: a1 too large for 32-bit buffer offsets");
-    if (a.C == 10) launch_head_big<10>(a, s);
-    else launch_head_big<16>(a, s);
-    CME_LAUNCH_CHECK(s);
-    return;
-  }
+  // (a wide head without the forward's partials -- only the head-alone profiling hook, MlpStep.run parts & 8 --
+  // takes the column head below; round 1-3's two-kernel split-H head for that case was removed in round 4)
   if (dt != DType::F64 && head32_ok(a) && (int64_t)a.H * a.lda < (int64_t)kOOB / 4) {  // MFMA head
     head32_kernel<<<cdiv(a.n, kH32Cols), 512, 0, s>>>(a);
     CME_LAUNCH_CHECK(s);

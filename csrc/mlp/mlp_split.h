@@ -14,11 +14,10 @@
 // With npw = npz = 1 the identical kernels ARE the bf16 mixed-precision path.
 //
 // The step becomes TWO kernels:
-//   A  mlp_split_fwdhead : per 16-sample block, all of z1 (MFMA) -> sigmoid ->
-//                          z2 -> softmax -> D -> dZ1 (+ its planes); nothing
-//                          round-trips through another launch.
-//   B  mlp_split_wgrad   : dW1 (MFMA, planes) with fused reg + SGD + W1-plane
-//                          refresh, dW2 and bias gradients as extra roles.
+//   A  forward GEMM + head (mlp_fwd1_head_ag at H <= 128, mlp_fwd1_wide_ag for the
+//      wide layers): z1 (MFMA) -> sigmoid -> z2 -> softmax -> D -> dZ1 in one launch;
+//   B  mlp_split_wgrad : dW1 (MFMA) with fused reg + SGD (+ W1-plane refresh where
+//      a forward reads the planes), dW2 and bias gradients as extra roles.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -84,16 +83,14 @@ struct SplitStepArgs {
   // on the activated accumulators), so the head never re-reads a1 for z2 (mlp_split_fwd1_z2_chunks)
   float* z2part = nullptr;
   // wide layers: bf16 copies of the shard (Xw = Xw_base + off*P, [n][P]; XTw = XTw_base + off, [P+1][ldxt])
-  // for the direct-to-LDS GEMM engine (glds_gemm.h); nullptr: the register-staged engine reads the uint8s
+  // for the direct-to-LDS GEMM engines (glds_gemm.h, rega_gemm.h); nullptr: the wave-split-K kernels read the uint8s
   const void* Xw = nullptr;
   const void* XTw = nullptr;
   // small layers (wave-split-K kernels), split3 only: bit0 = the forward GEMM reads fp32 W1, bit1 = the dW1
   // GEMM reads fp32 dZ1 (4 B per element, split into the exact bf16 planes in registers; the head then
-  // writes no dZ1 planes); clear bits: the stored planes (6 B per element, split once by their writer)
+  // writes no dZ1 planes); clear bits: the stored planes (6 B per element, split once by their writer).
+  // Policy (MlpStep::split_args, measured: bench/kbench.py): 1 at H <= 128, 3 above
   int a_fp32 = 1;
-  // small layers: the uint8 pixel operand of the wave-split-K GEMMs as ONE 16-byte load per lane per pair of
-  // K chunks (mma_tile.h VEC = 3) where rows are 16-byte aligned and K % 16 == 0; 0: two 4-byte loads per chunk
-  int u8_pairs = 1;
   // wide layers: the head left dW2 partials [cdiv(n, 32)][16][H] (HeadArgs::dw2part); the dW2 role then sums
   // them in column-tile order instead of forming D . a1^T from all of a1
   float* dw2part = nullptr;
@@ -102,9 +99,6 @@ struct SplitStepArgs {
   // wide split3 layers: the A-in-registers dW1 launch's in-place update (sgd = 1) leaves the W1 planes alone (the
   // 128 x 128 forward reads fp32 W1); the caller marks them stale and refreshes them before a forward that reads them
   int w1_planes_lazy = 0;
-  // wide bf16 (split1) layers: the A-in-registers dW1 launch's wave layout, 8 x 1 (1: each wave 16 rows x 128
-  // columns) or 4 x 2 (2: 32 rows x 64 columns, half the B-fragment LDS reads; A rows loaded by two waves)
-  int rega_wc = 1;
   // The all-gather forward + head launches' timed-out-wait word (MlpEngine.ag_err).  The weight-gradient
   // launch reads it and, when set, APPLIES NOTHING: no SGD / plane refresh (sgd = 1), no xGMI exchange (the
   // fused all-reduce: this rank stops taking part, its peers time out), and the gradient status word below
@@ -117,8 +111,6 @@ struct SplitStepArgs {
   // hook: row tile ag_test_skip of column tile 0 withholds its granules, so that tile's wait really times out
   // (-1: off)
   int ag_wait_us = (int)kHandoffWaitUs;
-  // the hand-off polls re-load only the granules still missing (granule.h gran_poll; 0: every granule every pass, A/B)
-  int poll_skip = 1;
   int ag_test_skip = -1;
 };
 
@@ -144,7 +136,6 @@ bool mlp_split_wide_fwd_reads_planes(const SplitStepArgs& a, int ag, int allow64
 // feature; -1 when above `cap`
 int mlp_split_fused_tiles(int P, int H, int cap);
 
-void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s);
 // tiled forward only: a1 = sigmoid(W1 X + b1) (pair with mlp_head for the 3-kernel step)
 void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s);
 // wide layers: the forward GEMM with the head fused in (all-gather form; fwd1_rega_kernel<..., AG> on 128 x 128
@@ -161,7 +152,6 @@ int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long lo
                      unsigned long long* gran, int64_t gran_count, int* err, int store_a1, int allow64,
                      hipStream_t s);
 void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s);
-int mlp_split_fwdhead_blocks(int n);
 
 // planes[p][i] for i < n: exact np-way bf16 split of W[i] (np = 1: plain rounding).
 void mlp_split_planes(const float* W, void* planes, int64_t n, int np, hipStream_t s);

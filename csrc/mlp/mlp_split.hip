@@ -8,7 +8,6 @@
 #include "granule.h"
 #include "head_math.h"
 #include "rega_gemm.h"
-#include "lds_gemm.h"
 #include "mma_tile.h"
 #include "fwd_tile.h"
 
@@ -32,183 +31,13 @@ __device__ __forceinline__ void split_store(float v, bf16* base, size_t plane_st
   }
 }
 
-constexpr int kFHCols = 16;   // samples per workgroup
-constexpr int kFHMB = 8;      // 16-row MFMA blocks per H-chunk (128 hidden units)
-constexpr int kFHKS = 8;      // waves splitting K
-constexpr int kFHT = 64 * kFHKS;
-
-// ======================================================================
-// Kernel A: forward + head for 16 samples, all hidden units.
-// ======================================================================
-template <int NPW, int NPZ, int NC, int VEC, bool AF>
-__global__ __launch_bounds__(kFHT) void fwdhead_kernel(SplitStepArgs a) {
-  __shared__ __attribute__((aligned(16))) float red[kFHKS * kFHMB * 4 * 64];  // 64 KB split-K partials
-  __shared__ float a1s[kFHMB * 16][kFHCols + 1];  // a1 of the current H-chunk
-  __shared__ float w2s[kFHMB * 16][NC];           // W2^T of the current H-chunk
-  __shared__ float zs[kFHKS][NC][kFHCols];
-  __shared__ float Ds[NC][kFHCols];
-  __shared__ float lred[kFHKS];
-
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int col = t & 15;  // the column this thread owns in every epilogue element
-  const int H = a.H, C = a.C, P = a.P, ld = a.ld;
-  const int b0 = blockIdx.x * kFHCols;
-  const bool single = H <= kFHMB * 16;
-  const bf16* W1p = static_cast<const bf16*>(a.W1p);
-  const uint8_t* X = static_cast<const uint8_t*>(a.X);
-
-  float zp[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) zp[c] = 0.f;
-
-  for (int m0 = 0; m0 < H; m0 += kFHMB * 16) {
-    const int M = min(kFHMB * 16, H - m0);
-    for (int i = t; i < M * NC; i += kFHT) {
-      const int h = i / NC, c = i - h * NC;
-      w2s[h][c] = c < C ? a.W2[c * H + m0 + h] : 0.f;
-    }
-    // (w2s is first read in the epilogue, after wsk_tile's internal barrier)
-    struct EpiFH {
-      const float* b1;
-      float* a1g;
-      float (*a1s)[kFHCols + 1];
-      float (*w2s)[NC];
-      float* zp;
-      int ld, b0;
-      float xscale;
-      float pre[kEpiMaxQ];
-      __device__ __forceinline__ void prefetch(int q, int row, int, bool ok) {
-        pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
-      }
-      __device__ __forceinline__ void operator()(int q, int row, int gcol, float v) {  // gcol: sample < n
-        const float s = sigm(v * xscale + pre[q]);
-        a1s[row][gcol - b0] = s;
-        a1g[(size_t)row * ld + gcol] = s;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) zp[c] += w2s[row][c] * s;
-      }
-    } epi{a.b1 + m0, a.a1 + (size_t)m0 * ld, a1s, w2s, zp, ld, b0, a.xscale, {}};
-    TileGeom g{M, a.n, P, 0, b0};
-    constexpr int U = NPW == 3 ? 1 : 2;  // keep one burst of loads <= ~100 VGPRs
-    if constexpr (AF)  // fp32 W1 split in registers (mma_tile.h)
-      wsk_tile<bf16, kFHMB, 1, kFHKS, true, true, VEC, U, 3, uint8_t>(a.W1 + (size_t)m0 * P, P, X, P, g, epi, red);
-    else
-      wsk_tile<bf16, kFHMB, 1, kFHKS, true, true, VEC, U, NPW, uint8_t>(W1p + (size_t)m0 * P, P, X, P, g, epi, red,
-                                                               H * P * (int)sizeof(bf16));
-  }
-  // ---- z2 = W2 a1 + b2 for the 16 columns: reduce the per-thread partials
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    zp[c] += __shfl_xor(zp[c], 16, 64);
-    zp[c] += __shfl_xor(zp[c], 32, 64);
-  }
-  if (lane < kFHCols) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) zs[wave][c][lane] = zp[c];
-  }
-  __syncthreads();
-
-  float lpart = 0.f;
-  if (t < kFHCols) {
-    const int b = b0 + t;
-    const bool valid = b < a.n;
-    float z[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < kFHKS; ++w) s += zs[w][c][t];
-      z[c] = c < C ? s + a.b2[c] : 0.f;
-    }
-    if (a.mode == 1) {  // predict
-      if (valid) {
-        int best = 0;
-        float bv = z[0];
-#pragma unroll
-        for (int c = 1; c < NC; ++c)
-          if (c < C && z[c] > bv) { bv = z[c]; best = c; }
-        a.pred[b] = best;
-      }
-    } else {
-      float m = 0.f;
-      if (a.shift) {
-        m = z[0];
-#pragma unroll
-        for (int c = 1; c < NC; ++c) m = (c < C && z[c] > m) ? z[c] : m;
-      }
-      float s = 0.f;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        z[c] = c < C ? __expf(z[c] - m) : 0.f;
-        s += z[c];
-      }
-      const float inv = 1.f / s;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) z[c] *= inv;
-      if (a.mode == 2) {
-        if (valid) {
-#pragma unroll
-          for (int c = 0; c < NC; ++c)
-            if (c < C) a.probs[(size_t)c * a.ldp + b] = z[c];
-        }
-      } else {
-        const int lab = valid ? a.labels[b] : -1;
-        if (valid && a.loss_partial) {
-          float pl = 1.f;
-#pragma unroll
-          for (int c = 0; c < NC; ++c) pl = c == lab ? z[c] : pl;
-          lpart = -__logf(pl);
-        }
-        const float sc = (float)a.scale;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          const float d = valid ? (z[c] - (c == lab ? 1.f : 0.f)) * sc : 0.f;
-          Ds[c][t] = d;
-          if (valid && c < C) a.D[(size_t)c * ld + b] = d;
-        }
-      }
-    }
-  }
-  if (a.mode != 0) return;
-  if (a.loss_partial) {  // wave 0 holds every column's loss term
-    if (wave == 0) {
-      const float v = wave_sum(lpart);
-      if (lane == 0) a.loss_partial[blockIdx.x] = v;
-    }
-  }
-  __syncthreads();
-
-  // ---- dZ1 = (W2^T D) .* a1 .* (1 - a1), written in fp32 and as NPZ bf16 planes
-  const int b = b0 + col;
-  if (b >= a.n) return;
-  bf16* dZp = static_cast<bf16*>(a.dZ1p);
-  const size_t zstride = (size_t)H * ld;
-  float Dc[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) Dc[c] = Ds[c][col];
-  for (int h = t >> 4; h < H; h += kFHT / kFHCols) {
-    float da = 0.f;
-    if (single) {
-#pragma unroll
-      for (int c = 0; c < NC; ++c) da += w2s[h][c] * Dc[c];
-    } else {
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-        if (c < C) da += a.W2[c * H + h] * Dc[c];
-    }
-    const float x = single ? a1s[h][col] : a.a1[(size_t)h * ld + b];
-    const float dz = da * x * (1.f - x);
-    const size_t zi = (size_t)h * ld + b;
-    a.dZ1[zi] = dz;
-    split_store<NPZ>(dz, dZp, zstride, zi);
-  }
-}
-
 // ======================================================================
 // Kernel A1 (tiled): a1 = sigmoid(W1 X + b1) on 16x32 tiles, K split over 8
-// waves, W1 as NPW exact bf16 planes.  Used with the separate head kernel
-// (mlp_kernels.hip) -- cheaper than fwdhead_kernel because every workgroup
-// streams only 16 rows of W1 instead of all of it.
+// waves, W1 as fp32 split in registers or NPW exact bf16 planes.  Used with the
+// separate head kernel (mlp_kernels.hip) where the fused forward + head launch
+// does not apply (H > 128, predict).  (Round 1-3's one-launch-per-16-samples
+// forward + head, which streamed ALL of W1 through every workgroup, was removed
+// in round 4: slower than this tiling and selected by no policy.)
 // ======================================================================
 constexpr int kF1MB = 1, kF1NB = 2, kF1KS = 8;
 
@@ -470,7 +299,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
 
 // The weight-gradient launch's workgroups past its t1 dW1 tiles: t2 dW2 tiles (+ the fused xGMI exchange)
 // followed by the bias-row workgroups.  `red`: kWKS * 4 * 64 floats of LDS, `s_xf`: 2 words of LDS.
-// Shared by wgrad_split_kernel and wgrad_big_kernel (the wide path's extra workgroups).
+// Shared by wgrad_split_kernel and the wide engines' launches (their extra workgroups).
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
                                             uint32_t* s_xf) {
   const float reg = (float)a.reg, lr = (float)a.lr;
@@ -565,133 +394,6 @@ __global__ __launch_bounds__(256) void sgd_planes_kernel(float* __restrict__ prm
     prm[i] = v;
     if (planes && i < w1n) split_store<NP>(v, planes, (size_t)w1n, (size_t)i);
   }
-}
-
-// ======================================================================
-// Wide configs (H >= 512): LDS double-buffered blocked GEMMs (lds_gemm.h)
-// for a1 = sigmoid(W1 X + b1) and dW1 = dZ1 X^T (+ reg / SGD / planes).
-// ======================================================================
-struct EpiSigBig {
-  const float* b1;
-  float* a1;
-  int ld;
-  float xscale;
-  // head z2 partials (nullptr: off): W2 [C][H], z2p [row tile][16][ld]
-  const float* W2;
-  float* z2p;
-  int H, C, N, bm;
-  static constexpr bool kTileHook = true;
-  __device__ __forceinline__ void operator()(int row, int col, float v) {
-    a1[(size_t)row * ld + col] = sigm(v * xscale + b1[row]);
-  }
-  // z2p[tile] = W2[:, tile rows] . sigmoid(acc): in the 16x16x4 f32 MFMA lane map, step i takes
-  // B[k = fg][n = fr] = a1(row0 + 16 mb + 4 fg + i, col fr) -- exactly accumulator element i -- and
-  // A[m = fr][k = fg] = W2[class fr][that row].  Row waves are summed through LDS.
-  template <int MB, int NB, int WRN>
-  __device__ __forceinline__ void tile(const f32x4 (&acc)[MB][NB], int wr, int wc, int fr, int fg, int row0,
-                                       int col0, char* lds) {
-    if (!z2p) return;
-    const __amdgpu_buffer_rsrc_t rw = make_rsrc(W2), rb = make_rsrc(b1);
-    float w[MB][4], bb[MB][4];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int h = row0 + 16 * mb + 4 * fg + i;
-        w[mb][i] = buf_load1<float>(rw, (fr < C && h < H) ? (fr * H + h) * 4 : kOOB);
-        bb[mb][i] = buf_load1<float>(rb, h < H ? h * 4 : kOOB);
-      }
-    f32x4 z[NB];
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) z[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          z[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mb][i], sigm(acc[mb][nb][i] * xscale + bb[mb][i]), z[nb],
-                                                      0, 0, 0);
-    const int lane = fg * 16 + fr;
-    f32x4* red = reinterpret_cast<f32x4*>(lds);  // [WRN][2][NB][64]
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) red[((wr * 2 + wc) * NB + nb) * 64 + lane] = z[nb];
-    __syncthreads();
-    if (wr != 0) return;
-    const int tile = row0 / bm;
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      f32x4 s = red[(wc * NB + nb) * 64 + lane];
-#pragma unroll
-      for (int r = 1; r < WRN; ++r) s += red[((r * 2 + wc) * NB + nb) * 64 + lane];
-      const int col = col0 + 16 * nb + fr;
-      if (col < N) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (4 * fg + i < C) z2p[((size_t)tile * 16 + 4 * fg + i) * ld + col] = s[i];  // (past C: zero, unread)
-      }
-    }
-  }
-};
-
-struct EpiW1Big {
-  float* W1;
-  float* gW1;
-  bf16* W1p;
-  size_t plane;
-  int P, sgd, npw;
-  float reg, lr, xscale;
-  float* b1;
-  float* gb1;
-  int perr;  // ag_err, loaded before the K loop: no update when set
-  __device__ __forceinline__ void operator()(int row, int col, float v) {
-    const bool upd = sgd && !poisoned(perr);
-    if (col == P) {  // all-ones feature row of XT: db1
-      if (upd) b1[row] -= lr * v;
-      else gb1[row] = v;
-      return;
-    }
-    const size_t i = (size_t)row * P + col;
-    const float w = W1[i];
-    const float g = v * xscale + reg * w;
-    if (upd) {
-      const float nw = w - lr * g;
-      W1[i] = nw;
-      if (npw == 3) split_store<3>(nw, W1p, plane, i);
-      else split_store<1>(nw, W1p, plane, i);
-    } else {
-      gW1[i] = g;
-    }
-  }
-};
-
-template <int BM, int BN, int NPW, int NT, int NKS = 0>
-__global__ __launch_bounds__(NT) void fwd1_big_kernel(SplitStepArgs a, int tn) {
-  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
-  EpiSigBig epi{a.b1, a.a1, a.ld, a.xscale, a.W2, a.z2part, a.H, a.C, a.n, BM};
-  lds_gemm_tile<BM, BN, NPW, uint8_t, EpiSigBig, NT, NKS>(static_cast<const bf16*>(a.W1p), a.P, a.H * a.P * (int)sizeof(bf16),
-                                      static_cast<const uint8_t*>(a.X), a.P, a.H, a.n, a.P, (id / tn) * BM,
-                                      (id % tn) * BN, epi, lds_dyn);
-}
-
-template <int BM, int BN, int NPZ, int NT, int NKS = 0>
-__global__ __launch_bounds__(NT) void wgrad_big_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
-  extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
-  if ((int)blockIdx.x >= tbig) {  // the dW2 / db2 roles riding in this launch (launched with NT == kWT only)
-    if constexpr (NT == kWT)
-      wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
-                  reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)));
-    return;
-  }
-  const int id = xcd_remap(blockIdx.x, tbig);
-  EpiW1Big epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, a.sgd, a.npw,
-               (float)a.reg, (float)a.lr, a.xscale, a.b1, a.gb1, ag_err_load(a.ag_err)};
-  const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
-  lds_gemm_tile<BM, BN, NPZ, uint8_t, EpiW1Big, NT, NKS>(static_cast<const bf16*>(a.dZ1p), a.ld, a.H * a.ld * (int)sizeof(bf16),
-                                      static_cast<const uint8_t*>(a.XT), a.ldxt, r1, a.P + a.bias_col, a.n,
-                                      a.w1_row0 + (id / tn) * BM, (id % tn) * BN, epi, lds_dyn);
-  mark_status(a, epi.perr);
 }
 
 // ---- the same two GEMMs on the direct-to-LDS engine (glds_gemm.h): bf16 copies of X / XT as B.
@@ -814,7 +516,7 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
     bool good = true;
     for (int k0 = 0; k0 < tm && good; k0 += 16)  // the partials summed in tile order, 16 per poll
       good = gran_poll<16>(g.z2g, (unsigned)(k0 * 16 + zc) * a.ld + zcol, stride, min(16, tm - k0), need, ep, limit,
-                           [&](int, float v) { zsum += v; }, a.poll_skip != 0);
+                           [&](int, float v) { zsum += v; });
     if (!good && lane == 0) {
       atomicExch(g.err, 1);
       sw[1] = 1u;
@@ -877,7 +579,7 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
 #pragma unroll
     for (int q = 0; q < NDS; ++q) v[q] = 0.f;
     const bool good = gran_poll<NDS>(g.dg, (unsigned)c0 * a.ld + n0 + j, (unsigned)(kRowsPerQ * a.ld), cnt, cnt > 0,
-                                     ep, limit, [&](int q, float x) { v[q] = x; }, a.poll_skip != 0);
+                                     ep, limit, [&](int q, float x) { v[q] = x; });
     if (!good && lane == 0) {
       atomicExch(g.err, 1);
       sw[2] = 1u;
@@ -1219,7 +921,7 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
 // a1 = sigmoid(W1 X + b1) on the A-in-registers engine (rega_gemm.h): W1 read as fp32 and split into the
 // exact bf16 planes in registers (AT = float), or the bf16 plane 0 (AT = bf16, split1); z2 partials of
 // this 128-row tile as in fwd1_glds_kernel
-template <typename AT, int WC, int NKS, bool AG = false, int APL = 1>
+template <typename AT, int WC, int NKS, bool AG = false>
 __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn, RegaAgArgs ag = {}) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   using G = RegaGeom<128, WC>;
@@ -1248,8 +950,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
     }
   f32x4 acc[MB][NB];
   const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.W1) : reinterpret_cast<const AT*>(a.W1p);
-  rega_gemm_mainloop<AT, 128, WC, NKS, 0, APL>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0,
-                                               lds_dyn, acc, APL == 3 ? H * a.P * 2 : 0);
+  rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
   if (AG) ag_stamp(a, 1);
   const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
 #pragma unroll
@@ -1324,7 +1025,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
 // dW1 = dZ1 XT on the A-in-registers engine: dZ1 read as fp32 (AT = float; the head writes it instead of
 // the three bf16 planes: 4 B per element stored and loaded instead of 6) or as its one bf16 plane (split1),
 // with wgrad_glds_kernel's fused reg + SGD + plane-refresh epilogue; the dW2 / db2 roles ride along
-template <typename AT, int WC, int NKS, int APL = 1>
+template <typename AT, int WC, int NKS>
 __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {
@@ -1333,7 +1034,7 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
     return;
   }
   using G = RegaGeom<128, WC>;
-  constexpr int MB = G::MB, NB = G::NB, BM = G::BM, NP = (sizeof(AT) == 4 || APL == 3) ? 3 : 1;
+  constexpr int MB = G::MB, NB = G::NB, BM = G::BM, NP = sizeof(AT) == 4 ? 3 : 1;
   const int id = xcd_remap(blockIdx.x, tbig);
   const int m0 = a.w1_row0 + (id / tn) * BM, n0 = (id % tn) * 128;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1346,10 +1047,10 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
   wc1.prefetch(a, m0, n0, M);
   const int perr = ag_err_load(a.ag_err);  // the step's forward timed out: no update
   f32x4 acc[MB][NB];
-  // fp32 dZ1 split in registers (AT = float), or its stored planes (bf16: one, APL = 3: three)
+  // fp32 dZ1 split in registers (AT = float), or its one bf16 plane (split1)
   const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
-  rega_gemm_mainloop<AT, 128, WC, NKS, 0, APL>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col,
-                                               a.n, m0, n0, lds_dyn, acc, APL == 3 ? a.H * a.ld * 2 : 0);
+  rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0,
+                                       n0, lds_dyn, acc);
   wc1.stage(lds_dyn, acc, rw, cw, m0, n0, fg, fr);
   // the W1 planes (npw == npz); split3 w1_planes_lazy: none (the 128 x 128 forward reads fp32 W1)
   wc1.apply(a, lds_dyn, m0, n0, M, a.sgd && !poisoned(perr), (NP == 3 && a.w1_planes_lazy) ? 0 : NP);
@@ -1371,12 +1072,8 @@ inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 inline bool al4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
 
 constexpr int kBigMinH = 512;  // below this the wave-split-K kernels win (too few tiles to fill the chip)
-constexpr int kBigThreads = 512;
 
-// true when the LDS-staged GEMM path applies: wide hidden layer and 16-byte aligned K-contiguous rows
-bool big_fwd_ok(const SplitStepArgs& a) {
-  return a.H >= kBigMinH && a.P % 16 == 0 && al16(a.W1p) && al16(a.X);
-}
+// the wide (blocked-GEMM) weight-gradient engines apply: wide hidden layer, 16-byte aligned K-contiguous rows
 bool big_wgrad_ok(const SplitStepArgs& a) {
   return a.H >= kBigMinH && a.n % 16 == 0 && a.ld % 8 == 0 && a.ldxt % 16 == 0 && al16(a.dZ1p) && al16(a.XT);
 }
@@ -1398,44 +1095,39 @@ bool rega_fwd_ok(const SplitStepArgs& a) {
 
 constexpr int kRegaWC = 1;  // wave layout of the A-in-registers kernels: 8 (rows) x 1 (bench/micro/rega_ablate.hip: WC = 2 splits every A value twice, +25 % at H = 4096)
 
-template <typename AT, int NKS, int APL = 1>
+template <typename AT, int NKS>
 void launch_fwd1_rega_k(const SplitStepArgs& a, hipStream_t s) {
   constexpr int L = std::max(ra::lds_bytes<128>(), 8 * 8 * 64 * 16);  // (z2 reduction scratch)
-  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, false, APL>>(L);
-  fwd1_rega_kernel<AT, kRegaWC, NKS, false, APL><<<cdiv(a.H, 128) * cdiv(a.n, 128), 512, L, s>>>(a, cdiv(a.n, 128));
+  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, false>>(L);
+  fwd1_rega_kernel<AT, kRegaWC, NKS, false><<<cdiv(a.H, 128) * cdiv(a.n, 128), 512, L, s>>>(a, cdiv(a.n, 128));
 }
 
 // the fused all-gather head: > 80 KB of LDS keeps it at one workgroup per CU (the hand-off's measured form)
-template <typename AT, int NKS, int APL = 1>
+template <typename AT, int NKS>
 void launch_fwd1_rega_ag_k(const SplitStepArgs& a, RegaAgArgs g, hipStream_t s) {
   constexpr int L = wide_ag_launch_lds(std::max({ra::lds_bytes<128>(), 8 * 8 * 64 * 16, wide_ag_lds_bytes<128, 128>()}));
-  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true, APL>>(L);
+  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true>>(L);
   g.ep_off = L - 16;
   g.tiling = 0;
   const int tn = cdiv(a.n, 128);
-  fwd1_rega_kernel<AT, kRegaWC, NKS, true, APL><<<g.tm * tn, 512, L, s>>>(a, tn, g);
+  fwd1_rega_kernel<AT, kRegaWC, NKS, true><<<g.tm * tn, 512, L, s>>>(a, tn, g);
 }
 
 // K = P = 784 (MNIST) is 25 stages of 32: the fully unrolled K loop; anything else the runtime loop
-template <typename AT, int APL = 1>
+template <typename AT>
 void launch_fwd1_rega(const SplitStepArgs& a, hipStream_t s) {
-  if (cdiv(a.P, ra::kBK) == 25) launch_fwd1_rega_k<AT, 25, APL>(a, s);
-  else launch_fwd1_rega_k<AT, 0, APL>(a, s);
+  if (cdiv(a.P, ra::kBK) == 25) launch_fwd1_rega_k<AT, 25>(a, s);
+  else launch_fwd1_rega_k<AT, 0>(a, s);
 }
 
+// the direct-to-LDS forward where the A-in-registers one does not apply (its 128 x 128 tiles would give < 192
+// workgroups: H = 512-1024 at a per-GPU batch of 800): 64 x 64 tiles
 template <int NP>
 void launch_fwd1_glds(const SplitStepArgs& a, hipStream_t s) {
-  const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
-  if (t128 >= 192) {
-    constexpr int L = gl::lds_bytes<128, 128, NP>();
-    set_lds_limit<fwd1_glds_kernel<128, 128, NP>>(L);
-    fwd1_glds_kernel<128, 128, NP><<<t128, 512, L, s>>>(a, cdiv(a.n, 128));
-  } else {
-    constexpr int L = std::max(gl::lds_bytes<64, 64, NP>(), 4 * 2 * 2 * 64 * 16);  // (tile hook scratch)
-    set_lds_limit<fwd1_glds_kernel<64, 64, NP>>(L);
-    const int tn = cdiv(a.n, 64);
-    fwd1_glds_kernel<64, 64, NP><<<cdiv(a.H, 64) * tn, 512, L, s>>>(a, tn);
-  }
+  constexpr int L = std::max(gl::lds_bytes<64, 64, NP>(), 4 * 2 * 2 * 64 * 16);  // (tile hook scratch)
+  set_lds_limit<fwd1_glds_kernel<64, 64, NP>>(L);
+  const int tn = cdiv(a.n, 64);
+  fwd1_glds_kernel<64, 64, NP><<<cdiv(a.H, 64) * tn, 512, L, s>>>(a, tn);
 }
 
 // the A-in-registers dW1 (and the head writing fp32 dZ1 instead of its planes, split3): wide layers whose
@@ -1448,25 +1140,22 @@ bool rega_wgrad_ok(const SplitStepArgs& a) {
          (a.npz == 3 ? (a.dZ1 != nullptr && al16(a.dZ1)) : al16(a.dZ1p));
 }
 
-template <typename AT, int NKS, int APL = 1>
+// (round 3's 4 x 2 wave layout for the bf16 loop, 39.9 -> 41.3 us at 784-4096-10, was removed in round 4:
+// profiles/wide_ag_ab_bf16_wave_layout_r3.jsonl)
+template <typename AT, int NKS>
 void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int tn = cdiv(a.P + a.bias_col, 128), tbig = cdiv(rows, 128) * tn;
   // (the K-loop ring, the epilogue's transposed 128 x (128 + 4) fp32 tile, the role workgroups' scratch)
   constexpr int L = std::max({ra::lds_bytes<128>(), W1Chunks<128, 128>::kLdsBytes, kWKS * 4 * 64 * (int)sizeof(float) + 16});
-  if constexpr (sizeof(AT) == 2 && APL == 1) if (a.rega_wc == 2) {  // (split1 only: for split3 the 4 x 2 layout splits every A value twice)
-    set_lds_limit<wgrad_rega_kernel<AT, 2, NKS>>(L);
-    wgrad_rega_kernel<AT, 2, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
-    return;
-  }
-  set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS, APL>>(L);
-  wgrad_rega_kernel<AT, kRegaWC, NKS, APL><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
+  set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS>>(L);
+  wgrad_rega_kernel<AT, kRegaWC, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
 }
 
-template <typename AT, int APL = 1>
+template <typename AT>
 void launch_wgrad_rega(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
-  if (cdiv(a.n, ra::kBK) == 25) launch_wgrad_rega_k<AT, 25, APL>(a, t2, tb, s);
-  else launch_wgrad_rega_k<AT, 0, APL>(a, t2, tb, s);
+  if (cdiv(a.n, ra::kBK) == 25) launch_wgrad_rega_k<AT, 25>(a, t2, tb, s);
+  else launch_wgrad_rega_k<AT, 0>(a, t2, tb, s);
 }
 
 // split-K dW1, second half: sum the ksplit partial slabs in slab order (deterministic), then the fused
@@ -1544,89 +1233,7 @@ void launch_wgrad_glds(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
   }
 }
 
-// 128x128 tiles when that still gives ~200+ workgroups, else 64x64
-// K-stage count 13 (K = 769..832: P = 784 for the forward, per-rank batch 800 for dW1) gets the
-// fully unrolled K loop; anything else the runtime loop
-template <int NP, int NT, int NKS>
-void launch_fwd1_big_k(const SplitStepArgs& a, hipStream_t s) {
-  const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
-  if (t128 >= 192) {
-    constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
-    set_lds_limit<fwd1_big_kernel<128, 128, NP, NT, NKS>>(L);
-    fwd1_big_kernel<128, 128, NP, NT, NKS><<<t128, NT, L, s>>>(a, cdiv(a.n, 128));
-  } else {
-    constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
-    set_lds_limit<fwd1_big_kernel<64, 64, NP, NT, NKS>>(L);
-    const int tn = cdiv(a.n, 64);
-    fwd1_big_kernel<64, 64, NP, NT, NKS><<<cdiv(a.H, 64) * tn, NT, L, s>>>(a, tn);
-  }
-}
-
-template <int NP, int NT>
-void launch_fwd1_big_nt(const SplitStepArgs& a, hipStream_t s) {
-  if (cdiv(a.P, lg::kBK) == 13) launch_fwd1_big_k<NP, NT, 13>(a, s);
-  else launch_fwd1_big_k<NP, NT, 0>(a, s);
-}
-
-template <int NP>
-void launch_fwd1_big(const SplitStepArgs& a, hipStream_t s) {
-  launch_fwd1_big_nt<NP, kBigThreads>(a, s);
-}
-
-// t2 / tb > 0: that many dW2-tile / bias-row role workgroups ride in the same launch after the dW1 tiles
-template <int NP, int NT, int NKS>
-void launch_wgrad_big_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
-  const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
-  const int NW = a.P + a.bias_col;
-  const int t128 = cdiv(rows, 128) * cdiv(NW, 128);
-  if (t128 >= 192) {
-    constexpr int L = lg::lds_bytes<128, 128, NP, uint8_t>();
-    set_lds_limit<wgrad_big_kernel<128, 128, NP, NT, NKS>>(L);
-    wgrad_big_kernel<128, 128, NP, NT, NKS><<<t128 + t2 + tb, NT, L, s>>>(a, cdiv(NW, 128), t128, t2);
-  } else {
-    constexpr int L = lg::lds_bytes<64, 64, NP, uint8_t>();
-    set_lds_limit<wgrad_big_kernel<64, 64, NP, NT, NKS>>(L);
-    const int tn = cdiv(NW, 64);
-    const int t64 = cdiv(rows, 64) * tn;
-    wgrad_big_kernel<64, 64, NP, NT, NKS><<<t64 + t2 + tb, NT, L, s>>>(a, tn, t64, t2);
-  }
-}
-
-template <int NP, int NT>
-void launch_wgrad_big_nt(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
-  if (cdiv(a.n, lg::kBK) == 13) launch_wgrad_big_k<NP, NT, 13>(a, t2, tb, s);
-  else launch_wgrad_big_k<NP, NT, 0>(a, t2, tb, s);
-}
-
-template <int NP>
-void launch_wgrad_big(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
-  static_assert(kBigThreads == kWT, "the role workgroups riding in the dW1 launch need kWT threads");
-  launch_wgrad_big_nt<NP, kBigThreads>(a, t2, tb, s);
-}
-
-template <int NPW, int NPZ, int NC>
-void launch_fwdhead(const SplitStepArgs& a, hipStream_t s) {
-  const bool af = NPW == 3 && mlp_split_fwd_fp32_w(a);
-  const bool vec = al4(a.X) && al16(af ? (const void*)a.W1 : a.W1p) && a.P % 8 == 0;
-  const dim3 grid(cdiv(a.n, kFHCols));
-  if (af) {
-    if (vec) fwdhead_kernel<NPW, NPZ, NC, 1, NPW == 3><<<grid, kFHT, 0, s>>>(a);
-    else fwdhead_kernel<NPW, NPZ, NC, 0, NPW == 3><<<grid, kFHT, 0, s>>>(a);
-  } else {
-    if (vec) fwdhead_kernel<NPW, NPZ, NC, 1, false><<<grid, kFHT, 0, s>>>(a);
-    else fwdhead_kernel<NPW, NPZ, NC, 0, false><<<grid, kFHT, 0, s>>>(a);
-  }
-}
-
-template <int NPW, int NPZ>
-void launch_fwdhead_nc(const SplitStepArgs& a, hipStream_t s) {
-  if (a.C == 10) launch_fwdhead<NPW, NPZ, 10>(a, s);
-  else launch_fwdhead<NPW, NPZ, 16>(a, s);
-}
-
 }  // namespace
-
-int mlp_split_fwdhead_blocks(int n) { return cdiv(n, kFHCols); }
 
 // the wave-split-K dW1 reads fp32 dZ1 (split3, a_fp32, 16-byte rows)
 bool small_wgrad_fp32_ok(const SplitStepArgs& a) {
@@ -1638,20 +1245,19 @@ bool small_wgrad_fp32_ok(const SplitStepArgs& a) {
 bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a) {
   if (a.npz != 3) return false;
   const bool big = big_wgrad_ok(a) && a.xf.world == 0;
-  // (wide: fp32 dZ1 unless a_fp32 bit1 is clear -- then the head writes the planes and the dW1 reads them)
-  return big ? (rega_wgrad_ok(a) && (a.a_fp32 & 2) && a.dZ1 != nullptr) : small_wgrad_fp32_ok(a);
+  // (wide: the A-in-registers dW1 always splits fp32 dZ1 -- profiles/wide_ag_ab_operand_forms_r3.jsonl)
+  return big ? rega_wgrad_ok(a) : small_wgrad_fp32_ok(a);
 }
 
 bool mlp_split_fwd_fp32_w(const SplitStepArgs& a) { return a.npw == 3 && (a.a_fp32 & 1) && a.W1 != nullptr && al16(a.W1); }
 
-// below kBigMinH every forward kernel (fwd1_split, fwd1_head(_ag), fwdhead) takes fp32 W1 when
+// below kBigMinH every forward kernel (fwd1_split, fwd1_head(_ag)) takes fp32 W1 when
 // mlp_split_fwd_fp32_w holds: nothing reads the W1 planes, so the weight update stops refreshing them
 bool mlp_split_w1_planes_read(const SplitStepArgs& a) { return a.H >= kBigMinH || !mlp_split_fwd_fp32_w(a); }
 
 int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a) {
-  if (!a.z2part || a.C > 16 || a.n <= 0 || !(glds_fwd_ok(a) || big_fwd_ok(a))) return 0;
-  const int t128 = cdiv(a.H, 128) * cdiv(a.n, 128);
-  return t128 >= 192 ? cdiv(a.H, 128) : cdiv(a.H, 64);  // must match launch_fwd1_big_nt's tile choice
+  if (!a.z2part || a.C > 16 || a.n <= 0 || !glds_fwd_ok(a)) return 0;
+  return rega_fwd_ok(a) ? cdiv(a.H, 128) : cdiv(a.H, 64);  // the forward's tiles: rega 128 rows, glds 64
 }
 
 namespace {
@@ -1676,17 +1282,16 @@ static int wide_ag_bm(const SplitStepArgs& a, int allow64) {
 
 bool mlp_split_wide_fwd_reads_planes(const SplitStepArgs& a, int ag, int allow64) {
   if (a.npw != 3) return true;
-  if (ag) return wide_ag_bm(a, allow64) != 128 || !mlp_split_fwd_fp32_w(a);  // 128: fwd1_rega_kernel; 64: glds
-  // mirrors mlp_split_fwd1's dispatch: rega (fp32 W1 or the planes), glds / big (planes), the small kernels (fp32
-  // W1 or planes)
-  if (rega_fwd_ok(a)) return !mlp_split_fwd_fp32_w(a);
-  if (glds_fwd_ok(a) || big_fwd_ok(a)) return true;
+  if (ag) return wide_ag_bm(a, allow64) != 128;  // 128: fwd1_rega_kernel (fp32 W1); 64: glds (planes)
+  // mirrors mlp_split_fwd1's dispatch: rega (fp32 W1), glds (planes), the small kernels (fp32 W1 or planes)
+  if (rega_fwd_ok(a)) return false;
+  if (glds_fwd_ok(a)) return true;
   return !mlp_split_fwd_fp32_w(a);
 }
 
 bool mlp_split_wgrad_leaves_planes_stale(const SplitStepArgs& a) {
   return a.w1_planes_lazy && a.npw == 3 && a.npz == 3 && a.sgd && (a.wg_parts & 1) && a.w1_rows != 0 &&
-         a.xf.world == 0 && big_wgrad_ok(a) && rega_wgrad_ok(a) && mlp_split_fwd_fp32_w(a);
+         a.xf.world == 0 && big_wgrad_ok(a) && rega_wgrad_ok(a);
 }
 
 bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64) {
@@ -1733,10 +1338,7 @@ int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long lo
   g.dg = gran + (size_t)g.tm * 16 * a.ld;
   if (bm == 128) {
     const bool k25 = cdiv(a.P, ra::kBK) == 25;
-    if (a.npw == 3 && !mlp_split_fwd_fp32_w(a)) {  // the stored W1 planes (a_fp32 bit0 clear)
-      if (k25) launch_fwd1_rega_ag_k<bf16, 25, 3>(a, g, s);
-      else launch_fwd1_rega_ag_k<bf16, 0, 3>(a, g, s);
-    } else if (a.npw == 3) {
+    if (a.npw == 3) {
       if (k25) launch_fwd1_rega_ag_k<float, 25>(a, g, s);
       else launch_fwd1_rega_ag_k<float, 0>(a, g, s);
     } else {
@@ -1758,8 +1360,7 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
               "split path: operand too large for 32-bit buffer offsets");
   CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
   if (rega_fwd_ok(a)) {
-    if (a.npw == 3 && !mlp_split_fwd_fp32_w(a)) launch_fwd1_rega<bf16, 3>(a, s);  // the stored W1 planes
-    else if (a.npw == 3) launch_fwd1_rega<float>(a, s);
+    if (a.npw == 3) launch_fwd1_rega<float>(a, s);
     else launch_fwd1_rega<bf16>(a, s);
     CME_LAUNCH_CHECK(s);
     return;
@@ -1767,12 +1368,6 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
   if (glds_fwd_ok(a)) {
     if (a.npw == 3) launch_fwd1_glds<3>(a, s);
     else launch_fwd1_glds<1>(a, s);
-    CME_LAUNCH_CHECK(s);
-    return;
-  }
-  if (big_fwd_ok(a)) {
-    if (a.npw == 3) launch_fwd1_big<3>(a, s);
-    else launch_fwd1_big<1>(a, s);
     CME_LAUNCH_CHECK(s);
     return;
   }
@@ -1785,19 +1380,6 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
   else fwd1_split_kernel<np, 0, af><<<grid, 64 * kF1KS, 0, s>>>(a, tn);
   if (af) { CME_F1(3, true) } else if (a.npw == 3) { CME_F1(3, false) } else { CME_F1(1, false) }
 #undef CME_F1
-  CME_LAUNCH_CHECK(s);
-}
-
-void mlp_split_fwdhead(const SplitStepArgs& a, hipStream_t s) {
-  if (a.n <= 0) return;
-  CME_REQUIRE(a.C >= 1 && a.C <= 16, "split path: 1 <= C <= 16");
-  CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
-  CME_REQUIRE((int64_t)a.H * a.P * 2 * a.npw < (int64_t)kOOB && (int64_t)a.n * a.P * 2 < (int64_t)kOOB,
-              "split path: operand too large for 32-bit buffer offsets");
-  if (a.npw == 3 && a.npz == 3) launch_fwdhead_nc<3, 3>(a, s);
-  else if (a.npw == 1 && a.npz == 1) launch_fwdhead_nc<1, 1>(a, s);
-  else if (a.npw == 1 && a.npz == 3) launch_fwdhead_nc<1, 3>(a, s);
-  else CME_REQUIRE(false, "split path: unsupported plane counts");
   CME_LAUNCH_CHECK(s);
 }
 
@@ -1814,8 +1396,7 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
     const int t2f = do_roles ? cdiv(a.H, 16) : 0;
     const int tbf = do_roles ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
     if (rega_wgrad_ok(a)) {
-      if (a.npz == 3 && !mlp_split_wgrad_fp32_dz(a)) launch_wgrad_rega<bf16, 3>(a, t2f, tbf, s);  // dZ1 planes
-      else if (a.npz == 3) launch_wgrad_rega<float>(a, t2f, tbf, s);
+      if (a.npz == 3) launch_wgrad_rega<float>(a, t2f, tbf, s);
       else launch_wgrad_rega<bf16>(a, t2f, tbf, s);
       CME_LAUNCH_CHECK(s);
       return;
@@ -1826,10 +1407,7 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
       CME_LAUNCH_CHECK(s);
       return;
     }
-    if (a.npz == 3) launch_wgrad_big<3>(a, t2f, tbf, s);
-    else launch_wgrad_big<1>(a, t2f, tbf, s);
-    CME_LAUNCH_CHECK(s);
-    return;
+    // (no direct-to-LDS copies: the wave-split-K kernel below)
   }
   const int w1rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int t1n = cdiv(a.P + a.bias_col, 16 * kWNB), t1 = do_w1 ? cdiv(w1rows, 16 * kWMB) * t1n : 0;
@@ -1849,7 +1427,7 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   const bool af = small_wgrad_fp32_ok(a);
   const bool base_ok = al16(af ? (const void*)a.dZ1 : a.dZ1p) && al4(a.XT) && a.ld % 8 == 0 && a.ldxt % 4 == 0;
   // (3: the XT bytes as 16-byte loads over chunk pairs, mma_tile.h: 16-byte XT rows, n % 16 == 0)
-  const bool pairs = a.u8_pairs && al16(a.XT) && a.ldxt % 16 == 0 && a.n % 16 == 0;
+  const bool pairs = al16(a.XT) && a.ldxt % 16 == 0 && a.n % 16 == 0;
   const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? (pairs ? 3 : 1) : (a.n % 4 == 0 ? 2 : 0));
   const dim3 grid(t1 + t2 + tb);
   SplitStepArgs b = a;

@@ -1,5 +1,5 @@
 // "A in registers" MFMA tile engine for the wide fp32 (split3) MLP GEMMs -- the fastest of the three wide
-// engines at H = 4096 (lds_gemm.h: register-staged, glds_gemm.h: direct-to-LDS, this one).
+// engines at H = 4096 (round 1 register-staged, glds_gemm.h: direct-to-LDS, this one).
 //
 // Why (bench/micro/glds_fill.hip, profiles/wide_engines_r2.md): at the ~128 x 128 tile that ~224
 // workgroups on 256 CUs allow, the wide GEMMs are bound by how many operand bytes each CU pulls from L2
@@ -37,11 +37,12 @@ constexpr int lds_bytes() {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// one stage's A operand of one lane: MB row blocks x 8 k-values (fp32: two dwordx4 per block; bf16: one per
-// stored plane -- APL = 3: the three exact bf16 planes of an fp32 operand, read instead of split)
-template <typename AT, int MB, int APL = 1>
+// one stage's A operand of one lane: MB row blocks x 8 k-values (fp32: two dwordx4 per block; bf16: one)
+// (round 3 also read the three stored bf16 planes of an fp32 operand here; measured slower than the split in
+// registers at 784-4096-10 -- profiles/wide_ag_ab_operand_forms_r3.jsonl -- and removed in round 4)
+template <typename AT, int MB>
 struct AFrag {
-  static constexpr int Q = (sizeof(AT) == 4 ? 2 : APL) * MB;  // dwordx4 per lane
+  static constexpr int Q = (sizeof(AT) == 4 ? 2 : 1) * MB;  // dwordx4 per lane
   u32x4 v[Q];
 };
 
@@ -57,12 +58,12 @@ __device__ __forceinline__ u32x4 load16_asm(__amdgpu_buffer_rsrc_t r, int voff) 
   return v;
 }
 
-template <int N, typename AT, int MB, int APL>
-__device__ __forceinline__ void wait_vm_regs(AFrag<AT, MB, APL>& f) {
+template <int N, typename AT, int MB>
+__device__ __forceinline__ void wait_vm_regs(AFrag<AT, MB>& f) {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 #pragma unroll
-  for (int q = 0; q < AFrag<AT, MB, APL>::Q; ++q) asm volatile("" : "+v"(f.v[q]));
+  for (int q = 0; q < AFrag<AT, MB>::Q; ++q) asm volatile("" : "+v"(f.v[q]));
 }
 
 // the three exact bf16 planes of 8 fp32 values (two dwordx4)
@@ -105,25 +106,21 @@ struct RegaGeom {
 // per trip before the A registers are used.
 // ABLATE (bench/micro/rega_ablate.hip only): 1 = no MFMA (fragments still read and split, kept live),
 // 2 = no loads after the prologue (the MFMAs run on whatever the ring holds)
-// APL = 3 (AT = bf16): A is three stored exact bf16 planes `aplane` bytes apart (the split made once by their
-// writer instead of by every column tile's waves: 6 B per element pulled instead of 4, no split VALU)
-template <typename AT, int BN, int WC = 1, int NKS = 0, int ABLATE = 0, int APL = 1>
+template <typename AT, int BN, int WC = 1, int NKS = 0, int ABLATE = 0>
 __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int lda,
                                                    const __hip_bfloat16* __restrict__ B, int ldb, int M, int N,
                                                    int K, int m0, int n0, char* __restrict__ lds,
-                                                   f32x4 (&acc)[RegaGeom<BN, WC>::MB][RegaGeom<BN, WC>::NB],
-                                                   int aplane = 0) {
+                                                   f32x4 (&acc)[RegaGeom<BN, WC>::MB][RegaGeom<BN, WC>::NB]) {
   using namespace ra;
   using G = RegaGeom<BN, WC>;
   constexpr int MB = G::MB, NB = G::NB, NW = 8;
   constexpr bool F32 = sizeof(AT) == 4;
-  static_assert(APL == 1 || (APL == 3 && !F32), "stored planes: bf16 A only");
   constexpr int SB = BN * kRowB;  // B bytes per stage
   static_assert(SB % (1024 * NW) == 0, "B DMA instructions must divide over the 8 waves");
   constexpr int LB = SB / 1024 / NW;            // B DMA instructions per wave per stage
-  constexpr int LA = AFrag<AT, MB, APL>::Q;     // A loads per lane per stage
+  constexpr int LA = AFrag<AT, MB>::Q;          // A loads per lane per stage
   constexpr int LS = LB + LA;                   // vmcnt per stage per wave
-  using AF = AFrag<AT, MB, APL>;
+  using AF = AFrag<AT, MB>;
 
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -164,8 +161,7 @@ __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int
         fa.v[2 * mb] = load16_asm<0>(rsa, ao);
         fa.v[2 * mb + 1] = load16_asm<16>(rsa, ao);
       } else {
-#pragma unroll
-        for (int p = 0; p < APL; ++p) fa.v[APL * mb + p] = load16_asm<0>(rsa, ao == kOOB ? kOOB : ao + p * aplane);
+        fa.v[mb] = load16_asm<0>(rsa, ao);
       }
     }
   };
@@ -177,7 +173,7 @@ __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int
 
   const int frag = (wc * 16 * NB + fr) * kRowB + ((fg ^ gl::swz(fr)) << 4);
   // one stage's MFMA operands in registers: NB B fragments (LDS) and the A planes (split of the A ring slot)
-  constexpr int NPL = F32 ? 3 : APL;
+  constexpr int NPL = F32 ? 3 : 1;
   struct Frags {
     bf16x8_t b[NB];
     bf16x8_t a[MB][NPL];
@@ -191,8 +187,7 @@ __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int
       if constexpr (F32) {
         split3(fa.v[2 * mb], fa.v[2 * mb + 1], F.a[mb][0], F.a[mb][1], F.a[mb][2]);
       } else {
-#pragma unroll
-        for (int p = 0; p < APL; ++p) __builtin_memcpy(&F.a[mb][p], &fa.v[APL * mb + p], 16);
+        __builtin_memcpy(&F.a[mb][0], &fa.v[mb], 16);
       }
     }
   };

@@ -376,6 +376,7 @@ def handoff_timeout_dp_worker(rank, world, comm, device, out_dir, allreduce):
     tr = DataParallelTrainer(NeuralNetwork([784, 100, 10]), comm=comm, device=dev, batch_size=1600,
                              allreduce=allreduce)
     tr.engine.set_fh_allgather(True)  # (off by default when ranks share a GPU; both launches fit here)
+    tr.recover = False  # (the in-process fallback: handoff_recover_dp_worker)
     tr.load(x, y)
     res = {"impl": tr.allreduce_impl}
     tr.train(1, 0.05, 1e-4)  # a clean epoch on both ranks
@@ -439,3 +440,48 @@ def tp_xgmi_main(out_dir, world, H):
     from cme213_sp18_amd.parallel.launcher import spawn
 
     spawn(tp_xgmi_worker, world, (out_dir, H), backend="gloo")
+
+
+def handoff_recover_dp_worker(rank, world, comm, device, out_dir, allreduce):
+    """train()'s in-process recovery, 2 ranks sharing GPU 0: rank 0's all-gather hand-off really times out in the
+    first epoch; both ranks restore the epoch-start snapshot and re-run it on the last-arriver head and the
+    communicator's all-reduce.  Compared bitwise with a run that used that path from the start."""
+    from cme213_sp18_amd import NeuralNetwork
+    from cme213_sp18_amd.parallel import DataParallelTrainer
+    from cme213_sp18_amd.utils.data import synthetic_mnist
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    x, y = synthetic_mnist(3200, seed=3)
+    nn = NeuralNetwork([784, 100, 10])
+    init = [p.copy() for p in nn.params]
+    tr = DataParallelTrainer(nn, comm=comm, device=dev, batch_size=1600, allreduce=allreduce)
+    tr.engine.set_fh_allgather(True)  # (off by default when ranks share a GPU; both launches fit here)
+    tr.load(x, y)
+    res = {"impl0": tr.allreduce_impl}
+    if rank == 0:
+        tr.engine.inject_handoff_timeout(0, 2000)
+    tr.train(2, 0.05, 1e-4)
+    torch.cuda.synchronize()
+    res["recovered"] = float(tr.recovered is not None)
+    res["impl1"] = tr.allreduce_impl
+    res["agree"] = float(tr.replicas_agree())
+    got = tr.engine.params.clone()
+    tr.close()
+    nn2 = NeuralNetwork([784, 100, 10])
+    for dst, src in zip(nn2.params, init):
+        dst[...] = src
+    ref = DataParallelTrainer(nn2, comm=comm, device=dev, batch_size=1600, allreduce="rccl")
+    ref.engine.set_fh_allgather(False)
+    ref.load(x, y)
+    ref.train(2, 0.05, 1e-4)
+    torch.cuda.synchronize()
+    res["equal_ref"] = float(torch.equal(got, ref.engine.params))
+    ref.close()
+    np.savez(os.path.join(out_dir, f"recover_{allreduce}_{rank}.npz"), **{k: np.array(v) for k, v in res.items()})
+
+
+def handoff_recover_dp_main(out_dir, allreduce):
+    from cme213_sp18_amd.parallel.launcher import spawn
+
+    spawn(handoff_recover_dp_worker, 2, (out_dir, allreduce), backend="gloo")

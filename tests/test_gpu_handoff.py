@@ -77,6 +77,7 @@ def test_real_timeout_raises_in_train_and_freezes_params(H):
     epoch, and not one of the epoch's steps changed a parameter."""
     x, y = synthetic_mnist(3200, seed=2)
     tr = DataParallelTrainer(NeuralNetwork([784, H, 10]), dtype="f32", batch_size=800)
+    tr.recover = False  # (the in-process fallback is pinned by the next test)
     tr.load(x, y)
     tr.train(1, 0.01, 1e-4)
     assert tr._allgather_live() and not tr.engine.kernel_error()
@@ -85,6 +86,31 @@ def test_real_timeout_raises_in_train_and_freezes_params(H):
     with pytest.raises(KernelHandoffTimeout):
         tr.train(1, 0.01, 1e-4)
     assert torch.equal(tr.engine.params, before)
+
+
+@pytest.mark.parametrize("H", [100, 4096])
+def test_train_recovers_from_handoff_timeout_bitwise(H):
+    """train() survives a REAL timed-out all-gather hand-off in its first epoch: the epoch-start snapshot is
+    restored, the forward + head switches to the last-arriver form (no workgroup waits for another) and the epoch
+    re-runs, with one warning.  The result is BITWISE the run that used that form from the start."""
+    x, y = synthetic_mnist(3200, seed=4)
+    nn = NeuralNetwork([784, H, 10])
+    init = [p.copy() for p in nn.params]
+    tr = DataParallelTrainer(nn, dtype="f32", batch_size=800)
+    tr.load(x, y)
+    tr.engine.inject_handoff_timeout(1, 2000)
+    st = tr.train(2, 0.01, 1e-4)
+    assert tr.recovered is not None and "hand-off" in tr.recovered, tr.recovered
+    assert not tr._allgather_live() and not tr.engine.kernel_error()
+    assert st.steps == 2 * 4 and tr.iter == 8
+    nn2 = NeuralNetwork([784, H, 10])
+    for dst, src in zip(nn2.params, init):
+        dst[...] = src
+    ref = DataParallelTrainer(nn2, dtype="f32", batch_size=800)
+    ref.engine.set_fh_allgather(False)
+    ref.load(x, y)
+    ref.train(2, 0.01, 1e-4)
+    assert torch.equal(tr.engine.params, ref.engine.params)
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
@@ -120,6 +146,25 @@ def test_wide_head_counters_survive_tiling_switch(dt):
     # (bf16: the two heads' dW2 partial sums round differently in fp32, and over 6 steps the bf16 rounding of
     # D / dZ1 turns some of those last-bit differences into bf16-ulp ones: 4e-4 .. 1.5e-3 measured)
     assert rel < (1e-5 if dt == "f32" else 3e-3), rel
+
+
+@pytest.mark.parametrize("allreduce", ["xgmi"])
+def test_dp_recovers_from_one_ranks_handoff_timeout(tmp_path, allreduce):
+    """2 data-parallel ranks sharing the GPU on the xGMI-fused all-reduce; rank 0's hand-off really times out in
+    the first epoch.  Both ranks raise together, restore the epoch-start snapshot, drop to the last-arriver head and
+    the communicator's all-reduce (the poisoned xGMI buckets are closed) and finish: replicas bitwise equal, and
+    bitwise the run that used that path from the start."""
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); from tests.dist_workers import handoff_recover_dp_main; "
+            f"handoff_recover_dp_main({str(tmp_path)!r}, {allreduce!r})")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    z = [dict(np.load(tmp_path / f"recover_{allreduce}_{rank}.npz")) for rank in range(2)]
+    for rank in range(2):
+        assert str(z[rank]["impl0"]).startswith("xgmi"), z[rank]["impl0"]
+        assert float(z[rank]["recovered"]) == 1.0 and not str(z[rank]["impl1"]).startswith("xgmi"), z[rank]
+        assert float(z[rank]["equal_ref"]) == 1.0, rank
+    assert float(z[0]["agree"]) == 1.0
 
 
 @pytest.mark.parametrize("allreduce", ["rccl", "xgmi"])
