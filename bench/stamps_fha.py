@@ -19,6 +19,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=800)
     ap.add_argument("--hidden", type=int, default=100)
+    ap.add_argument("--xcd-rows", type=int, default=None, help="MlpStep.xcd_rows (default: the engine's)")
     a = ap.parse_args(argv)
     import numpy as np
     import torch
@@ -34,6 +35,8 @@ def main(argv=None):
     e.load_dataset(x, y)
     step = e._hip_step()
     assert step.fh_allgather == 1
+    if a.xcd_rows is not None:
+        step.xcd_rows = a.xcd_rows
     st = torch.cuda.current_stream().cuda_stream
     buf = torch.zeros(4096 * 4, dtype=torch.int64, device="cuda")
     wbuf = torch.zeros(4096 * 8 * 4, dtype=torch.int64, device="cuda")

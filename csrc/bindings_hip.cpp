@@ -74,6 +74,10 @@ struct MlpStep {
   // the fused wide head on the 64 x 64 tiling (H = 512-1024): -1 = when a1 is not stored (measured faster only
   // then: profiles/wide_fused_head_r2.md), 1 = always, 0 = never
   int ag_tiles64 = -1;
+  // H <= 128: the XCD-row placement of the forward + head and dW1 launches (SplitStepArgs::xcd_rows; on: the W1
+  // rows and dZ1 rows each launch writes are read back by the next one from the same XCD's L2 -- step 14.0 ->
+  // 13.1-13.2 us at n = 800, 12.3 -> 11.7 us at n = 100, profiles/kbench_xcd_rows_r4.jsonl; 0 for A/B)
+  int xcd_rows = 1;
   int ag64() const { return ag_tiles64 >= 0 ? ag_tiles64 : (store_a1 ? 0 : 1); }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
@@ -119,6 +123,10 @@ struct MlpStep {
   }
   uintptr_t kpart = 0;  // split-K dW1 partial slabs (SplitStepArgs::kpart), kpart_cap floats; 0: no split-K
   int64_t kpart_cap = 0;
+  // the persistent small-batch engine (mlp_pstep): its counters / granules / status buffers (0: not available)
+  // and the switch (persistent = 1: run_steps takes it wherever mlp_pstep_ok holds)
+  uintptr_t ps_counters = 0, ps_gran = 0, ps_status = 0;
+  int persistent = 1;
 
   // Binds the engine's buffers and shapes in ONE call (MlpEngine._hip_step): every device pointer, count and
   // layout flag the step reads, by name; an unknown name is an error.  The runtime switches stay plain fields
@@ -147,6 +155,8 @@ struct MlpStep {
       else if (k == "ag_counters") ag_counters = u(); else if (k == "ag_slabs") ag_slabs = u();
       else if (k == "ag_gran") ag_gran = u(); else if (k == "ag_gran_count") ag_gran_count = v.cast<int64_t>();
       else if (k == "kpart") kpart = u(); else if (k == "kpart_cap") kpart_cap = v.cast<int64_t>();
+      else if (k == "ps_counters") ps_counters = u(); else if (k == "ps_gran") ps_gran = u();
+      else if (k == "ps_status") ps_status = u();
       else throw std::invalid_argument("MlpStep.bind: unknown name '" + k + "'");
     }
   }
@@ -183,6 +193,7 @@ struct MlpStep {
     a.gstatus = P_<float>(gstatus);
     a.ag_wait_us = ag_wait_us;
     a.ag_test_skip = ag_test_skip;
+    a.xcd_rows = xcd_rows && cme::mlp_split_xcd_rows_ok(a);
     return a;
   }
 
@@ -316,12 +327,42 @@ struct MlpStep {
                  double reg, double lr, int sgd, uintptr_t stream) {
     CME_REQUIRE(count >= 0 && n > 0 && n <= ld && B >= n && N_end >= B && (sgd == 1 || sgd == 2),
                 "MlpStep.run_steps: bad step plan");
+    if (count == 0) return;
+    if (uses_persistent(n, sgd)) {  // every step of the plan in ONE persistent launch
+      cme::PStepArgs p;
+      p.a = split_args(shard_off, n, scale, reg, lr, 1, 0);
+      p.gstart0 = gstart0;
+      p.count = count;
+      p.B = B;
+      p.shard_off = shard_off;
+      p.N_end = N_end;
+      p.a.X = reinterpret_cast<const void*>(X);  // (the kernel adds each step's offset itself)
+      p.a.XT = reinterpret_cast<const void*>(XT);
+      p.a.labels = P_<int>(labels);
+      p.counters = P_<unsigned long long>(ps_counters);
+      p.gran = P_<unsigned long long>(ps_gran);
+      p.status = P_<unsigned long long>(ps_status);
+      p.err = P_<int>(ag_err);
+      cme::mlp_pstep(p, S(stream));
+      return;
+    }
     int64_t gs = gstart0;
     for (int64_t i = 0; i < count; ++i) {
       if (gs + B > N_end) gs = 0;
       run(gs + shard_off, n, scale, reg, lr, sgd, 0, stream, 3);
       gs += B;
     }
+  }
+
+  // run_steps takes the persistent engine: a single process (sgd = 1), the split path with the all-ones XT feature,
+  // its buffers bound, and the shape it supports (mlp_pstep_ok: H <= 128, n <= 256, n % 4 == 0)
+  bool uses_persistent(int n, int sgd) const {
+    // (fh_allgather: the switch for in-launch waits between workgroups -- off where processes share a GPU and after
+    // a timed-out hand-off, DataParallelTrainer._recover_epoch)
+    if (!persistent || !fh_allgather || !split || sgd != 1 || !ps_counters || !ps_gran || !ps_status || !ag_err)
+      return false;
+    cme::SplitStepArgs a = split_args(0, n, 1.0, 0.0, 0.0, 1, 0);
+    return cme::mlp_pstep_ok(a);
   }
 
   // Weight-gradient pieces of a step whose forward + head already ran (parts=1): used by the
@@ -473,6 +514,9 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_test_skip", &MlpStep::ag_test_skip)
       .def_readwrite("store_a1", &MlpStep::store_a1)
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
+      .def_readwrite("xcd_rows", &MlpStep::xcd_rows)
+      .def_readwrite("persistent", &MlpStep::persistent)
+      .def("uses_persistent", &MlpStep::uses_persistent, py::arg("n"), py::arg("sgd"))
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
       .def_readwrite("planes_stale", &MlpStep::planes_stale)
       .def_readwrite("dw2p", &MlpStep::dw2p)

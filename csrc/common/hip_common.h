@@ -90,4 +90,13 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+inline int device_cu_count() {  // CUs of the current device, cached per device
+  static int cached[64] = {0};
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) HIP_CHECK(hipDeviceGetAttribute(&cached[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  return cached[dev];
+}
+
 }  // namespace cme

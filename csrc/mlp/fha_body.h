@@ -61,8 +61,9 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   __shared__ int s_bad;
   __shared__ unsigned s_ep;
   const int xcd = blk & 7, slot = blk >> 3;
-  const int ct = xcd + 8 * (slot / tm), rt = slot % tm;
-  if (ct >= tn) return;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
+  // column-tile grouping (the tm row tiles of a column tile on one XCD) or, xcd_rows, row tile rt on XCD rt
+  const int ct = f.xcd_rows ? slot : xcd + 8 * (slot / tm), rt = f.xcd_rows ? xcd : slot % tm;
+  if (ct >= tn || rt >= tm) return;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
   const int t = threadIdx.x, H = f.H, C = h.C, n = f.n;
   const int r0 = rt * 16, c0 = ct * kCols;
   unsigned long long* st = f.stamps ? f.stamps + (size_t)blk * 4 : nullptr;  // diagnostics only
@@ -70,11 +71,17 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     if (st && t == 0) st[i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  // the launch epoch: one add per workgroup now (by wave 7, which has no K range at K = 784 or 800: its wait
-  // for the add never delays a GEMM wave), its value used after the GEMM
+  // the launch epoch: one add per workgroup now, by wave 7, which has no K range at K = 784 or 800 -- so it also
+  // WAITS for the add here, while the other waves run their K loop, and publishes the epoch to LDS before the
+  // GEMM's reduction barrier.  (Waited for after the GEMM, the same vmcnt(0) also covered wave 7's a1 epilogue
+  // stores: a store round trip in front of the z2 publication of every workgroup, bench/stamps_fha.py.)
   constexpr int kEpochThread = 448;
-  gran_t ep_old = 0;
-  if (t == kEpochThread) ep_old = gran_epoch_add(counters + (size_t)ct * kAgCounterStride);
+  if (t == kEpochThread) {
+    gran_t ep_old = gran_epoch_add(counters + (size_t)ct * kAgCounterStride);
+    gran_epoch_wait(ep_old);
+    s_ep = (unsigned)(ep_old / (unsigned)tm) + 1u;
+    s_bad = 0;
+  }
   // the label of this thread's softmax column (t >> 4), fetched now: loaded where the softmax uses it, it was
   // a dependent memory round trip after the all-gather wait
   const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(
@@ -93,11 +100,6 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   // they are masked below.  w2s / b2s are complete after the barrier below.
   if (t < 256) w2s[wc][wr] = w2v;
   else if (t < 256 + 16) b2s[t - 256] = b2v;
-  if (t == kEpochThread) {
-    gran_epoch_wait(ep_old);
-    s_ep = (unsigned)(ep_old / (unsigned)tm) + 1u;
-    s_bad = 0;
-  }
   __syncthreads();
   const unsigned ep = s_ep;
   // ---- 1. z2 partial W2[:, tile rows] . a1[tile rows, 32 columns] on MFMA (waves 0 and 1: 16 columns each,

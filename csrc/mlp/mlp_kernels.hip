@@ -1124,14 +1124,6 @@ int resident_per_cu(int threads) {  // workgroups of Kern one CU holds at once (
   if (occ < 0) HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, Kern, threads, 0));
   return occ;
 }
-int cu_count() {
-  static int cached[64] = {0};
-  int dev = 0;
-  HIP_CHECK(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) return 0;
-  if (!cached[dev]) HIP_CHECK(hipDeviceGetAttribute(&cached[dev], hipDeviceAttributeMultiprocessorCount, dev));
-  return cached[dev];
-}
 }  // namespace
 
 // the wave-split-K forward's operand form: 3 = 16-byte pixel loads over chunk pairs (16-byte X rows), 1 = 4-byte
@@ -1145,7 +1137,7 @@ static int fha_vec(const SplitStepArgs& f) {
 
 bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f) {
   if (f.n <= 0) return true;
-  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32), nwg = 8 * tm * cdiv(tn, 8);
+  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32), nwg = tm * tn;
   const bool af = mlp_split_fwd_fp32_w(f);
   const int vec = fha_vec(f);
 #define CME_OCC(np, af)                                                            \
@@ -1154,7 +1146,7 @@ bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f) {
               : resident_per_cu<fwd1_head_ag_kernel<np, 0, af>>(512))
   const int occ = af ? CME_OCC(3, true) : (f.npw == 3 ? CME_OCC(3, false) : CME_OCC(1, false));
 #undef CME_OCC
-  return nwg <= occ * cu_count();
+  return nwg <= occ * device_cu_count();
 }
 
 void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long long* counters,
@@ -1170,7 +1162,7 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
                                         "last-arriver form, mlp_fwd1_head)");
   const bool af = mlp_split_fwd_fp32_w(f);
   const int vec = fha_vec(f);
-  const int nwg = 8 * tm * cdiv(tn, 8);
+  const int nwg = f.xcd_rows ? 8 * tn : 8 * tm * cdiv(tn, 8);
 #define CME_FHA(np, af)                                                                                  \
   if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
   else if (vec == 1) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn); \

@@ -248,11 +248,21 @@ template <int NPZ, int VEC, bool AF>
 __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
   __shared__ uint32_t s_xf[2];
-  const int bid = blockIdx.x;
+  // logical workgroup id: dW1 tiles [0, t1) row-major, then the roles.  xcd_rows: the first 8 * t1n blocks are the
+  // dW1 tiles with row tile rt on XCD rt (blockIdx % 8; slots of XCDs past the last row tile idle), roles after
+  int bid = blockIdx.x, tb;
+  if (a.xcd_rows) {
+    const int grid1 = 8 * t1n, xcd = bid & 7, slot = bid >> 3;
+    if (bid >= grid1) bid = t1 + (bid - grid1);
+    else if (xcd * t1n + slot >= t1) return;  // (uniform)
+    else bid = xcd * t1n + slot;
+    tb = bid;
+  } else {
+    tb = bid < t1 ? xcd_remap(bid, t1) : bid;
+  }
   const float reg = (float)a.reg, lr = (float)a.lr;
   const bool fused = a.xf.world > 0;
   if (bid < t1) {  // ---- dW1 tile
-    const int tb = xcd_remap(bid, t1);
     const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
     TileGeom g{r1, a.P + a.bias_col, a.n, a.w1_row0 + (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
     float *gw = a.gW1, *gb = a.gb1;
@@ -1086,8 +1096,6 @@ bool glds_wgrad_ok(const SplitStepArgs& a) {
          al16(a.XTw) && a.P % 4 == 0 && al16(a.W1);  // (W1Chunks: 16-byte W1 rows chunks)
 }
 
-// 128x128 tiles when that still gives ~200+ workgroups, else 64x64 (same choice as the register-staged
-// engine, so mlp_split_fwd1_z2_chunks holds for both)
 // the A-in-registers engine: 128 x 128 tiles only, and only when they still give ~200+ workgroups
 bool rega_fwd_ok(const SplitStepArgs& a) {
   return glds_fwd_ok(a) && cdiv(a.H, 128) * cdiv(a.n, 128) >= 192 && a.P % 4 == 0 && al16(a.W1);
@@ -1260,17 +1268,6 @@ int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a) {
   return rega_fwd_ok(a) ? cdiv(a.H, 128) : cdiv(a.H, 64);  // the forward's tiles: rega 128 rows, glds 64
 }
 
-namespace {
-int device_cu_count() {
-  static int cached[64] = {0};
-  int dev = 0;
-  HIP_CHECK(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) return 0;
-  if (!cached[dev]) HIP_CHECK(hipDeviceGetAttribute(&cached[dev], hipDeviceAttributeMultiprocessorCount, dev));
-  return cached[dev];
-}
-}  // namespace
-
 // the tile the fused head runs on: 128 (A-in-registers engine), 64 (the direct-to-LDS 64 x 64 tiling), 0 (none)
 // (64 x 64: faster than forward + head_wide_kernel only without the a1 store -- 784-1024-10 bf16 25.33 -> 25.06 us,
 // 784-512-10 f32 32.20 -> 31.13 us, profiles/wide_ag_ab_64_r2.jsonl; MlpStep.ag_tiles64 decides)
@@ -1429,9 +1426,11 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   // (3: the XT bytes as 16-byte loads over chunk pairs, mma_tile.h: 16-byte XT rows, n % 16 == 0)
   const bool pairs = al16(a.XT) && a.ldxt % 16 == 0 && a.n % 16 == 0;
   const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? (pairs ? 3 : 1) : (a.n % 4 == 0 ? 2 : 0));
-  const dim3 grid(t1 + t2 + tb);
   SplitStepArgs b = a;
   b.w1_planes = mlp_split_w1_planes_read(a) ? 1 : 0;
+  // the XCD-row placement only for the whole layer's dW1 (a bucketed row range keeps the plain order)
+  b.xcd_rows = a.xcd_rows && do_w1 && a.w1_row0 == 0 && a.w1_rows < 0 && cdiv(a.H, 16 * kWMB) <= 8;
+  const dim3 grid((b.xcd_rows ? 8 * t1n : t1) + t2 + tb);
 #define CME_WG(npz, af)                                                                   \
   if (vec == 3) wgrad_split_kernel<npz, 3, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);      \
   else if (vec == 1) wgrad_split_kernel<npz, 1, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \
@@ -1440,6 +1439,10 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   if (af) { CME_WG(3, true) } else if (a.npz == 3) { CME_WG(3, false) } else { CME_WG(1, false) }
 #undef CME_WG
   CME_LAUNCH_CHECK(s);
+}
+
+bool mlp_split_xcd_rows_ok(const SplitStepArgs& a) {
+  return a.H <= 16 * 8 && a.n > 0 && cdiv(a.n, 32) <= device_cu_count() / 8;
 }
 
 int mlp_split_fused_tiles(int P, int H, int cap) {

@@ -6,8 +6,8 @@
 //   variant 0 global : one thread per interior point
 //   variant 1 loop   : each thread walks ROWS consecutive y points keeping the
 //                      2b+1-tall column window in registers (1 new load per row)
-//   variant 2 lds    : (256 x 32) tile + b-wide halo staged in LDS once with
-//                      16-byte loads, every stencil read served from LDS
+//   variant 2 lds    : 256-column strip per wave, register column window for y,
+//                      the centre row exchanged through LDS for the x-neighbours
 //   variant 3 vec    : 4 x-points per lane with 16-byte loads/stores + the
 //                      register column window (fewest instructions per byte)
 #include <algorithm>
@@ -150,70 +150,78 @@ __device__ __forceinline__ void stencil_vec_body(float* __restrict__ next, const
 
 constexpr int kVecRows = 8;
 
-// variant 2 "lds": a 256 x 32 interior tile + its b-wide halo staged into LDS ONCE with 16-byte buffer
-// loads (every grid value of the tile read from memory once: (256 + 2b)(32 + 2b) / (256 * 32) = 1.29x at
-// order 8, vs 1.75x for vec's three overlapping float4 loads per output row), then each lane forms 4 x
-// points x 8 rows from LDS: per row the centre line as 3 x ds_read_b128 and the new bottom row's 4 values,
-// with the (2b+1)-tall column window in registers.
-constexpr int kLTX = 256, kLTY = 32;
+// variant 2 "lds" -- the capability the reference left empty (hw3code/gpuStencil.cu:263-308), built so that every
+// grid value is fetched from memory ONCE per sweep and every x-neighbour comes out of LDS:
+//   * a wave owns a 256-column strip (4 x points per lane, 16-byte loads) and walks kLdsRows rows down it with the
+//     (2b+1)-tall float4 column window in registers (the y-stencil: one new 16-byte load per lane per row);
+//   * the centre row goes through the wave's own LDS row buffer (64 float4 + a float4 of halo on each side, loaded
+//     by lanes 0 / 63 only), and each lane reads its left / right neighbour float4 back with ds_read_b128 -- the
+//     x-stencil costs 1 write + 2 16-byte LDS reads instead of vec's two extra 16-byte global loads per lane per
+//     row (the same bytes from L1 / L2 a second and third time);
+//   * the row buffer is double-buffered by row parity (one wave barrier per row, no workgroup barrier: the
+//     buffer is wave-private), stores are non-temporal (the next grid is written once and read one sweep later,
+//     after >> 256 MB of other traffic at the HBM-sized grids).
+constexpr int kLdsRows = 16;
 
-template <int ORDER>
+template <int ORDER, int ROWS>
 __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
-                                                 int gy, int nx, int ny, float xcfl, float ycfl, int tbx, int tby) {
+                                                 int gy, int nx, int ny, float xcfl, float ycfl, int bx, int by,
+                                                 f32x4 (*xrow)[66]) {
   constexpr int B = Coef<ORDER>::B;
-  constexpr int W4 = (kLTX + 2 * B + 3) / 4 + (B < 4 ? 1 : 0);  // staged float4 per row (+1: 3-wide reads)
-  constexpr int HH = kLTY + 2 * B;
-  __shared__ f32x4 tile[HH][W4];
-  const int c0 = tbx * kLTX, r0 = tby * kLTY;  // grid column / row of staged (0, 0)
+  constexpr int WIN = 2 * B + 1;
+  static_assert(B <= 4, "x-neighbours within one float4 of each side");
+  const int lane = threadIdx.x, w = threadIdx.y;
+  const int x0 = (bx * 64 + lane) * 4;  // first of this lane's 4 interior x
+  const int y0 = (by * 4 + w) * ROWS;
+  if (y0 >= ny) return;  // wave-uniform (no workgroup barrier below)
   const __amdgpu_buffer_rsrc_t rc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(curr), (short)0, (int)((int64_t)gx * gy * 4), 0x00020000);
-  const int tid = threadIdx.y * 64 + threadIdx.x;
-  for (int idx = tid; idx < HH * W4; idx += 256) {
-    const int r = idx / W4, q = idx - r * W4;
-    const int gr = r0 + r, gc = c0 + 4 * q;
-    // out-of-grid rows / columns past the row read 0 or the next row's first values: never used
-    tile[r][q] = ld4(rc, gr < gy ? (int64_t)gr * gx + gc : (int64_t)0x7FFFFFF0 / 4);
-  }
-  __syncthreads();
-  const int lane = threadIdx.x, xl = 4 * lane;  // interior local columns xl .. xl + 3
-  const int y0 = threadIdx.y * 8;
-  if (c0 + xl >= nx || r0 + y0 >= ny) return;
-  const float* t = reinterpret_cast<const float*>(&tile[0][0]);
-  constexpr int WP = W4 * 4;  // floats per staged row
-  // staged (row, col) of interior local (y, x): (y + B, x + B)
-  float win[2 * B + 1][4];
+  const int64_t col = x0 + B;
+  constexpr int64_t kOffOOB = (int64_t)0x7FFFFFF0 / 4;
+  f32x4 win[WIN];
 #pragma unroll
-  for (int k = 0; k < 2 * B; ++k)
+  for (int k = 0; k < WIN - 1; ++k) win[k] = ld4(rc, (int64_t)(y0 + k) * gx + col);
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
 #pragma unroll
-    for (int j = 0; j < 4; ++j) win[k][j] = t[(y0 + k) * WP + xl + B + j];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
+  for (int r = 0; r < ROWS; ++r) {
     const int y = y0 + r;
-    if (r0 + y >= ny) break;
+    if (y >= ny) break;
+    const int64_t rowc = (int64_t)(y + B) * gx + col;
+    win[WIN - 1] = ld4(rc, (int64_t)(y + 2 * B) * gx + col);
+    // the strip's halo float4s: lane 0 the one left of the strip, lane 63 the one right of it
+    const f32x4 hv = ld4(rc, lane == 0 ? rowc - 4 : (lane == 63 ? rowc + 4 : kOffOOB));
+    f32x4* row = xrow[r & 1];
+    row[1 + lane] = win[B];
+    if (lane == 0) row[0] = hv;
+    if (lane == 63) row[65] = hv;
+    wave_sync();
+    const f32x4 lf = row[lane], rt = row[lane + 2];
+    float line[12];  // x = x0 + B - 4 .. x0 + B + 7
 #pragma unroll
-    for (int j = 0; j < 4; ++j) win[2 * B][j] = t[(y + 2 * B) * WP + xl + B + j];
-    float line[12];  // staged columns xl .. xl + 11 of the centre row
-    const f32x4* lp = reinterpret_cast<const f32x4*>(t + (y + B) * WP + xl);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const f32x4 v = lp[q];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) line[4 * q + j] = v[j];
+    for (int j = 0; j < 4; ++j) {
+      line[j] = lf[j];
+      line[4 + j] = win[B][j];
+      line[8 + j] = rt[j];
     }
     f32x4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       o[j] = apply_stencil<ORDER>(
-          line[B + j], [&](int k) { return line[B + j + k]; }, [&](int k) { return win[B + k][j]; }, xcfl, ycfl);
-    const int gyy = r0 + y + B, gxx = c0 + xl + B;
-    float* dst = next + (int64_t)gyy * gx + gxx;
+          line[4 + j], [&](int k) { return line[4 + j + k]; }, [&](int k) { return win[B + k][j]; }, xcfl, ycfl);
+    float* dst = next + rowc;
+    if (x0 + 4 <= nx && (rowc & 3) == 0) {
+      __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(dst));
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (c0 + xl + j < nx) dst[j] = o[j];
+      for (int j = 0; j < 4; ++j)
+        if (x0 + j < nx) dst[j] = o[j];
+    }
 #pragma unroll
-    for (int k = 0; k < 2 * B; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) win[k][j] = win[k + 1][j];
+    for (int k = 0; k < WIN - 1; ++k) win[k] = win[k + 1];
   }
 }
 
@@ -260,7 +268,10 @@ __global__ __launch_bounds__(256) void stencil_fused(float* __restrict__ next, c
   const int bx = id % nbx, by = id / nbx;
   if constexpr (VARIANT == 0) stencil_global_body<ORDER>(next, curr, gx, nx, ny, xcfl, ycfl, bx, by);
   else if constexpr (VARIANT == 1) stencil_loop_body<ORDER, 8>(next, curr, gx, nx, ny, xcfl, ycfl, bx, by);
-  else if constexpr (VARIANT == 2) stencil_lds_body<ORDER>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by);
+  else if constexpr (VARIANT == 2) {
+    __shared__ f32x4 xrow[4][2][66];  // per wave: the centre row (+ halo), double-buffered by row parity
+    stencil_lds_body<ORDER, kLdsRows>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by, xrow[threadIdx.y]);
+  }
   else stencil_vec_body<ORDER, kVecRows>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by);
 }
 
@@ -269,7 +280,7 @@ void launch_v(float* next, const float* curr, int gx, int gy, float xcfl, float 
               hipStream_t s) {
   constexpr int B = Coef<ORDER>::B;
   const int nx = gx - 2 * B, ny = gy - 2 * B;
-  const int rows_per_block = VARIANT == 0 ? 4 : (VARIANT == 1 ? 4 * 8 : (VARIANT == 2 ? kLTY : 4 * kVecRows));
+  const int rows_per_block = VARIANT == 0 ? 4 : (VARIANT == 1 ? 4 * 8 : (VARIANT == 2 ? 4 * kLdsRows : 4 * kVecRows));
   const int cols_per_block = VARIANT >= 2 ? 256 : 64;
   const int nbx = (nx + cols_per_block - 1) / cols_per_block, nby = (ny + rows_per_block - 1) / rows_per_block;
   const int nint = nbx * nby;

@@ -662,9 +662,78 @@ def test_allgather_timeout_flag_raises_in_train(H):
 
     x, y = synthetic_mnist(1600, seed=2)
     tr = DataParallelTrainer(NeuralNetwork([784, H, 10]), dtype="f32", batch_size=800)
+    tr.recover = False  # (the in-process fallback: test_gpu_handoff.py)
     tr.load(x, y)
     tr.train(1, 0.01, 1e-4)  # clean epoch: no raise
     assert tr._allgather_live() and not tr.engine.kernel_error()
     tr.engine.ag_err.fill_(1)  # what a timed-out wait leaves behind
     with pytest.raises(KernelHandoffTimeout):
         tr.train(1, 0.01, 1e-4)
+
+
+@pytest.mark.parametrize("n", [800, 200, 100, 37])
+def test_xcd_row_placement_is_bitwise_neutral(n):
+    """H <= 128: placing row tile rt's workgroups on XCD rt in both step launches (MlpStep.xcd_rows) changes
+    where the work runs, not what it computes: params, planes and the loss partials are bitwise those of the
+    column-tile placement, over several steps including the fused xGMI all-reduce form (world 1)."""
+    from cme213_sp18_amd._native import hip as _hip
+
+    x, y = synthetic_mnist(4 * n + 64, seed=n)
+    nn = NeuralNetwork([784, 100, 10])
+    outs = []
+    for xr in (0, 1):
+        e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        e._hip_step().xcd_rows = xr
+        for i in range(3):
+            e.run(i * n, n, 1.0 / n, 1e-4, 0.05, sgd=True, with_loss=True)
+        xc = _hip().comm.XgmiComm(0, 1, e.params.numel(), 4, e.fused_allreduce_slots())
+
+        class _B:
+            c = xc
+
+        e.attach_xgmi(_B)
+        for i in range(3):
+            e.run(i * n + 7, n, 1.0 / n, 1e-4, 0.05, sgd=2)
+        torch.cuda.synchronize()
+        assert xc.error() == 0 and not e.kernel_error()
+        e.attach_xgmi(None)
+        xc.close()
+        outs.append((e.params.clone(), e.loss_buf.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("n", [100, 64, 128, 200, 256, 36])
+def test_persistent_engine_matches_two_launch_steps(n):
+    """The persistent small-batch engine (csrc/mlp/pstep.hip: every step of MlpStep.run_steps in ONE launch, each
+    workgroup keeping its 16 W1 rows in LDS) against the two-launch steps of the same plan (a wrap past the end of
+    the dataset included) and against the PyTorch fp32 step: the same exact split3 products, so the parameters agree
+    to fp32 reassociation."""
+    x, y = synthetic_mnist(6 * n + 20, seed=n)
+    N = 6 * n + 20
+    nn = NeuralNetwork([784, 100, 10])
+    outs = []
+    for mode in ("persistent", "two-launch", "torch"):
+        e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda", backend="torch" if mode == "torch" else "hip")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        if mode == "torch":
+            gs = 0
+            for _ in range(9):
+                if gs + n > N:
+                    gs = 0
+                e.run(gs, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+                gs += n
+        else:
+            st = e._hip_step()
+            st.persistent = int(mode == "persistent")
+            assert st.uses_persistent(n, 1) == (mode == "persistent")
+            s = torch.cuda.current_stream().cuda_stream
+            st.run_steps(0, 4, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1, s)  # steps 0..3
+            st.run_steps(4 * n, 5, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1, s)  # steps 4..8 (wraps at step 6)
+            torch.cuda.synchronize()
+            assert not e.kernel_error()
+        outs.append(e.params.clone())
+    assert _rel(outs[0], outs[1]) < 1e-5, _rel(outs[0], outs[1])
+    assert _rel(outs[0], outs[2]) < 2e-5, _rel(outs[0], outs[2])

@@ -181,3 +181,42 @@ def test_bench_tunes_allreduce_shared_gpu(gpus):
     assert len(tune) == (2 if gpus == 2 else 3) and any(k.startswith("xgmi") for k in tune), tune
     nums = {k: v for k, v in tune.items() if isinstance(v, (int, float))}
     assert nums and cfg["allreduce"] == min(nums, key=nums.get), (cfg["allreduce"], tune)
+
+
+def test_bench_probes_dp_vs_tp_and_records_prediction():
+    """bench.py --gpus 2 on a wide layer (784-1024-10, global batch 1600; 2 ranks sharing GPU 0): with
+    --parallel auto the data- and tensor-parallel steps are both probed, the faster one is timed, and the record
+    carries the probes, the chosen parallelism, the measured all-reduce and the cost model's prediction
+    (allreduce_pred_us); the weak-scaling run rides along as the secondary sub-record."""
+    import json
+
+    env = dict(os.environ, CME_SHARED_GPU="1", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--hidden", "1024",
+                        "--batch", "1600", "--steps", "10", "--warmup", "2", "--tune-steps", "10"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = rec["config"]
+    probes = cfg["parallel_tuning_us_per_step"]
+    assert set(probes) == {"dp2", "tp2"}, probes
+    nums = {k: v for k, v in probes.items() if isinstance(v, (int, float))}
+    assert nums and cfg["parallelism"] == min(nums, key=nums.get), (cfg["parallelism"], probes)
+    assert cfg["allreduce_pred_us"] > 0 and cfg["allreduce_us"] > 0, cfg
+    assert rec["scaling"] == "strong" and cfg["global_batch"] == 1600
+    assert rec["weak"]["global_batch"] == 3200 and rec["weak"]["parallelism"] == cfg["parallelism"]
+
+
+def test_bench_probe_budget_skips_candidates():
+    """A zero probe budget: the all-reduce policy's own pick still runs, every other candidate is recorded as
+    'skipped: budget' and the timed region runs the pick."""
+    import json
+
+    env = dict(os.environ, CME_SHARED_GPU="1", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "10",
+                        "--warmup", "2", "--tune-steps", "10", "--tune-budget-s", "0", "--secondary", "off"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    tune = rec["config"]["allreduce_tuning_us_per_step"]
+    assert "skipped: budget" in tune.values(), tune
+    assert "weak" not in rec
