@@ -507,13 +507,12 @@ struct EpiSigWT {
   }
 };
 
-// NBT 16-column blocks per a1 tile (32 or 64 columns; a 64-column tile halves the W1-plane re-reads
-// through L2 at half the workgroups, but serialises two head passes in the last arriver)
-template <int NPW, int VEC, int NBT, bool AF>
+// 32-column a1 tiles (64-column tiles measured 15.4 vs 10.3 us at 784-100-10, n = 800: the last arriver then
+// runs two head passes back to back)
+template <int NPW, int VEC, bool AF>
 __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArgs h, unsigned* __restrict__ counters,
                                                         int tm, int tn) {
-  constexpr int kCols = 16 * NBT;
-  __shared__ __attribute__((aligned(16))) float red[8 * 1 * NBT * 4 * 64];
+  __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];
   __shared__ __attribute__((aligned(16))) Head32Lds L;
   __shared__ int s_last;
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -527,9 +526,9 @@ __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArg
   // W2 / b2 for the head, staged by every workgroup before its GEMM (independent of a1; wsk_tile's
   // internal barrier orders these LDS writes before any head read)
   head32_stage(h, threadIdx.x, L);
-  TileGeom g{f.H, f.n, f.P, rt * 16, ct * kCols};
+  TileGeom g{f.H, f.n, f.P, rt * 16, ct * kH32Cols};
   EpiSigWT epi{f.b1, f.a1, f.ld, f.xscale, {}};
-  fwd_tile<NPW, NBT, VEC, NBT == 2 ? 4 : 2, AF>(f, g, epi, red);
+  fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores are done
   __syncthreads();
   stamp(1);
@@ -543,8 +542,7 @@ __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArg
   __syncthreads();
   stamp(2);
   if (!s_last) return;
-#pragma unroll
-  for (int q = 0; q < NBT / 2; ++q) head32<true>(h, ct * (NBT / 2) + q, threadIdx.x, L);
+  head32<true>(h, ct, threadIdx.x, L);
   if (st) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp(3);
@@ -1100,18 +1098,15 @@ void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters
   CME_REQUIRE(mlp_fwd1_head_ok(f, h), "fwd1_head: H <= 128, C <= 16, train-mode head over the same a1");
   CME_REQUIRE((int64_t)f.H * f.P * 2 * f.npw < (int64_t)kOOB && (int64_t)f.n * f.P < (int64_t)kOOB,
               "fwd1_head: operand too large for 32-bit buffer offsets");
-  // 32-column a1 tiles (64-column tiles measured 15.4 vs 10.3 us at 784-100-10, n=800: the last arriver
-  // then runs two head passes back to back)
-  constexpr int nbt = 2;
-  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 16 * nbt);
+  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, kH32Cols);
   CME_REQUIRE(counters != nullptr && tn <= max_tiles, "fwd1_head: counter array too small");
   const bool af = mlp_split_fwd_fp32_w(f);
   const bool vec = reinterpret_cast<uintptr_t>(f.X) % 4 == 0 &&
                    reinterpret_cast<uintptr_t>(af ? (const void*)f.W1 : f.W1p) % 16 == 0 && f.P % 8 == 0;
   const int nwg = 8 * tm * cdiv(tn, 8);
 #define CME_FH(np, af)                                                                     \
-  if (vec) fwd1_head_kernel<np, 1, nbt, af><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);   \
-  else fwd1_head_kernel<np, 0, nbt, af><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);
+  if (vec) fwd1_head_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);   \
+  else fwd1_head_kernel<np, 0, af><<<nwg, 512, 0, s>>>(f, h, counters, tm, tn);
   if (af) { CME_FH(3, true) } else if (f.npw == 3) { CME_FH(3, false) } else { CME_FH(1, false) }
 #undef CME_FH
   CME_LAUNCH_CHECK(s);

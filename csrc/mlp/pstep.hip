@@ -80,7 +80,8 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
         __hip_atomic_fetch_add(p.counters + (size_t)r * 32, (unsigned long long)p.count, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     s_base = (unsigned)old;
-    L.bad = 0;
+    // the error word is sticky (as for the two-launch step): set by an earlier launch, this one applies nothing
+    L.bad = __hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   }
   // ---- parameters of this tile into LDS
   for (int i = t; i < 16 * kPW1S; i += kPT) {
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
   const __amdgpu_buffer_rsrc_t rX = make_rsrc(a.X), rXT = make_rsrc(a.XT), rL = make_rsrc(a.labels);
   const int kch = (P + 31) / 32;  // forward K chunks (<= 25)
   int64_t gs = p.gstart0;
-  bool ok = true;
+  bool ok = !L.bad;
 
   for (int64_t s = 0; s < p.count && ok; ++s) {
     if (gs + p.B > p.N_end) gs = 0;
@@ -169,7 +170,8 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
     }
     // ================= 2. this tile's z2 partial W2[:, rows] . a1 -> granules (double-buffered by step parity)
     gran_t* z2g = p.gran + (size_t)(s & 1) * 8 * 16 * kPMaxN;  // [parity][tile][class][column]
-    for (int i = t; i < C * n; i += kPT) {
+    // (test hook, SplitStepArgs::ag_test_skip: this workgroup withholds its partials, every poll really times out)
+    for (int i = t; i < (a.ag_test_skip == r ? 0 : C * n); i += kPT) {
       const int c = i / n, col = i - c * n;
       float z = 0.f;
 #pragma unroll

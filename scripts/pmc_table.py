@@ -4,7 +4,8 @@ instruction mix) from the rocprofv3 passes of scripts/gpu_pmc_wide.sh.
 
     python scripts/pmc_table.py gpurun_out/pmch [--min-us 3] [--clock-ghz 2.4]
 
-Busy % = counter cycles / (median kernel duration x clock x 1024 SIMDs); SQ_ACTIVE_INST_* count quad-cycles
+Workgroups = the launch grid (a persistent kernel whose blockIdx % 8 != 0 workgroups exit at once uses 1/8 of
+them); TCP pending stall = TCP_PENDING_STALL_CYCLES / (duration x clock x 256 CUs).  Busy % = counter cycles / (median kernel duration x clock x 1024 SIMDs); SQ_ACTIVE_INST_* count quad-cycles
 (MI355X_MICROARCH.md), SQ_VALU_MFMA_BUSY_CYCLES counts cycles.  The duration is the kernel trace's median in
 the PMC pass (profiled runs: a lower bound on the busy share of an unprofiled launch).
 """
@@ -23,6 +24,7 @@ def main(argv=None):
     a = ap.parse_args(argv)
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
+    wgs = {}
     for f in ("l2", "waves", "lat", "lds"):
         p = os.path.join(a.dir, f + "_counter_collection.csv")
         if not os.path.exists(p):
@@ -31,9 +33,10 @@ def main(argv=None):
             acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for r in csv.DictReader(open(os.path.join(a.dir, f + "_kernel_trace.csv"))):
             dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    print("| kernel | median us | MFMA busy | VALU busy | wave cycles waiting | L2 hit | L1->L2 latency (cyc) "
-          "| VALU / wave | MFMA / wave | LDS bank conflicts |")
-    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
+            wgs[r["Kernel_Name"]] = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
+    print("| kernel | median us | workgroups | MFMA busy | VALU busy | wave cycles waiting | TCP pending stall | L2 hit "
+          "| L1->L2 latency (cyc) | VALU / wave | MFMA / wave | LDS bank conflicts |")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for k, v in sorted(acc.items(), key=lambda kv: -sorted(dur[kv[0]])[len(dur[kv[0]]) // 2]):
         d = sorted(dur[k])
         t = d[len(d) // 2]
@@ -49,9 +52,11 @@ def main(argv=None):
 
         cyc = t * 1e-6 * a.clock_ghz * 1e9 * 1024
         name = re.sub(r"\(.*$", "", k.replace("cme::(anonymous namespace)::", "").replace("void ", ""))
-        print(f"| `{name[:70]}` | {t:.2f} | {100 * div(g('SQ_VALU_MFMA_BUSY_CYCLES'), cyc):.1f} % | "
+        cu_cyc = cyc / 4  # (256 CUs)
+        print(f"| `{name[:70]}` | {t:.2f} | {wgs.get(k, 0)} | {100 * div(g('SQ_VALU_MFMA_BUSY_CYCLES'), cyc):.1f} % | "
               f"{100 * div(4 * g('SQ_ACTIVE_INST_VALU'), cyc):.1f} % | "
               f"{100 * div(g('SQ_WAIT_INST_ANY'), g('SQ_WAVE_CYCLES')):.0f} % | "
+              f"{100 * div(g('TCP_PENDING_STALL_CYCLES_sum'), cu_cyc):.1f} % | "
               f"{100 * div(g('TCC_HIT_sum'), g('TCC_HIT_sum') + g('TCC_MISS_sum')):.0f} % | "
               f"{div(g('TCP_TCC_READ_REQ_LATENCY_sum'), g('TCP_TCC_READ_REQ_sum')):.0f} | "
               f"{div(g('SQ_INSTS_VALU'), g('SQ_WAVES')):.0f} | {div(g('SQ_INSTS_MFMA'), g('SQ_WAVES')):.1f} | "

@@ -737,3 +737,31 @@ def test_persistent_engine_matches_two_launch_steps(n):
         outs.append(e.params.clone())
     assert _rel(outs[0], outs[1]) < 1e-5, _rel(outs[0], outs[1])
     assert _rel(outs[0], outs[2]) < 2e-5, _rel(outs[0], outs[2])
+
+
+def test_persistent_engine_timeout_applies_nothing():
+    """A real timed-out z2 hand-off inside the persistent launch (one workgroup withholds its partials,
+    MlpEngine.inject_handoff_timeout): the launch ends (every wait is bounded), sets the sticky error word and
+    writes NO parameter back; a later launch with the hook off applies nothing either (the word is sticky)."""
+    n = 100
+    x, y = synthetic_mnist(4 * n, seed=9)
+    nn = NeuralNetwork([784, 100, 10])
+    e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda")
+    e.set_params(*nn.params)
+    e.load_dataset(x, y)
+    st = e._hip_step()
+    assert st.uses_persistent(n, 1)
+    s = torch.cuda.current_stream().cuda_stream
+    st.run_steps(0, 3, n, 0, n, 4 * n, 1.0 / n, 1e-4, 0.05, 1, s)
+    torch.cuda.synchronize()
+    assert not e.kernel_error()
+    before = e.params.clone()
+    e.inject_handoff_timeout(2, 2000)
+    st.run_steps(0, 3, n, 0, n, 4 * n, 1.0 / n, 1e-4, 0.05, 1, s)
+    torch.cuda.synchronize()
+    assert e.kernel_error(), "the withheld partials did not time out"
+    assert torch.equal(e.params, before)
+    e.inject_handoff_timeout(-1)
+    st.run_steps(0, 3, n, 0, n, 4 * n, 1.0 / n, 1e-4, 0.05, 1, s)
+    torch.cuda.synchronize()
+    assert torch.equal(e.params, before)
