@@ -97,6 +97,7 @@ def main(argv=None):
                                  ("wgrad_sgd", part(2)), ("wgrad_grads", part(2, 0)),
                                  ("step_fused", part(3)), ("sgd_flat", lambda: e.sgd(0.0))):
                     row[name + "_us"] = round(timeit(fn, a.reps), 3)
+                step.persistent = 1
                 if step.uses_persistent(n, 1):  # the persistent engine: reps steps in ONE launch (run_steps)
                     import torch as _t
 

@@ -126,7 +126,7 @@ struct MlpStep {
   // the persistent small-batch engine (mlp_pstep): its counters / granules / status buffers (0: not available)
   // and the switch (persistent = 1: run_steps takes it wherever mlp_pstep_ok holds)
   uintptr_t ps_counters = 0, ps_gran = 0, ps_status = 0;
-  int persistent = 1;
+  int persistent = 0;  // (off by default until the engine is validated on the GPU: tests and kbench turn it on)
 
   // Binds the engine's buffers and shapes in ONE call (MlpEngine._hip_step): every device pointer, count and
   // layout flag the step reads, by name; an unknown name is an error.  The runtime switches stay plain fields

@@ -108,14 +108,12 @@ __device__ __forceinline__ void head_stage(const HeadArgs& a, int t, int nthr, P
   if (t < NC) ws[tot + t] = buf_load1<P>(rb, t < C ? t * (int)sizeof(P) : kOOB);
 }
 
-template <typename P, int NC, bool LDSW, int HPT>
+template <typename P, int NC, bool LDSW>
 __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, const int t, char* head_dyn,
                                            P (*zred)[NC][kHeadCols], float* lred) {
   // One head block (kHeadCols columns, 256 threads) -- vb: the block index, t: thread in [0, 256);
-  // every barrier below is reached by all threads of the workgroup.
-  // HPT > 0: every thread owns at most HPT hidden units (H <= HPT * NPART); their
-  // a1 values are loaded ONCE (one burst, before the W2 staging barrier) and
-  // reused by both passes.  HPT == 0: generic loop for large H.
+  // every barrier below is reached by all threads of the workgroup.  (fp64 and the head-alone profiling hook
+  // only: the fp32 / bf16 training steps take the MFMA heads)
   constexpr int COLS = kHeadCols;
   constexpr int NPART = 256 / COLS;
   const P* __restrict__ a1 = static_cast<const P*>(a.a1);
@@ -130,15 +128,6 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
   const int b = valid ? bcol : a.n - 1;  // clamped: loads stay in bounds, results discarded
   const int lab = a.mode == HEAD_TRAIN ? a.labels[b] : 0;
 
-  P xa[HPT > 0 ? HPT : 1];
-  if constexpr (HPT > 0) {
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(a1);
-#pragma unroll
-    for (int u = 0; u < HPT; ++u) {
-      const int h = part + u * NPART;
-      xa[u] = buf_load1<P>(rs, h < H ? (h * a.lda + b) * (int)sizeof(P) : kOOB);
-    }
-  }
   if constexpr (LDSW) {
     head_stage<P, NC>(a, t, 256, ws);
     __syncthreads();
@@ -152,14 +141,7 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
   P z[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) z[c] = P(0);
-  if constexpr (HPT > 0) {
-#pragma unroll
-    for (int u = 0; u < HPT; ++u) {
-      const int h = min(part + u * NPART, H - 1);  // xa == 0 past H
-#pragma unroll
-      for (int c = 0; c < NC; ++c) z[c] += w2(c, h) * xa[u];
-    }
-  } else {
+  {
     int h = part;
     for (; h + 3 * NPART < H; h += 4 * NPART) {
       P x[4];
@@ -276,23 +258,15 @@ __device__ __forceinline__ void head_block(const HeadArgs& a, const int vb, cons
       }
     }
   };
-  if constexpr (HPT > 0) {
-#pragma unroll
-    for (int u = 0; u < HPT; ++u) {
-      const int h = part + u * NPART;
-      if (h < H) emit(h, xa[u]);
-    }
-  } else {
-    for (int h = part; h < H; h += NPART) emit(h, a1[(size_t)h * a.lda + bcol]);
-  }
+  for (int h = part; h < H; h += NPART) emit(h, a1[(size_t)h * a.lda + bcol]);
 }
 
-template <typename P, int NC, bool LDSW, int HPT>
+template <typename P, int NC, bool LDSW>
 __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) char head_dyn[];
   __shared__ P zred[4][NC][kHeadCols];
   __shared__ float lred[4];
-  head_block<P, NC, LDSW, HPT>(a, blockIdx.x, threadIdx.x, head_dyn, zred, lred);
+  head_block<P, NC, LDSW>(a, blockIdx.x, threadIdx.x, head_dyn, zred, lred);
 }
 
 // ------------------------------------------------ K2 on MFMA: 32 columns per 512-thread workgroup
@@ -564,13 +538,8 @@ template <typename P, int NC>
 void launch_head(const HeadArgs& a, hipStream_t s) {
   const dim3 grid((a.n + kHeadCols - 1) / kHeadCols);
   const size_t lds = (size_t)head_lds_elems(a.H, NC) * sizeof(P);
-  constexpr int NPART = 256 / kHeadCols;
-  if (lds <= (size_t)kHeadLdsMax) {
-    if (a.H <= 8 * NPART) head_kernel<P, NC, true, 8><<<grid, 256, lds, s>>>(a);
-    else head_kernel<P, NC, true, 0><<<grid, 256, lds, s>>>(a);
-  } else {
-    head_kernel<P, NC, false, 0><<<grid, 256, 0, s>>>(a);
-  }
+  if (lds <= (size_t)kHeadLdsMax) head_kernel<P, NC, true><<<grid, 256, lds, s>>>(a);
+  else head_kernel<P, NC, false><<<grid, 256, 0, s>>>(a);
 }
 
 // ------------------------------------------------ K2 for wide layers (H >= 512)

@@ -750,6 +750,7 @@ def test_persistent_engine_timeout_applies_nothing():
     e.set_params(*nn.params)
     e.load_dataset(x, y)
     st = e._hip_step()
+    st.persistent = 1
     assert st.uses_persistent(n, 1)
     s = torch.cuda.current_stream().cuda_stream
     st.run_steps(0, 3, n, 0, n, 4 * n, 1.0 / n, 1e-4, 0.05, 1, s)
