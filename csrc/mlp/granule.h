@@ -82,4 +82,35 @@ __device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsi
   return true;
 }
 
+// The same poll over an arbitrary set of granules base[off[k]], k < N, of which this lane needs those whose bit is
+// set in `need` (the others take no load and count as arrived); f(k, value) for every needed k in k order.  One pass
+// issues every missing granule's load back to back, so a lane gathering several items pays ONE memory round trip
+// per pass, not one per item.  Wave-uniform; false after `limit_us` of wall time (f not called).
+template <int N, class F>
+__device__ __forceinline__ bool gran_poll_set(const gran_t* base, const unsigned (&off)[N], unsigned need, unsigned ep,
+                                              uint32_t limit_us, F&& f) {
+  static_assert(N <= 32, "ready mask");
+  constexpr unsigned kAll = N == 32 ? ~0u : (1u << N) - 1u;
+  unsigned rdy = ~need & kAll;
+  gran_t x[N];
+  const uint64_t t0 = wall_ticks(), limit = (uint64_t)limit_us * kTicksPerUs;
+  for (uint32_t pass = 1;; ++pass) {
+    if (rdy != kAll) {
+#pragma unroll
+      for (int k = 0; k < N; ++k)
+        if (!(rdy & (1u << k))) x[k] = gran_load(base + off[k]);
+#pragma unroll
+      for (int k = 0; k < N; ++k)
+        if (!(rdy & (1u << k))) rdy |= (unsigned)((unsigned)(x[k] >> 32) == ep) << k;
+    }
+    if (__all(rdy == kAll)) break;
+    if ((pass & 7) == 0 && wall_ticks() - t0 > limit) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    if (need & (1u << k)) f(k, __builtin_bit_cast(float, (unsigned)x[k]));
+  return true;
+}
+
 }  // namespace cme

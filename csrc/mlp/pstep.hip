@@ -21,7 +21,7 @@
 //   4. dZ1 = (W2_r^T D) .* a1 .* (1 - a1) into LDS; dW1 rows = dZ1 . XT_b (the feature-major pixel copy with its
 //      all-ones feature: column 784 is db1) on the same MFMA, each wave owning whole 16-column blocks -- the SGD
 //      update of W1 / b1 is applied to the LDS copy straight from the accumulators; dW2 = D . a1^T and db2 = D 1
-//      by plain fp32 loops (every workgroup computes db2 identically, so the b2 copies stay equal bit for bit).
+//      on the fp32 MFMA (every workgroup computes db2 identically, so the b2 copies stay equal bit for bit).
 // At the end every workgroup publishes its status, waits for all tm, and (no error anywhere) writes its rows back.
 // A poll that outlasts SplitStepArgs::ag_wait_us sets *err: every workgroup then stops and NOTHING is written back
 // (the parameters stay as they were before the launch; MlpEngine.kernel_error(), KernelHandoffTimeout).
@@ -49,7 +49,7 @@ struct PLds {
   float red[8 * 16 * 128];                   // z1 partial sums [wave][16][128 columns]; then D, dZ1 [16][kPAS]
   float a1[16][kPAS];
   float w2[16][16];                          // W2[class][row of this tile], zero past C / H
-  float b1[16], b2[16], db2[16];
+  float b1[16], b2[16];
   int bad;
 };
 static_assert(sizeof(PLds) <= 160 * 1024, "LDS budget");
@@ -116,6 +116,8 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
     gs += p.B;
     const unsigned tag = base + (unsigned)s + 1u;
     stamp(s, 0);
+    // (this step's label of column t, fetched now: loaded where the softmax uses it, it was a dependent round trip)
+    const int lab_pre = (int)__builtin_amdgcn_raw_buffer_load_b32(rL, t < n ? (int)((off + t) * 4) : kOOB, 0, 0);
     // ================= 1. z1 = W1_r . X_b^T, then a1: per half of <= 8 column blocks, the wave's 4 K chunks as ONE
     // burst of pixel loads (issued before any MFMA), partial sums of the 8 waves reduced through LDS
     for (int hb = 0; hb < nb; hb += 8) {
@@ -151,6 +153,7 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
         for (int q = 0; q < 3; ++q) __builtin_memcpy(&A[q], pl[q], 16);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+          if (hb + j >= nb) break;  // (wave-uniform: no MFMA on column blocks past n)
           unsigned int w[4] = {widen2(bw[u][j][0], 0), widen2(bw[u][j][0], 1), widen2(bw[u][j][1], 0),
                                widen2(bw[u][j][1], 1)};
           bf16x8_t B;
@@ -175,6 +178,26 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
       __syncthreads();
     }
     stamp(s, 1);
+    // ---- the dW1 GEMM's B operand (XT words of this wave's feature blocks w, w + 8, ...), issued NOW: its latency
+    // hides behind the z2 hand-off, the softmax and dZ1 instead of one round trip per feature block later.  All of
+    // them up to n = 128 (56 VGPRs); above, the first kPD, the rest kPD blocks ahead inside the loop.
+    constexpr int kFB = (kPCols + 15) / 16;  // 50 feature blocks
+    constexpr int kFBW = (kFB + 7) / 8;      // per wave
+    constexpr int kPD = KN <= 4 ? kFBW : 2;
+    auto load_xt = [&](int fb, unsigned int (&w)[KN][2]) {
+      const int feat = fb * 16 + fr;
+#pragma unroll
+      for (int kc = 0; kc < KN; ++kc) {
+        const int k = kc * 32 + 8 * fg;
+        const bool rok = fb < kFB && feat < kPCols;
+        const int o = (int)((int64_t)feat * a.ldxt + off + k);
+        w[kc][0] = __builtin_amdgcn_raw_buffer_load_b32(rXT, rok && k < n ? o : kOOB, 0, 0);
+        w[kc][1] = __builtin_amdgcn_raw_buffer_load_b32(rXT, rok && k + 4 < n ? o + 4 : kOOB, 0, 0);
+      }
+    };
+    unsigned int xw[kFBW][KN][2];
+#pragma unroll
+    for (int v = 0; v < kPD; ++v) load_xt(wave + 8 * v, xw[v]);
     // ================= 2. this tile's z2 partial W2[:, rows] . a1 -> granules (double-buffered by step parity)
     gran_t* z2g = p.gran + (size_t)(s & 1) * 8 * 16 * kPMaxN;  // [parity][tile][class][column]
     // (test hook, SplitStepArgs::ag_test_skip: this workgroup withholds its partials, every poll really times out)
@@ -189,16 +212,32 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
     // ================= 3. z2 = sum of the tm partials (tile order) + b2; softmax; D (into red, [16][kPAS])
     float* Ds = L.red;
     float* dzs = L.red + 16 * kPAS;
-    for (int i = t; i < C * n; i += kPT) {
-      const int c = i / n, col = i - c * n;
-      float z = 0.f;
-      const bool good = gran_poll<8>(z2g, (unsigned)(c * kPMaxN + col), 16u * kPMaxN, tm, true, tag,
-                                     (uint32_t)a.ag_wait_us, [&](int, float v) { z += v; });
+    // every (class, column) item's tm partials; a lane takes kIG items (granule j * 8 + tile) per poll pass, so
+    // ONE round trip per pass gathers them all (item i = i0 + j kPT + t: a wave's lanes read consecutive columns)
+    constexpr int kIG = 2;
+    for (int i0 = 0; i0 < C * n; i0 += kIG * kPT) {  // (uniform trip count)
+      unsigned offs[kIG * 8], need = 0u;
+#pragma unroll
+      for (int j = 0; j < kIG; ++j) {
+        const int i = i0 + j * kPT + t, c = i / n, col = i - c * n;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          offs[j * 8 + k] = (unsigned)((k * 16 + c) * kPMaxN + col);
+          if (i < C * n && k < tm) need |= 1u << (j * 8 + k);
+        }
+      }
+      float z[kIG] = {};
+      const bool good = gran_poll_set<kIG * 8>(z2g, offs, need, tag, (uint32_t)a.ag_wait_us,
+                                               [&](int k, float v) { z[k >> 3] += v; });  // (tile order)
       if (!good) {
         atomicExch(p.err, 1);
         L.bad = 1;
       }
-      Ds[c * kPAS + col] = z + L.b2[c];  // (z2 for now)
+#pragma unroll
+      for (int j = 0; j < kIG; ++j) {
+        const int i = i0 + j * kPT + t, c = i / n, col = i - c * n;
+        if (i < C * n) Ds[c * kPAS + col] = z[j] + L.b2[c];  // (z2 for now)
+      }
     }
     __syncthreads();
     stamp(s, 3);
@@ -206,8 +245,13 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
       ok = false;
       break;
     }
-    for (int col = t; col < n; col += kPT) {  // one column per thread: softmax + cross-entropy gradient
-      const int lab = (int)__builtin_amdgcn_raw_buffer_load_b32(rL, (int)((off + col) * 4), 0, 0);
+    for (int col = t; col < npad; col += kPT) {  // one column per thread: softmax + cross-entropy gradient
+      if (col >= n) {  // (D is zero past n: the dW2 / db2 chains read whole 4-column steps)
+#pragma unroll
+        for (int c = 0; c < 16; ++c) Ds[c * kPAS + col] = 0.f;
+        continue;
+      }
+      const int lab = lab_pre;  // (col == t: n <= 256 < kPT)
       float m = 0.f;
       if (a.shift) {
         m = Ds[col];
@@ -244,19 +288,26 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
     }
     __syncthreads();
     stamp(s, 5);
-    float gw2 = 0.f, gb2 = 0.f;  // thread c * 16 + h < 256: dW2[c][h]; thread 256 + c: db2[c]
-    if (t < 256) {
-      const int c = t >> 4, h = t & 15;
-      if (c < C)
-        for (int col = 0; col < n; ++col) gw2 += Ds[c * kPAS + col] * L.a1[h][col];
-    } else if (t < 256 + 16) {
-      const int c = t - 256;
-      if (c < C)
-        for (int col = 0; col < n; ++col) gb2 += Ds[c * kPAS + col];
+    // dW2 = D . a1^T and db2 = D 1 on v_mfma_f32_16x16x4_f32, waves 6 and 7 (they own 6 feature blocks, waves 0 and 1
+    // own 7) taking one half of the batch columns each: A(c, k) = D[c][k], B(k, h) = a1[h][k] (or 1 for db2); the two
+    // halves' 16 x 16 partials meet in LDS and are summed (half 0 + half 1) by the W2 / b2 update below
+    float* w2s = L.red + 32 * kPAS;  // [2][16][16] dW2 partials, then [2][16] db2 partials
+    if (wave >= 6) {
+      const int half = wave - 6, kh = npad / 2, k0 = half * kh;  // (npad % 16 == 0: kh % 4 == 0)
+      f32x4 gw = {0.f, 0.f, 0.f, 0.f}, gb = {0.f, 0.f, 0.f, 0.f};
+      for (int k = k0 + fg; k < k0 + kh; k += 4) {
+        const float dv = Ds[fr * kPAS + k];
+        gw = __builtin_amdgcn_mfma_f32_16x16x4f32(dv, L.a1[fr][k], gw, 0, 0, 0);
+        gb = __builtin_amdgcn_mfma_f32_16x16x4f32(dv, 1.f, gb, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        w2s[(half * 16 + 4 * fg + i) * 16 + fr] = gw[i];  // dW2[class 4 fg + i][row fr]
+        if (fr == 0) w2s[512 + half * 16 + 4 * fg + i] = gb[i];
+      }
     }
     // dW1 = dZ1 . XT_b: the dZ1 chunks split into their exact planes ONCE (registers), then wave w walks the
-    // 16-feature blocks w, w + 8, ... (feature 784 is the all-ones db1 column) with the next block's pixel words
-    // loaded while the current block is multiplied
+    // 16-feature blocks w, w + 8, ... (feature 784 is the all-ones db1 column) over the prefetched XT words
     bf16x8_t Az[KN][3];
 #pragma unroll
     for (int kc = 0; kc < KN; ++kc) {
@@ -268,30 +319,15 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) __builtin_memcpy(&Az[kc][q], pl[q], 16);
     }
-    constexpr int kFB = (kPCols + 15) / 16;  // 50 feature blocks
-    constexpr int kFBW = (kFB + 7) / 8;      // per wave
-    auto load_xt = [&](int fb, unsigned int (&w)[KN][2]) {
-      const int feat = fb * 16 + fr;
-#pragma unroll
-      for (int kc = 0; kc < KN; ++kc) {
-        const int k = kc * 32 + 8 * fg;
-        const bool rok = fb < kFB && feat < kPCols;
-        const int o = (int)((int64_t)feat * a.ldxt + off + k);
-        w[kc][0] = __builtin_amdgcn_raw_buffer_load_b32(rXT, rok && k < n ? o : kOOB, 0, 0);
-        w[kc][1] = __builtin_amdgcn_raw_buffer_load_b32(rXT, rok && k + 4 < n ? o + 4 : kOOB, 0, 0);
-      }
-    };
-    unsigned int xw[2][KN][2];
-    load_xt(wave, xw[0]);
 #pragma unroll
     for (int v = 0; v < kFBW; ++v) {
       const int fb = wave + 8 * v;
-      if (v + 1 < kFBW) load_xt(fb + 8, xw[(v + 1) & 1]);
+      if (v + kPD < kFBW) load_xt(fb + 8 * kPD, xw[v + kPD]);
       f32x4 g = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kc = 0; kc < KN; ++kc) {
-        unsigned int w[4] = {widen2(xw[v & 1][kc][0], 0), widen2(xw[v & 1][kc][0], 1), widen2(xw[v & 1][kc][1], 0),
-                             widen2(xw[v & 1][kc][1], 1)};
+        unsigned int w[4] = {widen2(xw[v][kc][0], 0), widen2(xw[v][kc][0], 1), widen2(xw[v][kc][1], 0),
+                             widen2(xw[v][kc][1], 1)};
         bf16x8_t B;
         __builtin_memcpy(&B, w, 16);
 #pragma unroll
@@ -318,12 +354,12 @@ __global__ __launch_bounds__(kPT) void pstep_kernel(PStepArgs p) {
     if (t < 256) {
       const int c = t >> 4, h = t & 15;
       if (c < C && r0 + h < H) {
-        const float w = L.w2[c][h];
+        const float w = L.w2[c][h], gw2 = w2s[c * 16 + h] + w2s[256 + c * 16 + h];
         L.w2[c][h] = w - lr * (gw2 + reg * w);
       }
     } else if (t < 256 + 16) {
       const int c = t - 256;
-      if (c < C) L.b2[c] -= lr * gb2;
+      if (c < C) L.b2[c] -= lr * (w2s[512 + c] + w2s[512 + 16 + c]);
     }
     __syncthreads();
     stamp(s, 7);
