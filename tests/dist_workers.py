@@ -260,6 +260,7 @@ def xgmi_stall_worker(rank, world, comm, device, out_dir):
     x, y = synthetic_mnist(3200, seed=3)
     nn = NeuralNetwork([784, 100, 10])
     tr = DataParallelTrainer(nn, comm=comm, device=dev, batch_size=800, use_graphs=False, allreduce="xgmi")
+    tr.recover = False  # (this part pins the raise; the in-process fallback: test_gpu_handoff.py)
     tr.load(x, y)
     res["B_fused"] = float(tr.fused_allreduce)
     e = tr.engine
