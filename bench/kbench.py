@@ -68,7 +68,9 @@ def main(argv=None):
         no_a1, no_dw2 = "+s0" in path, "+d0" in path
         m = re.search(r"\+x(\d)", path)
         xrows = int(m.group(1)) if m else None
-        path = re.sub(r"\+[sdx]\d", "", path)
+        m = re.search(r"\+p(\d)", path)  # "+p0" / "+p1": the XT L2 prefetch off / on (MlpStep.prefetch)
+        pref = int(m.group(1)) if m else None
+        path = re.sub(r"\+[sdxp]\d", "", path)
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -79,6 +81,8 @@ def main(argv=None):
                 join = e.join
                 if xrows is not None:
                     step.xcd_rows = xrows
+                if pref is not None:
+                    step.prefetch = pref
                 if no_a1:
                     e.set_store_a1(False)
                 if no_dw2:
@@ -88,7 +92,7 @@ def main(argv=None):
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(
@@ -97,6 +101,21 @@ def main(argv=None):
                                  ("wgrad_sgd", part(2)), ("wgrad_grads", part(2, 0)),
                                  ("step_fused", part(3)), ("sgd_flat", lambda: e.sgd(0.0))):
                     row[name + "_us"] = round(timeit(fn, a.reps), 3)
+                if e.np:  # the native step loop over consecutive batches (new pixels every step, as in training)
+                    import torch as _t
+
+                    N = e.num_samples
+                    step.persistent = 0
+                    step.run_steps(0, 4, n, 0, n, N, 1.0 / n, 1e-4, 0.0, 1, st())
+                    best = float("inf")
+                    for _ in range(5):
+                        s0, s1 = _t.cuda.Event(enable_timing=True), _t.cuda.Event(enable_timing=True)
+                        s0.record()
+                        step.run_steps(0, a.reps, n, 0, n, N, 1.0 / n, 1e-4, 0.0, 1, st())
+                        s1.record()
+                        s1.synchronize()
+                        best = min(best, s0.elapsed_time(s1) * 1e3 / a.reps)
+                    row["step_walk_us"] = round(best, 3)
                 step.persistent = 1
                 if step.uses_persistent(n, 1):  # the persistent engine: reps steps in ONE launch (run_steps)
                     import torch as _t

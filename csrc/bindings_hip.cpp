@@ -78,6 +78,7 @@ struct MlpStep {
   // rows and dZ1 rows each launch writes are read back by the next one from the same XCD's L2 -- step 14.0 ->
   // 13.1-13.2 us at n = 800, 12.3 -> 11.7 us at n = 100, profiles/kbench_xcd_rows_r4.jsonl; 0 for A/B)
   int xcd_rows = 1;
+  int prefetch = 1;  // SplitStepArgs::xt_prefetch
   int ag64() const { return ag_tiles64 >= 0 ? ag_tiles64 : (store_a1 ? 0 : 1); }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
@@ -194,6 +195,7 @@ struct MlpStep {
     a.ag_wait_us = ag_wait_us;
     a.ag_test_skip = ag_test_skip;
     a.xcd_rows = xcd_rows && cme::mlp_split_xcd_rows_ok(a);
+    a.xt_prefetch = prefetch && a.xcd_rows && bias_col;
     return a;
   }
 
@@ -515,6 +517,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("store_a1", &MlpStep::store_a1)
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
       .def_readwrite("xcd_rows", &MlpStep::xcd_rows)
+      .def_readwrite("prefetch", &MlpStep::prefetch)
       .def_readwrite("persistent", &MlpStep::persistent)
       .def("uses_persistent", &MlpStep::uses_persistent, py::arg("n"), py::arg("sgd"))
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
