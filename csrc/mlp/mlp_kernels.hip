@@ -926,37 +926,20 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ s, __hip_bfloat16* 
 
 // ----------------------------------------------------------- generic GEMM
 template <typename T>
-struct EpiColMajor {
+struct EpiColMajor {  // C = alpha op(A) op(B) + beta C, column-major; S: the arithmetic type (fp32 for bf16)
+  using S = std::conditional_t<std::is_same_v<T, __hip_bfloat16>, float, T>;
   T* __restrict__ C;
   int ldc;
-  T alpha, beta;
-  T pre[kEpiMaxQ];
+  S alpha, beta;
+  S pre[kEpiMaxQ];
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
-    pre[q] = buf_load1<T>(make_rsrc(C), (ok && beta != T(0)) ? (row + col * ldc) * (int)sizeof(T) : kOOB);
+    pre[q] = S(buf_load1<T>(make_rsrc(C), (ok && beta != S(0)) ? (row + col * ldc) * (int)sizeof(T) : kOOB));
   }
   template <typename A>
   __device__ __forceinline__ void operator()(int q, int row, int col, A v) {
-    const size_t i = (size_t)row + (size_t)col * ldc;
-    T r = alpha * T(v);
-    if (beta != T(0)) r += beta * pre[q];
-    C[i] = r;
-  }
-};
-template <>
-struct EpiColMajor<__hip_bfloat16> {
-  __hip_bfloat16* __restrict__ C;
-  int ldc;
-  float alpha, beta;
-  float pre[kEpiMaxQ];
-  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
-    pre[q] = __bfloat162float(
-        buf_load1<__hip_bfloat16>(make_rsrc(C), (ok && beta != 0.f) ? (row + col * ldc) * 2 : kOOB));
-  }
-  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
-    const size_t i = (size_t)row + (size_t)col * ldc;
-    float r = alpha * v;
-    if (beta != 0.f) r += beta * pre[q];
-    C[i] = __float2bfloat16(r);
+    S r = alpha * S(v);
+    if (beta != S(0)) r += beta * pre[q];
+    C[(size_t)row + (size_t)col * ldc] = T(r);
   }
 };
 
@@ -1013,13 +996,8 @@ void launch_gemm(bool tA, bool tB, int M, int N, int K, double alpha, const void
   E epi;
   epi.C = (T*)C;
   epi.ldc = ldc;
-  if constexpr (std::is_same_v<T, __hip_bfloat16>) {
-    epi.alpha = (float)alpha;
-    epi.beta = (float)beta;
-  } else {
-    epi.alpha = (T)alpha;
-    epi.beta = (T)beta;
-  }
+  epi.alpha = (typename E::S)alpha;
+  epi.beta = (typename E::S)beta;
   const int tn = cdiv(N, 16 * kGNB), tm = cdiv(M, 16 * kGMB);
   const dim3 grid(tm * tn);
   constexpr int V = MmaTraits<T>::V;
@@ -1158,7 +1136,7 @@ void mlp_head(DType dt, const HeadArgs& a, hipStream_t s) {
     return;
   }
   // (a wide head without the forward's partials -- only the head-alone profiling hook, MlpStep.run parts & 8 --
-  // takes the column head below; round 1-3's two-kernel split-H head for that case was removed in round 4)
+  // takes the column head below)
   if (dt != DType::F64 && head32_ok(a) && (int64_t)a.H * a.lda < (int64_t)kOOB / 4) {  // MFMA head
     head32_kernel<<<cdiv(a.n, kH32Cols), 512, 0, s>>>(a);
     CME_LAUNCH_CHECK(s);

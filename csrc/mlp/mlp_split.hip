@@ -31,14 +31,9 @@ __device__ __forceinline__ void split_store(float v, bf16* base, size_t plane_st
   }
 }
 
-// ======================================================================
-// Kernel A1 (tiled): a1 = sigmoid(W1 X + b1) on 16x32 tiles, K split over 8
-// waves, W1 as fp32 split in registers or NPW exact bf16 planes.  Used with the
-// separate head kernel (mlp_kernels.hip) where the fused forward + head launch
-// does not apply (H > 128, predict).  (Round 1-3's one-launch-per-16-samples
-// forward + head, which streamed ALL of W1 through every workgroup, was removed
-// in round 4: slower than this tiling and selected by no policy.)
-// ======================================================================
+// Kernel A1 (tiled): a1 = sigmoid(W1 X + b1) on 16x32 tiles, K split over 8 waves, W1 as fp32 split in
+// registers or NPW exact bf16 planes; with the separate head kernel where the fused forward + head launch does
+// not apply (H > 128, predict).
 constexpr int kF1MB = 1, kF1NB = 2, kF1KS = 8;
 
 struct EpiSig {
@@ -1148,8 +1143,6 @@ bool rega_wgrad_ok(const SplitStepArgs& a) {
          (a.npz == 3 ? (a.dZ1 != nullptr && al16(a.dZ1)) : al16(a.dZ1p));
 }
 
-// (round 3's 4 x 2 wave layout for the bf16 loop, 39.9 -> 41.3 us at 784-4096-10, was removed in round 4:
-// profiles/wide_ag_ab_bf16_wave_layout_r3.jsonl)
 template <typename AT, int NKS>
 void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
