@@ -78,7 +78,10 @@ struct MlpStep {
   // rows and dZ1 rows each launch writes are read back by the next one from the same XCD's L2 -- step 14.0 ->
   // 13.1-13.2 us at n = 800, 12.3 -> 11.7 us at n = 100, profiles/kbench_xcd_rows_r4.jsonl; 0 for A/B)
   int xcd_rows = 1;
-  int prefetch = 1;  // SplitStepArgs::xt_prefetch
+  // SplitStepArgs::pf_wgs, prefetch workgroups per XCD (0: off).  Walking-batch step (kbench step_walk_us, A/B twice):
+  // 0 -> 4: 14.55-14.63 -> 14.11-14.14 us at n = 800, 13.0-13.1 -> 12.64-12.66 at n = 100; 2 and 6 slower at n = 800
+  // (profiles/kbench_prefetch_wgs_r4.jsonl)
+  int prefetch = 4;
   int ag64() const { return ag_tiles64 >= 0 ? ag_tiles64 : (store_a1 ? 0 : 1); }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
@@ -195,7 +198,7 @@ struct MlpStep {
     a.ag_wait_us = ag_wait_us;
     a.ag_test_skip = ag_test_skip;
     a.xcd_rows = xcd_rows && cme::mlp_split_xcd_rows_ok(a);
-    a.xt_prefetch = prefetch && a.xcd_rows && bias_col;
+    a.pf_wgs = (a.xcd_rows && bias_col) ? prefetch : 0;
     return a;
   }
 
@@ -206,11 +209,14 @@ struct MlpStep {
   // parts: bit0 = forward + head, bit1 = weight gradients / update (profiling hook; default both);
   //        with bit0: +4 skips the head (forward GEMM only), +8 skips the forward GEMM (head only)
   void run(int64_t off, int n, double scale, double reg, double lr, int sgd, int with_loss, uintptr_t stream,
-           int parts = 3) {
+           int parts = 3, int64_t pf_next = -1) {
     CME_REQUIRE(n > 0 && n <= ld, "MlpStep.run: 0 < n <= ld required");
     if (split) {
       CME_REQUIRE(XT != 0 && W1p != 0 && dZ1p != 0, "MlpStep.run: split path needs XT, W1p, dZ1p");
       cme::SplitStepArgs a = split_args(off, n, scale, reg, lr, sgd == 2 ? 0 : sgd, with_loss);
+      // the next step's first sample (the native step loop knows it): its pixels are prefetched by this step's
+      // weight-gradient launch (SplitStepArgs::pf_X)
+      if (pf_next >= 0 && a.pf_wgs) a.pf_X = reinterpret_cast<const char*>(X) + (size_t)pf_next * P;
       if (sgd == 2) {  // all-reduce + SGD inside the wgrad launch
         CME_REQUIRE(xf.world > 0, "MlpStep.run(sgd=2): set_xgmi() first");
         a.xf = xf;
@@ -351,7 +357,8 @@ struct MlpStep {
     int64_t gs = gstart0;
     for (int64_t i = 0; i < count; ++i) {
       if (gs + B > N_end) gs = 0;
-      run(gs + shard_off, n, scale, reg, lr, sgd, 0, stream, 3);
+      const int64_t nx = gs + B + B > N_end ? 0 : gs + B;  // (the next step's batch, wrap included)
+      run(gs + shard_off, n, scale, reg, lr, sgd, 0, stream, 3, nx + shard_off);
       gs += B;
     }
   }
@@ -566,7 +573,7 @@ PYBIND11_MODULE(_hip, m) {
            },
            py::arg("x"), py::arg("n"), py::arg("a1buf"), py::arg("lda"), py::arg("pred"), py::arg("stream"))
       .def("run", &MlpStep::run, py::arg("off"), py::arg("n"), py::arg("scale"), py::arg("reg"), py::arg("lr"),
-           py::arg("sgd"), py::arg("with_loss"), py::arg("stream"), py::arg("parts") = 3);
+           py::arg("sgd"), py::arg("with_loss"), py::arg("stream"), py::arg("parts") = 3, py::arg("pf_next") = -1);
 
   m.def(
       "occupy_cus",

@@ -60,7 +60,6 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   __shared__ float ls[kCols];
   __shared__ int s_bad;
   __shared__ unsigned s_ep;
-  __shared__ __attribute__((aligned(16))) char pf_lds[1024];  // landing slot of the XT prefetch (never read)
   const int xcd = blk & 7, slot = blk >> 3;
   // column-tile grouping (the tm row tiles of a column tile on one XCD) or, xcd_rows, row tile rt on XCD rt
   const int ct = f.xcd_rows ? slot : xcd + 8 * (slot / tm), rt = f.xcd_rows ? xcd : slot % tm;
@@ -82,27 +81,6 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     gran_epoch_wait(ep_old);
     s_ep = (unsigned)(ep_old / (unsigned)tm) + 1u;
     s_bad = 0;
-  }
-  // XT prefetch (SplitStepArgs::xt_prefetch): wave 7, idle during the K loop, pulls XT[0 .. P][c0 .. c0 + 31] -- what
-  // this XCD's dW1 tiles read for these columns in the next launch -- into the XCD's L2 by LDS-DMA (the bytes land
-  // in a 1 KB slot nobody reads: no VGPRs).  Waited for at the end, long after they landed.
-  const bool pf = f.xt_prefetch && t >= 448;
-  if (pf) {
-    const __amdgpu_buffer_rsrc_t rxt = make_rsrc(f.XT);
-    const int lane = t - 448, rows = f.P + f.bias_col;
-    if (reinterpret_cast<uintptr_t>(f.XT) % 16 == 0 && f.ldxt % 16 == 0) {  // 16 B per lane: 2 lanes per row
-      for (int i = lane; i < 2 * rows; i += 64) {
-        const int c = c0 + 16 * (i & 1);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rxt, (__attribute__((address_space(3))) void*)pf_lds, 16,
-                                                 c < n ? (i >> 1) * f.ldxt + c : kOOB, 0, 0, 0);
-      }
-    } else {  // 4 B per lane: 8 lanes per row
-      for (int i = lane; i < 8 * rows; i += 64) {
-        const int c = c0 + 4 * (i & 7);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rxt, (__attribute__((address_space(3))) void*)pf_lds, 4,
-                                                 c < n ? (i >> 3) * f.ldxt + c : kOOB, 0, 0, 0);
-      }
-    }
   }
   // the label of this thread's softmax column (t >> 4), fetched now: loaded where the softmax uses it, it was
   // a dependent memory round trip after the all-gather wait
@@ -200,10 +178,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
       h.loss_partial[vb] = sl;
     }
   }
-  if (s_bad) {  // (zs holds D) a timed-out wait: nothing more is written
-    if (pf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the prefetch's LDS slot outlives its DMA)
-    return;
-  }
+  if (s_bad) return;  // (zs holds D) a timed-out wait: nothing more is written
   // ---- 4. dZ1 = (W2^T D) .* a1 .* (1 - a1) for this tile's 16 rows, one element per thread
   {
     const int r = t >> 5;  // (col as above)
@@ -243,7 +218,6 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
       }
     }
   }
-  if (pf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (landed long ago: the K loop ran meanwhile)
   if (st) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -117,10 +117,12 @@ struct SplitStepArgs {
   // then read back by the next launch from the same XCD's L2 instead of the die-level cache.  Set by the launcher
   // (mlp_split_xcd_rows_ok); 0: the column-tile grouping.
   int xcd_rows = 0;
-  // H <= 128 under xcd_rows: the forward + head launch's idle wave 7 pulls this step's feature-major pixels (the XT
-  // columns of its 32-column tile, all P + 1 features) into its XCD's L2 by LDS-DMA during the K loop, for the
-  // weight-gradient launch that follows on the same XCD (MlpStep.prefetch; 0 for A/B)
-  int xt_prefetch = 0;
+  // H <= 128 under xcd_rows: pf_wgs extra workgroups per XCD in each launch pull the pixels that XCD's workgroups
+  // read next into its L2, on CUs the step leaves idle: the forward + head launch this step's feature-major XT (for
+  // the weight-gradient launch), the weight-gradient launch the next step's X at pf_X (nullptr: none) for the next
+  // forward (MlpStep.prefetch; 0: off)
+  int pf_wgs = 0;
+  const void* pf_X = nullptr;
 };
 
 

@@ -7,6 +7,7 @@
 #include "glds_gemm.h"
 #include "granule.h"
 #include "head_math.h"
+#include "l2_touch.h"
 #include "rega_gemm.h"
 #include "mma_tile.h"
 #include "fwd_tile.h"
@@ -243,6 +244,13 @@ template <int NPZ, int VEC, bool AF>
 __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
   __shared__ uint32_t s_xf[2];
+  if (a.pf_wgs && (int)blockIdx.x >= (int)gridDim.x - 8 * a.pf_wgs) {  // a prefetch workgroup (SplitStepArgs::pf_wgs):
+    // the next step's X into the L2 of an XCD whose forward row tile reads all of it next
+    const int xcd = blockIdx.x & 7, part = ((int)blockIdx.x - ((int)gridDim.x - 8 * a.pf_wgs)) >> 3;
+    if (a.pf_X && xcd < (a.H + 15) / 16)
+      l2_touch(a.pf_X, 0, 1, 0, (int64_t)a.n * a.P, part, a.pf_wgs, reinterpret_cast<char*>(red));
+    return;
+  }
   // logical workgroup id: dW1 tiles [0, t1) row-major, then the roles.  xcd_rows: the first 8 * t1n blocks are the
   // dW1 tiles with row tile rt on XCD rt (blockIdx % 8; slots of XCDs past the last row tile idle), roles after
   int bid = blockIdx.x, tb;
@@ -1423,7 +1431,8 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   b.w1_planes = mlp_split_w1_planes_read(a) ? 1 : 0;
   // the XCD-row placement only for the whole layer's dW1 (a bucketed row range keeps the plain order)
   b.xcd_rows = a.xcd_rows && do_w1 && a.w1_row0 == 0 && a.w1_rows < 0 && cdiv(a.H, 16 * kWMB) <= 8;
-  const dim3 grid((b.xcd_rows ? 8 * t1n : t1) + t2 + tb);
+  b.pf_wgs = b.xcd_rows ? a.pf_wgs : 0;
+  const dim3 grid((b.xcd_rows ? 8 * t1n : t1) + t2 + tb + 8 * b.pf_wgs);  // (prefetch workgroups last)
 #define CME_WG(npz, af)                                                                   \
   if (vec == 3) wgrad_split_kernel<npz, 3, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);      \
   else if (vec == 1) wgrad_split_kernel<npz, 1, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \

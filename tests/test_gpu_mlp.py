@@ -781,3 +781,24 @@ def test_persistent_engine_timeout_applies_nothing():
     st.run_steps(0, 3, n, 0, n, 4 * n, 1.0 / n, 1e-4, 0.05, 1, s)
     torch.cuda.synchronize()
     assert torch.equal(e.params, before)
+
+
+@pytest.mark.parametrize("n", [800, 100])
+def test_prefetch_workgroups_are_bitwise_neutral(n):
+    """H <= 128 with the XCD-row placement: the prefetch workgroups (MlpStep.prefetch, SplitStepArgs::pf_wgs) only
+    pull pixels into L2 from otherwise idle CUs -- the native step loop's result is bitwise the same with them off."""
+    x, y = synthetic_mnist(5 * n + 16, seed=n + 1)
+    nn = NeuralNetwork([784, 100, 10])
+    outs = []
+    for pf in (0, 6):
+        e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        st = e._hip_step()
+        st.persistent = 0
+        st.prefetch = pf
+        st.run_steps(0, 7, n, 0, n, e.num_samples, 1.0 / n, 1e-4, 0.05, 1, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert not e.kernel_error()
+        outs.append(e.params.clone())
+    assert torch.equal(outs[0], outs[1])
