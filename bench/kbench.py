@@ -116,6 +116,15 @@ def main(argv=None):
                         s1.synchronize()
                         best = min(best, s0.elapsed_time(s1) * 1e3 / a.reps)
                     row["step_walk_us"] = round(best, 3)
+                    best = float("inf")  # the same native loop over ONE batch (N_end = n): host loop vs data walk
+                    for _ in range(5):
+                        s0, s1 = _t.cuda.Event(enable_timing=True), _t.cuda.Event(enable_timing=True)
+                        s0.record()
+                        step.run_steps(0, a.reps, n, 0, n, n, 1.0 / n, 1e-4, 0.0, 1, st())
+                        s1.record()
+                        s1.synchronize()
+                        best = min(best, s0.elapsed_time(s1) * 1e3 / a.reps)
+                    row["step_loop_same_us"] = round(best, 3)
                 step.persistent = 1
                 if step.uses_persistent(n, 1):  # the persistent engine: reps steps in ONE launch (run_steps)
                     import torch as _t

@@ -420,11 +420,12 @@ class MlpEngine:
         self._hip_step().set_xgmi(*self._xgmi_fuse)
 
     def run(self, off: int, n: int, scale: float, reg: float, lr: float, sgd, with_loss: bool = False,
-            parts: int = 3):
+            parts: int = 3, pf_next: int = -1):
         """Forward + backward on samples [off, off+n).  sgd=True: update params in
         place; False: write pre-scaled gradients into ``self.grads``; 2: all-reduce over the attached
         xGMI bucket and update inside the wgrad launch (attach_xgmi).  parts (hip backend): bit0 forward +
-        head, bit1 weight gradients / update -- the per-phase profiler runs the two halves separately."""
+        head, bit1 weight gradients / update -- the per-phase profiler runs the two halves separately.
+        pf_next >= 0: the next step's first sample, whose pixels this step's prefetch workgroups pull into L2."""
         if self.X is None:
             raise RuntimeError("load_dataset() first")
         if n > self.ld:
@@ -435,7 +436,7 @@ class MlpEngine:
             st = self._hip_step()
             st.run(int(off), int(n), float(scale), float(reg), float(lr), 2 if sgd == 2 else int(bool(sgd)),
                    int(bool(with_loss)),
-                   torch.cuda.current_stream(self.device).cuda_stream, int(parts))
+                   torch.cuda.current_stream(self.device).cuda_stream, int(parts), int(pf_next))
         elif parts & 1:  # the torch backend always runs the whole step
             self._torch_step(off, n, scale, reg, lr, sgd, with_loss)
 

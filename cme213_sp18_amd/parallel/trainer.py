@@ -425,8 +425,10 @@ class DataParallelTrainer:
         return ok
 
     def _enqueue_plan(self, plan: EpochPlan, lr: float, reg: float) -> None:
-        for s, ln in plan.steps:
-            self.step(s, ln, lr, reg)
+        steps = plan.steps
+        for i, (s, ln) in enumerate(steps):
+            nxt = steps[i + 1] if i + 1 < len(steps) else steps[0]  # (whose pixels this step prefetches)
+            self.step(s, ln, lr, reg, next_start=self.shard(*nxt)[0])
 
     def epoch_plan(self, N: int | None = None) -> EpochPlan:
         N = self.N if N is None else N
@@ -438,8 +440,10 @@ class DataParallelTrainer:
         n = length // self.R
         return start + self.rank * n, n
 
-    def step(self, start: int, length: int, lr: float, reg: float, with_loss: bool = False) -> None:
-        """Enqueue one global SGD step on the current stream (no host sync)."""
+    def step(self, start: int, length: int, lr: float, reg: float, with_loss: bool = False,
+             next_start: int = -1) -> None:
+        """Enqueue one global SGD step on the current stream (no host sync).  next_start: this rank's first sample
+        of the next step (the fused paths prefetch its pixels; -1: unknown)."""
         e = self.engine
         off, n = self.shard(start, length)
         if self.profiler is not None and n > 0:
@@ -451,9 +455,9 @@ class DataParallelTrainer:
             return
         scale = 1.0 / (n * self.R)
         if isinstance(self.comm, NullComm) and self.allreduce_mode != "host":  # 1 process: SGD fused into wgrad
-            e.run(off, n, scale, reg, lr, sgd=True, with_loss=with_loss)
+            e.run(off, n, scale, reg, lr, sgd=True, with_loss=with_loss, pf_next=next_start)
         elif self.fused_allreduce:
-            e.run(off, n, scale, reg / self.R, lr, sgd=2, with_loss=with_loss)
+            e.run(off, n, scale, reg / self.R, lr, sgd=2, with_loss=with_loss, pf_next=next_start)
         elif self._bucketed:
             self._step_bucketed(off, n, scale, reg / self.R, lr, with_loss)
         else:
