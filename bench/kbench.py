@@ -68,9 +68,11 @@ def main(argv=None):
         no_a1, no_dw2 = "+s0" in path, "+d0" in path
         m = re.search(r"\+x(\d)", path)
         xrows = int(m.group(1)) if m else None
-        m = re.search(r"\+p(\d)", path)  # "+p0" / "+p1": the XT L2 prefetch off / on (MlpStep.prefetch)
+        m = re.search(r"\+p(\d)", path)  # "+pK": K prefetch workgroups per XCD for X (MlpStep.prefetch)
         pref = int(m.group(1)) if m else None
-        path = re.sub(r"\+[sdxp]\d", "", path)
+        m = re.search(r"\+t(\d)", path)  # "+tK": K prefetch workgroups per XCD for XT (MlpStep.prefetch_xt)
+        pref_xt = int(m.group(1)) if m else None
+        path = re.sub(r"\+[sdxpt]\d", "", path)
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -83,6 +85,8 @@ def main(argv=None):
                     step.xcd_rows = xrows
                 if pref is not None:
                     step.prefetch = pref
+                if pref_xt is not None:
+                    step.prefetch_xt = pref_xt
                 if no_a1:
                     e.set_store_a1(False)
                 if no_dw2:
@@ -92,7 +96,7 @@ def main(argv=None):
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(
@@ -125,6 +129,13 @@ def main(argv=None):
                         s1.synchronize()
                         best = min(best, s0.elapsed_time(s1) * 1e3 / a.reps)
                     row["step_loop_same_us"] = round(best, 3)
+                    import time as _time  # host time to ENQUEUE the loop's launches (no sync inside)
+
+                    _t.cuda.synchronize()
+                    h0 = _time.perf_counter()
+                    step.run_steps(0, a.reps, n, 0, n, N, 1.0 / n, 1e-4, 0.0, 1, st())
+                    row["host_enqueue_us"] = round((_time.perf_counter() - h0) * 1e6 / a.reps, 3)
+                    _t.cuda.synchronize()
                 step.persistent = 1
                 if step.uses_persistent(n, 1):  # the persistent engine: reps steps in ONE launch (run_steps)
                     import torch as _t

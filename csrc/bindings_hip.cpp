@@ -82,6 +82,7 @@ struct MlpStep {
   // 0 -> 4: 14.55-14.63 -> 14.11-14.14 us at n = 800, 13.0-13.1 -> 12.64-12.66 at n = 100; 2 and 6 slower at n = 800
   // (profiles/kbench_prefetch_wgs_r4.jsonl)
   int prefetch = 4;
+  int prefetch_xt = 4;  // SplitStepArgs::pf_wgs_xt
   int ag64() const { return ag_tiles64 >= 0 ? ag_tiles64 : (store_a1 ? 0 : 1); }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
@@ -199,6 +200,7 @@ struct MlpStep {
     a.ag_test_skip = ag_test_skip;
     a.xcd_rows = xcd_rows && cme::mlp_split_xcd_rows_ok(a);
     a.pf_wgs = (a.xcd_rows && bias_col) ? prefetch : 0;
+    a.pf_wgs_xt = (a.xcd_rows && bias_col) ? prefetch_xt : 0;
     return a;
   }
 
@@ -525,6 +527,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
       .def_readwrite("xcd_rows", &MlpStep::xcd_rows)
       .def_readwrite("prefetch", &MlpStep::prefetch)
+      .def_readwrite("prefetch_xt", &MlpStep::prefetch_xt)
       .def_readwrite("persistent", &MlpStep::persistent)
       .def("uses_persistent", &MlpStep::uses_persistent, py::arg("n"), py::arg("sgd"))
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)

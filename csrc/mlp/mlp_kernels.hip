@@ -532,10 +532,10 @@ __global__ __launch_bounds__(512) void fwd1_head_ag_kernel(SplitStepArgs f, Head
                                                            gran_t* __restrict__ slabs, int* __restrict__ err, int tm,
                                                            int tn) {
   __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];
-  if (f.pf_wgs && (int)blockIdx.x >= (int)gridDim.x - 8 * f.pf_wgs) {  // a prefetch workgroup (SplitStepArgs::pf_wgs):
+  if (f.pf_wgs_xt && (int)blockIdx.x >= (int)gridDim.x - 8 * f.pf_wgs_xt) {  // a prefetch workgroup (pf_wgs_xt):
     // this step's XT into the L2 of an XCD whose dW1 tiles read it next (all P + 1 features x n columns)
-    const int xcd = blockIdx.x & 7, part = ((int)blockIdx.x - ((int)gridDim.x - 8 * f.pf_wgs)) >> 3;
-    if (xcd < tm) l2_touch(f.XT, 0, f.P + f.bias_col, f.ldxt, f.n, part, f.pf_wgs, reinterpret_cast<char*>(red));
+    const int xcd = blockIdx.x & 7, part = ((int)blockIdx.x - ((int)gridDim.x - 8 * f.pf_wgs_xt)) >> 3;
+    if (xcd < tm) l2_touch(f.XT, 0, f.P + f.bias_col, f.ldxt, f.n, part, f.pf_wgs_xt, reinterpret_cast<char*>(red));
     return;
   }
   fha_body<NPW, VEC, AF>(f, h, counters, slabs, err, tm, tn, blockIdx.x, red);
@@ -1111,7 +1111,7 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
                                         "last-arriver form, mlp_fwd1_head)");
   const bool af = mlp_split_fwd_fp32_w(f);
   const int vec = fha_vec(f);
-  const int nwg = f.xcd_rows ? 8 * tn + 8 * f.pf_wgs : 8 * tm * cdiv(tn, 8);  // (prefetch workgroups last)
+  const int nwg = f.xcd_rows ? 8 * tn + 8 * f.pf_wgs_xt : 8 * tm * cdiv(tn, 8);  // (prefetch workgroups last)
 #define CME_FHA(np, af)                                                                                  \
   if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
   else if (vec == 1) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn); \

@@ -121,7 +121,8 @@ struct SplitStepArgs {
   // read next into its L2, on CUs the step leaves idle: the forward + head launch this step's feature-major XT (for
   // the weight-gradient launch), the weight-gradient launch the next step's X at pf_X (nullptr: none) for the next
   // forward (MlpStep.prefetch; 0: off)
-  int pf_wgs = 0;
+  int pf_wgs = 0;     // ... in the weight-gradient launch (the next step's X)
+  int pf_wgs_xt = 0;  // ... in the forward + head launch (this step's XT)
   const void* pf_X = nullptr;
 };
 
