@@ -109,7 +109,6 @@ def main(argv=None):
                     import torch as _t
 
                     N = e.num_samples
-                    step.persistent = 0
                     step.run_steps(0, 4, n, 0, n, N, 1.0 / n, 1e-4, 0.0, 1, st())
                     best = float("inf")
                     for _ in range(5):
@@ -136,22 +135,6 @@ def main(argv=None):
                     step.run_steps(0, a.reps, n, 0, n, N, 1.0 / n, 1e-4, 0.0, 1, st())
                     row["host_enqueue_us"] = round((_time.perf_counter() - h0) * 1e6 / a.reps, 3)
                     _t.cuda.synchronize()
-                step.persistent = 1
-                if step.uses_persistent(n, 1):  # the persistent engine: reps steps in ONE launch (run_steps)
-                    import torch as _t
-
-                    N = e.num_samples
-                    step.run_steps(0, 2, n, 0, n, N, 1.0 / n, 1e-4, 0.0, 1, st())  # (warm-up)
-                    _t.cuda.synchronize()
-                    best = float("inf")
-                    for _ in range(5):
-                        s0, s1 = _t.cuda.Event(enable_timing=True), _t.cuda.Event(enable_timing=True)
-                        s0.record()
-                        step.run_steps(0, a.reps, n, 0, n, N, 1.0 / n, 1e-4, 0.0, 1, st())
-                        s1.record()
-                        s1.synchronize()
-                        best = min(best, s0.elapsed_time(s1) * 1e3 / a.reps)
-                    row["step_persistent_us"] = round(best, 3)
                 slots = e.fused_allreduce_slots()
                 if slots:  # wgrad with the xGMI all-reduce fused in, world 1 (the flag protocol, no peers)
                     from cme213_sp18_amd._native import hip as _hip

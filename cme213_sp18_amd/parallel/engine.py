@@ -173,7 +173,6 @@ class MlpEngine:
         # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
         self.fh_counters = None
         self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = None
-        self.ps_counters = self.ps_gran = self.ps_status = None
         if self.backend == "hip" and self.np and H <= 128 and C <= 16:
             tiles = (ld + 31) // 32
             self.fh_counters = torch.zeros(tiles, dtype=torch.int32, device=dev)
@@ -182,12 +181,6 @@ class MlpEngine:
             self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)  # one 256-B line each
             self.ag_slabs = torch.zeros(tiles * 8 * 16 * 32, dtype=torch.int64, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
-            # the persistent small-batch engine (csrc/mlp/pstep.hip, MlpStep.run_steps at n <= 256): per-workgroup
-            # tag counters, the z2 granules [2][8][16][256] and the end-of-launch status granules
-            if ld <= 256:
-                self.ps_counters = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
-                self.ps_gran = torch.zeros(2 * 8 * 16 * 256, dtype=torch.int64, device=dev)
-                self.ps_status = torch.zeros(8, dtype=torch.int64, device=dev)
         elif self.backend == "hip" and self.np and H >= 512 and C <= 16 and self.dw2buf is not None:
             # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_wide_ag) uses one
             # monotonic counter per column tile -- a separate array per tiling (128 x 128 / 64 x 64) -- and
@@ -375,8 +368,6 @@ class MlpEngine:
                          ag_counters=ptr(self.ag_counters))
             if self.kpart is not None:
                 b.update(kpart=ptr(self.kpart), kpart_cap=int(self.kpart.numel()))
-            if self.ps_counters is not None:
-                b.update(ps_counters=ptr(self.ps_counters), ps_gran=ptr(self.ps_gran), ps_status=ptr(self.ps_status))
             bias_col = bool(self.np and self.XT is not None and self.XT.shape[0] == self.P + 1)
             b.update(bias_col=int(bias_col))
             s.bind(b)

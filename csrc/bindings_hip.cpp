@@ -128,10 +128,6 @@ struct MlpStep {
   }
   uintptr_t kpart = 0;  // split-K dW1 partial slabs (SplitStepArgs::kpart), kpart_cap floats; 0: no split-K
   int64_t kpart_cap = 0;
-  // the persistent small-batch engine (mlp_pstep): its counters / granules / status buffers (0: not available)
-  // and the switch (persistent = 1: run_steps takes it wherever mlp_pstep_ok holds)
-  uintptr_t ps_counters = 0, ps_gran = 0, ps_status = 0;
-  int persistent = 0;  // (off by default until the engine is validated on the GPU: tests and kbench turn it on)
 
   // Binds the engine's buffers and shapes in ONE call (MlpEngine._hip_step): every device pointer, count and
   // layout flag the step reads, by name; an unknown name is an error.  The runtime switches stay plain fields
@@ -160,8 +156,6 @@ struct MlpStep {
       else if (k == "ag_counters") ag_counters = u(); else if (k == "ag_slabs") ag_slabs = u();
       else if (k == "ag_gran") ag_gran = u(); else if (k == "ag_gran_count") ag_gran_count = v.cast<int64_t>();
       else if (k == "kpart") kpart = u(); else if (k == "kpart_cap") kpart_cap = v.cast<int64_t>();
-      else if (k == "ps_counters") ps_counters = u(); else if (k == "ps_gran") ps_gran = u();
-      else if (k == "ps_status") ps_status = u();
       else throw std::invalid_argument("MlpStep.bind: unknown name '" + k + "'");
     }
   }
@@ -338,24 +332,6 @@ struct MlpStep {
     CME_REQUIRE(count >= 0 && n > 0 && n <= ld && B >= n && N_end >= B && (sgd == 1 || sgd == 2),
                 "MlpStep.run_steps: bad step plan");
     if (count == 0) return;
-    if (uses_persistent(n, sgd)) {  // every step of the plan in ONE persistent launch
-      cme::PStepArgs p;
-      p.a = split_args(shard_off, n, scale, reg, lr, 1, 0);
-      p.gstart0 = gstart0;
-      p.count = count;
-      p.B = B;
-      p.shard_off = shard_off;
-      p.N_end = N_end;
-      p.a.X = reinterpret_cast<const void*>(X);  // (the kernel adds each step's offset itself)
-      p.a.XT = reinterpret_cast<const void*>(XT);
-      p.a.labels = P_<int>(labels);
-      p.counters = P_<unsigned long long>(ps_counters);
-      p.gran = P_<unsigned long long>(ps_gran);
-      p.status = P_<unsigned long long>(ps_status);
-      p.err = P_<int>(ag_err);
-      cme::mlp_pstep(p, S(stream));
-      return;
-    }
     int64_t gs = gstart0;
     for (int64_t i = 0; i < count; ++i) {
       if (gs + B > N_end) gs = 0;
@@ -363,17 +339,6 @@ struct MlpStep {
       run(gs + shard_off, n, scale, reg, lr, sgd, 0, stream, 3, nx + shard_off);
       gs += B;
     }
-  }
-
-  // run_steps takes the persistent engine: a single process (sgd = 1), the split path with the all-ones XT feature,
-  // its buffers bound, and the shape it supports (mlp_pstep_ok: H <= 128, n <= 256, n % 4 == 0)
-  bool uses_persistent(int n, int sgd) const {
-    // (fh_allgather: the switch for in-launch waits between workgroups -- off where processes share a GPU and after
-    // a timed-out hand-off, DataParallelTrainer._recover_epoch)
-    if (!persistent || !fh_allgather || !split || sgd != 1 || !ps_counters || !ps_gran || !ps_status || !ag_err)
-      return false;
-    cme::SplitStepArgs a = split_args(0, n, 1.0, 0.0, 0.0, 1, 0);
-    return cme::mlp_pstep_ok(a);
   }
 
   // Weight-gradient pieces of a step whose forward + head already ran (parts=1): used by the
@@ -528,8 +493,6 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("xcd_rows", &MlpStep::xcd_rows)
       .def_readwrite("prefetch", &MlpStep::prefetch)
       .def_readwrite("prefetch_xt", &MlpStep::prefetch_xt)
-      .def_readwrite("persistent", &MlpStep::persistent)
-      .def("uses_persistent", &MlpStep::uses_persistent, py::arg("n"), py::arg("sgd"))
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
       .def_readwrite("planes_stale", &MlpStep::planes_stale)
       .def_readwrite("dw2p", &MlpStep::dw2p)

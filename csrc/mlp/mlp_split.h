@@ -148,21 +148,6 @@ bool mlp_split_wide_fwd_reads_planes(const SplitStepArgs& a, int ag, int allow64
 // at most one workgroup per CU of the XCD for each row tile's column tiles
 bool mlp_split_xcd_rows_ok(const SplitStepArgs& a);
 
-// Persistent small-batch engine (pstep.hip): `count` SGD steps of the whole single-process step in ONE launch of
-// cdiv(H, 16) workgroups, each owning 16 hidden rows (W1 rows, b1, W2 columns, a copy of b2) in LDS for the whole
-// launch; per step only the batch's pixels are read and the z2 partials all-gathered (granules).  The step plan is
-// MlpStep::run_steps's: step i reads samples [g + shard_off, + a.n) where g walks gstart0, +B, ... wrapping to 0
-// when g + B > N_end.
-struct PStepArgs {
-  SplitStepArgs a;                         // the step (n, scale, reg, lr, pointers; sgd = 1)
-  int64_t gstart0 = 0, count = 0, B = 0, shard_off = 0, N_end = 0;
-  unsigned long long* counters = nullptr;  // [tm][32] per-workgroup tag counters (monotonic, zero-initialised)
-  unsigned long long* gran = nullptr;      // z2 partial granules [2][8][16][256]
-  unsigned long long* status = nullptr;    // [8] end-of-launch status granules
-  int* err = nullptr;                      // set when a wait timed out (then nothing is written back)
-};
-bool mlp_pstep_ok(const SplitStepArgs& a);
-void mlp_pstep(const PStepArgs& p, hipStream_t s);
 
 // flag slots (workgroup tiles) of the fused-all-reduce wgrad launch for a P-H layer with the all-ones
 // feature; -1 when above `cap`

@@ -4,8 +4,7 @@ instruction mix) from the rocprofv3 passes of scripts/gpu_pmc_wide.sh.
 
     python scripts/pmc_table.py gpurun_out/pmch [--min-us 3] [--clock-ghz 2.4]
 
-Workgroups = the launch grid (a persistent kernel whose blockIdx % 8 != 0 workgroups exit at once uses 1/8 of
-them); TCP pending stall = TCP_PENDING_STALL_CYCLES / (duration x clock x 256 CUs).  Busy % = counter cycles / (median kernel duration x clock x 1024 SIMDs); SQ_ACTIVE_INST_* count quad-cycles
+Workgroups = the launch grid (XCD padding slots that exit at once included); TCP pending stall = TCP_PENDING_STALL_CYCLES / (duration x clock x 256 CUs).  Busy % = counter cycles / (median kernel duration x clock x 1024 SIMDs); SQ_ACTIVE_INST_* count quad-cycles
 (MI355X_MICROARCH.md), SQ_VALU_MFMA_BUSY_CYCLES counts cycles.  The duration is the kernel trace's median in
 the PMC pass (profiled runs: a lower bound on the busy share of an unprofiled launch).
 """

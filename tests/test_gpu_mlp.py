@@ -704,85 +704,6 @@ def test_xcd_row_placement_is_bitwise_neutral(n):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("n", [100, 64, 128, 200, 256, 36])
-def test_persistent_engine_matches_two_launch_steps(n):
-    """The persistent small-batch engine (csrc/mlp/pstep.hip: every step of MlpStep.run_steps in ONE launch, each
-    workgroup keeping its 16 W1 rows in LDS) against the two-launch steps of the same plan (a wrap past the end of
-    the dataset included) and against the PyTorch fp32 step: the same exact split3 products, so the parameters agree
-    to fp32 reassociation.  (Raw 0-255 pixels: a large step size amplifies rounding differences between ANY two
-    summation orders by ~3x per step -- bench/pstep_diag.py measured the two-launch step vs PyTorch diverging the
-    same way -- so the multi-step comparison uses lr = 0.01 and the one-step check pins the update itself.)"""
-    x, y = synthetic_mnist(6 * n + 20, seed=n)
-    N = 6 * n + 20
-    nn = NeuralNetwork([784, 100, 10])
-    outs = []
-    for mode in ("persistent", "two-launch", "torch"):
-        e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda", backend="torch" if mode == "torch" else "hip")
-        e.set_params(*nn.params)
-        e.load_dataset(x, y)
-        if mode == "torch":
-            gs = 0
-            for _ in range(9):
-                if gs + n > N:
-                    gs = 0
-                e.run(gs, n, 1.0 / n, 1e-4, 0.01, sgd=True)
-                gs += n
-        else:
-            st = e._hip_step()
-            st.persistent = int(mode == "persistent")
-            assert st.uses_persistent(n, 1) == (mode == "persistent")
-            s = torch.cuda.current_stream().cuda_stream
-            st.run_steps(0, 4, n, 0, n, N, 1.0 / n, 1e-4, 0.01, 1, s)  # steps 0..3
-            st.run_steps(4 * n, 5, n, 0, n, N, 1.0 / n, 1e-4, 0.01, 1, s)  # steps 4..8 (wraps at step 6)
-            torch.cuda.synchronize()
-            assert not e.kernel_error()
-        outs.append(e.params.clone())
-    assert _rel(outs[0], outs[1]) < 5e-5, _rel(outs[0], outs[1])  # (n = 36: 1.1e-5 measured, lr / n largest)
-    assert _rel(outs[0], outs[2]) < 5e-5, _rel(outs[0], outs[2])
-    # one step at lr = 0.05: the update itself (parameter deltas) agrees to fp32 reassociation
-    deltas = []
-    for mode in ("persistent", "two-launch"):
-        e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda")
-        e.set_params(*nn.params)
-        e.load_dataset(x, y)
-        p0 = e.params.clone()
-        st = e._hip_step()
-        st.persistent = int(mode == "persistent")
-        st.run_steps(n, 1, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1, torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        deltas.append(e.params - p0)
-    assert _rel(deltas[0], deltas[1]) < 1e-5, _rel(deltas[0], deltas[1])
-
-
-def test_persistent_engine_timeout_applies_nothing():
-    """A real timed-out z2 hand-off inside the persistent launch (one workgroup withholds its partials,
-    MlpEngine.inject_handoff_timeout): the launch ends (every wait is bounded), sets the sticky error word and
-    writes NO parameter back; a later launch with the hook off applies nothing either (the word is sticky)."""
-    n = 100
-    x, y = synthetic_mnist(4 * n, seed=9)
-    nn = NeuralNetwork([784, 100, 10])
-    e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda")
-    e.set_params(*nn.params)
-    e.load_dataset(x, y)
-    st = e._hip_step()
-    st.persistent = 1
-    assert st.uses_persistent(n, 1)
-    s = torch.cuda.current_stream().cuda_stream
-    st.run_steps(0, 3, n, 0, n, 4 * n, 1.0 / n, 1e-4, 0.05, 1, s)
-    torch.cuda.synchronize()
-    assert not e.kernel_error()
-    before = e.params.clone()
-    e.inject_handoff_timeout(2, 2000)
-    st.run_steps(0, 3, n, 0, n, 4 * n, 1.0 / n, 1e-4, 0.05, 1, s)
-    torch.cuda.synchronize()
-    assert e.kernel_error(), "the withheld partials did not time out"
-    assert torch.equal(e.params, before)
-    e.inject_handoff_timeout(-1)
-    st.run_steps(0, 3, n, 0, n, 4 * n, 1.0 / n, 1e-4, 0.05, 1, s)
-    torch.cuda.synchronize()
-    assert torch.equal(e.params, before)
-
-
 @pytest.mark.parametrize("n", [800, 100])
 def test_prefetch_workgroups_are_bitwise_neutral(n):
     """H <= 128 with the XCD-row placement: the prefetch workgroups (MlpStep.prefetch, SplitStepArgs::pf_wgs) only
@@ -795,7 +716,6 @@ def test_prefetch_workgroups_are_bitwise_neutral(n):
         e.set_params(*nn.params)
         e.load_dataset(x, y)
         st = e._hip_step()
-        st.persistent = 0
         st.prefetch = pf
         st.run_steps(0, 7, n, 0, n, e.num_samples, 1.0 / n, 1e-4, 0.05, 1, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
