@@ -641,6 +641,33 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
   ag_wave_sync();  // (each wave re-reads only its own block)
   constexpr int CPR = 4 * NB;  // 4-column chunks per row of the wave's block
   const __amdgpu_buffer_rsrc_t rdz = make_rsrc(h.dZ1), rpl = make_rsrc(h.dZ1_planes);
+  if (!h.dZ1 && h.npz == 1 && h.ldz % 8 == 0) {  // bf16 (split1): 8 columns per lane, ONE 16-byte plane store
+    constexpr int CPR8 = 2 * NB;
+#pragma unroll
+    for (int q = 0; q < 16 * CPR8 / 64; ++q) {
+      const int c = q * 64 + lane, rr = c / CPR8, c8 = (c % CPR8) * 8;
+      const int row = rw + rr, col = cw + c8;
+      const float* src = ts + (rw - m0 + rr) * LD + cw - n0 + c8;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(src), v1 = *reinterpret_cast<const f32x4*>(src + 4);
+      const bool rok = row < H;
+      unsigned short qb[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        qb[e] = __builtin_bit_cast(unsigned short, __float2bfloat16(v0[e]));
+        qb[4 + e] = __builtin_bit_cast(unsigned short, __float2bfloat16(v1[e]));
+      }
+      const int base = (row * h.ldz + col) * 2;
+      if (rok && col + 8 <= n) {
+        __attribute__((ext_vector_type(4))) unsigned w;
+        __builtin_memcpy(&w, qb, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(w, rpl, base, 0, 0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          __builtin_amdgcn_raw_buffer_store_b16(qb[e], rpl, (rok && col + e < n) ? base + 2 * e : kOOB, 0, 0);
+      }
+    }
+  } else
 #pragma unroll
   for (int q = 0; q < 16 * CPR / 64; ++q) {
     const int c = q * 64 + lane, rr = c / CPR, c4 = (c % CPR) * 4;
