@@ -641,7 +641,7 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
   ag_wave_sync();  // (each wave re-reads only its own block)
   constexpr int CPR = 4 * NB;  // 4-column chunks per row of the wave's block
   const __amdgpu_buffer_rsrc_t rdz = make_rsrc(h.dZ1), rpl = make_rsrc(h.dZ1_planes);
-  if (!h.dZ1 && h.npz == 1 && h.ldz % 8 == 0) {  // bf16 (split1): 8 columns per lane, ONE 16-byte plane store
+  if (NB % 2 == 0 && !h.dZ1 && h.npz == 1 && h.ldz % 8 == 0) {  // bf16 (split1): 8 columns per lane, one 16-byte store
     constexpr int CPR8 = 2 * NB;
 #pragma unroll
     for (int q = 0; q < 16 * CPR8 / 64; ++q) {
