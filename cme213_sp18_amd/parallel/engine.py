@@ -181,12 +181,6 @@ class MlpEngine:
             self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)  # one 256-B line each
             self.ag_slabs = torch.zeros(tiles * 8 * 16 * 32, dtype=torch.int64, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
-            # the K-split forward at per-GPU batches <= 256 (MlpStep.ksplit): split-epoch counters [8 tiles][32] and
-            # the producers' z1 granules [3 slices][8 column tiles][8 row tiles][16][32]
-            self.ag_kcounters = self.ag_kslabs = None
-            if ld <= 256:
-                self.ag_kcounters = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
-                self.ag_kslabs = torch.zeros(3 * 8 * 8 * 512, dtype=torch.int64, device=dev)
         elif self.backend == "hip" and self.np and H >= 512 and C <= 16 and self.dw2buf is not None:
             # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_wide_ag) uses one
             # monotonic counter per column tile -- a separate array per tiling (128 x 128 / 64 x 64) -- and
@@ -368,8 +362,6 @@ class MlpEngine:
             if self.fh_counters is not None:
                 b.update(fh_counters=ptr(self.fh_counters), fh_tiles=int(self.fh_counters.numel()),
                          ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs))
-                if getattr(self, "ag_kcounters", None) is not None:
-                    b.update(kcounters=ptr(self.ag_kcounters), kslabs=ptr(self.ag_kslabs))
             elif self.ag_gran is not None:  # the wide fused head
                 b.update(fh_tiles=int(self.ag_counters.numel()) // 64,  # [2 tilings][tiles][32]
                          ag_gran=ptr(self.ag_gran), ag_gran_count=int(self.ag_gran.numel()),

@@ -83,9 +83,6 @@ struct MlpStep {
   // (profiles/kbench_prefetch_wgs_r4.jsonl)
   int prefetch = 4;
   int prefetch_xt = 4;  // SplitStepArgs::pf_wgs_xt
-  // SplitStepArgs::ksplit (1 or cme::kKSplit) and its buffers: the K-split forward at per-GPU batches <= 256
-  int ksplit = 1;
-  uintptr_t kcounters = 0, kslabs = 0;
   int ag64() const { return ag_tiles64 >= 0 ? ag_tiles64 : (store_a1 ? 0 : 1); }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
@@ -157,7 +154,6 @@ struct MlpStep {
       else if (k == "z2p") z2p = u(); else if (k == "bias_col") bias_col = i();
       else if (k == "fh_counters") fh_counters = u(); else if (k == "fh_tiles") fh_tiles = i();
       else if (k == "ag_counters") ag_counters = u(); else if (k == "ag_slabs") ag_slabs = u();
-      else if (k == "kcounters") kcounters = u(); else if (k == "kslabs") kslabs = u();
       else if (k == "ag_gran") ag_gran = u(); else if (k == "ag_gran_count") ag_gran_count = v.cast<int64_t>();
       else if (k == "kpart") kpart = u(); else if (k == "kpart_cap") kpart_cap = v.cast<int64_t>();
       else throw std::invalid_argument("MlpStep.bind: unknown name '" + k + "'");
@@ -199,11 +195,6 @@ struct MlpStep {
     a.xcd_rows = xcd_rows && cme::mlp_split_xcd_rows_ok(a);
     a.pf_wgs = (a.xcd_rows && bias_col) ? prefetch : 0;
     a.pf_wgs_xt = (a.xcd_rows && bias_col) ? prefetch_xt : 0;
-    if (ksplit > 1 && a.xcd_rows && kcounters && kslabs && n <= 256 && H <= 128) {
-      a.ksplit = cme::kKSplit;
-      a.kcounters = P_<unsigned long long>(kcounters);
-      a.kslabs = P_<unsigned long long>(kslabs);
-    }
     return a;
   }
 
@@ -502,7 +493,6 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("xcd_rows", &MlpStep::xcd_rows)
       .def_readwrite("prefetch", &MlpStep::prefetch)
       .def_readwrite("prefetch_xt", &MlpStep::prefetch_xt)
-      .def_readwrite("ksplit", &MlpStep::ksplit)
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
       .def_readwrite("planes_stale", &MlpStep::planes_stale)
       .def_readwrite("dw2p", &MlpStep::dw2p)

@@ -35,61 +35,16 @@ struct EpiSigLds {
   float (*a1s)[33];  // [16][32 + 1] this workgroup's a1 tile
   int ld, r0, c0;
   float xscale;
-  bool raw;  // K-split slice 0: keep the raw partial z1 in a1s (the sigmoid follows the partials' sum)
   float pre[kEpiMaxQ];
   __device__ __forceinline__ void prefetch(int q, int row, int, bool ok) {
-    pre[q] = buf_load1<float>(make_rsrc(b1), (ok && !raw) ? row * 4 : kOOB);
+    pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
-    if (raw) {
-      a1s[row - r0][col - c0] = v;
-      return;
-    }
     const float s = ag_sigmoid(v * xscale + pre[q]);
     a1s[row - r0][col - c0] = s;
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), make_rsrc(a1), (row * ld + col) * 4, 0, 0);
   }
 };
-
-// K-split of the small-n forward (SplitStepArgs::ksplit): slice ks of K = P is [ks KSL, (ks + 1) KSL), the last one
-// running to P; KSL a whole number of 64-deep chunk pairs (the 16-byte pixel loads' unit)
-__device__ __forceinline__ int ksplit_len(int P, int S) { return 64 * (((P + 63) / 64) / S); }
-__device__ __forceinline__ gran_t* kslab(const SplitStepArgs& f, int ks, int ct, int rt) {  // ks >= 1
-  return f.kslabs + ((size_t)((ks - 1) * 8 + ct) * 8 + rt) * 512;
-}
-
-// A K-split producer: the z1 partial of tile (rt, ct) over K slice ks >= 1, published as granules tagged with this
-// launch's split epoch (one add per workgroup to the column tile's split counter: kKSplit x tm adds per launch).
-// It waits for nothing, so the consumers (slice 0, fha_body) may wait for it; the grid puts producers first.
-template <int NPW, int VEC, bool AF>
-__device__ __forceinline__ void fha_kproducer(const SplitStepArgs& f, int tm, int tn, int ks, int blk, float* red) {
-  __shared__ unsigned s_kep;
-  const int xcd = blk & 7, ct = blk >> 3, rt = xcd;  // (XCD-row placement only)
-  if (ct >= tn || rt >= tm) return;
-  const int t = threadIdx.x, S = f.ksplit, KSL = ksplit_len(f.P, S);
-  if (t == 448) {
-    gran_t old = gran_epoch_add(f.kcounters + (size_t)ct * 32);
-    gran_epoch_wait(old);
-    s_kep = (unsigned)(old / (unsigned)(S * tm)) + 1u;
-  }
-  const int k0 = ks * KSL, klen = ks == S - 1 ? f.P - k0 : KSL;
-  SplitStepArgs fk = f;
-  fk.W1 = f.W1 + k0;
-  fk.W1p = static_cast<__hip_bfloat16*>(f.W1p) + k0;
-  fk.X = static_cast<const uint8_t*>(f.X) + k0;
-  struct EpiGran {
-    gran_t* slab;
-    int r0, c0;
-    const unsigned* ep;
-    float pre[kEpiMaxQ];
-    __device__ __forceinline__ void prefetch(int, int, int, bool) {}
-    __device__ __forceinline__ void operator()(int, int row, int col, float v) {
-      gran_store(slab + (row - r0) * 32 + (col - c0), v, *ep);  // (after wsk_tile's reduction barrier: s_kep set)
-    }
-  } epi{kslab(f, ks, ct, rt), rt * 16, ct * 32, &s_kep, {}};
-  TileGeom g{f.H, f.n, klen, rt * 16, ct * 32};
-  fwd_tile<NPW, 2, VEC, 4, AF>(fk, g, epi, red);
-}
 
 // blk: the workgroup's slot in the XCD-grouped grid (the hardware XCD is blk & 7).  red: >= 8 * 2 * 4 * 64
 // floats of LDS.
@@ -121,18 +76,11 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   // GEMM's reduction barrier.  (Waited for after the GEMM, the same vmcnt(0) also covered wave 7's a1 epilogue
   // stores: a store round trip in front of the z2 publication of every workgroup, bench/stamps_fha.py.)
   constexpr int kEpochThread = 448;
-  const int S = f.ksplit;
-  __shared__ unsigned s_kep;
   if (t == kEpochThread) {
     gran_t ep_old = gran_epoch_add(counters + (size_t)ct * kAgCounterStride);
     gran_epoch_wait(ep_old);
     s_ep = (unsigned)(ep_old / (unsigned)tm) + 1u;
     s_bad = 0;
-    if (S > 1) {  // the K-split hand-off's epoch: the same column tile's split counter as its producers
-      gran_t k_old = gran_epoch_add(f.kcounters + (size_t)ct * 32);
-      gran_epoch_wait(k_old);
-      s_kep = (unsigned)(k_old / (unsigned)(S * tm)) + 1u;
-    }
   }
   // the label of this thread's softmax column (t >> 4), fetched now: loaded where the softmax uses it, it was
   // a dependent memory round trip after the all-gather wait
@@ -145,29 +93,13 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   const float w2v = buf_load1<float>(
       make_rsrc(h.W2), (t < 256 && wc < C && r0 + wr < H) ? (wc * H + r0 + wr) * 4 : kOOB);
   const float b2v = buf_load1<float>(make_rsrc(h.b2), (t >= 256 && t < 256 + 16 && t - 256 < C) ? (t - 256) * 4 : kOOB);
-  TileGeom g{H, n, S > 1 ? ksplit_len(f.P, S) : f.P, r0, c0};
-  EpiSigLds epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, S > 1, {}};
+  TileGeom g{H, n, f.P, r0, c0};
+  EpiSigLds epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
   fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
   // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
   // they are masked below.  w2s / b2s are complete after the barrier below.
   if (t < 256) w2s[wc][wr] = w2v;
   else if (t < 256 + 16) b2s[t - 256] = b2v;
-  if (S > 1) {  // K-split: z1 = slice 0 (a1s) + the producers' partials in slice order, then the epilogue
-    const int r = t >> 5, col = t & 31;
-    const bool ok = r0 + r < H && c0 + col < n;
-    const float bv = buf_load1<float>(make_rsrc(f.b1), ok ? (r0 + r) * 4 : kOOB);
-    float z = a1s[r][col];
-    const bool good = gran_poll<kKSplit - 1>(kslab(f, 1, ct, rt), (unsigned)(r * 32 + col), 8u * 8u * 512u, S - 1, ok,
-                                             s_kep, (uint32_t)f.ag_wait_us, [&](int, float v) { z += v; });
-    if (!good && (t & 63) == 0) {
-      atomicExch(err, 1);
-      s_bad = 1;
-    }
-    const float sv = ag_sigmoid(z * f.xscale + bv);
-    a1s[r][col] = sv;
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, sv), make_rsrc(f.a1),
-                                          ok ? ((r0 + r) * f.ld + c0 + col) * 4 : kOOB, 0, 0);
-  }
   __syncthreads();
   const unsigned ep = s_ep;
   // ---- 1. z2 partial W2[:, tile rows] . a1[tile rows, 32 columns] on MFMA (waves 0 and 1: 16 columns each,

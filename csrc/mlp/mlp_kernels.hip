@@ -538,16 +538,7 @@ __global__ __launch_bounds__(512) void fwd1_head_ag_kernel(SplitStepArgs f, Head
     if (xcd < tm) l2_touch(f.XT, 0, f.P + f.bias_col, f.ldxt, f.n, part, f.pf_wgs_xt, reinterpret_cast<char*>(red));
     return;
   }
-  int blk = blockIdx.x;
-  if (f.ksplit > 1) {  // K-split: the (ksplit - 1) x 8 tn producer workgroups come first, then the slice-0 tiles
-    const int np = (f.ksplit - 1) * 8 * tn;
-    if (blk < np) {
-      fha_kproducer<NPW, VEC, AF>(f, tm, tn, 1 + blk / (8 * tn), blk % (8 * tn), red);
-      return;
-    }
-    blk -= np;
-  }
-  fha_body<NPW, VEC, AF>(f, h, counters, slabs, err, tm, tn, blk, red);
+  fha_body<NPW, VEC, AF>(f, h, counters, slabs, err, tm, tn, blockIdx.x, red);
 }
 
 template <typename P, int NC>
@@ -1095,7 +1086,7 @@ static int fha_vec(const SplitStepArgs& f) {
 
 bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f) {
   if (f.n <= 0) return true;
-  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32), nwg = tm * tn * f.ksplit;
+  const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32), nwg = tm * tn;
   const bool af = mlp_split_fwd_fp32_w(f);
   const int vec = fha_vec(f);
 #define CME_OCC(np, af)                                                            \
@@ -1120,9 +1111,7 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
                                         "last-arriver form, mlp_fwd1_head)");
   const bool af = mlp_split_fwd_fp32_w(f);
   const int vec = fha_vec(f);
-  CME_REQUIRE(f.ksplit == 1 || (f.ksplit == kKSplit && f.xcd_rows && tn <= 8 && f.kcounters && f.kslabs),
-              "fwd1_head_ag: the K-split needs the XCD-row placement, n <= 256 and its buffers");
-  const int nwg = f.xcd_rows ? f.ksplit * 8 * tn + 8 * f.pf_wgs_xt : 8 * tm * cdiv(tn, 8);  // (prefetch WGs last)
+  const int nwg = f.xcd_rows ? 8 * tn + 8 * f.pf_wgs_xt : 8 * tm * cdiv(tn, 8);  // (prefetch workgroups last)
 #define CME_FHA(np, af)                                                                                  \
   if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
   else if (vec == 1) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn); \

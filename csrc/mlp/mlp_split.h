@@ -43,8 +43,6 @@ struct XgmiFuse {
   int64_t off_b1 = 0, off_W2 = 0, off_b2 = 0;  // flat-arena offsets ([W1|b1|W2|b2], 64-aligned)
 };
 
-constexpr int kKSplit = 4;  // slices of the small-n forward's K-split (SplitStepArgs::ksplit)
-
 struct SplitStepArgs {
   int P = 784, H = 100, C = 10, n = 0, ld = 0;
   int npw = 3, npz = 3;          // planes of W1 and of dZ1 (3: exact fp32, 1: bf16)
@@ -124,13 +122,6 @@ struct SplitStepArgs {
   // the weight-gradient launch), the weight-gradient launch the next step's X at pf_X (nullptr: none) for the next
   // forward (MlpStep.prefetch; 0: off)
   int pf_wgs = 0;     // ... in the weight-gradient launch (the next step's X)
-  // H <= 128, per-GPU batch <= 256, XCD-row placement: the all-gather forward + head splits K = P over kKSplit
-  // workgroups per 16 x 32 tile (fha_body.h: kKSplit - 1 producers publish their z1 partial as granules, the
-  // row-tile workgroup of slice 0 sums them and continues); kcounters [kKSplit][8][32] launch epochs,
-  // kslabs [kKSplit - 1][8 column tiles][8 row tiles][16][32] granules (MlpStep.ksplit; 1: off)
-  int ksplit = 1;
-  unsigned long long* kcounters = nullptr;
-  unsigned long long* kslabs = nullptr;
   int pf_wgs_xt = 0;  // ... in the forward + head launch (this step's XT)
   const void* pf_X = nullptr;
 };

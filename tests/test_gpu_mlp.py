@@ -723,26 +723,3 @@ def test_prefetch_workgroups_are_bitwise_neutral(n):
         outs.append(e.params.clone())
     assert torch.equal(outs[0], outs[1])
 
-
-@pytest.mark.parametrize("n", [256, 200, 100, 37])
-def test_ksplit_forward_matches_unsplit(n):
-    """The small-n forward's K-split (MlpStep.ksplit: three producer workgroups per tile publish their slice's z1
-    partial as granules, the slice-0 workgroup sums them in slice order) against the unsplit forward + head: the
-    same products in another summation order, over several steps of the native loop (a wrap included)."""
-    x, y = synthetic_mnist(5 * n + 16, seed=n + 3)
-    nn = NeuralNetwork([784, 100, 10])
-    outs = []
-    for ks in (1, 4):
-        e = MlpEngine(nn.H, dtype="f32", max_cols=n, device="cuda")
-        e.set_params(*nn.params)
-        e.load_dataset(x, y)
-        st = e._hip_step()
-        st.ksplit = ks
-        st.run_steps(0, 7, n, 0, n, e.num_samples, 1.0 / n, 1e-4, 0.01, 1, torch.cuda.current_stream().cuda_stream)
-        e.run(0, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
-        torch.cuda.synchronize()
-        assert not e.kernel_error()
-        outs.append((e.params.clone(), e.grads.clone(), e.loss_sum()))
-    assert _rel(outs[1][0], outs[0][0]) < 1e-5, _rel(outs[1][0], outs[0][0])
-    assert _rel(outs[1][1], outs[0][1]) < 1e-4, _rel(outs[1][1], outs[0][1])
-    assert abs(outs[1][2] - outs[0][2]) <= 1e-4 * abs(outs[0][2])
