@@ -72,6 +72,20 @@ def main(argv=None):
                           "wave_epilogue": pct(wr[:, 3]), "kloop_dur": pct(wr[:, 1] - wr[:, 0]),
                           # per workgroup (8 waves): first -> last wave entry, and first wave entry -> last K-loop end
                           **per_wg(wbuf, t0)}))
+        if rep == 3:  # per wave index, relative to its workgroup's entry stamp (wave 0, thread 0): median / p90
+            g = wbuf.view(-1, 8, 4).cpu().numpy().astype(np.int64)[: s.shape[0] if False else None]
+            wg = buf.view(-1, 4).cpu().numpy().astype(np.int64)
+            nb = min(g.shape[0], wg.shape[0])
+            g, wg = g[:nb], wg[:nb]
+            keep = (wg[:, 0] > 0) & (g[:, :, 0] > 0).all(axis=1)
+            g, wg = g[keep], wg[keep]
+            rel_w = (g - wg[:, None, 0:1]) / 100.0
+            print(json.dumps({"per_wave": {str(w): {"entry": pct(rel_w[:, w, 0])[1:3], "kloop_end": pct(rel_w[:, w, 1])[1:3],
+                                                    "kloop_dur": pct(rel_w[:, w, 1] - rel_w[:, w, 0])[1:3]}
+                                           for w in range(8)},
+                              "wg_published": pct((wg[:, 1] - wg[:, 0]) / 100.0)[1:3],
+                              "wg_arrived": pct((wg[:, 2] - wg[:, 0]) / 100.0)[1:3],
+                              "wg_end": pct((wg[:, 3] - wg[:, 0]) / 100.0)[1:3]}), flush=True)
         if rep == 3:  # per column tile (XCD-grouped grid: block b -> xcd b & 7, slot b >> 3, ct = xcd + 8 (slot // tm))
             tm = (a.hidden + 15) // 16
             allv = buf.view(-1, 4).cpu().numpy().astype(np.int64)
