@@ -128,6 +128,16 @@ def main(argv=None):
                         s1.synchronize()
                         best = min(best, s0.elapsed_time(s1) * 1e3 / a.reps)
                     row["step_loop_same_us"] = round(best, 3)
+                    # the same two loops captured into a HIP graph and replayed: stream launches vs graph nodes
+                    # for identical kernels and arguments
+                    cnt = [0]
+
+                    def walk1():  # one step of the walk per call: consecutive batches across the captured nodes
+                        step.run_steps(cnt[0] * n % (N - N % n), 1, n, 0, n, N, 1.0 / n, 1e-4, 0.0, 1, st())
+                        cnt[0] += 1
+                    row["step_walk_graph_us"] = round(timeit(walk1, a.reps), 3)
+                    row["step_same_graph_us"] = round(timeit(
+                        lambda: step.run_steps(0, 1, n, 0, n, n, 1.0 / n, 1e-4, 0.0, 1, st()), a.reps), 3)
                     import time as _time  # host time to ENQUEUE the loop's launches (no sync inside)
 
                     _t.cuda.synchronize()
