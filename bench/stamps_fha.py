@@ -73,7 +73,7 @@ def main(argv=None):
                           # per workgroup (8 waves): first -> last wave entry, and first wave entry -> last K-loop end
                           **per_wg(wbuf, t0)}))
         if rep == 3:  # per wave index, relative to its workgroup's entry stamp (wave 0, thread 0): median / p90
-            g = wbuf.view(-1, 8, 4).cpu().numpy().astype(np.int64)[: s.shape[0] if False else None]
+            g = wbuf.view(-1, 8, 4).cpu().numpy().astype(np.int64)
             wg = buf.view(-1, 4).cpu().numpy().astype(np.int64)
             nb = min(g.shape[0], wg.shape[0])
             g, wg = g[:nb], wg[:nb]
