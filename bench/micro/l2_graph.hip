@@ -3,7 +3,8 @@
 // profiles/graph_gap_r4/summary.txt.)  Kernel k_read: 256 workgroups (32 per XCD) read a 2 MiB-per-XCD part of a
 // 16 MiB buffer and record their own read time (s_memrealtime, 10 ns).  Sequence: read A, read A again -- as two
 // stream launches, and as two nodes of a captured graph.  The second read's per-workgroup time is reported; a
-// third case reads a buffer last touched before 128 MiB of other reads (cold in L2) for scale.
+// third case reads a buffer last touched before 128 MiB of other reads (cold in L2) for scale, and a pair
+// write A -> read A checks data the previous kernel WROTE.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o bench/micro/l2_graph bench/micro/l2_graph.hip
 #include <hip/hip_runtime.h>
@@ -45,6 +46,13 @@ __global__ __launch_bounds__(256) void k_read(const u32x4* __restrict__ buf, uns
   }
 }
 
+__global__ __launch_bounds__(256) void k_write(u32x4* __restrict__ buf) {  // the same per-workgroup part, written
+  const int x = blockIdx.x % 8, s = blockIdx.x / 8;
+  constexpr int kPart = kBytes / 8 / 16, kPiece = kPart / 32;
+  u32x4* p = buf + (size_t)x * kPart + (size_t)s * kPiece;
+  for (int i = threadIdx.x; i < kPiece; i += 256) p[i] = u32x4{(unsigned)i, 1u, 2u, 3u};
+}
+
 static void report(const char* name, unsigned* d_t) {
   std::vector<unsigned> h(kWG);
   CK(hipMemcpy(h.data(), d_t, kWG * 4, hipMemcpyDeviceToHost));
@@ -76,7 +84,23 @@ int main() {
   k_read<<<kWG, 256, 0, s>>>(a, t2);
   CK(hipStreamEndCapture(s, &g));
   CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  hipGraph_t gw;
+  hipGraphExec_t gwe;
+  CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  k_write<<<kWG, 256, 0, s>>>(a);
+  k_read<<<kWG, 256, 0, s>>>(a, t2);
+  CK(hipStreamEndCapture(s, &gw));
+  CK(hipGraphInstantiate(&gwe, gw, nullptr, nullptr, 0));
   for (int rep = 0; rep < 3; ++rep) {
+    evict();
+    k_write<<<kWG, 256, 0, s>>>(a);
+    k_read<<<kWG, 256, 0, s>>>(a, t2);
+    CK(hipStreamSynchronize(s));
+    report("stream: read of the buffer the previous kernel WROTE", t2);
+    evict();
+    CK(hipGraphLaunch(gwe, s));
+    CK(hipStreamSynchronize(s));
+    report("graph: read of the buffer the previous node WROTE", t2);
     evict();
     k_read<<<kWG, 256, 0, s>>>(a, t1);
     k_read<<<kWG, 256, 0, s>>>(a, t2);
@@ -91,6 +115,8 @@ int main() {
     CK(hipStreamSynchronize(s));
     report("stream: a buffer cold in L2", t2);
   }
+  CK(hipGraphExecDestroy(gwe));
+  CK(hipGraphDestroy(gw));
   CK(hipGraphExecDestroy(ge));
   CK(hipGraphDestroy(g));
   return 0;
