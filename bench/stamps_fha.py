@@ -20,6 +20,8 @@ def main(argv=None):
     ap.add_argument("--n", type=int, default=800)
     ap.add_argument("--hidden", type=int, default=100)
     ap.add_argument("--xcd-rows", type=int, default=None, help="MlpStep.xcd_rows (default: the engine's)")
+    ap.add_argument("--warm-fwd", action="store_true",
+                    help="one extra forward before the stamped one: W1 last READ, not written, by the previous launch")
     a = ap.parse_args(argv)
     import numpy as np
     import torch
@@ -51,6 +53,8 @@ def main(argv=None):
     for rep in range(4):
         for _ in range(20):
             step.run(0, a.n, 1.0 / a.n, 1e-4, 0.0, 1, 0, st, 3)
+        if a.warm_fwd:
+            step.run(0, a.n, 1.0 / a.n, 1e-4, 0.0, 1, 0, st, 1)
         torch.cuda.synchronize()
         buf.zero_()
         wbuf.zero_()
@@ -80,7 +84,7 @@ def main(argv=None):
             keep = (wg[:, 0] > 0) & (g[:, :, 0] > 0).all(axis=1)
             g, wg = g[keep], wg[keep]
             rel_w = (g - wg[:, None, 0:1]) / 100.0
-            print(json.dumps({"per_wave": {str(w): {"entry": pct(rel_w[:, w, 0])[1:3], "kloop_end": pct(rel_w[:, w, 1])[1:3],
+            print(json.dumps({"warm_fwd": a.warm_fwd, "per_wave": {str(w): {"entry": pct(rel_w[:, w, 0])[1:3], "kloop_end": pct(rel_w[:, w, 1])[1:3],
                                                     "kloop_dur": pct(rel_w[:, w, 1] - rel_w[:, w, 0])[1:3]}
                                            for w in range(8)},
                               "wg_published": pct((wg[:, 1] - wg[:, 0]) / 100.0)[1:3],
