@@ -237,15 +237,67 @@ def dp_tune_allreduce(ctx, global_batch: int, tune: dict) -> str:
     return modes[best]
 
 
+PROBE_FACTOR = 3.0  # a timed run this many times slower per step than its probe is not trusted
+
+
+def guard_probe(res: dict, steps: int, probe_us, retime=None) -> dict:
+    """First-contact guard: the timed run's us/step against the probe that chose its configuration (max over
+    ranks on both sides, so every rank decides alike).  More than PROBE_FACTOR x off: re-time once on the next
+    candidate (``retime() -> (result, its own probe us/step or None)``); still off (or nothing to fall back on):
+    the record is marked ``"invalid": "timed run inconsistent with probe"`` instead of reported clean.  The
+    decision and both timings go into ``config.probe_guard``."""
+    if not isinstance(probe_us, (int, float)) or not probe_us or probe_us == float("inf") or not res.get("ok"):
+        return res
+    us = 1e6 * res["dt"] / steps
+    first = {"timed_us_per_step": round(us, 3), "probe_us_per_step": round(probe_us, 3),
+             "what": res["config"].get("allreduce") if res.get("parallelism", "").startswith("dp")
+             else res.get("parallelism")}
+    if us <= PROBE_FACTOR * probe_us:
+        res["config"]["probe_guard"] = {"consistent": True, **first}
+        return res
+    if retime is not None:
+        res2, probe2 = retime()
+        us2 = 1e6 * res2["dt"] / steps
+        ref = probe2 if isinstance(probe2, (int, float)) and probe2 and probe2 != float("inf") else probe_us
+        second = {"timed_us_per_step": round(us2, 3), "probe_us_per_step": round(ref, 3),
+                  "what": res2["config"].get("allreduce") if res2.get("parallelism", "").startswith("dp")
+                  else res2.get("parallelism")}
+        res2["config"]["probe_guard"] = {"consistent": bool(res2.get("ok")) and us2 <= PROBE_FACTOR * ref,
+                                         "first": first, "retimed": second}
+        if res2["config"]["probe_guard"]["consistent"]:
+            return res2
+        res = res2
+    else:
+        res["config"]["probe_guard"] = {"consistent": False, "first": first}
+    res["ok"] = False
+    res["invalid"] = "timed run inconsistent with probe"
+    return res
+
+
 def run_dp(ctx, global_batch: int, allreduce: str | None = None, tune: dict | None = None) -> dict:
     """One data-parallel measurement: K timed steps of global batch ``global_batch`` (n = global_batch / R per
     rank).  The trainer is always prepared afresh for the timed region (from the initial weights, after W
-    warm-up steps), whichever candidate won the tuning."""
-    from cme213_sp18_amd.parallel.trainer import allreduce_cost_us
-
+    warm-up steps), whichever candidate won the tuning.  A timed run far off its probe is re-timed once on RCCL
+    (guard_probe)."""
     a = ctx.a
     tune = {} if tune is None else tune
     mode = allreduce if allreduce is not None else dp_tune_allreduce(ctx, global_batch, tune)
+    res = _run_dp_timed(ctx, global_batch, mode, tune)
+    impl = res["config"]["allreduce"]
+    retime = None
+    if ctx.R > 1 and impl != ctx.comm.name:
+        def retime():
+            tr, full = dp_prepare(ctx, global_batch, "rccl", a.warmup, a.tune_steps)
+            probe = dp_probe(ctx, tr, full, a.tune_steps)
+            tr.close()
+            return _run_dp_timed(ctx, global_batch, "rccl", tune), probe
+    return guard_probe(res, a.steps, tune.get(impl), retime)
+
+
+def _run_dp_timed(ctx, global_batch: int, mode: str, tune: dict) -> dict:
+    from cme213_sp18_amd.parallel.trainer import allreduce_cost_us
+
+    a = ctx.a
     tr, full = dp_prepare(ctx, global_batch, mode, a.warmup)
     if tr.allreduce_impl.startswith("xgmi") and mode in ("auto",) and not dp_healthy(tr):
         # a bounded peer wait timed out during the warm-up: every rank drops to RCCL together, from the
@@ -270,6 +322,7 @@ def run_dp(ctx, global_batch: int, allreduce: str | None = None, tune: dict | No
     e = tr.engine
     wire = e.params.numel() * (2 if tr.xgmi is not None and tr.xgmi.wire != e.params.dtype else e.params.element_size())
     shots = 0 if tr.xgmi is None else tr.xgmi.shots
+    fp_bytes = e.params.numel() * e.params.element_size()
     # strong scaling drops the remainder columns when R does not divide the batch (trainer.shard)
     images = a.steps * (global_batch // ctx.R) * ctx.R
     res.update(dt=dt, images=images, global_batch=global_batch, per_gpu_batch=global_batch // ctx.R,
@@ -277,7 +330,8 @@ def run_dp(ctx, global_batch: int, allreduce: str | None = None, tune: dict | No
                config={"hip_graphs": tr.use_graphs and not native_exec,
                        "executor": "native" if native_exec else ("graph" if tr.use_graphs else "eager"),
                        "allreduce": tr.allreduce_impl, **ar,
-                       "allreduce_pred_us": round(allreduce_cost_us(ctx.R, wire, shots), 2) if ctx.R > 1 else None,
+                       "allreduce_pred_us": round(allreduce_cost_us(ctx.R, wire, shots, fp_bytes=fp_bytes), 2)
+                       if ctx.R > 1 else None,
                        "allreduce_tuning_us_per_step": tune or None})
     tr.close()
     return res
@@ -432,6 +486,12 @@ def measure(ctx, scaling: str, parallel: str | None = None, allreduce: str | Non
         parallel = choose_parallel(ctx, gb, gb, ptune)
     if parallel == "tp":
         res = run_tp(ctx, gb)
+        if ptune:  # chosen by probing: a timed run far off its probe is re-timed once on data parallel
+            res = guard_probe(res, a.steps, ptune.get(res["parallelism"]),
+                              lambda: (run_dp(ctx, gb), ptune.get(f"dp{ctx.R}")))
+            if res["parallelism"].startswith("dp"):
+                parallel = "dp"
+                res["allreduce_mode"] = _mode_of(res["config"]["allreduce"], ctx)
     else:
         tune: dict = {}
         res = run_dp(ctx, gb, allreduce=allreduce, tune=tune)
@@ -486,6 +546,15 @@ def main(argv=None) -> int:
         shutdown()
         return 2
     ctx = Ctx(a, comm, device, placement)
+    cost = None
+    if ctx.R > 1 and a.backend == "hip":
+        # the all-reduce policy's constants measured on this node (<= ~2 s) instead of the planning numbers
+        from cme213_sp18_amd.parallel.trainer import measure_cost_model, set_cost_model
+
+        cost = measure_cost_model(comm, device)
+        set_cost_model(cost)
+        if cost is not None and ctx.rank == 0:
+            print(f"cost model measured on this node: {cost.as_record()}", file=sys.stderr, flush=True)
     res = measure(ctx, a.scaling)
     sec = None
     if ctx.R > 1 and a.secondary == "auto":
@@ -510,7 +579,8 @@ def main(argv=None) -> int:
             "data": DATA,
             "config": {"model": f"784-{a.hidden}-10 MLP", "global_batch": s["global_batch"], "seq_len": None,
                        "parallelism": s["parallelism"], "per_gpu_batch": s["per_gpu_batch"],
-                       "backend": a.backend, "mode": a.mode, **res["config"], **res["checks"], **ctx.placement},
+                       "backend": a.backend, "mode": a.mode, **res["config"], **res["checks"], **ctx.placement,
+                       **({"cost_model_measured": cost.as_record()} if cost is not None else {})},
         }
         if sec is not None:
             ss = summary(ctx, sec)

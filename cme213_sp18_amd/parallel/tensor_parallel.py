@@ -118,6 +118,12 @@ class TensorParallelTrainer:
     def close(self) -> None:
         """Collective: release the xGMI IPC bucket (every rank must call it)."""
         if self._xz is not None:
+            # the engine's cached step reads the bucket's error word as its ag_err: point it back at the engine's
+            # own word (or none) before that device memory is freed
+            st = self.engine._step
+            if st is not None:
+                e = self.engine
+                st.ag_err = e.ag_err.data_ptr() if e.ag_err is not None else 0
             self._xz.close()
             self._xz = None
         self._graphs.clear()
@@ -326,7 +332,8 @@ class TensorParallelTrainer:
                 # (collective) a z2 peer wait timed out on some rank: that rank's weight-gradient launches applied
                 # nothing from then on, so the shards no longer belong to one model -- every rank stops together
                 raise CommFailure(f"rank {self.rank}: an xGMI z2 all-reduce peer wait timed out on some rank; "
-                                  "no rank applied the affected update")
+                                  "that rank stopped updating its shard while its peers may have applied the "
+                                  "step, so the shards may be inconsistent -- restart from a checkpoint")
             if on_event is not None:
                 if dev.type == "cuda":
                     torch.cuda.synchronize(dev)

@@ -32,50 +32,121 @@ from .comm import Communicator, NullComm
 from .engine import MlpEngine
 
 
-XGMI_AUTO_MAX_BYTES = 2 << 20  # allreduce="auto" uses the xGMI one-shot kernel up to this bucket size
-XGMI2_AUTO_MAX_BYTES = 8 << 20  # ... and the two-shot kernel (4+ ranks) up to this one; RCCL beyond
 BUCKET_BYTES = 4 << 20         # dW1 all-reduce chunk of the overlapped RCCL backward
 
-# The cost model's planning constants (docs/PERFORMANCE.md "Communication policy"): one xGMI link per direction,
-# the fixed cost of one peer-kernel launch + hand-off (7.5 us measured with 2 ranks on one GPU), and RCCL's launch
-# + protocol cost.  Only the first multi-GPU run measures them: bench.py records the prediction
-# (allreduce_pred_us) beside the measured all-reduce (allreduce_us) so that run confirms or refutes them.
-XGMI_LINK_GBPS = 64.0
-XGMI_KERNEL_US = 7.5
-RCCL_FIXED_US = 25.0
+
+@dataclass
+class CostModel:
+    """The all-reduce policy's constants (docs/PERFORMANCE.md "Communication policy"): one xGMI link per direction
+    (GB/s), the fixed cost of one peer-kernel launch + hand-off (us), RCCL's fixed cost (us) and its ring's per-link
+    rate (GB/s).  The defaults are planning numbers (7.5 us is the one-shot kernel with 2 ranks sharing one GPU);
+    ``measure_cost_model`` replaces them with a micro-probe on the node (bench.py does at N > 1 and records them as
+    ``cost_model_measured``)."""
+
+    link_gbps: float = 64.0
+    kernel_us: float = 7.5
+    rccl_us: float = 25.0
+    rccl_gbps: float = 64.0
+    measured: bool = False
+
+    def as_record(self) -> dict:
+        return {"xgmi_link_GBps": round(self.link_gbps, 2), "xgmi_kernel_us": round(self.kernel_us, 2),
+                "rccl_fixed_us": round(self.rccl_us, 2), "rccl_link_GBps": round(self.rccl_gbps, 2),
+                "measured": self.measured}
 
 
-def allreduce_cost_us(R: int, wire_bytes: int, shots: int) -> float:
+COST_MODEL = CostModel()  # what the policy uses (set_cost_model replaces it)
+
+
+def set_cost_model(m: CostModel | None) -> None:
+    global COST_MODEL
+    COST_MODEL = m if m is not None else CostModel()
+
+
+def allreduce_cost_us(R: int, wire_bytes: int, shots: int, fp_bytes: int | None = None,
+                      model: CostModel | None = None) -> float:
     """Predicted time of one gradient all-reduce of ``wire_bytes`` over R ranks of one node: shots 1 = the xGMI
     one-shot kernel (L + S / B: every rank pulls the R - 1 peer buckets over R - 1 links at once), 2 = the
-    two-shot kernel (2 L + 2 S / (R B)), 0 = an RCCL ring (L_rccl + 2 S / (R B), before any overlap)."""
+    two-shot kernel (2 L + 2 S / (R B)), 0 = the RCCL path (L_rccl + 2 S / (R B_rccl) on the fp32 bucket
+    ``fp_bytes``, minus what the bucketed backward hides behind the dW1 GEMM: up to L_rccl once the gradient
+    spans more than one BUCKET_BYTES chunk -- a one-bucket gradient goes after the whole weight-gradient launch)."""
     if R <= 1:
         return 0.0
-    bw = XGMI_LINK_GBPS * 1e3  # bytes per us
+    m = model or COST_MODEL
+    bw = m.link_gbps * 1e3  # bytes per us
     if shots == 1:
-        return XGMI_KERNEL_US + wire_bytes / bw
+        return m.kernel_us + wire_bytes / bw
     if shots == 2:
-        return 2 * XGMI_KERNEL_US + 2 * wire_bytes / (R * bw)
-    return RCCL_FIXED_US + 2 * wire_bytes / (R * bw)
+        return 2 * m.kernel_us + 2 * wire_bytes / (R * bw)
+    fb = wire_bytes if fp_bytes is None else fp_bytes
+    ring = 2 * fb / (R * m.rccl_gbps * 1e3)
+    hidden = min(m.rccl_us, ring) if fb > BUCKET_BYTES else 0.0
+    return m.rccl_us + ring - hidden
 
 
-def auto_allreduce_shots(R: int, wire_bytes: int, fp_bytes: int, bf16_wire: bool) -> int:
-    """allreduce="auto" on one node: 1 = the xGMI one-shot kernel, 2 = the two-shot kernel, 0 = RCCL.
+def auto_allreduce_shots(R: int, wire_bytes: int, fp_bytes: int, bf16_wire: bool,
+                         model: CostModel | None = None) -> int:
+    """allreduce="auto" on one node: 1 = the xGMI one-shot kernel, 2 = the two-shot kernel, 0 = RCCL -- the
+    candidate with the least predicted time (allreduce_cost_us).  The two-shot moves the exact gradient only (not
+    the bf16 wire); RCCL always reduces the fp32 bucket.  With the planning constants: latency-bound buckets
+    (318 KB at H = 100) take the one-shot at any R, 784-1024-10's 3.3 MB the one-shot at R = 2 (the two-shot and
+    the ring move S per link there too) and the two-shot from R = 3, 784-4096-10's 13 MB the bucketed RCCL
+    backward, whose ring hides behind the dW1 GEMM."""
+    cands = {1: allreduce_cost_us(R, wire_bytes, 1, model=model),
+             0: allreduce_cost_us(R, wire_bytes, 0, fp_bytes=fp_bytes, model=model)}
+    if R >= 3 and not bf16_wire:
+        cands[2] = allreduce_cost_us(R, wire_bytes, 2, model=model)
+    return min(cands, key=lambda k: (cands[k], k))
 
-    Cost model (docs/PERFORMANCE.md "Communication policy"; B = one xGMI link, L = one kernel's fixed cost):
-    one-shot L + S / B (every rank pulls the R - 1 peer buckets over R - 1 links in parallel), two-shot
-    2 L + 2 S / (R B) (reduce-scatter + all-gather, 2 S / R per link), an RCCL ring L_rccl + 2 S / (R B) at best
-    but overlappable with the dW1 GEMM.  Latency-bound buckets (<= 2 MB: 318 KB at H = 100) take the one-shot.
-    At R = 2 the two-shot and the ring move S per link too, so the one-shot stays up to 8 MB (784-1024-10's
-    3.3 MB at N = 2).  From R = 3 the two-shot cuts the bytes per link to 2 S / R, up to 8 MB of fp32.  Past
-    that (784-4096-10: 13 MB) the bucketed RCCL backward, whose ring hides behind the dW1 GEMM."""
-    if wire_bytes <= XGMI_AUTO_MAX_BYTES:
-        return 1
-    if R == 2 and wire_bytes <= XGMI2_AUTO_MAX_BYTES:
-        return 1
-    if R >= 3 and not bf16_wire and fp_bytes <= XGMI2_AUTO_MAX_BYTES:
-        return 2
-    return 0
+
+def measure_cost_model(comm, device, small: int = 1024, large: int = 1 << 20, iters: int = 10) -> CostModel | None:
+    """Collective micro-probe of the cost model's constants on this node (~1-2 s): the xGMI one-shot all-reduce and
+    the communicator's (RCCL) all-reduce, each at ``small`` and ``large`` fp32 elements, max over ranks.  The small
+    bucket's time is the fixed cost; the slope is the per-link rate (one-shot: t = L + S / B; ring:
+    t = L + 2 (R - 1) / R S / B).  None where there is nothing to measure (one rank, no GPU, not a torch.distributed
+    group); an xGMI bucket the node cannot open leaves the planning constants for the xGMI terms."""
+    from .comm import TorchDistComm
+
+    R = comm.world_size
+    dev = torch.device(device)
+    if R <= 1 or dev.type != "cuda" or not isinstance(comm, TorchDistComm):
+        return None
+
+    def timed(fn) -> float:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(dev)
+        comm.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize(dev)
+        return comm.allreduce_scalar(1e6 * (time.perf_counter() - t0) / iters, op="max")
+
+    m = CostModel(measured=True)
+    t = {}
+    for numel in (small, large):
+        buf = torch.zeros(numel, dtype=torch.float32, device=dev)
+        t[("rccl", numel)] = timed(lambda: comm.allreduce_(buf))
+    ds = 4 * (large - small)
+    m.rccl_us = t[("rccl", small)]
+    m.rccl_gbps = 2 * (R - 1) / R * ds / max(t[("rccl", large)] - t[("rccl", small)], 1e-3) / 1e3
+    from .xgmi import XgmiBucket
+
+    try:
+        for numel in (small, large):
+            xb = XgmiBucket(comm.group, comm.rank, R, numel, torch.float32, dev, self_test=False)
+            buf = torch.zeros(numel, dtype=torch.float32, device=dev)
+            try:
+                t[("xgmi", numel)] = timed(lambda: xb.allreduce_(buf))
+            finally:
+                xb.close()
+        m.kernel_us = t[("xgmi", small)]
+        m.link_gbps = ds / max(t[("xgmi", large)] - t[("xgmi", small)], 1e-3) / 1e3
+    except RuntimeError:  # IPC unavailable: raised on every rank together (XgmiBucket's collective setup)
+        pass
+    return m
 
 
 class FaultInjected(RuntimeError):

@@ -212,7 +212,11 @@ struct MlpStep {
       cme::SplitStepArgs a = split_args(off, n, scale, reg, lr, sgd == 2 ? 0 : sgd, with_loss);
       // the next step's first sample (the native step loop knows it): its pixels are prefetched by this step's
       // weight-gradient launch (SplitStepArgs::pf_X)
-      if (pf_next >= 0 && a.pf_wgs) a.pf_X = reinterpret_cast<const char*>(X) + (size_t)pf_next * P;
+      // (only the rows that exist: the next step's shard may be shorter than this one, or past the dataset's end)
+      if (pf_next >= 0 && pf_next < N && a.pf_wgs) {
+        a.pf_X = reinterpret_cast<const char*>(X) + (size_t)pf_next * P;
+        a.pf_bytes = std::min<int64_t>(n, N - pf_next) * P;
+      }
       if (sgd == 2) {  // all-reduce + SGD inside the wgrad launch
         CME_REQUIRE(xf.world > 0, "MlpStep.run(sgd=2): set_xgmi() first");
         a.xf = xf;

@@ -124,6 +124,7 @@ struct SplitStepArgs {
   int pf_wgs = 0;     // ... in the weight-gradient launch (the next step's X)
   int pf_wgs_xt = 0;  // ... in the forward + head launch (this step's XT)
   const void* pf_X = nullptr;
+  int64_t pf_bytes = 0;  // bytes of pf_X to pull: the next step's rows that exist (a partial last batch is shorter)
 };
 
 

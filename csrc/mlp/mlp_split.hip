@@ -247,8 +247,8 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   if (a.pf_wgs && (int)blockIdx.x >= (int)gridDim.x - 8 * a.pf_wgs) {  // a prefetch workgroup (SplitStepArgs::pf_wgs):
     // the next step's X into the L2 of an XCD whose forward row tile reads all of it next
     const int xcd = blockIdx.x & 7, part = ((int)blockIdx.x - ((int)gridDim.x - 8 * a.pf_wgs)) >> 3;
-    if (a.pf_X && xcd < (a.H + 15) / 16)
-      l2_touch(a.pf_X, 0, 1, 0, (int64_t)a.n * a.P, part, a.pf_wgs, reinterpret_cast<char*>(red));
+    if (a.pf_X && a.pf_bytes > 0 && xcd < (a.H + 15) / 16)
+      l2_touch(a.pf_X, 0, 1, 0, a.pf_bytes, part, a.pf_wgs, reinterpret_cast<char*>(red));
     return;
   }
   // logical workgroup id: dW1 tiles [0, t1) row-major, then the roles.  xcd_rows: the first 8 * t1n blocks are the
