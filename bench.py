@@ -507,7 +507,7 @@ def _mode_of(impl: str, ctx) -> str:
     """The --allreduce value that reproduces an implementation name (for the secondary run)."""
     if ctx.R == 1:
         return "auto"
-    return {"xgmi": "xgmi", "xgmi-fused": "xgmi", "xgmi-2shot": "xgmi2", "xgmi-bf16wire": "xgmi",
+    return {"xgmi": "xgmi", "xgmi-fused": "xgmi", "xgmi-push": "xgmi", "xgmi-2shot": "xgmi2", "xgmi-bf16wire": "xgmi",
             "host-gloo": "host"}.get(impl, "rccl")
 
 

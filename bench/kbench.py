@@ -164,6 +164,20 @@ def main(argv=None):
                     row["xgmi1_err"] = xc.error()
                     e.attach_xgmi(None)
                     xc.close()
+                    # the owner-tile push form at world 1 (XgmiFuse::push): this rank owns every tile, nothing leaves
+                    # the workgroup -- what is left is the LDS staging of the gradient tile
+                    xp = _hip().comm.XgmiComm(0, 1, e.params.numel(), 4, slots, slots)
+
+                    class _P:
+                        c = xp
+
+                    e.attach_xgmi(_P, push=True)
+                    row["wgrad_push1_us"] = round(timeit(part(2, 2), a.reps), 3)
+                    row["step_push1_us"] = round(timeit(part(3, 2), a.reps), 3)
+                    torch.cuda.synchronize()
+                    row["push1_err"] = xp.error()
+                    e.attach_xgmi(None)
+                    xp.close()
                 flops = 2 * n * (784 * H * 2 + 10 * H * 3)
                 row["step_tflops"] = round(flops / (row["step_fused_us"] * 1e-6) / 1e12, 3)
                 print(json.dumps(row), flush=True)

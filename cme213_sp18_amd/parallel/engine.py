@@ -398,16 +398,20 @@ class MlpEngine:
             return 0
         return max(0, int(hip().mlp_split_fused_tiles(self.P, self.H, 1 << 30)))
 
-    def attach_xgmi(self, bucket) -> None:
+    def attach_xgmi(self, bucket, push: bool = False) -> None:
         """Bind an open XgmiBucket (created with flag_slots >= fused_allreduce_slots()) to the step;
-        ``None`` detaches.  run(..., sgd=2) then all-reduces and applies SGD inside the wgrad launch."""
+        ``None`` detaches.  run(..., sgd=2) then all-reduces and applies SGD inside the wgrad launch: the one-shot
+        pull (every rank reads every peer's tile), or with ``push`` the owner-tile form (XgmiFuse::push: tile t
+        reduced and applied by rank t % world, pushed both ways as tagged granules; the bucket needs
+        slab_tiles >= fused_allreduce_slots())."""
         if bucket is None:
             self._xgmi_fuse = None
             if self._step is not None:
                 self._step.set_xgmi(0, 0, 0, 0, 0)
             return
         o = self.layout.offsets
-        self._xgmi_fuse = (int(bucket.c.desc_address), int(bucket.c.nblocks), int(o[1]), int(o[2]), int(o[3]))
+        self._xgmi_fuse = (int(bucket.c.desc_address), int(bucket.c.nblocks), int(o[1]), int(o[2]), int(o[3]),
+                           int(bool(push)))
         self._hip_step().set_xgmi(*self._xgmi_fuse)
 
     def run(self, off: int, n: int, scale: float, reg: float, lr: float, sgd, with_loss: bool = False,

@@ -184,7 +184,7 @@ class DataParallelTrainer:
                  batch_size: int = 800, backend: str = "hip", shift: bool = True, use_graphs: bool = True,
                  normalize: bool = False, path: str = "auto", allreduce: str = "auto", overlap: bool = True,
                  overlap_chunks: int = 0, fuse_allreduce: bool = True, executor: str = "auto",
-                 grad_wire: str = "auto"):
+                 grad_wire: str = "auto", fused_form: str = "push"):
         self.nn = nn
         # how run_plan enqueues a plan: "auto" = the native C++ step loop (MlpStep.run_steps) for plans of
         # consecutive full batches on the fused paths (pure device work), else the captured HIP graph;
@@ -199,6 +199,12 @@ class DataParallelTrainer:
         if grad_wire not in ("auto", "f32", "bf16"):
             raise ValueError("grad_wire must be auto, f32 or bf16")
         self.grad_wire = grad_wire
+        # the all-reduce fused into the weight-gradient launch (H <= 128): "push" = the owner-tile form (each tile
+        # reduced by one rank, pushed both ways as tagged granules: 2 one-way hops, 2 S / R payload per link),
+        # "pull" = the one-shot (every rank reads every peer's tile after its flag: S per link)
+        if fused_form not in ("push", "pull"):
+            raise ValueError("fused_form must be push or pull")
+        self.fused_form = fused_form
         # RCCL path: dW1 row chunks all-reduced while the next chunk is computed (0: ~BUCKET_BYTES each).
         # Setting it also forces the overlapped path with ONE rank of a real process group (nccl world 1),
         # so a one-GPU box exercises the side-stream + graph-captured backward.
@@ -249,7 +255,8 @@ class DataParallelTrainer:
 
                 try:
                     xb = XgmiBucket(self.comm.group, self.rank, self.R, self.engine.params.numel(),
-                                    torch.float32, self.engine.device, flag_slots=slots)
+                                    torch.float32, self.engine.device, flag_slots=slots,
+                                    slab_tiles=slots if self.fused_form == "push" else 0)
                     if xb.ok:
                         self._xgmi_fused = xb
                     else:
@@ -452,7 +459,8 @@ class DataParallelTrainer:
         self._graphs.clear()
         if self._xgmi_fused is not None:
             self.fused_allreduce = self._check_fused()
-            self.allreduce_impl = "xgmi-fused" if self.fused_allreduce else "xgmi"
+            self.allreduce_impl = ("xgmi-push" if self.fused_form == "push" else "xgmi-fused") \
+                if self.fused_allreduce else "xgmi"
 
     def _check_fused(self) -> bool:
         """One step from the same state through both all-reduce paths (separate xGMI kernel, and
@@ -474,7 +482,7 @@ class DataParallelTrainer:
         self._restore(snap)
         ok = True
         try:
-            e.attach_xgmi(self._xgmi_fused)
+            e.attach_xgmi(self._xgmi_fused, push=self.fused_form == "push")
             for _ in range(3):  # both buffer halves, and back to the first
                 self._restore(snap)
                 e.run(off, n, scale, reg, lr, sgd=2)

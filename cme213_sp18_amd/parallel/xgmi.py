@@ -36,12 +36,14 @@ class XgmiBucket:
     MODE_ALLREDUCE2 = 3
 
     def __init__(self, group, rank: int, world: int, numel: int, dtype: torch.dtype, device, self_test: bool = True,
-                 flag_slots: int = 0, wire: torch.dtype | None = None, shots: int = 1):
+                 flag_slots: int = 0, wire: torch.dtype | None = None, shots: int = 1, slab_tiles: int = 0):
         """wire: the element type in the IPC buffers -- ``dtype`` (default), or torch.bfloat16 for float32
         gradients (half the bytes over xGMI; every rank sums the R bf16 values in fp32, in rank order).
         shots: 1 = one-shot (every rank pulls every peer's whole bucket: S bytes per link), 2 = two-shot
         (reduce-scatter + sharded update + all-gather over peer reads: 2 S / R bytes per link, one more
-        round trip; exact wire only).  A bucket keeps one form: their epochs and flags differ."""
+        round trip; exact wire only).  A bucket keeps one form: their epochs and flags differ.
+        slab_tiles: receive areas for the owner-tile push form of the all-reduce fused into the weight-gradient
+        launch (one slot set per launch tile; MlpEngine.attach_xgmi(push=True)), 0: none."""
         import torch.distributed as dist
 
         if world > hip().comm.MAX_RANKS:
@@ -54,6 +56,7 @@ class XgmiBucket:
         if shots not in (1, 2) or (shots == 2 and wire != dtype):
             raise ValueError("xGMI bucket: shots 1, or 2 with the exact wire")
         self.shots = shots
+        self.slab_tiles = int(slab_tiles)
         self.rank, self.world, self.numel, self.dtype, self.wire = rank, world, int(numel), dtype, wire
         self.group = group
         self.device = torch.device(device)
@@ -65,7 +68,7 @@ class XgmiBucket:
             # IPC failure makes ALL ranks give up together instead of leaving peers in a collective
             mine, err = None, None
             try:
-                self.c = hip().comm.XgmiComm(rank, world, self.numel, elt, int(flag_slots))
+                self.c = hip().comm.XgmiComm(rank, world, self.numel, elt, int(flag_slots), self.slab_tiles)
                 mine = self.c.handles()
             except Exception as ex:  # noqa: BLE001 - reported collectively below
                 err = f"rank {rank}: {ex}"

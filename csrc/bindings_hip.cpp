@@ -47,6 +47,7 @@ struct MlpStep {
   int split = 0, npw = 3, npz = 3;
   uintptr_t stamps = 0;  // diagnostics only
   uintptr_t hstamps = 0;  // diagnostics only: head-block stamps
+  uintptr_t wstamps = 0;  // diagnostics only: weight-gradient workgroup stamps (SplitStepArgs::wstamps)
   uintptr_t z2p = 0;     // wide-layer head scratch (head_big_scratch_floats), 0: column head
   uintptr_t dw2p = 0;    // wide layers: dW2 partials [cdiv(ld, 32)][16][H] left by the head (0: the dW2 GEMM)
   int bias_col = 0;      // XT has an all-ones feature row P: db1 comes out of the dW1 GEMM
@@ -86,7 +87,8 @@ struct MlpStep {
   int ag64() const { return ag_tiles64 >= 0 ? ag_tiles64 : (store_a1 ? 0 : 1); }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
-  void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2) {
+  // push != 0: the owner-tile push form (XgmiFuse::push; the bucket must have slab_tiles >= the launch's tiles)
+  void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2, int push = 0) {
     if (!desc) {
       xf = cme::XgmiFuse{};
       return;
@@ -113,6 +115,17 @@ struct MlpStep {
     f.off_b1 = off_b1;
     f.off_W2 = off_W2;
     f.off_b2 = off_b2;
+    if (push) {
+      CME_REQUIRE(d->myslab && d->slab_tiles >= cme::mlp_split_fused_tiles(P, H, 1 << 30),
+                  "MlpStep.set_xgmi(push): the bucket's receive areas are missing or smaller than the launch's tiles");
+      f.push = 1;
+      f.myslab = d->myslab;
+      f.slab_tiles = d->slab_tiles;
+      for (int r = 0; r < d->world; ++r) {
+        CME_REQUIRE(d->peerslabs[r], "MlpStep.set_xgmi(push): peer receive areas not mapped");
+        f.peerslab[r] = d->peerslabs[r];
+      }
+    }
     xf = f;
   }
   float xscale = 1.f;    // split path: inputs are uint8 * xscale
@@ -179,6 +192,7 @@ struct MlpStep {
     a.loss_partial = with_loss ? P_<float>(loss) : nullptr;
     a.scale = scale; a.reg = reg; a.lr = lr; a.sgd = sgd; a.shift = shift; a.mode = 0;
     a.stamps = reinterpret_cast<unsigned long long*>(stamps);
+    a.wstamps = reinterpret_cast<unsigned long long*>(wstamps);
     a.bias_col = bias_col;
     // split3 small layers, measured (bench/kbench.py): fp32 W1 split in registers always (one split per weight
     // per column tile is cheaper than pulling 6 B); fp32 dZ1 only above H = 128, where the separate head's plane
@@ -502,6 +516,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("dw2p", &MlpStep::dw2p)
       .def_readwrite("stamps", &MlpStep::stamps)
       .def_readwrite("hstamps", &MlpStep::hstamps)
+      .def_readwrite("wstamps", &MlpStep::wstamps)
       .def("refresh_planes", &MlpStep::refresh_planes, py::arg("stream"))
       .def("w1_planes_read",
            [](const MlpStep& st) {  // a forward kernel of this step reads the W1 planes (else: not refreshed)
@@ -517,7 +532,8 @@ PYBIND11_MODULE(_hip, m) {
       .def("tp_forward", &MlpStep::tp_forward)
       .def("tp_head", &MlpStep::tp_head)
       .def("set_xgmi", &MlpStep::set_xgmi, py::arg("desc"), py::arg("slots"), py::arg("off_b1"), py::arg("off_W2"),
-           py::arg("off_b2"))
+           py::arg("off_b2"), py::arg("push") = 0)
+      .def_property_readonly("xgmi_push", [](const MlpStep& st) { return st.xf.push; })
       .def("run_steps", &MlpStep::run_steps, py::arg("gstart0"), py::arg("count"), py::arg("B"), py::arg("shard_off"),
            py::arg("n"), py::arg("N_end"), py::arg("scale"), py::arg("reg"), py::arg("lr"), py::arg("sgd"),
            py::arg("stream"),

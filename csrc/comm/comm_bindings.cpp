@@ -88,7 +88,8 @@ class XgmiComm {
  public:
   // flag_slots: minimum number of [kMaxRanks]-word flag rows (a kernel that signals per workgroup tile
   // -- the wgrad launch with the all-reduce fused in -- needs one per tile; default one per chunk)
-  XgmiComm(int rank, int world, int64_t n, int elt_bytes, int64_t flag_slots = 0) {
+  // slab_tiles: tiles of the owner-tile push form's receive areas (0: none; XgmiDesc::myslab)
+  XgmiComm(int rank, int world, int64_t n, int elt_bytes, int64_t flag_slots = 0, int64_t slab_tiles = 0) {
     CME_REQUIRE(world >= 1 && world <= kMaxRanks, "XgmiComm: 1 <= world <= 8");
     CME_REQUIRE(rank >= 0 && rank < world, "XgmiComm: bad rank");
     CME_REQUIRE(elt_bytes == 2 || elt_bytes == 4 || elt_bytes == 8, "XgmiComm: bf16 wire, f32 or f64");
@@ -102,14 +103,19 @@ class XgmiComm {
     // IPC handle.  Rounded to 2 MiB so the runtime never sub-allocates it (hipIpcGetMemHandle rejects
     // sub-allocated pointers); fine-grained device memory (IpcPool::fine_grained; hipDeviceMallocUncached
     // pages did not export reliably), with every flag access a system-scope atomic.
+    CME_REQUIRE(slab_tiles >= 0, "XgmiComm: slab_tiles >= 0");
     flags_off_ = (2 * d_.npad * elt_bytes + 4095) / 4096 * 4096;
-    sig_off_ = flags_off_ + (flag_bytes() + 4095) / 4096 * 4096;
+    slab_off_ = flags_off_ + (flag_bytes() + 4095) / 4096 * 4096;
+    const size_t slab_bytes = (size_t)slab_tiles * (kMaxRanks + 1) * kSlabTile * sizeof(unsigned long long);
+    sig_off_ = slab_off_ + (slab_bytes + 4095) / 4096 * 4096;
     d_.mybuf = ipc_pool().take(round_alloc(sig_off_ + sizeof(Signature)), &alloc_bytes_);
     HIP_CHECK(hipMemset(d_.mybuf, 0, alloc_bytes_));
     std::random_device rd;
     sig_ = Signature{kSigMagic, (uint64_t)rank, ((uint64_t)rd() << 32) ^ rd(), alloc_bytes_};
     HIP_CHECK(hipMemcpy(static_cast<char*>(d_.mybuf) + sig_off_, &sig_, sizeof(sig_), hipMemcpyHostToDevice));
     d_.myflags = reinterpret_cast<uint32_t*>(static_cast<char*>(d_.mybuf) + flags_off_);
+    d_.slab_tiles = slab_tiles;
+    if (slab_tiles) d_.myslab = reinterpret_cast<unsigned long long*>(static_cast<char*>(d_.mybuf) + slab_off_);
     HIP_CHECK(hipMalloc(&d_.epochs, nblocks_ * sizeof(uint32_t)));
     HIP_CHECK(hipMemset(d_.epochs, 0, nblocks_ * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&d_.err, sizeof(int)));
@@ -117,6 +123,7 @@ class XgmiComm {
     HIP_CHECK(hipDeviceSynchronize());
     d_.peers[rank] = d_.mybuf;
     d_.peerflags[rank] = d_.myflags;
+    d_.peerslabs[rank] = d_.myslab;
   }
   ~XgmiComm() { close(); }
 
@@ -133,6 +140,8 @@ class XgmiComm {
       d_.peers[r] = open_handle(all[r].first);
       opened_.push_back(d_.peers[r]);
       d_.peerflags[r] = reinterpret_cast<uint32_t*>(static_cast<char*>(d_.peers[r]) + flags_off_);
+      if (d_.slab_tiles)
+        d_.peerslabs[r] = reinterpret_cast<unsigned long long*>(static_cast<char*>(d_.peers[r]) + slab_off_);
       // the mapping must show THAT rank's buffer (its signature, written at its construction)
       CME_REQUIRE(all[r].second.size() == sizeof(Signature), "XgmiComm.open: bad signature size");
       Signature want, seen;
@@ -175,6 +184,7 @@ class XgmiComm {
       if (r != d_.rank) {
         d_.peers[r] = nullptr;
         d_.peerflags[r] = nullptr;
+        d_.peerslabs[r] = nullptr;
       }
     ready_ = false;
   }
@@ -206,7 +216,8 @@ class XgmiComm {
   XgmiDesc d_;
   int64_t nblocks_ = 0;
   int elt_ = 4;  // wire element bytes: 2 (bf16), 4 (f32), 8 (f64)
-  size_t flags_off_ = 0, sig_off_ = 0, alloc_bytes_ = 0;
+  static constexpr int kSlabTile = 512;  // granules per tile slot (mlp_split.hip kXpTile)
+  size_t flags_off_ = 0, slab_off_ = 0, sig_off_ = 0, alloc_bytes_ = 0;
   Signature sig_{};
   bool ready_ = false;
   std::vector<void*> opened_;
@@ -220,8 +231,8 @@ void bind_comm(py::module_& m) {
   using cme::comm::XgmiComm;
   auto sm = m.def_submodule("comm", "xGMI peer-to-peer all-reduce (IPC buffers, SGD fused)");
   py::class_<XgmiComm>(sm, "XgmiComm")
-      .def(py::init<int, int, int64_t, int, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("n"),
-           py::arg("elt_bytes"), py::arg("flag_slots") = 0)
+      .def(py::init<int, int, int64_t, int, int64_t, int64_t>(), py::arg("rank"), py::arg("world"), py::arg("n"),
+           py::arg("elt_bytes"), py::arg("flag_slots") = 0, py::arg("slab_tiles") = 0)
       .def("handles", &XgmiComm::handles)
       .def("open", &XgmiComm::open)
       .def("run", &XgmiComm::run, py::arg("dtype"), py::arg("grads"), py::arg("params"), py::arg("lr"),

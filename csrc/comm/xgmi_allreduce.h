@@ -29,6 +29,11 @@ struct XgmiDesc {
   uint32_t* peerflags[kMaxRanks] = {};
   uint32_t* epochs = nullptr;         // [nblocks] local
   int* err = nullptr;                 // set to 1 when a wait timed out
+  // the owner-tile push form's receive areas (XgmiFuse::push), [slab_tiles][8 + 1][512] 8-byte granules inside
+  // every rank's IPC allocation; slab_tiles == 0: none
+  unsigned long long* myslab = nullptr;
+  unsigned long long* peerslabs[kMaxRanks] = {};
+  int64_t slab_tiles = 0;
 };
 
 int64_t xgmi_padded_count(int64_t n);

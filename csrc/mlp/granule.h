@@ -37,6 +37,18 @@ __device__ __forceinline__ gran_t gran_load(const gran_t* p) {  // sc1 load (L2-
   return __hip_atomic_load(const_cast<gran_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The same granules across GPUs (the xGMI owner-tile exchange, mlp_split.hip xp_*): ONE 8-byte system-scope
+// store (sc0 sc1, write-through to the IPC-mapped fine-grained buffer of a peer, or of this rank) and a
+// system-coherent load -- the peer's store reaches memory as one 8-byte write, so a load that sees the tag sees
+// the value.
+__device__ __forceinline__ void gran_store_sys(gran_t* p, float v, unsigned ep) {
+  __hip_atomic_store(p, ((gran_t)ep << 32) | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ gran_t gran_load_sys(const gran_t* p) {
+  return __hip_atomic_load(const_cast<gran_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Poll the granules base[off + k * stride] (k < cnt <= N; lanes with !need take no part) until every tag is
 // `ep`, then hand the values to f(k, value) in k order (0 for k >= cnt).  The N addresses are formed once,
 // before the poll loop; a pass is N back-to-back global_load_dwordx2 sc1 and one wait.  Wave-uniform; false

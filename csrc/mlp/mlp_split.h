@@ -41,6 +41,17 @@ struct XgmiFuse {
   int rank = 0, world = 0;
   int64_t npad = 0;
   int64_t off_b1 = 0, off_W2 = 0, off_b2 = 0;  // flat-arena offsets ([W1|b1|W2|b2], 64-aligned)
+  // Owner-tile push form (push != 0; XgmiComm created with slab_tiles >= the launch's tiles): gradient tile t is
+  // reduced and applied by rank t % world alone.  Every other rank PUSHES its tile there as system-scope data-tagged
+  // granules (one 8-byte {value, epoch} store each, into the owner's receive area), the owner polls its OWN memory,
+  // sums the R tiles in rank order (its own from LDS: the one-shot's bits), applies the update and pushes the new
+  // values back the same way.  Two one-way hops per tile, 2 S / R payload bytes per link (x2 for the tags), no
+  // write-through drain, no flag, no remote read; at world 1 nothing leaves the workgroup.  Receive areas, in
+  // every rank's IPC buffer: [slab_tiles][8][512] gradient granules, then [slab_tiles][512] result granules.
+  int push = 0;
+  unsigned long long* myslab = nullptr;
+  unsigned long long* peerslab[8] = {};
+  int64_t slab_tiles = 0;
 };
 
 struct SplitStepArgs {
@@ -64,6 +75,9 @@ struct SplitStepArgs {
   float* probs = nullptr;
   int ldp = 0;
   unsigned long long* stamps = nullptr;  // diagnostics: per-wave s_memrealtime stamps (see mma_tile.h)
+  // diagnostics: per-workgroup stamps of the small weight-gradient launch (thread 0: entry, tile + epilogue done,
+  // exchange done, end; [blockIdx][4]) -- bench/stamps_push.py
+  unsigned long long* wstamps = nullptr;
   // weight-gradient launch selection (bucketed all-reduce overlap): wg_parts bit0 = dW1 rows
   // [w1_row0, w1_row0 + w1_rows) (w1_rows < 0: all), bit1 = dW2 + bias gradients
   int wg_parts = 3, w1_row0 = 0, w1_rows = -1;

@@ -147,6 +147,90 @@ __device__ __forceinline__ void xf_end(const XgmiFuse& x, int tile, const uint32
   if (threadIdx.x == 0) x.epochs[tile] = s_xf[0];
 }
 
+// ---- the owner-tile push form (XgmiFuse::push) ------------------------------------------------------------
+constexpr int kXpTile = 512;  // granule slots per tile (a dW1 tile is 16 x 32; a dW2 tile 16 x 16 + C)
+
+__device__ __forceinline__ gran_t* xp_grad_slot(gran_t* slab, int tile, int src) {
+  return slab + ((size_t)tile * 8 + src) * kXpTile;
+}
+__device__ __forceinline__ gran_t* xp_result_slot(const XgmiFuse& x, gran_t* slab, int tile) {
+  return slab + ((size_t)x.slab_tiles * 8 + tile) * kXpTile;
+}
+
+// Bounded poll of the granules p[k] with bit k of `need` set until each carries tag ep (system-coherent loads of
+// this rank's own receive area); v[k] = their values.  Wave-uniform; false once the wait outlasts the peer bound.
+template <int N>
+__device__ __forceinline__ bool xp_poll(const gran_t* const (&p)[N], unsigned need, unsigned ep, float (&v)[N]) {
+  constexpr unsigned kAll = (1u << N) - 1u;
+  unsigned rdy = ~need & kAll;
+  gran_t g[N];
+  const uint64_t t0 = wall_ticks();
+  for (uint32_t pass = 1;; ++pass) {
+    if (rdy != kAll) {
+#pragma unroll
+      for (int k = 0; k < N; ++k)
+        if (!(rdy & (1u << k))) g[k] = gran_load_sys(p[k]);
+#pragma unroll
+      for (int k = 0; k < N; ++k)
+        if (!(rdy & (1u << k))) rdy |= (unsigned)((unsigned)(g[k] >> 32) == ep) << k;
+    }
+    if (__all(rdy == kAll)) break;
+    if ((pass & 7) == 0 && wall_ticks() - t0 > kXfWaitTicks) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = (need & (1u << k)) ? __builtin_bit_cast(float, (unsigned)g[k]) : 0.f;
+  return true;
+}
+
+// One tile through the owner-tile exchange.  Thread e < ne holds tile element e; xs[e] (LDS, complete) is this
+// rank's gradient of it and `old` (owner only, loaded by the caller before the exchange) its current value.
+// Returns true (block-uniform) with *nv the element's new value -- the owner's old - lr * (rank-order sum), the
+// one-shot's expression, so both forms leave the same bits -- or false when a wait timed out (err set; the
+// caller applies nothing, and a non-owner that times out never hears of it: its owner's wait times out too).
+__device__ __forceinline__ bool xp_exchange(const XgmiFuse& x, int tile, uint32_t* s_xf, const float* xs, int ne,
+                                            bool valid, float old, float lr, float* nv) {
+  const unsigned ep = s_xf[0];
+  const int owner = tile % x.world, e = threadIdx.x;
+  const bool mine = valid && e < ne;
+  bool ok;
+  if (x.rank != owner) {
+    if (mine) gran_store_sys(xp_grad_slot(x.peerslab[owner], tile, x.rank) + e, xs[e], ep);
+    const gran_t* p[1] = {xp_result_slot(x, x.myslab, tile) + (mine ? e : 0)};
+    float v[1];
+    ok = xp_poll<1>(p, mine ? 1u : 0u, ep, v);
+    *nv = v[0];
+  } else {
+    const gran_t* p[8];
+    unsigned need = 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const bool want = mine && r < x.world && r != x.rank;
+      p[r] = xp_grad_slot(x.myslab, tile, want ? r : 0) + (mine ? e : 0);
+      need |= (unsigned)want << r;
+    }
+    float v[8];
+    ok = xp_poll<8>(p, need, ep, v);
+    if (ok && mine) {
+      const float own = xs[e];
+      float sum = x.rank == 0 ? own : v[0];
+      for (int r = 1; r < x.world; ++r) sum += r == x.rank ? own : v[r];
+      *nv = old - lr * sum;
+    }
+  }
+  if (!ok && (e & 63) == 0) {
+    atomicExch(x.err, 1);
+    s_xf[1] = 1;
+  }
+  __syncthreads();
+  if (s_xf[1]) return false;
+  if (x.rank == owner && mine) {  // the update to every other rank
+    for (int r = 0; r < x.world; ++r)
+      if (r != x.rank) gran_store_sys(xp_result_slot(x, x.peerslab[r], tile) + e, *nv, ep);
+  }
+  return true;
+}
+
 // ======================================================================
 // Kernel B: dW1 (MFMA over dZ1 planes x X^T) + fused reg/SGD/plane refresh,
 //           dW2 and bias gradients as extra workgroup roles.
@@ -179,15 +263,33 @@ struct EpiW2 {
   float pre[kEpiMaxQ];
   const int* ag_err;  // the step's forward timed out: no update (the gradient goes to gW2, unused)
   int perr = 0;
+  // sys == 2 (the push form): gradient / current weight into LDS xs / xo[class * 16 + column - n0]; the epoch and
+  // error words as in EpiW1
+  float *xs = nullptr, *xo = nullptr;
+  int n0 = 0;
+  const uint32_t* xep = nullptr;
+  const int* xerr = nullptr;
+  uint32_t ep0 = 0;
+  int xe = 0;
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
     pre[q] = buf_load1<float>(make_rsrc(W2), ok ? (row * H + col) * 4 : kOOB);
-    if (q == 0) perr = ag_err_load(ag_err);
+    if (q == 0) {
+      perr = ag_err_load(ag_err);
+      if (xep) {
+        ep0 = *xep;
+        xe = __hip_atomic_load(xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     const size_t i = (size_t)row * H + col;
     const float w = pre[q];
     const float g = v + reg * w;
     if (sgd && !poisoned(perr)) W2[i] = w - lr * g;
+    else if (sys == 2) {
+      xs[row * 16 + col - n0] = g;
+      xo[row * 16 + col - n0] = w;
+    }
     else if (sys) xf_store(gW2, (int64_t)i, g);
     else gW2[i] = g;
   }
@@ -206,17 +308,35 @@ struct EpiW1 {
   int sys;  // gradients into a peer-visible IPC buffer (write-through)
   const int* ag_err;  // the step's forward timed out: no update (the gradient goes to gW1, unused)
   int perr = 0;
+  // sys == 2 (the push form): the gradient into LDS xs[(row - m0) * 32 + col - n0] and the current weight (or b1)
+  // into xo; the tile's exchange epoch word and the bucket's error word are loaded with the other epilogue
+  // operands, before the K loop (xep, xerr -> ep0, xe), so the exchange starts with no memory round trip
+  float *xs = nullptr, *xo = nullptr;
+  int m0 = 0, n0 = 0;
+  const uint32_t* xep = nullptr;
+  const int* xerr = nullptr;
+  uint32_t ep0 = 0;
+  int xe = 0;
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
     // (the all-ones feature column P: b1[row], so its update is not a dependent load after the K loop)
     if (col == P) pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
     else pre[q] = buf_load1<float>(make_rsrc(W1), (ok && col < P) ? (row * P + col) * 4 : kOOB);
-    if (q == 0) perr = ag_err_load(ag_err);
+    if (q == 0) {
+      perr = ag_err_load(ag_err);
+      if (xep) {
+        ep0 = *xep;
+        xe = __hip_atomic_load(xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     const bool upd = sgd && !poisoned(perr);
     if (col == P) {  // the all-ones feature: db1[row] (no input scale, no regulariser)
       if (upd) b1[row] = pre[q] - lr * v;
-      else if (sys) xf_store(gb1, row, v);
+      else if (sys == 2) {
+        xs[(row - m0) * 32 + col - n0] = v;
+        xo[(row - m0) * 32 + col - n0] = pre[q];
+      } else if (sys) xf_store(gb1, row, v);
       else gb1[row] = v;
       return;
     }
@@ -228,6 +348,9 @@ struct EpiW1 {
       W1[i] = nw;
       if (npw == 3) split_store<3>(nw, W1p, plane, i);
       else if (npw == 1) split_store<1>(nw, W1p, plane, i);  // (0: no forward kernel reads the planes)
+    } else if (sys == 2) {
+      xs[(row - m0) * 32 + col - n0] = g;
+      xo[(row - m0) * 32 + col - n0] = w;
     } else if (sys) {
       xf_store(gW1, (int64_t)i, g);
     } else {
@@ -237,13 +360,20 @@ struct EpiW1 {
 };
 
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
-                                            uint32_t* s_xf);
+                                            uint32_t* s_xf, float* xs);
 
 // AF (split3): dZ1 read in fp32 and split into its exact planes in registers (the head then writes no planes)
 template <int NPZ, int VEC, bool AF>
 __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
   __shared__ uint32_t s_xf[2];
+  __shared__ float xsx[2 * kXpTile];  // the push form's staged gradient tile, then the current values
+  float *xs = xsx, *xo = xsx + kXpTile;
+  unsigned long long* wst = a.wstamps ? a.wstamps + (size_t)blockIdx.x * 4 : nullptr;  // diagnostics only
+  auto wstamp = [&](int i) {
+    if (wst && threadIdx.x == 0) wst[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  wstamp(0);
   if (a.pf_wgs && (int)blockIdx.x >= (int)gridDim.x - 8 * a.pf_wgs) {  // a prefetch workgroup (SplitStepArgs::pf_wgs):
     // the next step's X into the L2 of an XCD whose forward row tile reads all of it next
     const int xcd = blockIdx.x & 7, part = ((int)blockIdx.x - ((int)gridDim.x - 8 * a.pf_wgs)) >> 3;
@@ -269,14 +399,24 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
     TileGeom g{r1, a.P + a.bias_col, a.n, a.w1_row0 + (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
     float *gw = a.gW1, *gb = a.gb1;
-    // fused: gradients straight into this step's half of the IPC buffer (unless this rank is in error)
-    const bool live = fused && xf_begin(a.xf, bid, s_xf, a.ag_err);
+    // fused: gradients straight into this step's half of the IPC buffer (unless this rank is in error); the push
+    // form stages them in LDS and decides whether to take part after the K loop (its words are prefetched)
+    const bool push = fused && a.xf.push;
+    const bool live = fused && !push && xf_begin(a.xf, bid, s_xf, a.ag_err);
     if (live) {
       gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(s_xf[0] & 1u) * a.xf.npad;
       gb = gw + a.xf.off_b1;
     }
     EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.w1_planes ? a.npw : 0, reg, lr,
-              a.xscale, {}, a.b1, gb, live ? 1 : 0, a.ag_err};
+              a.xscale, {}, a.b1, gb, push ? 2 : (live ? 1 : 0), a.ag_err};
+    if (push) {
+      epi.xs = xs;
+      epi.xo = xo;
+      epi.m0 = g.m0;
+      epi.n0 = g.n0;
+      epi.xep = a.xf.epochs + bid;
+      epi.xerr = a.xf.err;
+    }
     constexpr int U = 4;
     if constexpr (AF)
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, 3, uint8_t>(a.dZ1, a.ld, static_cast<const uint8_t*>(a.XT),
@@ -285,7 +425,30 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
                                                                 static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
                                                                 red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
-    if (live && xf_exchange(a.xf, bid, s_xf)) {  // all-reduced with the peers: SGD + bf16 planes
+    wstamp(1);
+    if (push) {  // the owner-tile exchange: thread e holds element (e / 32, e % 32) of the tile
+      const int e = threadIdx.x, row = g.m0 + e / 32, col = g.n0 + e % 32;
+      const bool ok = e < 512 && row < g.M && col < g.N;
+      const int64_t i = (int64_t)row * a.P + col;
+      if (threadIdx.x == 0) {  // (thread 0's view of the words decides for the whole workgroup)
+        s_xf[0] = epi.ep0 + 1;
+        s_xf[1] = (epi.xe | epi.perr) != 0;
+      }
+      __syncthreads();  // xs / xo complete
+      float nv;
+      if (!s_xf[1] && xp_exchange(a.xf, bid, s_xf, xs, 512, ok, ok ? xo[e] : 0.f, lr, &nv) && ok) {
+        if (col < a.P) {
+          a.W1[i] = nv;
+          if (a.w1_planes) {
+            if (a.npw == 3) split_store<3>(nv, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
+            else split_store<1>(nv, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
+          }
+        } else {
+          a.b1[row] = nv;
+        }
+      }
+      if (!s_xf[1]) xf_end(a.xf, bid, s_xf);
+    } else if (live && xf_exchange(a.xf, bid, s_xf)) {  // all-reduced with the peers: SGD + bf16 planes
       const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf.npad;
       constexpr int TW = 16 * kWNB;
       for (int e = threadIdx.x; e < 16 * kWMB * TW; e += kWT) {
@@ -304,17 +467,27 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       }
       xf_end(a.xf, bid, s_xf);
     }
+    wstamp(2);
     mark_status(a, epi.perr);
+    if (wst) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      wstamp(3);
+    }
     return;
   }
-  wgrad_roles(a, bid, t1, t2, red, s_xf);
+  wgrad_roles(a, bid, t1, t2, red, s_xf, xs);
+  if (wst) {  // (no barrier: the roles' returns are not block-uniform)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wstamp(3);
+  }
 }
 
 // The weight-gradient launch's workgroups past its t1 dW1 tiles: t2 dW2 tiles (+ the fused xGMI exchange)
 // followed by the bias-row workgroups.  `red`: kWKS * 4 * 64 floats of LDS, `s_xf`: 2 words of LDS.
 // Shared by wgrad_split_kernel and the wide engines' launches (their extra workgroups).
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
-                                            uint32_t* s_xf) {
+                                            uint32_t* s_xf, float* xs) {
   const float reg = (float)a.reg, lr = (float)a.lr;
   const bool fused = a.xf.world > 0;
   const int lane = threadIdx.x & 63;
@@ -324,10 +497,20 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     const int tb = bid - t1;
     TileGeom g{a.C, a.H, a.n, 0, tb * 16};
     float* gw = a.gW2;
-    const bool live = fused && xf_begin(a.xf, bid, s_xf, a.ag_err);
-    const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf.npad;
-    if (live) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
-    EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, live ? 1 : 0, reg, lr, {}, a.ag_err};
+    const bool push = fused && a.xf.push;
+    const bool live = fused && (push || xf_begin(a.xf, bid, s_xf, a.ag_err));
+    const int64_t half = push ? 0 : (int64_t)(s_xf[0] & 1u) * a.xf.npad;
+    if (live && !push) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
+    EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, push ? 2 : (live ? 1 : 0), reg, lr, {}, a.ag_err};
+    float b2old = 0.f;  // (push, tile 0: b2 for the owner's update, loaded before the K loop)
+    if (push) {
+      epi.xs = xs;
+      epi.xo = xs + kXpTile;
+      epi.n0 = tb * 16;
+      epi.xep = a.xf.epochs + bid;
+      epi.xerr = a.xf.err;
+      if (tb == 0 && threadIdx.x >= 256 && threadIdx.x < 256 + a.C) b2old = a.b2[threadIdx.x - 256];
+    }
     if (a.dw2part) {  // the head's per-column-tile partials, summed in tile order (16 rows x C classes)
       const int nct = (a.n + a.dw2_cols - 1) / a.dw2_cols, e = threadIdx.x, c = e >> 4, h = tb * 16 + (e & 15);
       const bool ok = e < 256 && c < a.C && h < a.H;
@@ -353,8 +536,26 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     if (with_b2) {
       for (int c = wv; c < a.C; c += kWKS) {
         const float sc = wave_sum(row_sum(a.D + (size_t)c * a.ld, a.n, lane));
-        if (lane == 0) xf_store(static_cast<float*>(a.xf.mybuf), half + a.xf.off_b2 + c, sc);
+        if (lane == 0) {
+          if (push) xs[256 + c] = sc;
+          else xf_store(static_cast<float*>(a.xf.mybuf), half + a.xf.off_b2 + c, sc);
+        }
       }
+    }
+    if (push) {  // the owner-tile exchange: element e < 256 is W2[e / 16][tb * 16 + e % 16], 256 + c is b2[c]
+      const int e = threadIdx.x, c = e / 16, h = tb * 16 + e % 16;
+      const bool isb = e >= 256, ok = isb ? (with_b2 && e - 256 < a.C) : (c < a.C && h < a.H);
+      const int64_t i = isb ? e - 256 : (int64_t)c * a.H + h;
+      if (threadIdx.x == 0) {
+        s_xf[0] = epi.ep0 + 1;
+        s_xf[1] = (epi.xe | epi.perr) != 0;
+      }
+      __syncthreads();  // xs / xo complete
+      const float old = !ok ? 0.f : isb ? b2old : xs[kXpTile + e];
+      float nv;
+      if (!s_xf[1] && xp_exchange(a.xf, bid, s_xf, xs, 256 + a.C, ok, old, lr, &nv) && ok) (isb ? a.b2 : a.W2)[i] = nv;
+      if (!s_xf[1]) xf_end(a.xf, bid, s_xf);
+      return;
     }
     if (!xf_exchange(a.xf, bid, s_xf)) return;
     const int ne = 16 * 16 + (with_b2 ? a.C : 0);
@@ -911,7 +1112,9 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {  // the dW2 / db2 roles riding in this launch
     wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
-                reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)));
+                reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)),
+                reinterpret_cast<float*>(lds_dyn + kWKS * 4 * 64 * sizeof(float) + 16));  // (never fused: unused;
+                                                                                            //  2 x kXpTile floats)
     return;
   }
   using G = GldsGeom<BM, BN>;
@@ -1070,7 +1273,9 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {
     wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
-                reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)));
+                reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)),
+                reinterpret_cast<float*>(lds_dyn + kWKS * 4 * 64 * sizeof(float) + 16));  // (never fused: unused;
+                                                                                            //  2 x kXpTile floats)
     return;
   }
   using G = RegaGeom<128, WC>;

@@ -295,7 +295,12 @@ def xgmi_stall_main(out_dir):
 
 # ------------------------------------------------------------------ one rank per GPU (needs >= N GPUs)
 DP_MODES = (  # (name, H, trainer kwargs)
-    ("xgmi-fused", 100, dict(allreduce="xgmi")),
+    ("xgmi-fused", 100, dict(allreduce="xgmi", fused_form="pull")),
+    # the owner-tile push form of the fused all-reduce (XgmiFuse::push): bitwise the one-shot's result
+    ("xgmi-push", 100, dict(allreduce="xgmi", fused_form="push")),
+    # H = 32 (52 weight-gradient tiles per rank): small enough for 4 ranks' fused launches on one GPU at once
+    ("xgmi-fused-h32", 32, dict(allreduce="xgmi", fused_form="pull")),
+    ("xgmi-push-h32", 32, dict(allreduce="xgmi", fused_form="push")),
     ("xgmi", 100, dict(allreduce="xgmi", fuse_allreduce=False)),
     ("rccl", 100, dict(allreduce="rccl")),
     ("rccl-bucketed", 4096, dict(allreduce="rccl", overlap_chunks=4)),
@@ -346,7 +351,7 @@ def multigpu_dp_worker(rank, world, comm, device, out_dir, modes, scalings, step
             digests = [None] * world
             dist.all_gather_object(digests, hashlib.sha1(got.numpy().tobytes()).hexdigest(), group=comm.group)
             key = f"{name}/{scaling}"
-            res[key] = {"impl": impl, "replicas_equal": len(set(digests)) == 1,
+            res[key] = {"impl": impl, "replicas_equal": len(set(digests)) == 1, "digest": digests[0],
                         "rel_vs_single": float((got - want).abs().max() / want.abs().max()),
                         "moved": float((got - p0).abs().max())}
     if rank == 0:

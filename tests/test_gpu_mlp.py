@@ -730,7 +730,8 @@ def test_prefetch_of_a_partial_last_batch_stays_in_the_dataset(executor):
     """N % B != 0 (N = 1000, B = 300): the step before the partial last batch prefetches the next step's pixels --
     only the 100 rows that exist (MlpStep.run clamps SplitStepArgs::pf_bytes; before the clamp the prefetch read
     300 rows from row 900 of a 1000-row allocation).  Bitwise the same with the prefetch workgroups off, and
-    close to the PyTorch backend."""
+    close to the PyTorch backend (lr 1e-2: at 5e-2 the raw-pixel model is chaotic enough that even fp32 and fp64
+    PyTorch runs differ by 4e-3)."""
     x, y = synthetic_mnist(1000, seed=11)
     nn = NeuralNetwork([784, 100, 10])
     outs = []
@@ -739,12 +740,12 @@ def test_prefetch_of_a_partial_last_batch_stays_in_the_dataset(executor):
         tr.load(x, y)
         tr.engine._hip_step().prefetch = pf
         assert tr.epoch_plan().steps[-1] == (900, 100)
-        tr.train(2, 0.05, 1e-4)
+        tr.train(2, 0.01, 1e-4)
         torch.cuda.synchronize()
         assert not tr.engine.kernel_error()
         outs.append(tr.engine.params.clone())
     assert torch.equal(outs[0], outs[1])
     ref = DataParallelTrainer(nn.copy(), dtype="f32", batch_size=300, backend="torch", use_graphs=False)
     ref.load(x, y)
-    ref.train(2, 0.05, 1e-4)
+    ref.train(2, 0.01, 1e-4)
     assert _rel(outs[1].cpu(), ref.engine.params.cpu()) < 1e-5

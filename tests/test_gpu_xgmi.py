@@ -94,9 +94,21 @@ def test_xgmi_stalled_peer_applies_nothing_and_fails_everywhere(tmp_path):
 def test_dp_paths_shared_gpu_rehearsal(tmp_path):
     """The one-rank-per-GPU DP test's worker, rehearsed with 2 ranks sharing GPU 0 over gloo (every path
     except RCCL itself): replicas bitwise equal, result == the single-process run of the same global batch."""
-    _run_multigpu(tmp_path, 2, "gloo", ("xgmi-fused", "xgmi", "xgmi-bf16wire", "xgmi-2shot", "xgmi-2shot-f32", "rccl",
-                                        "host"), ("weak", "strong"),
-                  dict(os.environ, CME_SHARED_GPU="1", OMP_NUM_THREADS="2"))
+    res = _run_multigpu(tmp_path, 2, "gloo", ("xgmi-fused", "xgmi-push", "xgmi", "xgmi-bf16wire", "xgmi-2shot",
+                                              "xgmi-2shot-f32", "rccl", "host"), ("weak", "strong"),
+                        dict(os.environ, CME_SHARED_GPU="1", OMP_NUM_THREADS="2"))
+    for s in ("weak", "strong"):  # the owner-tile push form leaves the one-shot's bits
+        assert res[f"xgmi-push/{s}"]["digest"] == res[f"xgmi-fused/{s}"]["digest"], s
+
+
+def test_dp_owner_tile_push_four_ranks_shared_gpu(tmp_path):
+    """The owner-tile push form of the fused all-reduce (tile t reduced and applied by rank t % 4, pushed both ways
+    as tagged granules) with 4 ranks sharing GPU 0 at H = 32 (every rank's fused launch co-resident): replicas
+    bitwise equal, bitwise the one-shot (pull) form's result, and == the single-process run of the global batch."""
+    res = _run_multigpu(tmp_path, 4, "gloo", ("xgmi-fused-h32", "xgmi-push-h32"), ("weak", "strong"),
+                        dict(os.environ, CME_SHARED_GPU="1", OMP_NUM_THREADS="2"))
+    for s in ("weak", "strong"):
+        assert res[f"xgmi-push-h32/{s}"]["digest"] == res[f"xgmi-fused-h32/{s}"]["digest"], s
 
 
 def test_dp_two_shot_four_ranks_shared_gpu(tmp_path):
@@ -123,7 +135,8 @@ def _run_multigpu(tmp_path, world, backend, modes, scalings, env):
         bf16ish = "bf16wire" in key or key.startswith("xgmi-2shot/")
         assert v["rel_vs_single"] <= (2e-3 if bf16ish else 2e-6), (key, v)
         if key.startswith("xgmi"):
-            assert v["impl"] == key.split("/")[0].replace("-2shot-f32", "-2shot"), (key, v)
+            assert v["impl"] == key.split("/")[0].replace("-2shot-f32", "-2shot").replace("-h32", ""), (key, v)
+    return res
 
 
 def _gpus() -> int:
@@ -142,7 +155,8 @@ def test_dp_one_rank_per_gpu(tmp_path, world):
     graph, host-staged) at weak and strong scaling against the single-process run of the same global batch."""
     if _gpus() < world:
         pytest.skip(f"needs {world} GPUs, {_gpus()} visible")
-    modes = ("xgmi-fused", "xgmi", "xgmi-bf16wire", "xgmi-2shot", "xgmi-2shot-f32", "rccl", "rccl-bucketed", "host")
+    modes = ("xgmi-fused", "xgmi-push", "xgmi", "xgmi-bf16wire", "xgmi-2shot", "xgmi-2shot-f32", "rccl",
+             "rccl-bucketed", "host")
     _run_multigpu(tmp_path, world, "nccl", modes, ("weak", "strong"), dict(os.environ, OMP_NUM_THREADS="2"))
 
 
