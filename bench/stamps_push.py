@@ -66,7 +66,7 @@ def main(argv=None):
                 live = s[:, 0] > 0
                 t0 = s[live, 0].min()
                 rel = np.where(s > 0, (s - t0) * 10.0 / 1000.0, np.nan)
-                tiles = rel[:t1 + 8 * 25]  # the dW1 slots (XCD-row placement: 8 x t1n slots)
+                tiles = rel[:8 * 25]  # the dW1 slots (XCD-row placement: 8 x t1n slots; XCD 7's are idle)
                 tiles = tiles[~np.isnan(tiles[:, 3])]
                 roles = rel[8 * 25:8 * 25 + 9]
                 rows.append({"entry": pct(tiles[:, 0]), "tile_done": pct(tiles[:, 1]), "exchanged": pct(tiles[:, 2]),

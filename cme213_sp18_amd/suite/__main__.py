@@ -241,7 +241,8 @@ def main(argv=None) -> int:
     s.add_argument("--json", action="store_true")
     s = sub.add_parser("pagerank")
     s.add_argument("--quick", action="store_true")
-    s.add_argument("--variant", type=int, default=2)
+    s.add_argument("--variant", type=int, default=3,
+                   help="3: pre-multiplied gather (default); 0: thread per node; 1: 8 lanes per node; 2: auto (0)")
     s.add_argument("--json", action="store_true")
     s = sub.add_parser("stencil")
     s.add_argument("-g", action="store_true", help="global-memory kernel")

@@ -122,20 +122,39 @@ class DeviceGraph:
     def reset(self):
         self.a.copy_(self.initial)
 
-    def propagate(self, src, dst, variant: int = 2):
+    def propagate(self, src, dst, variant: int = 0):
         kernels().pagerank_propagate(self.indptr.data_ptr(), self.edges.data_ptr(), src.data_ptr(), dst.data_ptr(),
                                      self.inv.data_ptr(), self.n, variant, stream_handle())
 
-    def iterate(self, iters: int = PAGERANK_ITERS, variant: int = 2) -> torch.Tensor:
-        """Ping-pong ``iters`` propagations (pagerank.cu:100-117); returns the final buffer."""
+    def lanes_per_node(self) -> int:
+        """Lanes per node of the pre-multiplied kernel, by average degree (one lane per ~2-4 edges)."""
+        avg = self.num_edges / max(1, self.n)
+        return 1 if avg < 3 else 2 if avg < 6 else 4 if avg < 12 else 8
+
+    def iterate(self, iters: int = PAGERANK_ITERS, variant: int = 3) -> torch.Tensor:
+        """Ping-pong ``iters`` propagations (pagerank.cu:100-117); returns the final buffer.  variant 3 (default):
+        the pre-multiplied gather (w = values .* inv_deg formed once, then carried by every propagation); 0 / 1:
+        thread / 8 lanes per node gathering values and inv_deg; 2: the reference-shaped auto pick (0)."""
         src, dst = self.a, self.b
+        if variant != 3:
+            for _ in range(iters):
+                self.propagate(src, dst, variant)
+                src, dst = dst, src
+            return src
+        if getattr(self, "wa", None) is None:
+            self.wa, self.wb = torch.empty_like(self.a), torch.empty_like(self.a)
+        k, st, lpn = kernels(), stream_handle(), self.lanes_per_node()
+        wsrc, wdst = self.wa, self.wb
+        k.pagerank_premul(src.data_ptr(), self.inv.data_ptr(), wsrc.data_ptr(), self.n, st)
         for _ in range(iters):
-            self.propagate(src, dst, variant)
+            k.pagerank_propagate_w(self.indptr.data_ptr(), self.edges.data_ptr(), wsrc.data_ptr(), dst.data_ptr(),
+                                   wdst.data_ptr(), self.inv.data_ptr(), self.n, lpn, st)
             src, dst = dst, src
+            wsrc, wdst = wdst, wsrc
         return src
 
 
-def pagerank_gpu(g: Graph, iters: int = PAGERANK_ITERS, variant: int = 2) -> np.ndarray:
+def pagerank_gpu(g: Graph, iters: int = PAGERANK_ITERS, variant: int = 3) -> np.ndarray:
     return DeviceGraph(g).iterate(iters, variant).cpu().numpy()
 
 
@@ -152,7 +171,7 @@ def check_pagerank(gpu: np.ndarray, cpu: np.ndarray, max_ulps: int = PAGERANK_MA
 
 
 def benchmark_pagerank(nodes=(1 << 15, 1 << 16, 1 << 17, 1 << 18, 1 << 19, 1 << 20), edges=range(2, 20),
-                       iters: int = PAGERANK_ITERS, reps: int = 5, check: bool = True, variant: int = 2) -> list[dict]:
+                       iters: int = PAGERANK_ITERS, reps: int = 5, check: bool = True, variant: int = 3) -> list[dict]:
     """The GB/s sweep of main_q2.cu:151-233 (nodes 2^15..2^20 x avg edges 2..19)."""
     rows = []
     for e in edges:

@@ -157,6 +157,28 @@ __device__ __forceinline__ gran_t* xp_result_slot(const XgmiFuse& x, gran_t* sla
   return slab + ((size_t)x.slab_tiles * 8 + tile) * kXpTile;
 }
 
+// The push form's per-tile words, issued at workgroup entry by thread 0 WITHOUT a wait and waited for after the K
+// loop (xp_words_wait): the tile's exchange epoch -- one returning add to epochs[tile] per launch (old + 1 is this
+// launch's epoch on every rank: each launch adds one) -- and the bucket's and the forward's error words.  As inline
+// asm they are counted by the hardware in issue order (every later vmcnt wait only gets stricter) and hipcc can
+// neither sink them to their use after the K loop nor wait for them early: plain loads there were sunk behind the
+// loop, a cold memory round trip (the words were written by the previous launch) in front of every exchange --
+// 1.25 us per tile at world 1 (bench/stamps_push.py).
+struct XpWords {
+  uint32_t ep_old = 0;
+  int err = 0, agerr = 0;
+};
+__device__ __forceinline__ XpWords xp_words_issue(const XgmiFuse& x, int tile, const int* ag_err) {
+  XpWords w;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(w.ep_old) : "v"(x.epochs + tile), "v"(1u) : "memory");
+  asm volatile("global_load_dword %0, %1, off sc1" : "=v"(w.err) : "v"(x.err) : "memory");
+  if (ag_err) asm volatile("global_load_dword %0, %1, off sc1" : "=v"(w.agerr) : "v"(ag_err) : "memory");
+  return w;
+}
+__device__ __forceinline__ void xp_words_wait(XpWords& w) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(w.ep_old), "+v"(w.err), "+v"(w.agerr)::"memory");
+}
+
 // Bounded poll of the granules p[k] with bit k of `need` set until each carries tag ep (system-coherent loads of
 // this rank's own receive area); v[k] = their values.  Wave-uniform; false once the wait outlasts the peer bound.
 template <int N>
@@ -263,23 +285,12 @@ struct EpiW2 {
   float pre[kEpiMaxQ];
   const int* ag_err;  // the step's forward timed out: no update (the gradient goes to gW2, unused)
   int perr = 0;
-  // sys == 2 (the push form): gradient / current weight into LDS xs / xo[class * 16 + column - n0]; the epoch and
-  // error words as in EpiW1
+  // sys == 2 (the push form): gradient / current weight into LDS xs / xo[class * 16 + column - n0]
   float *xs = nullptr, *xo = nullptr;
   int n0 = 0;
-  const uint32_t* xep = nullptr;
-  const int* xerr = nullptr;
-  uint32_t ep0 = 0;
-  int xe = 0;
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
     pre[q] = buf_load1<float>(make_rsrc(W2), ok ? (row * H + col) * 4 : kOOB);
-    if (q == 0) {
-      perr = ag_err_load(ag_err);
-      if (xep) {
-        ep0 = *xep;
-        xe = __hip_atomic_load(xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    if (q == 0) perr = ag_err_load(ag_err);
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     const size_t i = (size_t)row * H + col;
@@ -309,25 +320,14 @@ struct EpiW1 {
   const int* ag_err;  // the step's forward timed out: no update (the gradient goes to gW1, unused)
   int perr = 0;
   // sys == 2 (the push form): the gradient into LDS xs[(row - m0) * 32 + col - n0] and the current weight (or b1)
-  // into xo; the tile's exchange epoch word and the bucket's error word are loaded with the other epilogue
-  // operands, before the K loop (xep, xerr -> ep0, xe), so the exchange starts with no memory round trip
+  // into xo
   float *xs = nullptr, *xo = nullptr;
   int m0 = 0, n0 = 0;
-  const uint32_t* xep = nullptr;
-  const int* xerr = nullptr;
-  uint32_t ep0 = 0;
-  int xe = 0;
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
     // (the all-ones feature column P: b1[row], so its update is not a dependent load after the K loop)
     if (col == P) pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
     else pre[q] = buf_load1<float>(make_rsrc(W1), (ok && col < P) ? (row * P + col) * 4 : kOOB);
-    if (q == 0) {
-      perr = ag_err_load(ag_err);
-      if (xep) {
-        ep0 = *xep;
-        xe = __hip_atomic_load(xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    if (q == 0) perr = ag_err_load(ag_err);
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     const bool upd = sgd && !poisoned(perr);
@@ -409,13 +409,13 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     }
     EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.w1_planes ? a.npw : 0, reg, lr,
               a.xscale, {}, a.b1, gb, push ? 2 : (live ? 1 : 0), a.ag_err};
+    XpWords xw;
     if (push) {
       epi.xs = xs;
       epi.xo = xo;
       epi.m0 = g.m0;
       epi.n0 = g.n0;
-      epi.xep = a.xf.epochs + bid;
-      epi.xerr = a.xf.err;
+      if (threadIdx.x == 0) xw = xp_words_issue(a.xf, bid, a.ag_err);
     }
     constexpr int U = 4;
     if constexpr (AF)
@@ -430,9 +430,10 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       const int e = threadIdx.x, row = g.m0 + e / 32, col = g.n0 + e % 32;
       const bool ok = e < 512 && row < g.M && col < g.N;
       const int64_t i = (int64_t)row * a.P + col;
-      if (threadIdx.x == 0) {  // (thread 0's view of the words decides for the whole workgroup)
-        s_xf[0] = epi.ep0 + 1;
-        s_xf[1] = (epi.xe | epi.perr) != 0;
+      if (threadIdx.x == 0) {  // (thread 0's words decide for the whole workgroup)
+        xp_words_wait(xw);
+        s_xf[0] = xw.ep_old + 1;
+        s_xf[1] = (xw.err | xw.agerr) != 0;
       }
       __syncthreads();  // xs / xo complete
       float nv;
@@ -447,7 +448,6 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
           a.b1[row] = nv;
         }
       }
-      if (!s_xf[1]) xf_end(a.xf, bid, s_xf);
     } else if (live && xf_exchange(a.xf, bid, s_xf)) {  // all-reduced with the peers: SGD + bf16 planes
       const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf.npad;
       constexpr int TW = 16 * kWNB;
@@ -503,12 +503,12 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     if (live && !push) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
     EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, push ? 2 : (live ? 1 : 0), reg, lr, {}, a.ag_err};
     float b2old = 0.f;  // (push, tile 0: b2 for the owner's update, loaded before the K loop)
+    XpWords xw;
     if (push) {
       epi.xs = xs;
       epi.xo = xs + kXpTile;
       epi.n0 = tb * 16;
-      epi.xep = a.xf.epochs + bid;
-      epi.xerr = a.xf.err;
+      if (threadIdx.x == 0) xw = xp_words_issue(a.xf, bid, a.ag_err);
       if (tb == 0 && threadIdx.x >= 256 && threadIdx.x < 256 + a.C) b2old = a.b2[threadIdx.x - 256];
     }
     if (a.dw2part) {  // the head's per-column-tile partials, summed in tile order (16 rows x C classes)
@@ -547,14 +547,14 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
       const bool isb = e >= 256, ok = isb ? (with_b2 && e - 256 < a.C) : (c < a.C && h < a.H);
       const int64_t i = isb ? e - 256 : (int64_t)c * a.H + h;
       if (threadIdx.x == 0) {
-        s_xf[0] = epi.ep0 + 1;
-        s_xf[1] = (epi.xe | epi.perr) != 0;
+        xp_words_wait(xw);
+        s_xf[0] = xw.ep_old + 1;
+        s_xf[1] = (xw.err | xw.agerr) != 0;
       }
       __syncthreads();  // xs / xo complete
       const float old = !ok ? 0.f : isb ? b2old : xs[kXpTile + e];
       float nv;
       if (!s_xf[1] && xp_exchange(a.xf, bid, s_xf, xs, 256 + a.C, ok, old, lr, &nv) && ok) (isb ? a.b2 : a.W2)[i] = nv;
-      if (!s_xf[1]) xf_end(a.xf, bid, s_xf);
       return;
     }
     if (!xf_exchange(a.xf, bid, s_xf)) return;

@@ -62,6 +62,65 @@ __global__ void pagerank_kernel(const uint32_t* __restrict__ indptr, const uint3
   }
 }
 
+// ---- PageRank, pre-multiplied gather operand (variant 3).  The pull kernel above gathers TWO random floats per
+// edge, in[src] and inv_deg[src]: an 8 MB random working set at 1 M nodes, twice one XCD's 4 MB L2, so every
+// other gather misses to the Infinity Cache (1 M nodes x degree 19: 478 GB/s on the reference's bytes model).
+// Here each propagation also writes w_out[i] = out[i] * inv_deg[i] (a coalesced read and write), and the next
+// one gathers w[src] alone: one random float per edge from a 4 MB array -- half the gathers, half the working
+// set.  The streamed operands (row pointers, edge lists) are read non-temporally so they do not push w out of L2.
+// LPN lanes per row; each lane keeps UNR edge loads, then UNR gathers, in flight per trip.  The product
+// in[src] * inv_deg[src] is the same rounded fp32 value whether formed here or when gathered (the reference's
+// host loop adds the rounded products too, hw2code/main_q2.cu:49-85).
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+
+__global__ __launch_bounds__(256) void pagerank_premul_kernel(const float* __restrict__ in,
+                                                              const float* __restrict__ inv_deg,
+                                                              float* __restrict__ w, int n) {
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) w[i] = in[i] * inv_deg[i];
+}
+
+template <int LPN, int UNR>
+__global__ __launch_bounds__(256) void pagerank_w_kernel(const uint32_t* __restrict__ indptr,
+                                                         const uint32_t* __restrict__ edges,
+                                                         const float* __restrict__ w_in, float* __restrict__ out,
+                                                         float* __restrict__ w_out,
+                                                         const float* __restrict__ inv_deg, int n) {
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int sub = threadIdx.x % LPN;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x / LPN;
+  const float base = 0.5f / (float)n;
+  for (int64_t node = gt / LPN; node < n; node += stride) {
+    const uint32_t b = ld_nt(indptr + node), e = ld_nt(indptr + node + 1);
+    float sum = 0.f;
+    for (uint32_t j0 = b + sub; j0 < e; j0 += LPN * UNR) {
+      uint32_t src[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const uint32_t j = j0 + u * LPN;
+        src[u] = j < e ? ld_nt(edges + j) : 0xFFFFFFFFu;
+      }
+      float v[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) v[u] = src[u] != 0xFFFFFFFFu ? w_in[src[u]] : 0.f;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) sum += v[u];  // (edge order per lane: j0, j0 + LPN, ...)
+    }
+    if constexpr (LPN > 1) {
+#pragma unroll
+      for (int o = LPN / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o, LPN);
+    }
+    if (sub == 0) {
+      const float r = base + 0.5f * sum;
+      out[node] = r;
+      w_out[node] = r * inv_deg[node];
+    }
+  }
+}
+
 // ------------------------------------------------------------ even/odd sum
 // Streaming reduction: every thread keeps UNR independent 16-byte loads in flight per iteration
 // (contiguous chunk of the array per workgroup, coalesced across the wave) and accumulates the
@@ -152,6 +211,27 @@ void pagerank_propagate(const uint32_t* indptr, const uint32_t* edges, const flo
   } else {
     const int grid = std::min((int)(((int64_t)n * 8 + block - 1) / block), 8192);
     pagerank_kernel<8><<<grid, block, 0, s>>>(indptr, edges, in, out, inv_deg, n);
+  }
+  CME_LAUNCH_CHECK(s);
+}
+
+void pagerank_premul(const float* in, const float* inv_deg, float* w, int n, hipStream_t s) {
+  if (n <= 0) return;
+  pagerank_premul_kernel<<<std::min((n + 255) / 256, 8192), 256, 0, s>>>(in, inv_deg, w, n);
+  CME_LAUNCH_CHECK(s);
+}
+
+void pagerank_propagate_w(const uint32_t* indptr, const uint32_t* edges, const float* w_in, float* out, float* w_out,
+                          const float* inv_deg, int n, int lpn, hipStream_t s) {
+  if (n <= 0) return;
+  const int block = 256;
+  const int grid = (int)std::min<int64_t>(((int64_t)n * lpn + block - 1) / block, 16384);
+  switch (lpn) {
+    case 1: pagerank_w_kernel<1, 4><<<grid, block, 0, s>>>(indptr, edges, w_in, out, w_out, inv_deg, n); break;
+    case 2: pagerank_w_kernel<2, 4><<<grid, block, 0, s>>>(indptr, edges, w_in, out, w_out, inv_deg, n); break;
+    case 4: pagerank_w_kernel<4, 4><<<grid, block, 0, s>>>(indptr, edges, w_in, out, w_out, inv_deg, n); break;
+    case 8: pagerank_w_kernel<8, 2><<<grid, block, 0, s>>>(indptr, edges, w_in, out, w_out, inv_deg, n); break;
+    default: CME_REQUIRE(false, "pagerank_propagate_w: lanes per node must be 1, 2, 4 or 8");
   }
   CME_LAUNCH_CHECK(s);
 }

@@ -25,6 +25,15 @@ void bind_suite(py::module_& m) {
                        P<const float>(inv), n, variant, S(s));
   }, py::arg("indptr"), py::arg("edges"), py::arg("inp"), py::arg("out"), py::arg("inv_deg"), py::arg("n"),
      py::arg("variant") = 2, py::arg("stream") = 0);
+  sm.def("pagerank_premul", [](uintptr_t in, uintptr_t inv, uintptr_t w, int n, uintptr_t s) {
+    pagerank_premul(P<const float>(in), P<const float>(inv), P<float>(w), n, S(s));
+  }, py::arg("inp"), py::arg("inv_deg"), py::arg("w"), py::arg("n"), py::arg("stream") = 0);
+  sm.def("pagerank_propagate_w", [](uintptr_t indptr, uintptr_t edges, uintptr_t w_in, uintptr_t out, uintptr_t w_out,
+                                    uintptr_t inv, int n, int lpn, uintptr_t s) {
+    pagerank_propagate_w(P<const uint32_t>(indptr), P<const uint32_t>(edges), P<const float>(w_in), P<float>(out),
+                         P<float>(w_out), P<const float>(inv), n, lpn, S(s));
+  }, py::arg("indptr"), py::arg("edges"), py::arg("w_in"), py::arg("out"), py::arg("w_out"), py::arg("inv_deg"),
+     py::arg("n"), py::arg("lpn"), py::arg("stream") = 0);
   sm.def("stencil_step", [](uintptr_t next, uintptr_t curr, int gx, int gy, int order, float xcfl, float ycfl,
                             int variant, uintptr_t s) {
     stencil_step(P<float>(next), P<const float>(curr), gx, gy, order, xcfl, ycfl, variant, S(s));

@@ -28,6 +28,12 @@ void shift_bytes(const uint8_t* in, uint8_t* out, int64_t n, uint8_t shift, int 
 // variant 0: thread per node, 1: wave per node (long rows), 2: auto by avg degree
 void pagerank_propagate(const uint32_t* indptr, const uint32_t* edges, const float* in, float* out,
                         const float* inv_deg, int n, int variant, hipStream_t s);
+// the pre-multiplied form: w = in .* inv_deg once (pagerank_premul), then every propagation gathers w alone and
+// writes out[i] = 0.5/N + 0.5 * sum_j w_in[e_j] and w_out[i] = out[i] * inv_deg[i] for the next one; lpn lanes per
+// node (1, 2, 4, 8)
+void pagerank_premul(const float* in, const float* inv_deg, float* w, int n, hipStream_t s);
+void pagerank_propagate_w(const uint32_t* indptr, const uint32_t* edges, const float* w_in, float* out, float* w_out,
+                          const float* inv_deg, int n, int lpn, hipStream_t s);
 
 // ------------------------------------------------------------- hw3 stencil
 // next(interior) = Stencil<order>(curr); variant 0 global, 1 register-blocked loop, 2 LDS tile

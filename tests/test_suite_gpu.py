@@ -66,8 +66,8 @@ def test_shift_benchmark_runs():
     assert set(r["gbps"]) == set(hw2.SHIFT_WIDTHS)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
-@pytest.mark.parametrize("nodes,edges", [(1000, 2), (1 << 15, 7), (1 << 17, 19)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("nodes,edges", [(1000, 2), (1 << 15, 7), (1 << 17, 19), (1 << 20, 19), (4097, 4)])
 def test_pagerank_gpu(variant, nodes, edges):
     g = hw2.generate_graph(nodes, edges, seed=nodes + edges)
     out = hw2.pagerank_gpu(g, 6, variant)
