@@ -72,7 +72,9 @@ def main(argv=None):
         pref = int(m.group(1)) if m else None
         m = re.search(r"\+t(\d)", path)  # "+tK": K prefetch workgroups per XCD for XT (MlpStep.prefetch_xt)
         pref_xt = int(m.group(1)) if m else None
-        path = re.sub(r"\+[sdxpt]\d", "", path)
+        m = re.search(r"\+g(\d)", path)  # "+gK": the wide 128 x 128 K loop's engine (MlpStep.wide_eng)
+        weng = int(m.group(1)) if m else None
+        path = re.sub(r"\+[sdxptg]\d", "", path)
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -85,6 +87,8 @@ def main(argv=None):
                     step.xcd_rows = xrows
                 if pref is not None:
                     step.prefetch = pref
+                if weng is not None:
+                    step.wide_eng = weng
                 if pref_xt is not None:
                     step.prefetch_xt = pref_xt
                 if no_a1:
@@ -96,7 +100,7 @@ def main(argv=None):
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else "") + (f"+g{weng}" if weng is not None else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(

@@ -40,7 +40,7 @@ def main(argv=None):
         st = torch.cuda.current_stream().cuda_stream
         slots = e.fused_allreduce_slots()
         t1 = 7 * 25
-        buf = torch.zeros(1024 * 4, dtype=torch.int64, device="cuda")
+        buf = torch.zeros(1024 * 8, dtype=torch.int64, device="cuda")
         for form in ("sgd", "pull", "push"):
             xc = None
             sgd = 1
@@ -62,14 +62,17 @@ def main(argv=None):
                 step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st, 2)
                 step.wstamps = 0
                 torch.cuda.synchronize()
-                s = buf.view(-1, 4).cpu().numpy().astype(np.int64)
+                s = buf.view(-1, 8).cpu().numpy().astype(np.int64)
                 live = s[:, 0] > 0
                 t0 = s[live, 0].min()
                 rel = np.where(s > 0, (s - t0) * 10.0 / 1000.0, np.nan)
                 tiles = rel[:8 * 25]  # the dW1 slots (XCD-row placement: 8 x t1n slots; XCD 7's are idle)
                 tiles = tiles[~np.isnan(tiles[:, 3])]
                 roles = rel[8 * 25:8 * 25 + 9]
-                rows.append({"entry": pct(tiles[:, 0]), "tile_done": pct(tiles[:, 1]), "exchanged": pct(tiles[:, 2]),
+                sub = {}
+                if form == "push":  # the exchange's phases (xp_exchange stamps): words waited, poll done, barrier
+                    sub = {"words_ready": pct(tiles[:, 4]), "polled": pct(tiles[:, 5]), "barrier": pct(tiles[:, 6])}
+                rows.append({**sub, "entry": pct(tiles[:, 0]), "tile_done": pct(tiles[:, 1]), "exchanged": pct(tiles[:, 2]),
                              "end": pct(tiles[:, 3]), "roles_end": pct(roles[~np.isnan(roles[:, 3]), 3]),
                              "launch_end": round(float(np.nanmax(rel[:, 3])), 3)})
             med = {k: [round(float(np.median([r[k][i] for r in rows])), 3) for i in range(4)] for k in rows[0]

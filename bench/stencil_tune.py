@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""The LDS stencil's knobs at order 8 on an HBM-sized grid (csrc/suite/stencil.hip stencil_lds_tune): rows per wave,
+rows loaded ahead, non-temporal streamed loads.  Interior sweeps only, ping-ponged; every form's result after the
+sweeps is compared BITWISE with the production LDS variant's (same arithmetic, so any difference is a bug).  GB/s of
+compulsory bytes (read the grid, write the interior once per sweep).
+
+    python bench/stencil_tune.py [--n 12288] [--iters 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=12288)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args(argv)
+    import torch
+
+    from cme213_sp18_amd._native import hip
+
+    k = hip().suite
+    g = a.n
+    torch.manual_seed(0)
+    init = torch.rand(g * g, dtype=torch.float32, device="cuda")
+    A, Bf = torch.empty_like(init), torch.empty_like(init)
+    st = torch.cuda.current_stream().cuda_stream
+    xcfl = ycfl = 0.0001
+
+    def run(fn):
+        A.copy_(init)
+        Bf.copy_(init)
+        src, dst = A, Bf
+        for _ in range(a.iters):
+            fn(dst, src)
+            src, dst = dst, src
+        return src
+
+    def timeit(fn):
+        run(fn)
+        best = float("inf")
+        for _ in range(a.reps):
+            A.copy_(init)
+            Bf.copy_(init)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            src, dst = A, Bf
+            for _ in range(a.iters):
+                fn(dst, src)
+                src, dst = dst, src
+            e1.record()
+            e1.synchronize()
+            best = min(best, e0.elapsed_time(e1))
+        return best
+
+    nx = g - 8
+    comp = a.iters * (g * g + nx * nx) * 4  # read the grid, write the interior
+    prod = lambda d, s: k.stencil_step(d.data_ptr(), s.data_ptr(), g, g, 8, xcfl, ycfl, 2, st)  # noqa: E731
+    ref = run(prod).clone()
+    ms = timeit(prod)
+    print(json.dumps({"form": "production lds (32 rows, 4 ahead)", "ms": round(ms, 3),
+                      "compulsory_GBps": round(comp / (ms * 1e-3) / 1e9, 1)}), flush=True)
+    # nt: bit 0 non-temporal streamed loads, bit 1 the alternate-direction walk (ALT)
+    for rows, ahead, nt in ((32, 4, 0), (32, 8, 0), (32, 8, 1), (64, 8, 0), (32, 4, 2), (32, 8, 2), (64, 8, 2),
+                            (16, 8, 2)):
+        fn = lambda d, s, r=rows, h=ahead, t=nt: k.stencil_lds_tune(d.data_ptr(), s.data_ptr(), g, g, xcfl, ycfl,  # noqa: E731
+                                                                    r, h, t, st)
+        out = run(fn)
+        same = bool(torch.equal(out, ref))
+        ms = timeit(fn)
+        print(json.dumps({"rows": rows, "ahead": ahead, "nt": nt, "ms": round(ms, 3), "bitwise_equal": same,
+                          "compulsory_GBps": round(comp / (ms * 1e-3) / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

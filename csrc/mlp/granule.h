@@ -71,7 +71,11 @@ __device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsi
   bool done = !need;
   unsigned rdy = 0u;  // bit k: granule k carried the epoch in an earlier pass (x[k] is final)
   gran_t x[N];
-  const uint64_t t0 = wall_ticks(), limit = (uint64_t)limit_us * kTicksPerUs;
+  // The wall clock is read only once a pass has come back incomplete: s_memrealtime is a scalar-memory read, and
+  // read up front its latency (~0.5 us, bench/stamps_push.py) sat in front of the first LDS access after a poll
+  // that needed no second pass (lgkmcnt counts it with the LDS operations).
+  uint64_t t0 = 0;
+  const uint64_t limit = (uint64_t)limit_us * kTicksPerUs;
   for (uint32_t pass = 1;; ++pass) {
     if (!done) {
 #pragma unroll
@@ -84,7 +88,8 @@ __device__ __forceinline__ bool gran_poll(const gran_t* base, unsigned off, unsi
     if (__all(done)) break;
     // (the clock -- a scalar-memory read and its wait -- every 8th pass only: the first passes, where a hand-off
     // normally completes, poll at full rate)
-    if ((pass & 7) == 0 && wall_ticks() - t0 > limit) return false;
+    if (pass == 1) t0 = wall_ticks();
+    else if ((pass & 7) == 0 && wall_ticks() - t0 > limit) return false;
     __builtin_amdgcn_s_sleep(2);
   }
   if (need) {
@@ -105,7 +110,8 @@ __device__ __forceinline__ bool gran_poll_set(const gran_t* base, const unsigned
   constexpr unsigned kAll = N == 32 ? ~0u : (1u << N) - 1u;
   unsigned rdy = ~need & kAll;
   gran_t x[N];
-  const uint64_t t0 = wall_ticks(), limit = (uint64_t)limit_us * kTicksPerUs;
+  uint64_t t0 = 0;  // (read once a pass comes back incomplete: gran_poll)
+  const uint64_t limit = (uint64_t)limit_us * kTicksPerUs;
   for (uint32_t pass = 1;; ++pass) {
     if (rdy != kAll) {
 #pragma unroll
@@ -116,7 +122,8 @@ __device__ __forceinline__ bool gran_poll_set(const gran_t* base, const unsigned
         if (!(rdy & (1u << k))) rdy |= (unsigned)((unsigned)(x[k] >> 32) == ep) << k;
     }
     if (__all(rdy == kAll)) break;
-    if ((pass & 7) == 0 && wall_ticks() - t0 > limit) return false;
+    if (pass == 1) t0 = wall_ticks();
+    else if ((pass & 7) == 0 && wall_ticks() - t0 > limit) return false;
     __builtin_amdgcn_s_sleep(2);
   }
 #pragma unroll

@@ -105,6 +105,10 @@ struct SplitStepArgs {
   // writes no dZ1 planes); clear bits: the stored planes (6 B per element, split once by their writer).
   // Policy (MlpStep::split_args, measured: bench/kbench.py): 1 at H <= 128, 3 above
   int a_fp32 = 1;
+  // wide layers (the 128 x 128 A-in-registers tiling): the K loop's engine -- 0 rega_gemm.h (A fragments straight
+  // into registers, 32-deep stages), 1 g64_gemm.h (both operands LDS-DMA'd in full rows, 64-deep steps); the same
+  // bits either way (MlpStep.wide_eng)
+  int wide_eng = 0;
   // wide layers: the head left dW2 partials [cdiv(n, 32)][16][H] (HeadArgs::dw2part); the dW2 role then sums
   // them in column-tile order instead of forming D . a1^T from all of a1
   float* dw2part = nullptr;

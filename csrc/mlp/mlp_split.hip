@@ -9,6 +9,7 @@
 #include "head_math.h"
 #include "l2_touch.h"
 #include "rega_gemm.h"
+#include "g64_gemm.h"
 #include "mma_tile.h"
 #include "fwd_tile.h"
 
@@ -120,10 +121,11 @@ __device__ __forceinline__ bool xf_exchange(const XgmiFuse& x, int tile, uint32_
     // and drained by every wave above, so a release would only write back the L2's OTHER dirty lines
     // (W1/plane updates no peer reads) once per tile.  bench.py checks the replicas bitwise after warm-up.
     __hip_atomic_store(x.peerflags[t] + tile * 8 + x.rank, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t t0 = wall_ticks();
+    uint64_t t0 = 0;  // (the clock only once the flag is missing: granule.h gran_poll)
     const uint32_t* f = x.myflags + tile * 8 + t;
     while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - ep) < 0) {
-      if (wall_ticks() - t0 > kXfWaitTicks) {
+      if (t0 == 0) t0 = wall_ticks();
+      else if (wall_ticks() - t0 > kXfWaitTicks) {
         atomicExch(x.err, 1);
         s_xf[1] = 1;  // (the waiting lanes may race here: they all store 1)
         break;
@@ -186,7 +188,7 @@ __device__ __forceinline__ bool xp_poll(const gran_t* const (&p)[N], unsigned ne
   constexpr unsigned kAll = (1u << N) - 1u;
   unsigned rdy = ~need & kAll;
   gran_t g[N];
-  const uint64_t t0 = wall_ticks();
+  uint64_t t0 = 0;  // (the clock only once a pass comes back incomplete: granule.h gran_poll)
   for (uint32_t pass = 1;; ++pass) {
     if (rdy != kAll) {
 #pragma unroll
@@ -197,7 +199,8 @@ __device__ __forceinline__ bool xp_poll(const gran_t* const (&p)[N], unsigned ne
         if (!(rdy & (1u << k))) rdy |= (unsigned)((unsigned)(g[k] >> 32) == ep) << k;
     }
     if (__all(rdy == kAll)) break;
-    if ((pass & 7) == 0 && wall_ticks() - t0 > kXfWaitTicks) return false;
+    if (pass == 1) t0 = wall_ticks();
+    else if ((pass & 7) == 0 && wall_ticks() - t0 > kXfWaitTicks) return false;
     __builtin_amdgcn_s_sleep(1);
   }
 #pragma unroll
@@ -211,7 +214,8 @@ __device__ __forceinline__ bool xp_poll(const gran_t* const (&p)[N], unsigned ne
 // one-shot's expression, so both forms leave the same bits -- or false when a wait timed out (err set; the
 // caller applies nothing, and a non-owner that times out never hears of it: its owner's wait times out too).
 __device__ __forceinline__ bool xp_exchange(const XgmiFuse& x, int tile, uint32_t* s_xf, const float* xs, int ne,
-                                            bool valid, float old, float lr, float* nv) {
+                                            bool valid, float old, float lr, float* nv,
+                                            unsigned long long* st = nullptr) {  // (st: diagnostics only)
   const unsigned ep = s_xf[0];
   const int owner = tile % x.world, e = threadIdx.x;
   const bool mine = valid && e < ne;
@@ -240,11 +244,13 @@ __device__ __forceinline__ bool xp_exchange(const XgmiFuse& x, int tile, uint32_
       *nv = old - lr * sum;
     }
   }
+  if (st && e == 0) st[5] = __builtin_amdgcn_s_memrealtime();
   if (!ok && (e & 63) == 0) {
     atomicExch(x.err, 1);
     s_xf[1] = 1;
   }
   __syncthreads();
+  if (st && e == 0) st[6] = __builtin_amdgcn_s_memrealtime();
   if (s_xf[1]) return false;
   if (x.rank == owner && mine) {  // the update to every other rank
     for (int r = 0; r < x.world; ++r)
@@ -369,7 +375,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   __shared__ uint32_t s_xf[2];
   __shared__ float xsx[2 * kXpTile];  // the push form's staged gradient tile, then the current values
   float *xs = xsx, *xo = xsx + kXpTile;
-  unsigned long long* wst = a.wstamps ? a.wstamps + (size_t)blockIdx.x * 4 : nullptr;  // diagnostics only
+  unsigned long long* wst = a.wstamps ? a.wstamps + (size_t)blockIdx.x * 8 : nullptr;  // diagnostics only
   auto wstamp = [&](int i) {
     if (wst && threadIdx.x == 0) wst[i] = __builtin_amdgcn_s_memrealtime();
   };
@@ -436,8 +442,9 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
         s_xf[1] = (xw.err | xw.agerr) != 0;
       }
       __syncthreads();  // xs / xo complete
+      wstamp(4);
       float nv;
-      if (!s_xf[1] && xp_exchange(a.xf, bid, s_xf, xs, 512, ok, ok ? xo[e] : 0.f, lr, &nv) && ok) {
+      if (!s_xf[1] && xp_exchange(a.xf, bid, s_xf, xs, 512, ok, ok ? xo[e] : 0.f, lr, &nv, wst) && ok) {
         if (col < a.P) {
           a.W1[i] = nv;
           if (a.w1_planes) {
@@ -1164,7 +1171,7 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
 // a1 = sigmoid(W1 X + b1) on the A-in-registers engine (rega_gemm.h): W1 read as fp32 and split into the
 // exact bf16 planes in registers (AT = float), or the bf16 plane 0 (AT = bf16, split1); z2 partials of
 // this 128-row tile as in fwd1_glds_kernel
-template <typename AT, int WC, int NKS, bool AG = false>
+template <typename AT, int WC, int NKS, bool AG = false, int ENG = 0>
 __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn, RegaAgArgs ag = {}) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   using G = RegaGeom<128, WC>;
@@ -1193,7 +1200,13 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
     }
   f32x4 acc[MB][NB];
   const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.W1) : reinterpret_cast<const AT*>(a.W1p);
-  rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
+  if constexpr (ENG == 1) {
+    static_assert(WC == 1, "g64 engine: the 8 x 1 wave layout");
+    g64_gemm_mainloop<AT, (NKS > 0 ? (NKS * 32 + 63) / 64 : 0)>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0,
+                                                               n0, lds_dyn, acc);
+  } else {
+    rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
+  }
   if (AG) ag_stamp(a, 1);
   const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(a.a1);
 #pragma unroll
@@ -1268,7 +1281,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
 // dW1 = dZ1 XT on the A-in-registers engine: dZ1 read as fp32 (AT = float; the head writes it instead of
 // the three bf16 planes: 4 B per element stored and loaded instead of 6) or as its one bf16 plane (split1),
 // with wgrad_glds_kernel's fused reg + SGD + plane-refresh epilogue; the dW2 / db2 roles ride along
-template <typename AT, int WC, int NKS>
+template <typename AT, int WC, int NKS, int ENG = 0>
 __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {
@@ -1294,8 +1307,14 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
   f32x4 acc[MB][NB];
   // fp32 dZ1 split in registers (AT = float), or its one bf16 plane (split1)
   const AT* A = sizeof(AT) == 4 ? reinterpret_cast<const AT*>(a.dZ1) : reinterpret_cast<const AT*>(a.dZ1p);
-  rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0,
-                                       n0, lds_dyn, acc);
+  if constexpr (ENG == 1) {
+    static_assert(WC == 1, "g64 engine: the 8 x 1 wave layout");
+    g64_gemm_mainloop<AT, (NKS > 0 ? (NKS * 32 + 63) / 64 : 0)>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M,
+                                                               P + a.bias_col, a.n, m0, n0, lds_dyn, acc);
+  } else {
+    rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0,
+                                         n0, lds_dyn, acc);
+  }
   wc1.stage(lds_dyn, acc, rw, cw, m0, n0, fg, fr);
   // the W1 planes (npw == npz); split3 w1_planes_lazy: none (the 128 x 128 forward reads fp32 W1)
   wc1.apply(a, lds_dyn, m0, n0, M, a.sgd && !poisoned(perr), (NP == 3 && a.w1_planes_lazy) ? 0 : NP);
@@ -1340,20 +1359,33 @@ constexpr int kRegaWC = 1;  // wave layout of the A-in-registers kernels: 8 (row
 
 template <typename AT, int NKS>
 void launch_fwd1_rega_k(const SplitStepArgs& a, hipStream_t s) {
-  constexpr int L = std::max(ra::lds_bytes<128>(), 8 * 8 * 64 * 16);  // (z2 reduction scratch)
-  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, false>>(L);
-  fwd1_rega_kernel<AT, kRegaWC, NKS, false><<<cdiv(a.H, 128) * cdiv(a.n, 128), 512, L, s>>>(a, cdiv(a.n, 128));
+  constexpr int L = std::max({ra::lds_bytes<128>(), g64::lds_bytes<AT>(), 8 * 8 * 64 * 16});  // (z2 reduction scratch)
+  const int grid = cdiv(a.H, 128) * cdiv(a.n, 128);
+  if (a.wide_eng == 1) {
+    set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, false, 1>>(L);
+    fwd1_rega_kernel<AT, kRegaWC, NKS, false, 1><<<grid, 512, L, s>>>(a, cdiv(a.n, 128));
+  } else {
+    set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, false>>(L);
+    fwd1_rega_kernel<AT, kRegaWC, NKS, false><<<grid, 512, L, s>>>(a, cdiv(a.n, 128));
+  }
 }
 
 // the fused all-gather head: > 80 KB of LDS keeps it at one workgroup per CU (the hand-off's measured form)
 template <typename AT, int NKS>
 void launch_fwd1_rega_ag_k(const SplitStepArgs& a, RegaAgArgs g, hipStream_t s) {
-  constexpr int L = wide_ag_launch_lds(std::max({ra::lds_bytes<128>(), 8 * 8 * 64 * 16, wide_ag_lds_bytes<128, 128>()}));
-  set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true>>(L);
+  constexpr int L = wide_ag_launch_lds(
+      std::max({ra::lds_bytes<128>(), g64::lds_bytes<AT>(), 8 * 8 * 64 * 16, wide_ag_lds_bytes<128, 128>()}));
+  static_assert(L <= 160 * 1024, "fused wide head: LDS");
   g.ep_off = L - 16;
   g.tiling = 0;
   const int tn = cdiv(a.n, 128);
-  fwd1_rega_kernel<AT, kRegaWC, NKS, true><<<g.tm * tn, 512, L, s>>>(a, tn, g);
+  if (a.wide_eng == 1) {
+    set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true, 1>>(L);
+    fwd1_rega_kernel<AT, kRegaWC, NKS, true, 1><<<g.tm * tn, 512, L, s>>>(a, tn, g);
+  } else {
+    set_lds_limit<fwd1_rega_kernel<AT, kRegaWC, NKS, true>>(L);
+    fwd1_rega_kernel<AT, kRegaWC, NKS, true><<<g.tm * tn, 512, L, s>>>(a, tn, g);
+  }
 }
 
 // K = P = 784 (MNIST) is 25 stages of 32: the fully unrolled K loop; anything else the runtime loop
@@ -1388,9 +1420,15 @@ void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) 
   const int rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int tn = cdiv(a.P + a.bias_col, 128), tbig = cdiv(rows, 128) * tn;
   // (the K-loop ring, the epilogue's transposed 128 x (128 + 4) fp32 tile, the role workgroups' scratch)
-  constexpr int L = std::max({ra::lds_bytes<128>(), W1Chunks<128, 128>::kLdsBytes, kWKS * 4 * 64 * (int)sizeof(float) + 16});
-  set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS>>(L);
-  wgrad_rega_kernel<AT, kRegaWC, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
+  constexpr int L = std::max({ra::lds_bytes<128>(), g64::lds_bytes<AT>(), W1Chunks<128, 128>::kLdsBytes,
+                              kWKS * 4 * 64 * (int)sizeof(float) + 16 + 2 * kXpTile * (int)sizeof(float)});
+  if (a.wide_eng == 1) {
+    set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS, 1>>(L);
+    wgrad_rega_kernel<AT, kRegaWC, NKS, 1><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
+  } else {
+    set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS>>(L);
+    wgrad_rega_kernel<AT, kRegaWC, NKS><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
+  }
 }
 
 template <typename AT>

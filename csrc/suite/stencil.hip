@@ -169,10 +169,26 @@ constexpr int kVecRows = 8;
 constexpr int kLdsRows = 32;
 constexpr int kLdsAhead = 4;
 
-template <int ORDER, int ROWS>
-__device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
+// 16-byte load with a cache policy (CP: 0 default, 2 non-temporal: streamed, read once)
+template <int CP>
+__device__ __forceinline__ f32x4 ld4p(__amdgpu_buffer_rsrc_t r, int64_t elem) {
+  const auto w = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(elem * 4), 0, CP);
+  return __builtin_bit_cast(f32x4, w);
+}
+
+// ALT: waves of odd global index (by * 4 + w) walk their rows bottom-up.  A wave re-reads the 2b rows of y-halo past
+// each end of its block; walking down, a block's bottom halo is its lower neighbour's first rows, read ~a block's
+// time apart -- long enough at the HBM-sized grids for the XCD's L2 to have dropped them (25 % more HBM reads at
+// 32 rows, order 8).  Walking in alternate directions, two neighbouring blocks reach their shared boundary at the
+// same time (both at the start, or both at the end), so one of the two reads of each halo row hits L2 (the
+// neighbouring workgroup is blockIdx + nbx: the same XCD whenever nbx % 8 == 0, e.g. 12288-wide grids).  The window
+// is indexed by grid offset (win[B + dir * k] is row center + k), so every output is the same sum in the same order:
+// bitwise the one-direction kernel.
+template <int ORDER, int ROWS, int AHEAD = kLdsAhead, int CP = 0, int DIR = 1>
+__device__ __forceinline__ void stencil_lds_walk(float* __restrict__ next, const float* __restrict__ curr, int gx,
                                                  int gy, int nx, int ny, float xcfl, float ycfl, int bx, int by,
                                                  f32x4 (*xrow)[66]) {
+  constexpr int kLdsAhead = AHEAD;
   constexpr int B = Coef<ORDER>::B;
   constexpr int WIN = 2 * B + 1;
   static_assert(B <= 4, "x-neighbours within one float4 of each side");
@@ -180,25 +196,31 @@ __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const
   const int x0 = (bx * 64 + lane) * 4;  // first of this lane's 4 interior x
   const int y0 = (by * 4 + w) * ROWS;
   if (y0 >= ny) return;  // wave-uniform (no workgroup barrier below)
+  const int nrows = min(ROWS, ny - y0);
+  constexpr int dir = DIR;  // (a compile-time walk direction: the window's indices stay static, in registers)
+  // interior row of walk step r, and the grid row each step's window gains (its new edge row)
+  const int yfirst = dir > 0 ? y0 : y0 + nrows - 1;
+  auto ystep = [&](int r) { return yfirst + dir * r; };
+  auto qrow = [&](int r) { return ystep(r) + B + dir * B; };
   const __amdgpu_buffer_rsrc_t rc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(curr), (short)0, (int)((int64_t)gx * gy * 4), 0x00020000);
   const int64_t col = x0 + B;
   constexpr int64_t kOffOOB = (int64_t)0x7FFFFFF0 / 4;
-  f32x4 win[WIN];
+  f32x4 win[WIN];  // walk order: win[k] = grid row (center + (k - B) * dir)
 #pragma unroll
-  for (int k = 0; k < WIN - 1; ++k) win[k] = ld4(rc, (int64_t)(y0 + k) * gx + col);
+  for (int k = 0; k < WIN - 1; ++k) win[k] = ld4(rc, (int64_t)(ystep(0) + B + (k - B) * dir) * gx + col);
   // the strip's halo float4s of the centre row: lane 0 the one left of the strip, lane 63 the one right of it
-  auto halo = [&](int y) {
-    const int64_t rc0 = (int64_t)(y + B) * gx + col;
-    return ld4(rc, y < ny ? (lane == 0 ? rc0 - 4 : (lane == 63 ? rc0 + 4 : kOffOOB)) : kOffOOB);
+  auto halo = [&](int r) {
+    const int64_t rc0 = (int64_t)(ystep(r) + B) * gx + col;
+    return ld4p<CP>(rc, r < nrows ? (lane == 0 ? rc0 - 4 : (lane == 63 ? rc0 + 4 : kOffOOB)) : kOffOOB);
   };
-  // queues: q[i] = the window's new bottom row for row y0 + i (grid row y0 + i + 2B), hq[i] its halo (rows past the
-  // grid read the range-checked 0 and are never used)
+  // queues: q[i] = the window's new edge row for walk step i, hq[i] its halo (steps past the block read the
+  // range-checked 0 and are never used)
   f32x4 q[kLdsAhead], hq[kLdsAhead];
 #pragma unroll
   for (int i = 0; i < kLdsAhead; ++i) {
-    q[i] = ld4(rc, y0 + i < ny ? (int64_t)(y0 + i + 2 * B) * gx + col : kOffOOB);
-    hq[i] = halo(y0 + i);
+    q[i] = ld4p<CP>(rc, i < nrows ? (int64_t)qrow(i) * gx + col : kOffOOB);
+    hq[i] = halo(i);
   }
   auto wave_sync = [] {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -207,8 +229,8 @@ __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const
   };
 #pragma unroll
   for (int r = 0; r < ROWS; ++r) {
-    const int y = y0 + r;
-    if (y >= ny) break;
+    if (r >= nrows) break;
+    const int y = ystep(r);
     const int64_t rowc = (int64_t)(y + B) * gx + col;
     win[WIN - 1] = q[0];
     const f32x4 hv = hq[0];
@@ -217,9 +239,9 @@ __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const
       q[i] = q[i + 1];
       hq[i] = hq[i + 1];
     }
-    const int ya = y + kLdsAhead;  // the row whose loads go out now
-    q[kLdsAhead - 1] = ld4(rc, (r + kLdsAhead < ROWS && ya < ny) ? (int64_t)(ya + 2 * B) * gx + col : kOffOOB);
-    hq[kLdsAhead - 1] = halo(r + kLdsAhead < ROWS ? ya : ny);
+    const int ra = r + kLdsAhead;  // the walk step whose loads go out now
+    q[kLdsAhead - 1] = ld4p<CP>(rc, ra < nrows ? (int64_t)qrow(ra) * gx + col : kOffOOB);
+    hq[kLdsAhead - 1] = halo(ra);
     f32x4* row = xrow[r & 1];
     row[1 + lane] = win[B];
     if (lane == 0) row[0] = hv;
@@ -237,7 +259,8 @@ __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       o[j] = apply_stencil<ORDER>(
-          line[4 + j], [&](int k) { return line[4 + j + k]; }, [&](int k) { return win[B + k][j]; }, xcfl, ycfl);
+          line[4 + j], [&](int k) { return line[4 + j + k]; }, [&](int k) { return win[B + dir * k][j]; }, xcfl,
+          ycfl);
     float* dst = next + rowc;
     if (x0 + 4 <= nx && (rowc & 3) == 0) {
       __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(dst));
@@ -249,6 +272,16 @@ __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const
 #pragma unroll
     for (int k = 0; k < WIN - 1; ++k) win[k] = win[k + 1];
   }
+}
+
+template <int ORDER, int ROWS, int AHEAD = kLdsAhead, int CP = 0, bool ALT = false>
+__device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
+                                                 int gy, int nx, int ny, float xcfl, float ycfl, int bx, int by,
+                                                 f32x4 (*xrow)[66]) {
+  if (ALT && ((by * 4 + threadIdx.y) & 1))  // (wave-uniform)
+    stencil_lds_walk<ORDER, ROWS, AHEAD, CP, -1>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by, xrow);
+  else
+    stencil_lds_walk<ORDER, ROWS, AHEAD, CP, 1>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by, xrow);
 }
 
 // border strips: rows [0,b) and [gy-b,gy) (full width), columns [0,b) and [gx-b,gx) of the middle rows;
@@ -325,7 +358,50 @@ void launch(float* next, const float* curr, int gx, int gy, float xcfl, float yc
   else launch_v<ORDER, 3>(next, curr, gx, gy, xcfl, ycfl, scale, with_bc, s);
 }
 
+// the LDS variant's knobs, order 8, interior only (bench/stencil_tune.py): rows per wave, rows loaded ahead,
+// the streamed loads' cache policy
+template <int ROWS, int AHEAD, int CP, bool ALT>
+__global__ __launch_bounds__(256) void stencil_lds_tune_kernel(float* __restrict__ next, const float* __restrict__ curr,
+                                                               int gx, int gy, int nx, int ny, float xcfl, float ycfl,
+                                                               int nbx) {
+  __shared__ f32x4 xrow[4][2][66];
+  const int id = blockIdx.x;
+  stencil_lds_body<8, ROWS, AHEAD, CP, ALT>(next, curr, gx, gy, nx, ny, xcfl, ycfl, id % nbx, id / nbx,
+                                            xrow[threadIdx.y]);
+}
+
+template <int ROWS, int AHEAD, int CP, bool ALT = false>
+void launch_lds_tune(float* next, const float* curr, int gx, int gy, float xcfl, float ycfl, hipStream_t s) {
+  const int nx = gx - 8, ny = gy - 8;
+  const int nbx = (nx + 255) / 256, nby = (ny + 4 * ROWS - 1) / (4 * ROWS);
+  stencil_lds_tune_kernel<ROWS, AHEAD, CP, ALT><<<nbx * nby, dim3(64, 4), 0, s>>>(next, curr, gx, gy, nx, ny, xcfl,
+                                                                                  ycfl, nbx);
+}
+
 }  // namespace
+
+void stencil_lds_tune(float* next, const float* curr, int gx, int gy, float xcfl, float ycfl, int rows, int ahead,
+                      int nt, hipStream_t s) {
+  CME_REQUIRE((int64_t)gx * gy * 4 < (int64_t)0x7FFFFFF0, "stencil_lds_tune: grid too large for 32-bit offsets");
+  const int key = rows * 100 + ahead * 10 + (nt & 1) + (nt & 2 ? 100000 : 0);  // nt bit 1: alternate walk
+  switch (key) {
+    case 103240: launch_lds_tune<32, 4, 0, true>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 103280: launch_lds_tune<32, 8, 0, true>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 106480: launch_lds_tune<64, 8, 0, true>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 101680: launch_lds_tune<16, 8, 0, true>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 3240: launch_lds_tune<32, 4, 0>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 3241: launch_lds_tune<32, 4, 2>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 3280: launch_lds_tune<32, 8, 0>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 3281: launch_lds_tune<32, 8, 2>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 6440: launch_lds_tune<64, 4, 0>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 6480: launch_lds_tune<64, 8, 0>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 6481: launch_lds_tune<64, 8, 2>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 12880: launch_lds_tune<128, 8, 0>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 12881: launch_lds_tune<128, 8, 2>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    default: CME_REQUIRE(false, "stencil_lds_tune: (rows, ahead, nt) not instantiated");
+  }
+  CME_LAUNCH_CHECK(s);
+}
 
 void stencil_step(float* next, const float* curr, int gx, int gy, int order, float xcfl, float ycfl, int variant,
                   hipStream_t s) {

@@ -34,6 +34,11 @@ void bind_suite(py::module_& m) {
                          P<float>(w_out), P<const float>(inv), n, lpn, S(s));
   }, py::arg("indptr"), py::arg("edges"), py::arg("w_in"), py::arg("out"), py::arg("w_out"), py::arg("inv_deg"),
      py::arg("n"), py::arg("lpn"), py::arg("stream") = 0);
+  sm.def("stencil_lds_tune", [](uintptr_t next, uintptr_t curr, int gx, int gy, float xcfl, float ycfl, int rows,
+                                int ahead, int nt, uintptr_t s) {
+    stencil_lds_tune(P<float>(next), P<const float>(curr), gx, gy, xcfl, ycfl, rows, ahead, nt, S(s));
+  }, py::arg("next"), py::arg("curr"), py::arg("gx"), py::arg("gy"), py::arg("xcfl"), py::arg("ycfl"),
+     py::arg("rows"), py::arg("ahead"), py::arg("nt"), py::arg("stream") = 0);
   sm.def("stencil_step", [](uintptr_t next, uintptr_t curr, int gx, int gy, int order, float xcfl, float ycfl,
                             int variant, uintptr_t s) {
     stencil_step(P<float>(next), P<const float>(curr), gx, gy, order, xcfl, ycfl, variant, S(s));

@@ -42,6 +42,10 @@ void stencil_step(float* next, const float* curr, int gx, int gy, int order, flo
 // one launch per time step: interior stencil AND next(border) = curr(border) * scale (with_bc)
 void stencil_step_bc(float* next, const float* curr, int gx, int gy, int order, float xcfl, float ycfl, int variant,
                      float scale, bool with_bc, hipStream_t s);
+// the LDS variant at order 8 with its knobs exposed (rows per wave 32/64/128, rows loaded ahead 4/8, non-temporal
+// streamed loads), interior only: bench/stencil_tune.py
+void stencil_lds_tune(float* next, const float* curr, int gx, int gy, float xcfl, float ycfl, int rows, int ahead,
+                      int nt, hipStream_t s);
 // next(border) = curr(border) * scale  (border width b)
 void stencil_bc(float* next, const float* curr, int gx, int gy, int b, float scale, hipStream_t s);
 

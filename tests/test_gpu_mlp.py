@@ -749,3 +749,32 @@ def test_prefetch_of_a_partial_last_batch_stays_in_the_dataset(executor):
     ref.load(x, y)
     ref.train(2, 0.01, 1e-4)
     assert _rel(outs[1].cpu(), ref.engine.params.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("dt,path", [("f32", "split3"), ("bf16", "split1")])
+@pytest.mark.parametrize("H,n", [(4096, 800), (4096, 200), (4096, 336), (2048, 800)])
+def test_g64_wide_engine_is_bitwise_the_rega_engine(dt, path, H, n):
+    """The wide 128 x 128 K loop on the LDS-DMA engine (csrc/mlp/g64_gemm.h: both operands staged in full rows,
+    64-deep K steps) runs the same MFMA sequence per accumulator as the A-in-registers engine (rega_gemm.h): a
+    few training steps leave BITWISE the same parameters and loss partials, with the fused head (trainer setting)
+    and without it, and the weight gradients in gradient mode agree bitwise too."""
+    x, y = synthetic_mnist(3 * n + 7, seed=H + n)
+    nn = NeuralNetwork([784, H, 10])
+    outs = {}
+    for eng in (0, 1):
+        for fused in (True, False):
+            e = MlpEngine(nn.H, dtype=dt, max_cols=n, device="cuda", path=path)
+            e.set_params(*nn.params)
+            e.load_dataset(x, y)
+            e.set_store_a1(not fused)
+            e.set_fh_allgather(fused)
+            e._hip_step().wide_eng = eng
+            for k in range(3):
+                e.run(k * n, n, 1.0 / n, 1e-4, 0.05, sgd=True, with_loss=True)
+            e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=False)
+            torch.cuda.synchronize()
+            assert not e.kernel_error()
+            outs[(eng, fused)] = (e.params.clone(), e.grads.clone(), e.loss_buf.clone())
+    for fused in (True, False):
+        a, b = outs[(0, fused)], outs[(1, fused)]
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]), fused
