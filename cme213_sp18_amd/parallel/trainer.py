@@ -47,12 +47,13 @@ class CostModel:
     kernel_us: float = 7.5
     rccl_us: float = 25.0
     rccl_gbps: float = 64.0
+    hop_us: float = 1.0  # one one-way xGMI latency (a flag or a granule store seen by the peer): planning only
     measured: bool = False
 
     def as_record(self) -> dict:
         return {"xgmi_link_GBps": round(self.link_gbps, 2), "xgmi_kernel_us": round(self.kernel_us, 2),
                 "rccl_fixed_us": round(self.rccl_us, 2), "rccl_link_GBps": round(self.rccl_gbps, 2),
-                "measured": self.measured}
+                "hop_us_planning": self.hop_us, "measured": self.measured}
 
 
 COST_MODEL = CostModel()  # what the policy uses (set_cost_model replaces it)
@@ -82,6 +83,26 @@ def allreduce_cost_us(R: int, wire_bytes: int, shots: int, fp_bytes: int | None 
     ring = 2 * fb / (R * m.rccl_gbps * 1e3)
     hidden = min(m.rccl_us, ring) if fb > BUCKET_BYTES else 0.0
     return m.rccl_us + ring - hidden
+
+
+def fused_exchange_us(R: int, wire_bytes: int, form: str, model: CostModel | None = None) -> float:
+    """Predicted cost of the all-reduce fused into the weight-gradient launch, beyond the launch's own work
+    (bench/predict_scaling.py states the same model): "pull" (the one-shot: a flag one way, then a remote read
+    round trip of every peer's tile, S bytes per link) 3 hops + S / B; "push" (the owner-tile form: the tile one
+    way to its owner, the update one way back, 2 S / R payload per link each way, doubled by the 8-byte tagged
+    granules) 2 hops + 4 S / (R B)."""
+    m = model or COST_MODEL
+    bw = m.link_gbps * 1e3
+    if form == "pull":
+        return 3 * m.hop_us + wire_bytes / bw
+    return 2 * m.hop_us + 4 * wire_bytes / (R * bw)
+
+
+def auto_fused_form(R: int, wire_bytes: int, model: CostModel | None = None) -> str:
+    """The fused all-reduce's form by the cost model: the owner-tile push once its 4 S / R bytes per link and
+    one hop fewer beat the one-shot's S (R >= 4 at 784-100-10 with the planning constants), else the pull."""
+    return "push" if fused_exchange_us(R, wire_bytes, "push", model) < fused_exchange_us(R, wire_bytes, "pull",
+                                                                                          model) else "pull"
 
 
 def auto_allreduce_shots(R: int, wire_bytes: int, fp_bytes: int, bf16_wire: bool,
@@ -184,7 +205,7 @@ class DataParallelTrainer:
                  batch_size: int = 800, backend: str = "hip", shift: bool = True, use_graphs: bool = True,
                  normalize: bool = False, path: str = "auto", allreduce: str = "auto", overlap: bool = True,
                  overlap_chunks: int = 0, fuse_allreduce: bool = True, executor: str = "auto",
-                 grad_wire: str = "auto", fused_form: str = "push"):
+                 grad_wire: str = "auto", fused_form: str = "auto"):
         self.nn = nn
         # how run_plan enqueues a plan: "auto" = the native C++ step loop (MlpStep.run_steps) for plans of
         # consecutive full batches on the fused paths (pure device work), else the captured HIP graph;
@@ -201,9 +222,10 @@ class DataParallelTrainer:
         self.grad_wire = grad_wire
         # the all-reduce fused into the weight-gradient launch (H <= 128): "push" = the owner-tile form (each tile
         # reduced by one rank, pushed both ways as tagged granules: 2 one-way hops, 2 S / R payload per link),
-        # "pull" = the one-shot (every rank reads every peer's tile after its flag: S per link)
-        if fused_form not in ("push", "pull"):
-            raise ValueError("fused_form must be push or pull")
+        # "pull" = the one-shot (every rank reads every peer's tile after its flag: S per link), "auto" = the cost
+        # model's pick (auto_fused_form: push from 4 ranks at 784-100-10)
+        if fused_form not in ("push", "pull", "auto"):
+            raise ValueError("fused_form must be push, pull or auto")
         self.fused_form = fused_form
         # RCCL path: dW1 row chunks all-reduced while the next chunk is computed (0: ~BUCKET_BYTES each).
         # Setting it also forces the overlapped path with ONE rank of a real process group (nccl world 1),
@@ -250,6 +272,8 @@ class DataParallelTrainer:
         if (self.xgmi is not None and fuse_allreduce and self.xgmi.wire == self.engine.params.dtype
                 and self.xgmi.shots == 1):
             slots = self.engine.fused_allreduce_slots()
+            if self.fused_form == "auto":
+                self.fused_form = auto_fused_form(self.R, self.engine.params.numel() * 4)
             if slots and self.engine.params.dtype == torch.float32 and self._fused_fits(slots):
                 from .xgmi import XgmiBucket
 

@@ -111,3 +111,13 @@ def test_cost_model_probe_needs_a_gpu_group():
     from cme213_sp18_amd.parallel.comm import NullComm
 
     assert T.measure_cost_model(NullComm(), "cpu") is None
+
+
+def test_fused_form_policy_pushes_from_four_ranks():
+    """The fused all-reduce's form by the cost model (planning constants): the one-shot pull at 2 ranks (the push
+    form's tagged granules move 4 S / R = 2 S per link there), the owner-tile push from 4 ranks."""
+    T.set_cost_model(None)
+    s = 79_552 * 4
+    assert T.auto_fused_form(2, s) == "pull"
+    assert T.auto_fused_form(4, s) == "push" and T.auto_fused_form(8, s) == "push"
+    assert T.fused_exchange_us(8, s, "push") < T.fused_exchange_us(8, s, "pull")
