@@ -178,6 +178,10 @@ def main(argv=None):
                     e.attach_xgmi(_P, push=True)
                     row["wgrad_push1_us"] = round(timeit(part(2, 2), a.reps), 3)
                     row["step_push1_us"] = round(timeit(part(3, 2), a.reps), 3)
+                    for dbg in (1, 2, 3):  # ablations (SplitStepArgs::xp_dbg): no exchange, no put, neither
+                        step.xp_dbg = dbg
+                        row[f"wgrad_push1_dbg{dbg}_us"] = round(timeit(part(2, 2), a.reps), 3)
+                    step.xp_dbg = 0
                     torch.cuda.synchronize()
                     row["push1_err"] = xp.error()
                     e.attach_xgmi(None)

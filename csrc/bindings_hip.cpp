@@ -84,7 +84,10 @@ struct MlpStep {
   // (profiles/kbench_prefetch_wgs_r4.jsonl)
   int prefetch = 4;
   int prefetch_xt = 4;  // SplitStepArgs::pf_wgs_xt
-  int wide_eng = 0;     // SplitStepArgs::wide_eng: the 128 x 128 wide K loop's engine (0 rega, 1 g64)
+  int wide_eng = -1;    // SplitStepArgs::wide_eng: the 128 x 128 wide K loop's engine (0 rega, 1 g64; -1: g64 for bf16
+                        // A, rega for fp32 -- 784-4096-10 step bf16 39.1 -> 38.1 us, fp32 55.4 -> 58.0 with g64,
+                        // profiles/r5/kbench_wide_engines.jsonl)
+  int xp_dbg = 0;       // SplitStepArgs::xp_dbg (diagnostics)
   int ag64() const { return ag_tiles64 >= 0 ? ag_tiles64 : (store_a1 ? 0 : 1); }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
@@ -210,7 +213,8 @@ struct MlpStep {
     a.xcd_rows = xcd_rows && cme::mlp_split_xcd_rows_ok(a);
     a.pf_wgs = (a.xcd_rows && bias_col) ? prefetch : 0;
     a.pf_wgs_xt = (a.xcd_rows && bias_col) ? prefetch_xt : 0;
-    a.wide_eng = wide_eng;
+    a.wide_eng = wide_eng >= 0 ? wide_eng : (npw == 1 ? 1 : 0);
+    a.xp_dbg = xp_dbg;
     return a;
   }
 
@@ -514,6 +518,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("prefetch", &MlpStep::prefetch)
       .def_readwrite("prefetch_xt", &MlpStep::prefetch_xt)
       .def_readwrite("wide_eng", &MlpStep::wide_eng)
+      .def_readwrite("xp_dbg", &MlpStep::xp_dbg)
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
       .def_readwrite("planes_stale", &MlpStep::planes_stale)
       .def_readwrite("dw2p", &MlpStep::dw2p)

@@ -109,6 +109,9 @@ struct SplitStepArgs {
   // into registers, 32-deep stages), 1 g64_gemm.h (both operands LDS-DMA'd in full rows, 64-deep steps); the same
   // bits either way (MlpStep.wide_eng)
   int wide_eng = 0;
+  // diagnostics only (bench/kbench.py xp rows): ablations of the push form at world 1 -- bit0: no exchange
+  // (old - lr * own), bit1: no W1 / b1 put, bit2: dW1 tiles skip the LDS staging wait (no barrier)
+  int xp_dbg = 0;
   // wide layers: the head left dW2 partials [cdiv(n, 32)][16][H] (HeadArgs::dw2part); the dW2 role then sums
   // them in column-tile order instead of forming D . a1^T from all of a1
   float* dw2part = nullptr;

@@ -443,8 +443,9 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       }
       __syncthreads();  // xs / xo complete
       wstamp(4);
-      float nv;
-      if (!s_xf[1] && xp_exchange(a.xf, bid, s_xf, xs, 512, ok, ok ? xo[e] : 0.f, lr, &nv, wst) && ok) {
+      float nv = ok ? xo[e] - lr * xs[e] : 0.f;
+      if (!s_xf[1] && ((a.xp_dbg & 1) || xp_exchange(a.xf, bid, s_xf, xs, 512, ok, ok ? xo[e] : 0.f, lr, &nv, wst)) &&
+          ok && !(a.xp_dbg & 2)) {
         if (col < a.P) {
           a.W1[i] = nv;
           if (a.w1_planes) {

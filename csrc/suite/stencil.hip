@@ -168,6 +168,7 @@ constexpr int kVecRows = 8;
 //     (64 rows on the HBM-sized grids measured the same as 32: 5.54 vs 5.57 ms at 12288^2 x 20.)
 constexpr int kLdsRows = 32;
 constexpr int kLdsAhead = 4;
+constexpr bool kLdsAlt = true;  // the production variant's walk (stencil_lds_body ALT; bench/stencil_tune.py)
 
 // 16-byte load with a cache policy (CP: 0 default, 2 non-temporal: streamed, read once)
 template <int CP>
@@ -329,7 +330,8 @@ __global__ __launch_bounds__(256) void stencil_fused(float* __restrict__ next, c
   else if constexpr (VARIANT == 1) stencil_loop_body<ORDER, 8>(next, curr, gx, nx, ny, xcfl, ycfl, bx, by);
   else if constexpr (VARIANT == 2) {
     __shared__ f32x4 xrow[4][2][66];  // per wave: the centre row (+ halo), double-buffered by row parity
-    stencil_lds_body<ORDER, kLdsRows>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by, xrow[threadIdx.y]);
+    stencil_lds_body<ORDER, kLdsRows, kLdsAhead, 0, kLdsAlt>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by,
+                                                            xrow[threadIdx.y]);
   }
   else stencil_vec_body<ORDER, kVecRows>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by);
 }
