@@ -74,7 +74,9 @@ def main(argv=None):
         pref_xt = int(m.group(1)) if m else None
         m = re.search(r"\+g(\d)", path)  # "+gK": the wide 128 x 128 K loop's engine (MlpStep.wide_eng)
         weng = int(m.group(1)) if m else None
-        path = re.sub(r"\+[sdxptg]\d", "", path)
+        m = re.search(r"\+l(\d)", path)  # "+lK": the g64 engine's L2 pre-touch off / on (MlpStep.g64_touch)
+        gtouch = int(m.group(1)) if m else None
+        path = re.sub(r"\+[sdxptgl]\d", "", path)
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -89,6 +91,8 @@ def main(argv=None):
                     step.prefetch = pref
                 if weng is not None:
                     step.wide_eng = weng
+                if gtouch is not None:
+                    step.g64_touch = gtouch
                 if pref_xt is not None:
                     step.prefetch_xt = pref_xt
                 if no_a1:
@@ -100,7 +104,7 @@ def main(argv=None):
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else "") + (f"+g{weng}" if weng is not None else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else "") + (f"+g{weng}" if weng is not None else "") + (f"+l{gtouch}" if gtouch is not None else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(
@@ -178,7 +182,9 @@ def main(argv=None):
                     e.attach_xgmi(_P, push=True)
                     row["wgrad_push1_us"] = round(timeit(part(2, 2), a.reps), 3)
                     row["step_push1_us"] = round(timeit(part(3, 2), a.reps), 3)
-                    for dbg in (1, 2, 3):  # ablations (SplitStepArgs::xp_dbg): no exchange, no put, neither
+                    # ablations (SplitStepArgs::xp_dbg): 1 no dW1 exchange, 2 no dW1 put, 3 neither, 4 no dW2 exchange,
+                    # 8 no db2 row sums, 16 dW1 tiles stop after the GEMM, 32 dW2 tiles stop after the GEMM
+                    for dbg in (16, 20, 24, 32, 33, 34, 35, 48):
                         step.xp_dbg = dbg
                         row[f"wgrad_push1_dbg{dbg}_us"] = round(timeit(part(2, 2), a.reps), 3)
                     step.xp_dbg = 0

@@ -88,6 +88,8 @@ struct MlpStep {
                         // A, rega for fp32 -- 784-4096-10 step bf16 39.1 -> 38.1 us, fp32 55.4 -> 58.0 with g64,
                         // profiles/r5/kbench_wide_engines.jsonl)
   int xp_dbg = 0;       // SplitStepArgs::xp_dbg (diagnostics)
+  int g64_touch = 0;    // SplitStepArgs::g64_touch (measured slower: 784-4096-10 bf16 38.1 -> 41.7 us,
+                        // fp32 57.5 -> 62.6, profiles/r5/kbench_wide_touch.jsonl)
   int ag64() const { return ag_tiles64 >= 0 ? ag_tiles64 : (store_a1 ? 0 : 1); }
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
@@ -215,6 +217,7 @@ struct MlpStep {
     a.pf_wgs_xt = (a.xcd_rows && bias_col) ? prefetch_xt : 0;
     a.wide_eng = wide_eng >= 0 ? wide_eng : (npw == 1 ? 1 : 0);
     a.xp_dbg = xp_dbg;
+    a.g64_touch = g64_touch;
     return a;
   }
 
@@ -519,6 +522,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("prefetch_xt", &MlpStep::prefetch_xt)
       .def_readwrite("wide_eng", &MlpStep::wide_eng)
       .def_readwrite("xp_dbg", &MlpStep::xp_dbg)
+      .def_readwrite("g64_touch", &MlpStep::g64_touch)
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
       .def_readwrite("planes_stale", &MlpStep::planes_stale)
       .def_readwrite("dw2p", &MlpStep::dw2p)

@@ -23,6 +23,7 @@
 // caller's ONE dynamic LDS array of >= g64::lds_bytes<AT>() bytes.
 #pragma once
 
+#include "l2_touch.h"
 #include "rega_gemm.h"
 
 namespace cme {
@@ -43,17 +44,26 @@ template <typename AT>
 constexpr int stage_bytes() {
   return a_bytes<AT>() + kBBytes;
 }
+constexpr int kJunk = 8 * 1024;  // the L2 pre-touch's landing slot (1 KB per wave, never read)
 template <typename AT>
 constexpr int lds_bytes() {
-  return stages<AT>() * stage_bytes<AT>();
+  return stages<AT>() * stage_bytes<AT>() + kJunk;
 }
+
+// L2 pre-touch (g64_gemm_mainloop): the workgroups of one XCD that read the same A rows / B rows split pulling
+// ALL of them into the XCD's L2 at entry, so only the first K step waits a memory latency and the rest stream from
+// L2.  a_part / a_parts: this workgroup's share of its A rows [m0, m0 + 128) x K (parts 0: no touch); b_* the same
+// for B.  Speed only: any split is correct.
+struct Touch {
+  int a_part = 0, a_parts = 0, b_part = 0, b_parts = 0;
+};
 
 }  // namespace g64
 
 template <typename AT, int NKS = 0>
 __device__ __forceinline__ void g64_gemm_mainloop(const AT* __restrict__ A, int lda, const __hip_bfloat16* __restrict__ B,
                                                   int ldb, int M, int N, int K, int m0, int n0, char* __restrict__ lds,
-                                                  f32x4 (&acc)[1][8]) {
+                                                  f32x4 (&acc)[1][8], g64::Touch touch = {}) {
   using namespace g64;
   constexpr bool F32 = sizeof(AT) == 4;
   constexpr int S = stages<AT>();
@@ -138,6 +148,13 @@ __device__ __forceinline__ void g64_gemm_mainloop(const AT* __restrict__ A, int 
     else gl::wait_vm<0>();
   };
 
+  if (touch.a_parts > 0) {  // (older than every DMA below: the first K step's counted wait covers them)
+    char* junk = lds + S * SB;
+    l2_touch_nowait(A, (int64_t)m0 * lda * (int)sizeof(AT), min(128, M - m0), (int64_t)lda * (int)sizeof(AT),
+                    (int64_t)K * (int)sizeof(AT), touch.a_part, touch.a_parts, junk);
+    l2_touch_nowait(B, (int64_t)n0 * ldb * 2, min(128, N - n0), (int64_t)ldb * 2, (int64_t)K * 2, touch.b_part,
+                    touch.b_parts, junk);
+  }
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(s);

@@ -112,6 +112,8 @@ struct SplitStepArgs {
   // diagnostics only (bench/kbench.py xp rows): ablations of the push form at world 1 -- bit0: no exchange
   // (old - lr * own), bit1: no W1 / b1 put, bit2: dW1 tiles skip the LDS staging wait (no barrier)
   int xp_dbg = 0;
+  // the g64 wide engine pulls each XCD's A and B tiles into its L2 at entry (g64::Touch; MlpStep.g64_touch)
+  int g64_touch = 1;
   // wide layers: the head left dW2 partials [cdiv(n, 32)][16][H] (HeadArgs::dw2part); the dW2 role then sums
   // them in column-tile order instead of forming D . a1^T from all of a1
   float* dw2part = nullptr;

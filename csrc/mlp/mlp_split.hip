@@ -432,6 +432,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
                                                                 static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
                                                                 red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
     wstamp(1);
+    if (push && (a.xp_dbg & 16)) return;  // (diagnostics: no exchange work at all after the tile)
     if (push) {  // the owner-tile exchange: thread e holds element (e / 32, e % 32) of the tile
       const int e = threadIdx.x, row = g.m0 + e / 32, col = g.n0 + e % 32;
       const bool ok = e < 512 && row < g.M && col < g.N;
@@ -510,14 +511,12 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     const int64_t half = push ? 0 : (int64_t)(s_xf[0] & 1u) * a.xf.npad;
     if (live && !push) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
     EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, push ? 2 : (live ? 1 : 0), reg, lr, {}, a.ag_err};
-    float b2old = 0.f;  // (push, tile 0: b2 for the owner's update, loaded before the K loop)
     XpWords xw;
     if (push) {
       epi.xs = xs;
       epi.xo = xs + kXpTile;
       epi.n0 = tb * 16;
       if (threadIdx.x == 0) xw = xp_words_issue(a.xf, bid, a.ag_err);
-      if (tb == 0 && threadIdx.x >= 256 && threadIdx.x < 256 + a.C) b2old = a.b2[threadIdx.x - 256];
     }
     if (a.dw2part) {  // the head's per-column-tile partials, summed in tile order (16 rows x C classes)
       const int nct = (a.n + a.dw2_cols - 1) / a.dw2_cols, e = threadIdx.x, c = e >> 4, h = tb * 16 + (e & 15);
@@ -539,45 +538,65 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     } else {
       wsk_tile<float, 1, 1, kWKS, true, true, 0, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red);
     }
-    if (!live) return;
-    const bool with_b2 = tb == 0;  // db2 (fused mode has no separate bias role): one wave per class
-    if (with_b2) {
-      for (int c = wv; c < a.C; c += kWKS) {
-        const float sc = wave_sum(row_sum(a.D + (size_t)c * a.ld, a.n, lane));
-        if (lane == 0) {
-          if (push) xs[256 + c] = sc;
-          else xf_store(static_cast<float*>(a.xf.mybuf), half + a.xf.off_b2 + c, sc);
-        }
-      }
-    }
-    if (push) {  // the owner-tile exchange: element e < 256 is W2[e / 16][tb * 16 + e % 16], 256 + c is b2[c]
+    if (!live || (push && (a.xp_dbg & 32))) return;  // (xp_dbg 32: diagnostics, the roles stop after the GEMM)
+    if (push) {  // the owner-tile exchange: element e < 256 is W2[e / 16][tb * 16 + e % 16]
       const int e = threadIdx.x, c = e / 16, h = tb * 16 + e % 16;
-      const bool isb = e >= 256, ok = isb ? (with_b2 && e - 256 < a.C) : (c < a.C && h < a.H);
-      const int64_t i = isb ? e - 256 : (int64_t)c * a.H + h;
+      const bool ok = e < 256 && c < a.C && h < a.H;
+      const int64_t i = (int64_t)c * a.H + h;
       if (threadIdx.x == 0) {
         xp_words_wait(xw);
         s_xf[0] = xw.ep_old + 1;
         s_xf[1] = (xw.err | xw.agerr) != 0;
       }
       __syncthreads();  // xs / xo complete
-      const float old = !ok ? 0.f : isb ? b2old : xs[kXpTile + e];
-      float nv;
-      if (!s_xf[1] && xp_exchange(a.xf, bid, s_xf, xs, 256 + a.C, ok, old, lr, &nv) && ok) (isb ? a.b2 : a.W2)[i] = nv;
+      const float old = ok ? xs[kXpTile + e] : 0.f;
+      float nv = ok ? old - lr * xs[e] : 0.f;  // (xp_dbg 4: diagnostics, no exchange -- world 1's own value)
+      if (!s_xf[1] && ((a.xp_dbg & 4) || xp_exchange(a.xf, bid, s_xf, xs, 256, ok, old, lr, &nv)) && ok) a.W2[i] = nv;
       return;
     }
     if (!xf_exchange(a.xf, bid, s_xf)) return;
-    const int ne = 16 * 16 + (with_b2 ? a.C : 0);
-    for (int e = threadIdx.x; e < ne; e += kWT) {
-      if (e < 256) {
-        const int c = e / 16, h = tb * 16 + e % 16;
-        if (c >= a.C || h >= a.H) continue;
-        const int64_t i = (int64_t)c * a.H + h;
-        a.W2[i] -= lr * xf_sum(a.xf, half + a.xf.off_W2 + i);
-      } else {
-        const int c = e - 256;
-        a.b2[c] -= lr * xf_sum(a.xf, half + a.xf.off_b2 + c);
+    for (int e = threadIdx.x; e < 256; e += kWT) {
+      const int c = e / 16, h = tb * 16 + e % 16;
+      if (c >= a.C || h >= a.H) continue;
+      const int64_t i = (int64_t)c * a.H + h;
+      a.W2[i] -= lr * xf_sum(a.xf, half + a.xf.off_W2 + i);
+    }
+    xf_end(a.xf, bid, s_xf);
+    return;
+  }
+  if (fused) {  // ---- db2 (the fused launch's last role, exchange tile t1 + t2): one wave per class, in parallel
+    //               with the dW1 / dW2 tiles (inside the first dW2 tile it was a dependent pass over D after the
+    //               tile's GEMM, on the launch's critical path: -0.9 us at world 1, bench/kbench.py xp_dbg rows)
+    if (bid != t1 + t2) return;
+    const bool push = a.xf.push;
+    const bool live = push || xf_begin(a.xf, bid, s_xf, a.ag_err);
+    if (!live) return;
+    const int64_t half = push ? 0 : (int64_t)(s_xf[0] & 1u) * a.xf.npad;
+    XpWords xw;
+    if (push && threadIdx.x == 0) xw = xp_words_issue(a.xf, bid, a.ag_err);
+    const float bold = (int)threadIdx.x < a.C ? a.b2[threadIdx.x] : 0.f;
+    for (int c = wv; c < a.C; c += kWKS) {
+      const float sc = wave_sum(row_sum(a.D + (size_t)c * a.ld, a.n, lane));
+      if (lane == 0) {
+        if (push) xs[c] = sc;
+        else xf_store(static_cast<float*>(a.xf.mybuf), half + a.xf.off_b2 + c, sc);
       }
     }
+    if (push) {
+      const int e = threadIdx.x;
+      const bool ok = e < a.C;
+      if (threadIdx.x == 0) {
+        xp_words_wait(xw);
+        s_xf[0] = xw.ep_old + 1;
+        s_xf[1] = (xw.err | xw.agerr) != 0;
+      }
+      __syncthreads();  // xs complete
+      float nv = ok ? bold - lr * xs[e] : 0.f;
+      if (!s_xf[1] && ((a.xp_dbg & 8) || xp_exchange(a.xf, bid, s_xf, xs, a.C, ok, bold, lr, &nv)) && ok) a.b2[e] = nv;
+      return;
+    }
+    if (!xf_exchange(a.xf, bid, s_xf)) return;
+    for (int c = threadIdx.x; c < a.C; c += kWT) a.b2[c] = bold - lr * xf_sum(a.xf, half + a.xf.off_b2 + c);
     xf_end(a.xf, bid, s_xf);
     return;
   }
@@ -1172,6 +1191,22 @@ __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn
 // a1 = sigmoid(W1 X + b1) on the A-in-registers engine (rega_gemm.h): W1 read as fp32 and split into the
 // exact bf16 planes in registers (AT = float), or the bf16 plane 0 (AT = bf16, split1); z2 partials of
 // this 128-row tile as in fwd1_glds_kernel
+// The g64 engine's L2 pre-touch shares (g64::Touch) for a 128 x 128 tiling of `nwg` workgroups, tn column tiles,
+// remapped by xcd_remap (each XCD holds a contiguous id range, i.e. whole rows of tiles when its range is a multiple
+// of tn): the tn workgroups of a tile row share its A rows, the tile rows of one XCD share each B column tile.
+// SplitStepArgs::g64_touch 0: none.
+__device__ __forceinline__ g64::Touch g64_touch(const SplitStepArgs& a, int id, int nwg, int tn) {
+  g64::Touch t;
+  if (!a.g64_touch) return t;
+  const int per_xcd = (nwg + 7) / 8, rows_per_xcd = per_xcd / tn;
+  if (rows_per_xcd < 1 || per_xcd % tn != 0) return t;
+  t.a_part = id % tn;
+  t.a_parts = tn;
+  t.b_part = (id / tn) % rows_per_xcd;
+  t.b_parts = rows_per_xcd;
+  return t;
+}
+
 template <typename AT, int WC, int NKS, bool AG = false, int ENG = 0>
 __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn, RegaAgArgs ag = {}) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
@@ -1204,7 +1239,7 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
   if constexpr (ENG == 1) {
     static_assert(WC == 1, "g64 engine: the 8 x 1 wave layout");
     g64_gemm_mainloop<AT, (NKS > 0 ? (NKS * 32 + 63) / 64 : 0)>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0,
-                                                               n0, lds_dyn, acc);
+                                                               n0, lds_dyn, acc, g64_touch(a, id, gridDim.x, tn));
   } else {
     rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.P, static_cast<const bf16*>(a.Xw), a.P, H, n, a.P, m0, n0, lds_dyn, acc);
   }
@@ -1311,7 +1346,8 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
   if constexpr (ENG == 1) {
     static_assert(WC == 1, "g64 engine: the 8 x 1 wave layout");
     g64_gemm_mainloop<AT, (NKS > 0 ? (NKS * 32 + 63) / 64 : 0)>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M,
-                                                               P + a.bias_col, a.n, m0, n0, lds_dyn, acc);
+                                                               P + a.bias_col, a.n, m0, n0, lds_dyn, acc,
+                                                               g64_touch(a, id, tbig, tn));
   } else {
     rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0,
                                          n0, lds_dyn, acc);
@@ -1683,10 +1719,10 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   const int t2 = do_roles ? cdiv(a.H, 16) : 0;
   if (fused)
     CME_REQUIRE(do_w1 && do_roles && a.bias_col && a.w1_row0 == 0 && a.w1_rows < 0 && a.C <= 16 &&
-                    a.xf.world <= 8 && t1 + t2 <= mlp_split_fused_tiles(a.P, a.H, 1 << 30),
+                    a.xf.world <= 8 && t1 + t2 + 1 <= mlp_split_fused_tiles(a.P, a.H, 1 << 30),
                 "wgrad: fused all-reduce needs the whole small-layer step with the all-ones XT feature");
-  // fused mode: db2 comes from the first dW2 tile (no separate bias role)
-  const int tb = (do_roles && !fused) ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
+  // fused mode: db2 is one role workgroup of its own (exchange tile t1 + t2)
+  const int tb = !do_roles ? 0 : fused ? 1 : cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS);
   if (t1 + t2 + tb == 0) {
     CME_LAUNCH_CHECK(s);
     return;
@@ -1719,7 +1755,8 @@ bool mlp_split_xcd_rows_ok(const SplitStepArgs& a) {
 }
 
 int mlp_split_fused_tiles(int P, int H, int cap) {
-  const int t = cdiv(P + 1, 16 * kWNB) * cdiv(H, 16 * kWMB) + cdiv(H, 16);
+  // dW1 tiles, dW2 tiles, the db2 workgroup
+  const int t = cdiv(P + 1, 16 * kWNB) * cdiv(H, 16 * kWMB) + cdiv(H, 16) + 1;
   return t <= cap ? t : -1;
 }
 
