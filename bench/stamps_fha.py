@@ -22,6 +22,8 @@ def main(argv=None):
     ap.add_argument("--xcd-rows", type=int, default=None, help="MlpStep.xcd_rows (default: the engine's)")
     ap.add_argument("--warm-fwd", action="store_true",
                     help="one extra forward before the stamped one: W1 last READ, not written, by the previous launch")
+    ap.add_argument("--head-dw2", type=int, default=None, help="MlpStep.head_dw2 (default: the engine's)")
+    ap.add_argument("--store-a1", type=int, default=None, help="MlpEngine.set_store_a1 (default: the engine's)")
     a = ap.parse_args(argv)
     import numpy as np
     import torch
@@ -39,6 +41,10 @@ def main(argv=None):
     assert step.fh_allgather == 1
     if a.xcd_rows is not None:
         step.xcd_rows = a.xcd_rows
+    if a.head_dw2 is not None:
+        step.head_dw2 = a.head_dw2
+    if a.store_a1 is not None:
+        e.set_store_a1(bool(a.store_a1))
     st = torch.cuda.current_stream().cuda_stream
     buf = torch.zeros(4096 * 4, dtype=torch.int64, device="cuda")
     wbuf = torch.zeros(4096 * 8 * 4, dtype=torch.int64, device="cuda")
@@ -70,7 +76,7 @@ def main(argv=None):
         w = wbuf.view(-1, 4).cpu().numpy().astype(np.int64)
         w = w[w[:, 0] > 0]
         wr = (w - t0) * 10.0 / 1000.0
-        print(json.dumps({"wgs": int(len(s)), "entry": pct(rel[:, 0]), "published": pct(rel[:, 1]),
+        print(json.dumps({"head_dw2": int(step.head_dw2), "store_a1": int(step.store_a1), "wgs": int(len(s)), "entry": pct(rel[:, 0]), "published": pct(rel[:, 1]),
                           "all_arrived": pct(rel[:, 2]), "wait": pct(rel[:, 2] - rel[:, 1]), "end": pct(rel[:, 3]),
                           "wave_entry": pct(wr[:, 0]), "wave_kloop": pct(wr[:, 1]), "wave_reduced": pct(wr[:, 2]),
                           "wave_epilogue": pct(wr[:, 3]), "kloop_dur": pct(wr[:, 1] - wr[:, 0]),

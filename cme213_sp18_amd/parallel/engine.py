@@ -167,12 +167,15 @@ class MlpEngine:
             self.z2buf = torch.zeros(int(hip().head_big_scratch_floats(H, ld)), dtype=torch.float32, device=dev)
             # dW2 partials the wide head leaves per 32-column tile ([tile][16][H]) for the weight-gradient launch
             self.dw2buf = torch.zeros((ld + 31) // 32 * 16 * H, dtype=torch.float32, device=dev)
+        elif self.backend == "hip" and self.np and H <= 128 and C <= 16:
+            # ... and the H <= 128 all-gather forward + head (MlpStep.head_dw2)
+            self.dw2buf = torch.zeros((ld + 31) // 32 * 16 * H, dtype=torch.float32, device=dev)
         nblk = (ld + 15) // 16
         self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
         # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
         # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
         self.fh_counters = None
-        self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = None
+        self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = self.w2g = None
         if self.backend == "hip" and self.np and H <= 128 and C <= 16:
             tiles = (ld + 31) // 32
             self.fh_counters = torch.zeros(tiles, dtype=torch.int32, device=dev)
@@ -181,6 +184,10 @@ class MlpEngine:
             self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)  # one 256-B line each
             self.ag_slabs = torch.zeros(tiles * 8 * 16 * 32, dtype=torch.int64, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
+            # the dW2 role split over workgroups (SplitStepArgs::w2_ks <= 8): per 16-column tile a monotonic epoch
+            # counter (one 64-B line) and 7 x 256 partial-tile granules (tags only grow: never re-zeroed)
+            t2 = (H + 15) // 16
+            self.w2g = torch.zeros(t2 * 8 + t2 * 7 * 256, dtype=torch.int64, device=dev)
         elif self.backend == "hip" and self.np and H >= 512 and C <= 16 and self.dw2buf is not None:
             # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_wide_ag) uses one
             # monotonic counter per column tile -- a separate array per tiling (128 x 128 / 64 x 64) -- and
@@ -361,7 +368,7 @@ class MlpEngine:
                          dZ1p=ptr(self.dZ1p))
             if self.fh_counters is not None:
                 b.update(fh_counters=ptr(self.fh_counters), fh_tiles=int(self.fh_counters.numel()),
-                         ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs))
+                         ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs), w2g=ptr(self.w2g))
             elif self.ag_gran is not None:  # the wide fused head
                 b.update(fh_tiles=int(self.ag_counters.numel()) // 64,  # [2 tilings][tiles][32]
                          ag_gran=ptr(self.ag_gran), ag_gran_count=int(self.ag_gran.numel()),

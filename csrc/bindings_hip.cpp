@@ -87,6 +87,15 @@ struct MlpStep {
   int wide_eng = -1;    // SplitStepArgs::wide_eng: the 128 x 128 wide K loop's engine (0 rega, 1 g64; -1: g64 for bf16
                         // A, rega for fp32 -- 784-4096-10 step bf16 39.1 -> 38.1 us, fp32 55.4 -> 58.0 with g64,
                         // profiles/r5/kbench_wide_engines.jsonl)
+  // SplitStepArgs::w2_ks, the dW2 role's workgroups per tile (H <= 128 launches without the fused exchange or the
+  // head's dW2 partials; needs w2g).  Measured no faster, so off by default: 784-100-10 roles-only launch at n = 800
+  // 5.02 (1) / 4.98 (2) / 5.06 (4) / 5.21 us (8), and +0.7 us at n = 400 -- the granule hand-off to slice 0 costs
+  // what the shorter K loops save (profiles/r5/kbench_w2_split.jsonl, stamps_roles_w2_split.jsonl)
+  int w2_ks = 1;
+  uintptr_t w2g = 0;
+  // H <= 128, the all-gather forward + head: it also leaves the dW2 partials per 32 columns (fha_body step 5) for
+  // the weight-gradient launch's dW2 role (needs dw2p); 0: the role forms D . a1^T over the batch itself
+  int head_dw2 = 1;
   int xp_dbg = 0;       // SplitStepArgs::xp_dbg (diagnostics)
   int g64_touch = 0;    // SplitStepArgs::g64_touch (measured slower: 784-4096-10 bf16 38.1 -> 41.7 us,
                         // fp32 57.5 -> 62.6, profiles/r5/kbench_wide_touch.jsonl)
@@ -175,6 +184,7 @@ struct MlpStep {
       else if (k == "ag_counters") ag_counters = u(); else if (k == "ag_slabs") ag_slabs = u();
       else if (k == "ag_gran") ag_gran = u(); else if (k == "ag_gran_count") ag_gran_count = v.cast<int64_t>();
       else if (k == "kpart") kpart = u(); else if (k == "kpart_cap") kpart_cap = v.cast<int64_t>();
+      else if (k == "w2g") w2g = u();
       else throw std::invalid_argument("MlpStep.bind: unknown name '" + k + "'");
     }
   }
@@ -218,6 +228,8 @@ struct MlpStep {
     a.wide_eng = wide_eng >= 0 ? wide_eng : (npw == 1 ? 1 : 0);
     a.xp_dbg = xp_dbg;
     a.g64_touch = g64_touch;
+    a.w2g = P_<unsigned long long>(w2g);
+    a.w2_ks = (w2g && ag_err) ? w2_ks : 1;  // (a slice timeout reports through ag_err)
     return a;
   }
 
@@ -264,8 +276,19 @@ struct MlpStep {
             // training (store_a1 off): with the all-ones XT feature the dW1 launch reads only the dZ1 planes (db1 is
             // its column P) unless it splits fp32 dZ1 itself -- the fp32 dZ1 store is then skipped
             cme::HeadArgs hg = h;
+            cme::SplitStepArgs fa = a;
             if (!store_a1 && bias_col && !dz32 && hg.dZ1_planes) hg.dZ1 = nullptr;
-            cme::mlp_fwd1_head_ag(a, hg, P_<unsigned long long>(ag_counters), P_<unsigned long long>(ag_slabs),
+            if (head_dw2 && dw2p && C <= 16) {  // the head leaves the dW2 partials (fha_body step 5); then
+              // nothing after this launch reads a1: not stored in training (store_a1 off)
+              hg.dw2part = P_<float>(dw2p);
+              a.dw2part = hg.dw2part;
+              a.dw2_cols = 32;
+              if (!store_a1) {
+                fa.a1 = nullptr;
+                hg.a1 = nullptr;
+              }
+            }
+            cme::mlp_fwd1_head_ag(fa, hg, P_<unsigned long long>(ag_counters), P_<unsigned long long>(ag_slabs),
                                   P_<int>(ag_err), fh_tiles, S(stream));
           } else if (fh_counters && !(parts & 12) && cme::mlp_fwd1_head_ok(a, h)) {  // one launch
             cme::mlp_fwd1_head(a, h, P_<unsigned>(fh_counters), fh_tiles, S(stream));
@@ -512,6 +535,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readonly("split", &MlpStep::split)
       .def_readwrite("shift", &MlpStep::shift)
       .def_readwrite("ag_err", &MlpStep::ag_err)
+      .def_readwrite("w2_ks", &MlpStep::w2_ks)
+      .def_readwrite("head_dw2", &MlpStep::head_dw2)
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
       .def_readwrite("ag_wait_us", &MlpStep::ag_wait_us)
       .def_readwrite("ag_test_skip", &MlpStep::ag_test_skip)

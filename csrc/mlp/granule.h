@@ -23,9 +23,9 @@ using gran_t = unsigned long long;
 // and in the per-stage-barrier GEMM engines, on the critical path of every wave.  As inline asm the add is
 // counted by the hardware in issue order like any load, so every later vmcnt wait covers it (waits only get
 // stricter), and gran_epoch_wait names the result register so no use of it is scheduled above the wait.
-__device__ __forceinline__ gran_t gran_epoch_add(gran_t* p) {
+__device__ __forceinline__ gran_t gran_epoch_add(gran_t* p, gran_t amount = 1) {
   gran_t old;
-  asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0" : "=v"(old) : "v"(p), "v"((gran_t)1) : "memory");
+  asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0" : "=v"(old) : "v"(p), "v"(amount) : "memory");
   return old;
 }
 __device__ __forceinline__ void gran_epoch_wait(gran_t& old) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(old)::"memory"); }
