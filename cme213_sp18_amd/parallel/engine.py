@@ -168,8 +168,8 @@ class MlpEngine:
             # dW2 partials the wide head leaves per 32-column tile ([tile][16][H]) for the weight-gradient launch
             self.dw2buf = torch.zeros((ld + 31) // 32 * 16 * H, dtype=torch.float32, device=dev)
         elif self.backend == "hip" and self.np and H <= 128 and C <= 16:
-            # ... and the H <= 128 all-gather forward + head (MlpStep.head_dw2)
-            self.dw2buf = torch.zeros((ld + 31) // 32 * 16 * H, dtype=torch.float32, device=dev)
+            # ... and the H <= 128 all-gather forward + head (MlpStep.head_dw2: two 16-column partials per tile)
+            self.dw2buf = torch.zeros((ld + 31) // 32 * 2 * 16 * H, dtype=torch.float32, device=dev)
         nblk = (ld + 15) // 16
         self.loss_buf = torch.zeros(max(nblk, 1), dtype=torch.float32, device=dev)
         # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
@@ -286,10 +286,12 @@ class MlpEngine:
         self._step = None
 
     def set_store_a1(self, on: bool) -> None:
-        """Wide split layers with the head fused into the forward launch: False skips the a1 store (no kernel
-        of the training step reads a1 there: dZ1 and the dW2 partials come out of the same launch).  (At
-        H <= 128 the all-gather head leaving dW2 partials so that a1 need not be stored measured 0.2-0.3 us
-        per step SLOWER, profiles/kbench_dw2_partials_r3.jsonl: the dW2 roles are not the critical path.)"""
+        """Split layers with the head fused into the forward launch: False skips the a1 store whenever that launch
+        also leaves the dW2 partials (no kernel of the training step reads a1 then: dZ1 and the partials come out
+        of the same launch).  Wide layers: always; H <= 128: from n = 512 columns (MlpStep.head_dw2 auto), where
+        the weight-gradient launch's dW2 GEMM over the whole batch was that launch's critical path
+        (bench/stamps_roles.py: roles end 5.99 -> 3.74 us at n = 800; below, the partials cost the forward more
+        than they save -- profiles/r5/)."""
         self.store_a1 = bool(on)
         if self._step is not None:
             self._step.store_a1 = int(self.store_a1)

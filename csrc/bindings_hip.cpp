@@ -93,9 +93,10 @@ struct MlpStep {
   // what the shorter K loops save (profiles/r5/kbench_w2_split.jsonl, stamps_roles_w2_split.jsonl)
   int w2_ks = 1;
   uintptr_t w2g = 0;
-  // H <= 128, the all-gather forward + head: it also leaves the dW2 partials per 32 columns (fha_body step 5) for
-  // the weight-gradient launch's dW2 role (needs dw2p); 0: the role forms D . a1^T over the batch itself
-  int head_dw2 = 1;
+  // H <= 128, the all-gather forward + head: it also leaves the dW2 partials per 32 columns (fha_body step 4a) for
+  // the weight-gradient launch's dW2 role (needs dw2p); 0: the role forms D . a1^T over the batch itself; -1 (auto):
+  // from n = 512 columns, where the role's GEMM is the weight-gradient launch's critical path
+  int head_dw2 = -1;
   int xp_dbg = 0;       // SplitStepArgs::xp_dbg (diagnostics)
   int g64_touch = 0;    // SplitStepArgs::g64_touch (measured slower: 784-4096-10 bf16 38.1 -> 41.7 us,
                         // fp32 57.5 -> 62.6, profiles/r5/kbench_wide_touch.jsonl)
@@ -278,11 +279,11 @@ struct MlpStep {
             cme::HeadArgs hg = h;
             cme::SplitStepArgs fa = a;
             if (!store_a1 && bias_col && !dz32 && hg.dZ1_planes) hg.dZ1 = nullptr;
-            if (head_dw2 && dw2p && C <= 16) {  // the head leaves the dW2 partials (fha_body step 5); then
+            if ((head_dw2 > 0 || (head_dw2 < 0 && n >= 512)) && dw2p && C <= 16) {  // the head leaves the dW2 partials (fha_body step 5); then
               // nothing after this launch reads a1: not stored in training (store_a1 off)
               hg.dw2part = P_<float>(dw2p);
               a.dw2part = hg.dw2part;
-              a.dw2_cols = 32;
+              a.dw2_cols = 16;  // (fha_body step 4a: two partials per 32-column tile)
               if (!store_a1) {
                 fa.a1 = nullptr;
                 hg.a1 = nullptr;

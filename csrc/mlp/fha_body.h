@@ -180,7 +180,40 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     }
   }
   if (s_bad) return;  // (zs holds D) a timed-out wait: nothing more is written
-  // ---- 4. dZ1 = (W2^T D) .* a1 .* (1 - a1) for this tile's 16 rows, one element per thread
+  // ---- 4a. (h.dw2part) this tile's dW2 partials D[:, 16 columns] . a1[tile rows, 16 columns]^T into
+  // dw2part[16-column block][16 classes][H] (SplitStepArgs::dw2part, dw2_cols = 16): the weight-gradient launch's
+  // dW2 role then sums cdiv(n, 16) partials per element (32 KB per 16-row tile at n = 800) instead of pulling D and
+  // its a1 rows over the whole batch (~114 KB through one CU: the launch's critical path, bench/stamps_roles.py),
+  // and nothing reads a1 after this launch.  Two waves, 4 x v_mfma_f32_16x16x4_f32 each from the LDS tiles (lane:
+  // class l & 15 / row l & 15, k = column 4 s + (l >> 4)); zs holds D (0 past n and past C).  (One wave over all
+  // 32 columns: forward + head +0.37 us; the 8 MFMAs' chain sat in front of that wave's dZ1 stores.)
+  if (h.dw2part && t >= 384) {  // waves 6 and 7: columns [16 (w - 6), + 16) each, its own partial
+    const int l = t & 63, l16 = l & 15, kg = l >> 4, half = (t >> 6) - 6;
+    const bool rok = r0 + l16 < H;
+    // (every LDS operand read first, unmasked -- the addresses are inside the tiles -- and masked by a select, so
+    // the 8 reads issue back to back and the 4 MFMAs follow without a wait between them)
+    float za[4], ab[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      za[s] = zs[l16][16 * half + 4 * s + kg];
+      ab[s] = a1s[l16][16 * half + 4 * s + kg];
+    }
+    f32x4 p = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      p = __builtin_amdgcn_mfma_f32_16x16x4f32(za[s], (rok && c0 + 16 * half + 4 * s + kg < n) ? ab[s] : 0.f, p, 0,
+                                               0, 0);
+    const __amdgpu_buffer_rsrc_t rp = make_rsrc(h.dw2part);
+    const int pt = 2 * ct + half;  // partial index: 16 columns each
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cls = 4 * kg + i;
+      const float v = p[i];  // (a copy: hipcc bit-casts an ext-vector element lvalue as element 0)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rp,
+                                            (rok && cls < C) ? ((pt * 16 + cls) * H + r0 + l16) * 4 : kOOB, 0, 0);
+    }
+  }
+  // ---- 4b. dZ1 = (W2^T D) .* a1 .* (1 - a1) for this tile's 16 rows, one element per thread
   {
     const int r = t >> 5;  // (col as above)
     const int row = r0 + r, gcol = c0 + col;
@@ -217,36 +250,6 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
         const int off = (int)((p * pstride + (size_t)row * h.ldz + ce) * 2);
         if ((p & 1) == (col & 1)) __builtin_amdgcn_raw_buffer_store_b32(w, rp, pok ? off : kOOB, 0, 0);
       }
-    }
-  }
-  // ---- 5. (h.dw2part) this tile's dW2 partial D[:, 32 columns] . a1[tile rows, 32 columns]^T into
-  // dw2part[column tile][16 classes][H] (SplitStepArgs::dw2part, dw2_cols = 32): the weight-gradient launch's dW2
-  // role then sums cdiv(n, 32) partials per element (25.6 KB per 16-row tile at n = 800) instead of pulling D and
-  // its a1 rows over the whole batch (~114 KB through one CU: the launch's critical path, bench/stamps_roles.py),
-  // and nothing reads a1 after this launch.  One wave, 8 x v_mfma_f32_16x16x4_f32 over the 32 columns from the
-  // LDS tiles (lane: class l & 15 / row l & 15, k = column 4 s + (l >> 4)); zs holds D (0 past n and past C).
-  if (h.dw2part && t >= 448) {
-    const int l = t & 63, l16 = l & 15, kg = l >> 4;
-    const bool rok = r0 + l16 < H;
-    // (every LDS operand read first, unmasked -- the addresses are inside the tiles -- and masked by a select, so
-    // the 16 reads issue back to back and the 8 MFMAs follow without a wait between them)
-    float za[8], ab[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      za[s] = zs[l16][4 * s + kg];
-      ab[s] = a1s[l16][4 * s + kg];
-    }
-    f32x4 p = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-      p = __builtin_amdgcn_mfma_f32_16x16x4f32(za[s], (rok && c0 + 4 * s + kg < n) ? ab[s] : 0.f, p, 0, 0, 0);
-    const __amdgpu_buffer_rsrc_t rp = make_rsrc(h.dw2part);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cls = 4 * kg + i;
-      const float v = p[i];  // (a copy: hipcc bit-casts an ext-vector element lvalue as element 0)
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rp,
-                                            (rok && cls < C) ? ((ct * 16 + cls) * H + r0 + l16) * 4 : kOOB, 0, 0);
     }
   }
   if (st) {
