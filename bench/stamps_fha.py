@@ -96,6 +96,24 @@ def main(argv=None):
                               "wg_published": pct((wg[:, 1] - wg[:, 0]) / 100.0)[1:3],
                               "wg_arrived": pct((wg[:, 2] - wg[:, 0]) / 100.0)[1:3],
                               "wg_end": pct((wg[:, 3] - wg[:, 0]) / 100.0)[1:3]}), flush=True)
+        # per column tile: its last publication -> each of its workgroups' arrival (the hand-off's own latency)
+        tm_ = (a.hidden + 15) // 16
+        allv = buf.view(-1, 4).cpu().numpy().astype(np.int64)
+        byct = {}
+        for b in range(allv.shape[0]):
+            if allv[b, 0] <= 0:
+                continue
+            xcd, slot = b & 7, b >> 3
+            ct = slot if step.xcd_rows else xcd + 8 * (slot // tm_)
+            byct.setdefault(ct, []).append(allv[b])
+        lat, first = [], []
+        for ct, v in byct.items():
+            v = np.array(v)
+            lastpub = v[:, 1].max()
+            lat += list((v[:, 2] - lastpub) / 100.0)
+            first.append((v[:, 2].min() - lastpub) / 100.0)
+        print(json.dumps({"handoff_after_last_publish": pct(lat), "first_arrival_after_last_publish": pct(first)}),
+              flush=True)
         if rep == 3:  # per column tile (XCD-grouped grid: block b -> xcd b & 7, slot b >> 3, ct = xcd + 8 (slot // tm))
             tm = (a.hidden + 15) // 16
             allv = buf.view(-1, 4).cpu().numpy().astype(np.int64)
