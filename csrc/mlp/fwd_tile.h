@@ -59,32 +59,34 @@ template <int NPW, int NB, int VEC, int U, bool AF, class Epi>
 __device__ __forceinline__ void fwd_tile(const SplitStepArgs& f, const TileGeom& g, Epi& epi, float* red,
                                          unsigned long long* stamps = nullptr, char* img = nullptr) {
   const uint8_t* X = static_cast<const uint8_t*>(f.X);
+  const int krot = f.k_rot ? (g.n0 / (16 * NB)) % 7 : -1;  // (SplitStepArgs::k_rot)
   if constexpr (AF) {
     static_assert(NPW == 3, "fp32 W1 is split into three planes");
     if constexpr (VEC == 1 || VEC == 3) {
       if (img) {
         fwd_stage<NB>(f.W1, 4, X, f.P, g.M, g.N, g.m0, g.n0, img);
         wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t, float, true>(
-            f.W1, f.P, X, f.P, g, epi, red, 0, stamps, img, fimg::a_slots(f.P, 4) * 16, img + fimg::a_bytes(f.P, 4),
+            f.W1, f.P, X, f.P, g, epi, red, 0, stamps, krot, img, fimg::a_slots(f.P, 4) * 16, img + fimg::a_bytes(f.P, 4),
             f.P);
         return;
       }
     }
-    wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t>(f.W1, f.P, X, f.P, g, epi, red, 0, stamps);
+    wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t>(f.W1, f.P, X, f.P, g, epi, red, 0, stamps,
+                                                                       krot);
   } else {
     if constexpr (NPW == 1 && (VEC == 1 || VEC == 3)) {
       if (img) {
         const __hip_bfloat16* W = static_cast<const __hip_bfloat16*>(f.W1p);
         fwd_stage<NB>(W, 2, X, f.P, g.M, g.N, g.m0, g.n0, img);
         wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 1, uint8_t, __hip_bfloat16, true>(
-            W, f.P, X, f.P, g, epi, red, 0, stamps, img, fimg::a_slots(f.P, 2) * 16, img + fimg::a_bytes(f.P, 2),
+            W, f.P, X, f.P, g, epi, red, 0, stamps, krot, img, fimg::a_slots(f.P, 2) * 16, img + fimg::a_bytes(f.P, 2),
             f.P);
         return;
       }
     }
     wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, NPW, uint8_t>(
         static_cast<const __hip_bfloat16*>(f.W1p), f.P, X, f.P, g, epi, red, f.H * f.P * (int)sizeof(__hip_bfloat16),
-        stamps);
+        stamps, krot);
   }
 }
 

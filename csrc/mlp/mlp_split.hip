@@ -424,13 +424,14 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       if (threadIdx.x == 0) xw = xp_words_issue(a.xf, bid, a.ag_err);
     }
     constexpr int U = 4;
+    const int krot = a.k_rot ? (tb % t1n) % (kWKS - 1) : -1;  // (SplitStepArgs::k_rot: by column tile)
     if constexpr (AF)
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, 3, uint8_t>(a.dZ1, a.ld, static_cast<const uint8_t*>(a.XT),
-                                                                       a.ldxt, g, epi, red, 0, a.stamps);
+                                                                       a.ldxt, g, epi, red, 0, a.stamps, krot);
     else
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
                                                                 static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
-                                                                red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
+                                                                red, a.H * a.ld * (int)sizeof(bf16), a.stamps, krot);
     wstamp(1);
     if (push && (a.xp_dbg & 16)) return;  // (diagnostics: no exchange work at all after the tile)
     if (push) {  // the owner-tile exchange: thread e holds element (e / 32, e % 32) of the tile

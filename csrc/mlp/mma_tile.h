@@ -298,8 +298,9 @@ template <typename T, int MB, int NB, int KS, bool AK, bool BK, int VEC, int U, 
 __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, const TB* __restrict__ B, int ldb,
                                          TileGeom g, Epi& epi,
                                          typename MmaTraits<T>::acc_t* __restrict__ red, int plane_bytes = 0,
-                                         unsigned long long* stamps = nullptr, const char* ldsA = nullptr,
-                                         int ldsA_row = 0, const char* ldsB = nullptr, int ldsB_row = 0) {
+                                         unsigned long long* stamps = nullptr, int krot = -1,
+                                         const char* ldsA = nullptr, int ldsA_row = 0, const char* ldsB = nullptr,
+                                         int ldsB_row = 0) {
   using Tr = MmaTraits<T>;
   using accv_t = typename Tr::accv_t;
   using acc_t = typename Tr::acc_t;
@@ -356,8 +357,13 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A), rsB = make_rsrc(B);
   const int nch = (g.K + KC - 1) / KC;
   const int cpw = (nch + KS - 1) / KS;
-  const int kbeg = wave * cpw * KC;
-  const int kend = min(g.K, (wave + 1) * cpw * KC);
+  // krot >= 0: waves 0 .. KS - 2 take the K ranges rotated by krot (wave w the range of (w + krot) % (KS - 1)), so
+  // the workgroups of one XCD that share an operand's rows (the column tiles of a row tile) do not all request the
+  // same lines at the same moment; the last wave keeps its range.  A permutation of the ranges: only the order of
+  // the cross-wave sum changes (deterministic per tile; every form of one GEMM passes the same krot)
+  const int wk = (krot >= 0 && wave < KS - 1) ? (wave + krot) % (KS - 1) : wave;
+  const int kbeg = wk * cpw * KC;
+  const int kend = min(g.K, (wk + 1) * cpw * KC);
 
   constexpr bool AF32 = std::is_same_v<TA, float> && !std::is_same_v<T, float>;
   static_assert(!AF32 || (std::is_same_v<T, __hip_bfloat16> && NPA == 3 && AK), "fp32 A: split3 bf16, K-contiguous");
