@@ -97,14 +97,6 @@ struct MlpStep {
   // the weight-gradient launch's dW2 role (needs dw2p); 0: the role forms D . a1^T over the batch itself; -1 (auto):
   // from n = 512 columns, where the role's GEMM is the weight-gradient launch's critical path
   int head_dw2 = -1;
-  // SplitStepArgs::fwd_lds: measured SLOWER, off (forward + head 8.50 -> 9.54 us f32, 7.56 -> 8.24 bf16 at n = 800:
-  // the whole-tile LDS-DMA fill is not faster than the fragment loads, and nothing overlaps it;
-  // profiles/r5/kbench_fwd_lds_image.jsonl)
-  int fwd_lds = 0;
-  // SplitStepArgs::k_rot: measured no faster, off (walking step 15.27 -> 15.19 us at n = 800, 13.67 -> 13.91-13.97 at
-  // n = 100; profiles/r5/kbench_k_rot.jsonl): the column tiles' simultaneous requests for the same rows are not
-  // what bounds the K loops
-  int k_rot = 0;
   int xp_dbg = 0;       // SplitStepArgs::xp_dbg (diagnostics)
   int g64_touch = 0;    // SplitStepArgs::g64_touch (measured slower: 784-4096-10 bf16 38.1 -> 41.7 us,
                         // fp32 57.5 -> 62.6, profiles/r5/kbench_wide_touch.jsonl)
@@ -238,8 +230,6 @@ struct MlpStep {
     a.xp_dbg = xp_dbg;
     a.g64_touch = g64_touch;
     a.w2g = P_<unsigned long long>(w2g);
-    a.fwd_lds = fwd_lds;
-    a.k_rot = k_rot;
     a.w2_ks = (w2g && ag_err) ? w2_ks : 1;  // (a slice timeout reports through ag_err)
     return a;
   }
@@ -548,8 +538,6 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_err", &MlpStep::ag_err)
       .def_readwrite("w2_ks", &MlpStep::w2_ks)
       .def_readwrite("head_dw2", &MlpStep::head_dw2)
-      .def_readwrite("fwd_lds", &MlpStep::fwd_lds)
-      .def_readwrite("k_rot", &MlpStep::k_rot)
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
       .def_readwrite("ag_wait_us", &MlpStep::ag_wait_us)
       .def_readwrite("ag_test_skip", &MlpStep::ag_test_skip)

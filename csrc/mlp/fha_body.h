@@ -52,8 +52,7 @@ struct EpiSigLds {
 template <int NPW, int VEC, bool AF>
 __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs& h,
                                          unsigned long long* __restrict__ counters, gran_t* __restrict__ slabs,
-                                         int* __restrict__ err, int tm, int tn, int blk, float* red,
-                                         char* img = nullptr) {
+                                         int* __restrict__ err, int tm, int tn, int blk, float* red) {
   constexpr int kCols = 32;
   __shared__ float a1s[16][kCols + 1];
   __shared__ float w2s[16][17];        // W2[class][row of this tile], zero past C / H
@@ -97,8 +96,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   const float b2v = buf_load1<float>(make_rsrc(h.b2), (t >= 256 && t < 256 + 16 && t - 256 < C) ? (t - 256) * 4 : kOOB);
   TileGeom g{H, n, f.P, r0, c0};
   EpiSigLds epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
-  // (h.stamps: per-wave GEMM timeline, diagnostics; img: the LDS-image form, SplitStepArgs::fwd_lds)
-  fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red, h.stamps, img);
+  fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
   // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
   // they are masked below.  w2s / b2s are complete after the barrier below.
   if (t < 256) w2s[wc][wr] = w2v;

@@ -532,14 +532,13 @@ __global__ __launch_bounds__(512) void fwd1_head_ag_kernel(SplitStepArgs f, Head
                                                            gran_t* __restrict__ slabs, int* __restrict__ err, int tm,
                                                            int tn) {
   __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];
-  extern __shared__ __attribute__((aligned(1024))) char fwd_img[];  // SplitStepArgs::fwd_lds (launch-sized)
   if (f.pf_wgs_xt && (int)blockIdx.x >= (int)gridDim.x - 8 * f.pf_wgs_xt) {  // a prefetch workgroup (pf_wgs_xt):
     // this step's XT into the L2 of an XCD whose dW1 tiles read it next (all P + 1 features x n columns)
     const int xcd = blockIdx.x & 7, part = ((int)blockIdx.x - ((int)gridDim.x - 8 * f.pf_wgs_xt)) >> 3;
     if (xcd < tm) l2_touch(f.XT, 0, f.P + f.bias_col, f.ldxt, f.n, part, f.pf_wgs_xt, reinterpret_cast<char*>(red));
     return;
   }
-  fha_body<NPW, VEC, AF>(f, h, counters, slabs, err, tm, tn, blockIdx.x, red, f.fwd_lds ? fwd_img : nullptr);
+  fha_body<NPW, VEC, AF>(f, h, counters, slabs, err, tm, tn, blockIdx.x, red);
 }
 
 template <typename P, int NC>
@@ -1069,17 +1068,10 @@ void mlp_fwd1_head(const SplitStepArgs& f, const HeadArgs& h, unsigned* counters
 
 namespace {
 template <auto Kern>
-int resident_per_cu(int threads, int dyn = 0) {  // workgroups of Kern one CU holds at once, cached per dyn LDS size
-  static int occ = -1, occ_dyn = -1, last_dyn = -1;
-  if (dyn == 0) {
-    if (occ < 0) HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, Kern, threads, 0));
-    return occ;
-  }
-  if (dyn != last_dyn) {
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_dyn, Kern, threads, (size_t)dyn));
-    last_dyn = dyn;
-  }
-  return occ_dyn;
+int resident_per_cu(int threads) {  // workgroups of Kern one CU holds at once (static LDS only), cached
+  static int occ = -1;
+  if (occ < 0) HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, Kern, threads, 0));
+  return occ;
 }
 }  // namespace
 
@@ -1092,43 +1084,15 @@ static int fha_vec(const SplitStepArgs& f) {
   return x % 16 == 0 && f.P % 16 == 0 ? 3 : 1;
 }
 
-template <auto Kern>
-void fha_lds_limit(int bytes) {  // dynamic LDS above the default limit: one attribute call per size per kernel
-  static int set = -1;
-  if (bytes > 0 && bytes != set) {
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(Kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  bytes));
-    set = bytes;
-  }
-}
-
-// dynamic LDS of the all-gather forward + head launch: the forward tile's LDS image (SplitStepArgs::fwd_lds) when
-// that form applies (fp32 W1 or one bf16 plane, 4- or 16-byte pixel loads, P % 16 == 0), else 0
-static int fha_img_bytes(const SplitStepArgs& f) {
-  const bool af = mlp_split_fwd_fp32_w(f);
-  const int vec = fha_vec(f);
-  if (!f.fwd_lds || !fimg::ok(f.P) || (vec != 1 && vec != 3) || !(af || f.npw == 1)) return 0;
-  return fimg::bytes(f.P, af ? 4 : 2, 2);
-}
-
 bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f) {
   if (f.n <= 0) return true;
   const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32), nwg = tm * tn;
   const bool af = mlp_split_fwd_fp32_w(f);
-  const int vec = fha_vec(f), dyn = fha_img_bytes(f);
-  if (dyn > 0) {  // (the occupancy query needs the kernel's dynamic LDS limit raised first)
-    if (af) {
-      fha_lds_limit<fwd1_head_ag_kernel<3, 3, true>>(dyn);
-      fha_lds_limit<fwd1_head_ag_kernel<3, 1, true>>(dyn);
-    } else {
-      fha_lds_limit<fwd1_head_ag_kernel<1, 3, false>>(dyn);
-      fha_lds_limit<fwd1_head_ag_kernel<1, 1, false>>(dyn);
-    }
-  }
+  const int vec = fha_vec(f);
 #define CME_OCC(np, af)                                                            \
-  (vec == 3   ? resident_per_cu<fwd1_head_ag_kernel<np, 3, af>>(512, dyn)          \
-   : vec == 1 ? resident_per_cu<fwd1_head_ag_kernel<np, 1, af>>(512, dyn)          \
-              : resident_per_cu<fwd1_head_ag_kernel<np, 0, af>>(512, dyn))
+  (vec == 3   ? resident_per_cu<fwd1_head_ag_kernel<np, 3, af>>(512)               \
+   : vec == 1 ? resident_per_cu<fwd1_head_ag_kernel<np, 1, af>>(512)               \
+              : resident_per_cu<fwd1_head_ag_kernel<np, 0, af>>(512))
   const int occ = af ? CME_OCC(3, true) : (f.npw == 3 ? CME_OCC(3, false) : CME_OCC(1, false));
 #undef CME_OCC
   return nwg <= occ * device_cu_count();
@@ -1148,13 +1112,10 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
   const bool af = mlp_split_fwd_fp32_w(f);
   const int vec = fha_vec(f);
   const int nwg = f.xcd_rows ? 8 * tn + 8 * f.pf_wgs_xt : 8 * tm * cdiv(tn, 8);  // (prefetch workgroups last)
-  const int dyn = fha_img_bytes(f);
-  SplitStepArgs fk = f;
-  fk.fwd_lds = dyn > 0;
 #define CME_FHA(np, af)                                                                                  \
-  if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, dyn, s>>>(fk, h, counters, slabs, err, tm, tn);  \
-  else if (vec == 1) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, dyn, s>>>(fk, h, counters, slabs, err, tm, tn); \
-  else fwd1_head_ag_kernel<np, 0, af><<<nwg, 512, dyn, s>>>(fk, h, counters, slabs, err, tm, tn);
+  if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
+  else if (vec == 1) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn); \
+  else fwd1_head_ag_kernel<np, 0, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);
   if (af) { CME_FHA(3, true) } else if (f.npw == 3) { CME_FHA(3, false) } else { CME_FHA(1, false) }
 #undef CME_FHA
   CME_LAUNCH_CHECK(s);

@@ -125,14 +125,6 @@ struct SplitStepArgs {
   // Set by the launcher from the request (MlpStep.w2_ks); timeouts set *ag_err like the all-gather hand-offs.
   int w2_ks = 1;
   unsigned long long* w2g = nullptr;
-  // the all-gather forward + head (H <= 128): the forward tile's operands staged whole into LDS by LDS-DMA before
-  // the K loop (fwd_tile.h fwd_stage; bitwise the global form).  Set from MlpStep.fwd_lds; the launcher clears it
-  // where the form does not apply
-  int fwd_lds = 0;
-  // small layers: the wave-split-K GEMMs (forward tile, dW1 tiles) rotate their waves' K ranges by column tile
-  // (mma_tile.h wsk_tile krot), so the column tiles of one row tile -- which read the same operand rows -- do not
-  // request the same lines at the same moment.  Set from MlpStep.k_rot
-  int k_rot = 0;
   int w1_planes = 1;  // (set by mlp_split_wgrad) the small-layer W1 update refreshes the W1 planes
   // wide split3 layers: the A-in-registers dW1 launch's in-place update (sgd = 1) leaves the W1 planes alone (the
   // 128 x 128 forward reads fp32 W1); the caller marks them stale and refreshes them before a forward that reads them

@@ -365,16 +365,24 @@ struct EpiW1 {
   }
 };
 
+template <int FU>
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
                                             uint32_t* s_xf, float* xs);
 
-// AF (split3): dZ1 read in fp32 and split into its exact planes in registers (the head then writes no planes)
-template <int NPZ, int VEC, bool AF>
+// AF (split3): dZ1 read in fp32 and split into its exact planes in registers (the head then writes no planes).
+// FU: the gradient all-reduce fused in -- 0 none (SGD or the gradient bucket), 1 the one-shot pull, 2 the
+// owner-tile push (SplitStepArgs::xf).  A template, not a runtime test: with the xGMI forms compiled into the one
+// kernel, the single-process step's weight-gradient launch ran 0.8 us longer (rocprofv3, 784-100-10 at n = 800:
+// 5.70 -> 6.51 us on one box, profiles/r5/regression_bisect.md) for code it never executes.
+template <int NPZ, int VEC, bool AF, int FU>
 __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
   __shared__ uint32_t s_xf[2];
-  __shared__ float xsx[2 * kXpTile];  // the push form's staged gradient tile, then the current values
-  float *xs = xsx, *xo = xsx + kXpTile;
+  // the push form's staged gradient tile, then the current values (FU = 2); otherwise xs is the upper half of
+  // `red`, which the dW2 role's GEMM leaves unused (the dW2 slices' partial tile)
+  __shared__ float xsx[FU == 2 ? 2 * kXpTile : 1];
+  float* xs = FU == 2 ? xsx : red + kWKS * 4 * 64;
+  float* xo = xs + kXpTile;
   unsigned long long* wst = a.wstamps ? a.wstamps + (size_t)blockIdx.x * 8 : nullptr;  // diagnostics only
   auto wstamp = [&](int i) {
     if (wst && threadIdx.x == 0) wst[i] = __builtin_amdgcn_s_memrealtime();
@@ -400,14 +408,14 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     tb = bid < t1 ? xcd_remap(bid, t1) : bid;
   }
   const float reg = (float)a.reg, lr = (float)a.lr;
-  const bool fused = a.xf.world > 0;
+  constexpr bool fused = FU > 0;
   if (bid < t1) {  // ---- dW1 tile
     const int r1 = a.w1_rows < 0 ? a.H : a.w1_row0 + a.w1_rows;
     TileGeom g{r1, a.P + a.bias_col, a.n, a.w1_row0 + (tb / t1n) * 16 * kWMB, (tb % t1n) * 16 * kWNB};
     float *gw = a.gW1, *gb = a.gb1;
     // fused: gradients straight into this step's half of the IPC buffer (unless this rank is in error); the push
     // form stages them in LDS and decides whether to take part after the K loop (its words are prefetched)
-    const bool push = fused && a.xf.push;
+    constexpr bool push = FU == 2;
     const bool live = fused && !push && xf_begin(a.xf, bid, s_xf, a.ag_err);
     if (live) {
       gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(s_xf[0] & 1u) * a.xf.npad;
@@ -424,14 +432,13 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       if (threadIdx.x == 0) xw = xp_words_issue(a.xf, bid, a.ag_err);
     }
     constexpr int U = 4;
-    const int krot = a.k_rot ? (tb % t1n) % (kWKS - 1) : -1;  // (SplitStepArgs::k_rot: by column tile)
     if constexpr (AF)
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, 3, uint8_t>(a.dZ1, a.ld, static_cast<const uint8_t*>(a.XT),
-                                                                       a.ldxt, g, epi, red, 0, a.stamps, krot);
+                                                                       a.ldxt, g, epi, red, 0, a.stamps);
     else
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
                                                                 static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
-                                                                red, a.H * a.ld * (int)sizeof(bf16), a.stamps, krot);
+                                                                red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
     wstamp(1);
     if (push && (a.xp_dbg & 16)) return;  // (diagnostics: no exchange work at all after the tile)
     if (push) {  // the owner-tile exchange: thread e holds element (e / 32, e % 32) of the tile
@@ -486,7 +493,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     }
     return;
   }
-  wgrad_roles(a, bid, t1, t2, red, s_xf, xs);
+  wgrad_roles<FU>(a, bid, t1, t2, red, s_xf, xs);
   if (wst) {  // (no barrier: the roles' returns are not block-uniform)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wstamp(3);
@@ -565,10 +572,11 @@ __device__ __forceinline__ void wgrad_w2_slices(const SplitStepArgs& a, int rid,
 // The weight-gradient launch's workgroups past its t1 dW1 tiles: t2 dW2 tiles (+ the fused xGMI exchange)
 // followed by the bias-row workgroups.  `red`: kWKS * 4 * 64 floats of LDS, `s_xf`: 2 words of LDS.
 // Shared by wgrad_split_kernel and the wide engines' launches (their extra workgroups).
+template <int FU>
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
                                             uint32_t* s_xf, float* xs) {
   const float reg = (float)a.reg, lr = (float)a.lr;
-  const bool fused = a.xf.world > 0;
+  constexpr bool fused = FU > 0;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (bid < t1 + t2 && a.w2_ks > 1) {  // ---- dW2 with K split over workgroups (the launcher: no fused exchange)
@@ -580,7 +588,7 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     const int tb = bid - t1;
     TileGeom g{a.C, a.H, a.n, 0, tb * 16};
     float* gw = a.gW2;
-    const bool push = fused && a.xf.push;
+    constexpr bool push = FU == 2;
     const bool live = fused && (push || xf_begin(a.xf, bid, s_xf, a.ag_err));
     const int64_t half = push ? 0 : (int64_t)(s_xf[0] & 1u) * a.xf.npad;
     if (live && !push) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
@@ -642,7 +650,7 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     //               with the dW1 / dW2 tiles (inside the first dW2 tile it was a dependent pass over D after the
     //               tile's GEMM, on the launch's critical path: -0.9 us at world 1, bench/kbench.py xp_dbg rows)
     if (bid != t1 + t2) return;
-    const bool push = a.xf.push;
+    constexpr bool push = FU == 2;
     const bool live = push || xf_begin(a.xf, bid, s_xf, a.ag_err);
     if (!live) return;
     const int64_t half = push ? 0 : (int64_t)(s_xf[0] & 1u) * a.xf.npad;
@@ -1212,7 +1220,7 @@ template <int BM, int BN, int NPZ>
 __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {  // the dW2 / db2 roles riding in this launch
-    wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
+    wgrad_roles<0>(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
                 reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)),
                 reinterpret_cast<float*>(lds_dyn + kWKS * 4 * 64 * sizeof(float) + 16));  // (never fused: unused;
                                                                                             //  2 x kXpTile floats)
@@ -1395,7 +1403,7 @@ template <typename AT, int WC, int NKS, int ENG = 0>
 __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {
-    wgrad_roles(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
+    wgrad_roles<0>(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
                 reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)),
                 reinterpret_cast<float*>(lds_dyn + kWKS * 4 * 64 * sizeof(float) + 16));  // (never fused: unused;
                                                                                             //  2 x kXpTile floats)
@@ -1823,13 +1831,23 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   b.xcd_rows = a.xcd_rows && do_w1 && a.w1_row0 == 0 && a.w1_rows < 0 && cdiv(a.H, 16 * kWMB) <= 8;
   b.pf_wgs = b.xcd_rows ? a.pf_wgs : 0;
   const dim3 grid((b.xcd_rows ? 8 * t1n : t1) + t2 + tb + 8 * b.pf_wgs);  // (prefetch workgroups last)
-#define CME_WG(npz, af)                                                                   \
-  if (vec == 3) wgrad_split_kernel<npz, 3, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);      \
-  else if (vec == 1) wgrad_split_kernel<npz, 1, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \
-  else if (vec == 2) wgrad_split_kernel<npz, 2, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \
-  else wgrad_split_kernel<npz, 0, af><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
+  const int fu = !fused ? 0 : a.xf.push ? 2 : 1;
+#define CME_WG3(npz, af, FU)                                                                    \
+  if (vec == 3) wgrad_split_kernel<npz, 3, af, FU><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);      \
+  else if (vec == 1) wgrad_split_kernel<npz, 1, af, FU><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \
+  else if (vec == 2) wgrad_split_kernel<npz, 2, af, FU><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \
+  else wgrad_split_kernel<npz, 0, af, FU><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
+#define CME_WG(npz, af)     \
+  if (fu == 2) {            \
+    CME_WG3(npz, af, 2)     \
+  } else if (fu == 1) {     \
+    CME_WG3(npz, af, 1)     \
+  } else {                  \
+    CME_WG3(npz, af, 0)     \
+  }
   if (af) { CME_WG(3, true) } else if (a.npz == 3) { CME_WG(3, false) } else { CME_WG(1, false) }
 #undef CME_WG
+#undef CME_WG3
   CME_LAUNCH_CHECK(s);
 }
 

@@ -287,20 +287,12 @@ struct TileGeom {
 // TA = float (with T = bf16, NPA = 3, AK): A is the fp32 operand itself, 4 B per element pulled instead of
 // the 6 B of three stored planes, split into its exact planes in registers (split_trunc) while the MFMAs
 // of the previous unroll step run.
-//
-// LDSI (the forward's LDS-image form, fwd_tile.h fwd_stage): the operand tiles were staged whole into LDS by
-// LDS-DMA (full 128-B lines from global instead of fragment-shaped loads); A row r (0 <= r < 16 MB) of the tile at
-// ldsA + r * ldsA_row, element k at + k * sizeof(TA) (fp32 A, or ONE bf16 plane), B row r at ldsB + r * ldsB_row + k
-// (uint8 B).  Everything else -- the per-wave K ranges, the chunk pairing, the split and the MFMA order -- is the
-// global form's, so the results are bitwise the same.
 template <typename T, int MB, int NB, int KS, bool AK, bool BK, int VEC, int U, int NPA = 1, typename TB = T,
-          typename TA = T, bool LDSI = false, class Epi>
+          typename TA = T, class Epi>
 __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, const TB* __restrict__ B, int ldb,
                                          TileGeom g, Epi& epi,
                                          typename MmaTraits<T>::acc_t* __restrict__ red, int plane_bytes = 0,
-                                         unsigned long long* stamps = nullptr, int krot = -1,
-                                         const char* ldsA = nullptr, int ldsA_row = 0, const char* ldsB = nullptr,
-                                         int ldsB_row = 0) {
+                                         unsigned long long* stamps = nullptr) {
   using Tr = MmaTraits<T>;
   using accv_t = typename Tr::accv_t;
   using acc_t = typename Tr::acc_t;
@@ -357,13 +349,8 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A), rsB = make_rsrc(B);
   const int nch = (g.K + KC - 1) / KC;
   const int cpw = (nch + KS - 1) / KS;
-  // krot >= 0: waves 0 .. KS - 2 take the K ranges rotated by krot (wave w the range of (w + krot) % (KS - 1)), so
-  // the workgroups of one XCD that share an operand's rows (the column tiles of a row tile) do not all request the
-  // same lines at the same moment; the last wave keeps its range.  A permutation of the ranges: only the order of
-  // the cross-wave sum changes (deterministic per tile; every form of one GEMM passes the same krot)
-  const int wk = (krot >= 0 && wave < KS - 1) ? (wave + krot) % (KS - 1) : wave;
-  const int kbeg = wk * cpw * KC;
-  const int kend = min(g.K, (wk + 1) * cpw * KC);
+  const int kbeg = wave * cpw * KC;
+  const int kend = min(g.K, (wave + 1) * cpw * KC);
 
   constexpr bool AF32 = std::is_same_v<TA, float> && !std::is_same_v<T, float>;
   static_assert(!AF32 || (std::is_same_v<T, __hip_bfloat16> && NPA == 3 && AK), "fp32 A: split3 bf16, K-contiguous");
@@ -385,26 +372,7 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = VEC == 3 ? kc + (u & ~1) * KC + 2 * V * grp + (u & 1) * V : kc + u * KC + V * grp;
-      if constexpr (LDSI) {
-        static_assert(BU8 && AK && (AF32 || NPA == 1) && (VEC == 1 || VEC == 3), "LDS image: fp32 / one-plane A, u8 B");
-#pragma unroll
-        for (int i = 0; i < MB; ++i) {
-          const bool ok = g.m0 + 16 * i + c < g.M && k < kend;  // (vectors fully in or out: kend % V == 0)
-          const char* pa = ldsA + (16 * i + c) * ldsA_row + k * (int)sizeof(TA);
-          if constexpr (AF32) {
-            const auto w0 = *reinterpret_cast<const uint4*>(pa), w1 = *reinterpret_cast<const uint4*>(pa + 16);
-            const uint4 z = {0u, 0u, 0u, 0u};
-            const uint4 v0 = ok ? w0 : z, v1 = ok ? w1 : z;
-            __builtin_memcpy(ar[u][i], &v0, 16);
-            __builtin_memcpy(reinterpret_cast<char*>(ar[u][i]) + 16, &v1, 16);
-          } else {
-            const auto w0 = *reinterpret_cast<const uint4*>(pa);
-            const uint4 z = {0u, 0u, 0u, 0u};
-            const uint4 v0 = ok ? w0 : z;
-            __builtin_memcpy(af[u][0][i], &v0, 16);
-          }
-        }
-      } else if constexpr (AF32) {
+      if constexpr (AF32) {
 #pragma unroll
         for (int i = 0; i < MB; ++i) load_frag<float, V, true, VA>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, ar[u][i]);
       } else {
@@ -418,23 +386,7 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
       for (int j = 0; j < NB; ++j) {
         if constexpr (BU8) {
           static_assert(std::is_same_v<T, __hip_bfloat16> && BK, "u8 B operand: bf16 MFMA, K-contiguous");
-          if constexpr (VEC == 3 && LDSI) {
-            if ((u & 1) == 0) {  // (as below, from the LDS image)
-              const int r = g.n0 + 16 * j + c;
-              const auto w0 = *reinterpret_cast<const uint4*>(ldsB + (16 * j + c) * ldsB_row + k);
-              const uint4 z = {0u, 0u, 0u, 0u};
-              const uint4 w = (r < g.N && k + 16 <= kend) ? w0 : z;
-              braw[u][j].w[0] = w.x;
-              braw[u][j].w[1] = w.y;
-              braw[u + 1][j].w[0] = w.z;
-              braw[u + 1][j].w[1] = w.w;
-            }
-          } else if constexpr (VEC == 1 && LDSI) {
-            const int r = g.n0 + 16 * j + c;
-            const auto w0 = *reinterpret_cast<const uint2*>(ldsB + (16 * j + c) * ldsB_row + k);
-            braw[u][j].w[0] = (r < g.N && k + 4 <= kend) ? w0.x : 0u;
-            braw[u][j].w[1] = (r < g.N && k + 8 <= kend) ? w0.y : 0u;
-          } else if constexpr (VEC == 3) {
+          if constexpr (VEC == 3) {
             if ((u & 1) == 0) {  // the pair's 16 bytes: words 0-1 -> chunk u, words 2-3 -> chunk u + 1
               const int r = g.n0 + 16 * j + c;
               const auto w = __builtin_amdgcn_raw_buffer_load_b128(

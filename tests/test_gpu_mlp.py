@@ -840,28 +840,3 @@ def test_head_dw2_partials_match_the_role_gemm(n, store_a1):
     for a, b in zip(got[0][:2] + got[0][3:], got[1][:2] + got[1][3:]):
         assert torch.equal(a, b)
     assert not hipe.kernel_error()
-
-
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-@pytest.mark.parametrize("H,n", [(100, 800), (100, 100), (128, 513), (37, 45)])
-def test_forward_lds_image_is_bitwise_the_global_form(dtype, H, n):
-    """The all-gather forward + head with its forward tile staged whole into LDS by LDS-DMA (MlpStep.fwd_lds:
-    full-line fills instead of fragment-shaped loads) against the global-load form: a1, D, dZ1 and the parameters
-    after several SGD steps BITWISE equal (same K ranges, pairing, split and MFMA order)."""
-    x, y = synthetic_mnist(2 * n + 7, seed=H)
-    nn = NeuralNetwork([784, H, 10])
-    outs = []
-    for lds in (0, 1):
-        e = MlpEngine(nn.H, dtype, max_cols=n, device="cuda")
-        e.set_params(*nn.params)
-        e.load_dataset(x, y, normalize=True)
-        e._hip_step().fwd_lds = lds
-        for off in (0, n, 7, 0):
-            e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True)
-        e.run(3, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
-        torch.cuda.synchronize()
-        assert not e.kernel_error()
-        outs.append([t.clone().cpu() for t in (e.a1, e.D, e.dZ1, e.params, e.grads)] + [e.loss_sum()])
-    for a, b in zip(outs[0][:-1], outs[1][:-1]):
-        assert torch.equal(a, b)
-    assert outs[0][-1] == outs[1][-1]
