@@ -104,6 +104,10 @@ struct MlpStep {
   // data-parallel step with the xGMI gradient all-reduce + SGD fused into the wgrad launch (run(sgd=2))
   cme::XgmiFuse xf;
   // push != 0: the owner-tile push form (XgmiFuse::push; the bucket must have slab_tiles >= the launch's tiles)
+  cme::XgmiFuse* xf_dev = nullptr;  // its device copy (SplitStepArgs::xf): allocated once, so captured graphs stay valid
+  ~MlpStep() {
+    if (xf_dev) (void)hipFree(xf_dev);
+  }
   void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2, int push = 0) {
     if (!desc) {
       xf = cme::XgmiFuse{};
@@ -143,6 +147,8 @@ struct MlpStep {
       }
     }
     xf = f;
+    if (!xf_dev) HIP_CHECK(hipMalloc(&xf_dev, sizeof(cme::XgmiFuse)));
+    HIP_CHECK(hipMemcpy(xf_dev, &xf, sizeof(cme::XgmiFuse), hipMemcpyHostToDevice));
   }
   float xscale = 1.f;    // split path: inputs are uint8 * xscale
   uintptr_t W1p = 0, dZ1p = 0;
@@ -254,8 +260,10 @@ struct MlpStep {
         a.pf_bytes = std::min<int64_t>(n, N - pf_next) * P;
       }
       if (sgd == 2) {  // all-reduce + SGD inside the wgrad launch
-        CME_REQUIRE(xf.world > 0, "MlpStep.run(sgd=2): set_xgmi() first");
-        a.xf = xf;
+        CME_REQUIRE(xf.world > 0 && xf_dev, "MlpStep.run(sgd=2): set_xgmi() first");
+        a.xf = xf_dev;
+        a.xf_world = xf.world;
+        a.xf_push = xf.push;
       }
       if (parts & 1) {
         {  // the forward GEMM + the head (fused into one launch where the shapes allow)

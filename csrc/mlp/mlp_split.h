@@ -91,7 +91,11 @@ struct SplitStepArgs {
   // XT carries an extra all-ones feature row P: the dW1 GEMM's column P is then sum_b dZ1[h][b] = db1[h]
   // (exact, same planes), so db1 / b1 come out of the dW1 launch and the role kernel only does dW2 / db2
   int bias_col = 0;
-  XgmiFuse xf;
+  // the fused all-reduce (run(sgd = 2)): a DEVICE copy of the XgmiFuse, uploaded once by MlpStep::set_xgmi, and its
+  // two scalars the launcher tests.  (By value it was 288 of the launch's ~950 kernel-argument bytes, written by
+  // the host on every launch: the native loop's host enqueue time per step is what that costs.)
+  const XgmiFuse* xf = nullptr;
+  int xf_world = 0, xf_push = 0;
   // wide layers (LDS GEMM forward): when set, the forward GEMM's tile epilogue also leaves the head's
   // z2 partial sums, z2part[row tile][16][ld] = W2[:, tile rows] . a1[tile rows, :] (v_mfma_f32_16x16x4
   // on the activated accumulators), so the head never re-reads a1 for z2 (mlp_split_fwd1_z2_chunks)

@@ -416,10 +416,10 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     // fused: gradients straight into this step's half of the IPC buffer (unless this rank is in error); the push
     // form stages them in LDS and decides whether to take part after the K loop (its words are prefetched)
     constexpr bool push = FU == 2;
-    const bool live = fused && !push && xf_begin(a.xf, bid, s_xf, a.ag_err);
+    const bool live = fused && !push && xf_begin(*a.xf, bid, s_xf, a.ag_err);
     if (live) {
-      gw = static_cast<float*>(a.xf.mybuf) + (int64_t)(s_xf[0] & 1u) * a.xf.npad;
-      gb = gw + a.xf.off_b1;
+      gw = static_cast<float*>(a.xf->mybuf) + (int64_t)(s_xf[0] & 1u) * a.xf->npad;
+      gb = gw + a.xf->off_b1;
     }
     EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.w1_planes ? a.npw : 0, reg, lr,
               a.xscale, {}, a.b1, gb, push ? 2 : (live ? 1 : 0), a.ag_err};
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       epi.xo = xo;
       epi.m0 = g.m0;
       epi.n0 = g.n0;
-      if (threadIdx.x == 0) xw = xp_words_issue(a.xf, bid, a.ag_err);
+      if (threadIdx.x == 0) xw = xp_words_issue(*a.xf, bid, a.ag_err);
     }
     constexpr int U = 4;
     if constexpr (AF)
@@ -453,7 +453,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       __syncthreads();  // xs / xo complete
       wstamp(4);
       float nv = ok ? xo[e] - lr * xs[e] : 0.f;
-      if (!s_xf[1] && ((a.xp_dbg & 1) || xp_exchange(a.xf, bid, s_xf, xs, 512, ok, ok ? xo[e] : 0.f, lr, &nv, wst)) &&
+      if (!s_xf[1] && ((a.xp_dbg & 1) || xp_exchange(*a.xf, bid, s_xf, xs, 512, ok, ok ? xo[e] : 0.f, lr, &nv, wst)) &&
           ok && !(a.xp_dbg & 2)) {
         if (col < a.P) {
           a.W1[i] = nv;
@@ -465,24 +465,24 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
           a.b1[row] = nv;
         }
       }
-    } else if (live && xf_exchange(a.xf, bid, s_xf)) {  // all-reduced with the peers: SGD + bf16 planes
-      const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf.npad;
+    } else if (live && xf_exchange(*a.xf, bid, s_xf)) {  // all-reduced with the peers: SGD + bf16 planes
+      const int64_t half = (int64_t)(s_xf[0] & 1u) * a.xf->npad;
       constexpr int TW = 16 * kWNB;
       for (int e = threadIdx.x; e < 16 * kWMB * TW; e += kWT) {
         const int row = g.m0 + e / TW, col = g.n0 + e % TW;
         if (row >= g.M || col >= g.N) continue;
         if (col < a.P) {
           const int64_t i = (int64_t)row * a.P + col;
-          const float w = a.W1[i] - lr * xf_sum(a.xf, half + i);
+          const float w = a.W1[i] - lr * xf_sum(*a.xf, half + i);
           a.W1[i] = w;
           if (!a.w1_planes) continue;
           if (a.npw == 3) split_store<3>(w, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
           else split_store<1>(w, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
         } else {
-          a.b1[row] -= lr * xf_sum(a.xf, half + a.xf.off_b1 + row);
+          a.b1[row] -= lr * xf_sum(*a.xf, half + a.xf->off_b1 + row);
         }
       }
-      xf_end(a.xf, bid, s_xf);
+      xf_end(*a.xf, bid, s_xf);
     }
     wstamp(2);
     mark_status(a, epi.perr);
@@ -589,16 +589,16 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     TileGeom g{a.C, a.H, a.n, 0, tb * 16};
     float* gw = a.gW2;
     constexpr bool push = FU == 2;
-    const bool live = fused && (push || xf_begin(a.xf, bid, s_xf, a.ag_err));
-    const int64_t half = push ? 0 : (int64_t)(s_xf[0] & 1u) * a.xf.npad;
-    if (live && !push) gw = static_cast<float*>(a.xf.mybuf) + half + a.xf.off_W2;
+    const bool live = fused && (push || xf_begin(*a.xf, bid, s_xf, a.ag_err));
+    const int64_t half = push ? 0 : (int64_t)(s_xf[0] & 1u) * a.xf->npad;
+    if (live && !push) gw = static_cast<float*>(a.xf->mybuf) + half + a.xf->off_W2;
     EpiW2 epi{a.W2, gw, a.H, fused ? 0 : a.sgd, push ? 2 : (live ? 1 : 0), reg, lr, {}, a.ag_err};
     XpWords xw;
     if (push) {
       epi.xs = xs;
       epi.xo = xs + kXpTile;
       epi.n0 = tb * 16;
-      if (threadIdx.x == 0) xw = xp_words_issue(a.xf, bid, a.ag_err);
+      if (threadIdx.x == 0) xw = xp_words_issue(*a.xf, bid, a.ag_err);
     }
     if (a.dw2part) {  // the head's per-column-tile partials, summed in tile order (16 rows x C classes)
       const int nct = (a.n + a.dw2_cols - 1) / a.dw2_cols, e = threadIdx.x, c = e >> 4, h = tb * 16 + (e & 15);
@@ -633,17 +633,17 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
       __syncthreads();  // xs / xo complete
       const float old = ok ? xs[kXpTile + e] : 0.f;
       float nv = ok ? old - lr * xs[e] : 0.f;  // (xp_dbg 4: diagnostics, no exchange -- world 1's own value)
-      if (!s_xf[1] && ((a.xp_dbg & 4) || xp_exchange(a.xf, bid, s_xf, xs, 256, ok, old, lr, &nv)) && ok) a.W2[i] = nv;
+      if (!s_xf[1] && ((a.xp_dbg & 4) || xp_exchange(*a.xf, bid, s_xf, xs, 256, ok, old, lr, &nv)) && ok) a.W2[i] = nv;
       return;
     }
-    if (!xf_exchange(a.xf, bid, s_xf)) return;
+    if (!xf_exchange(*a.xf, bid, s_xf)) return;
     for (int e = threadIdx.x; e < 256; e += kWT) {
       const int c = e / 16, h = tb * 16 + e % 16;
       if (c >= a.C || h >= a.H) continue;
       const int64_t i = (int64_t)c * a.H + h;
-      a.W2[i] -= lr * xf_sum(a.xf, half + a.xf.off_W2 + i);
+      a.W2[i] -= lr * xf_sum(*a.xf, half + a.xf->off_W2 + i);
     }
-    xf_end(a.xf, bid, s_xf);
+    xf_end(*a.xf, bid, s_xf);
     return;
   }
   if (fused) {  // ---- db2 (the fused launch's last role, exchange tile t1 + t2): one wave per class, in parallel
@@ -651,17 +651,17 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     //               tile's GEMM, on the launch's critical path: -0.9 us at world 1, bench/kbench.py xp_dbg rows)
     if (bid != t1 + t2) return;
     constexpr bool push = FU == 2;
-    const bool live = push || xf_begin(a.xf, bid, s_xf, a.ag_err);
+    const bool live = push || xf_begin(*a.xf, bid, s_xf, a.ag_err);
     if (!live) return;
-    const int64_t half = push ? 0 : (int64_t)(s_xf[0] & 1u) * a.xf.npad;
+    const int64_t half = push ? 0 : (int64_t)(s_xf[0] & 1u) * a.xf->npad;
     XpWords xw;
-    if (push && threadIdx.x == 0) xw = xp_words_issue(a.xf, bid, a.ag_err);
+    if (push && threadIdx.x == 0) xw = xp_words_issue(*a.xf, bid, a.ag_err);
     const float bold = (int)threadIdx.x < a.C ? a.b2[threadIdx.x] : 0.f;
     for (int c = wv; c < a.C; c += kWKS) {
       const float sc = wave_sum(row_sum(a.D + (size_t)c * a.ld, a.n, lane));
       if (lane == 0) {
         if (push) xs[c] = sc;
-        else xf_store(static_cast<float*>(a.xf.mybuf), half + a.xf.off_b2 + c, sc);
+        else xf_store(static_cast<float*>(a.xf->mybuf), half + a.xf->off_b2 + c, sc);
       }
     }
     if (push) {
@@ -674,12 +674,12 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
       }
       __syncthreads();  // xs complete
       float nv = ok ? bold - lr * xs[e] : 0.f;
-      if (!s_xf[1] && ((a.xp_dbg & 8) || xp_exchange(a.xf, bid, s_xf, xs, a.C, ok, bold, lr, &nv)) && ok) a.b2[e] = nv;
+      if (!s_xf[1] && ((a.xp_dbg & 8) || xp_exchange(*a.xf, bid, s_xf, xs, a.C, ok, bold, lr, &nv)) && ok) a.b2[e] = nv;
       return;
     }
-    if (!xf_exchange(a.xf, bid, s_xf)) return;
-    for (int c = threadIdx.x; c < a.C; c += kWT) a.b2[c] = bold - lr * xf_sum(a.xf, half + a.xf.off_b2 + c);
-    xf_end(a.xf, bid, s_xf);
+    if (!xf_exchange(*a.xf, bid, s_xf)) return;
+    for (int c = threadIdx.x; c < a.C; c += kWT) a.b2[c] = bold - lr * xf_sum(*a.xf, half + a.xf->off_b2 + c);
+    xf_end(*a.xf, bid, s_xf);
     return;
   }
   // ---- bias gradients: one wave per row; rows [0,H) -> db1 from dZ1, [H,H+C) -> db2 from D
@@ -1642,7 +1642,7 @@ bool small_wgrad_fp32_ok(const SplitStepArgs& a) {
 // wave-split-K kernel) so that the head and every wgrad call of a step agree on what dZ1 form exists.
 bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a) {
   if (a.npz != 3) return false;
-  const bool big = big_wgrad_ok(a) && a.xf.world == 0;
+  const bool big = big_wgrad_ok(a) && a.xf_world == 0;
   // (wide: the A-in-registers dW1 always splits fp32 dZ1 -- profiles/wide_ag_ab_operand_forms_r3.jsonl)
   return big ? rega_wgrad_ok(a) : small_wgrad_fp32_ok(a);
 }
@@ -1678,7 +1678,7 @@ bool mlp_split_wide_fwd_reads_planes(const SplitStepArgs& a, int ag, int allow64
 
 bool mlp_split_wgrad_leaves_planes_stale(const SplitStepArgs& a) {
   return a.w1_planes_lazy && a.npw == 3 && a.npz == 3 && a.sgd && (a.wg_parts & 1) && a.w1_rows != 0 &&
-         a.xf.world == 0 && big_wgrad_ok(a) && rega_wgrad_ok(a);
+         a.xf_world == 0 && big_wgrad_ok(a) && rega_wgrad_ok(a);
 }
 
 bool mlp_fwd1_wide_ag_ok(const SplitStepArgs& a, const HeadArgs& h, int allow64) {
@@ -1775,7 +1775,7 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   CME_REQUIRE((int64_t)a.H * a.ld * 2 * a.npz < (int64_t)kOOB && (int64_t)a.P * a.ldxt < (int64_t)kOOB,
               "split path: operand too large for 32-bit buffer offsets");
   CME_REQUIRE(a.w1_row0 >= 0 && (a.w1_rows < 0 || a.w1_row0 + a.w1_rows <= a.H), "wgrad: bad dW1 row range");
-  const bool fused = a.xf.world > 0;
+  const bool fused = a.xf_world > 0;
   const bool big = big_wgrad_ok(a) && !fused;
   const bool do_w1 = (a.wg_parts & 1) && a.w1_rows != 0, do_roles = (a.wg_parts & 2) != 0;
   // the dW2 role's workgroup split (SplitStepArgs::w2_ks): the small-layer launch below only, without the fused
@@ -1809,7 +1809,7 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   const int t2 = do_roles ? cdiv(a.H, 16) * w2ks : 0;
   if (fused)
     CME_REQUIRE(do_w1 && do_roles && a.bias_col && a.w1_row0 == 0 && a.w1_rows < 0 && a.C <= 16 &&
-                    a.xf.world <= 8 && t1 + t2 + 1 <= mlp_split_fused_tiles(a.P, a.H, 1 << 30),
+                    a.xf_world <= 8 && t1 + t2 + 1 <= mlp_split_fused_tiles(a.P, a.H, 1 << 30),
                 "wgrad: fused all-reduce needs the whole small-layer step with the all-ones XT feature");
   // fused mode: db2 is one role workgroup of its own (exchange tile t1 + t2)
   const int tb = !do_roles ? 0 : fused ? 1 : cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS);
@@ -1831,7 +1831,7 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   b.xcd_rows = a.xcd_rows && do_w1 && a.w1_row0 == 0 && a.w1_rows < 0 && cdiv(a.H, 16 * kWMB) <= 8;
   b.pf_wgs = b.xcd_rows ? a.pf_wgs : 0;
   const dim3 grid((b.xcd_rows ? 8 * t1n : t1) + t2 + tb + 8 * b.pf_wgs);  // (prefetch workgroups last)
-  const int fu = !fused ? 0 : a.xf.push ? 2 : 1;
+  const int fu = !fused ? 0 : a.xf_push ? 2 : 1;
 #define CME_WG3(npz, af, FU)                                                                    \
   if (vec == 3) wgrad_split_kernel<npz, 3, af, FU><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);      \
   else if (vec == 1) wgrad_split_kernel<npz, 1, af, FU><<<grid, kWT, 0, s>>>(b, t1, t1n, t2); \
