@@ -21,6 +21,7 @@ def main(argv=None):
     ap.add_argument("--n", type=int, default=12288)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--forms", default="all", choices=["all", "stores"])
     a = ap.parse_args(argv)
     import torch
 
@@ -68,9 +69,11 @@ def main(argv=None):
     ms = timeit(prod)
     print(json.dumps({"form": "production lds (32 rows, 4 ahead)", "ms": round(ms, 3),
                       "compulsory_GBps": round(comp / (ms * 1e-3) / 1e9, 1)}), flush=True)
-    # nt: bit 0 non-temporal streamed loads, bit 1 the alternate-direction walk (ALT)
-    for rows, ahead, nt in ((32, 4, 0), (32, 8, 0), (32, 8, 1), (64, 8, 0), (32, 4, 2), (32, 8, 2), (64, 8, 2),
-                            (16, 8, 2)):
+    # nt: bit 0 non-temporal streamed loads, bit 1 the alternate-direction walk (ALT), bit 2 plain stores
+    forms = ((32, 4, 0), (32, 8, 0), (32, 8, 1), (64, 8, 0), (32, 4, 2), (32, 8, 2), (64, 8, 2), (16, 8, 2))
+    if a.forms == "stores":
+        forms = ((32, 4, 2), (32, 4, 6), (32, 6, 2), (32, 6, 6), (64, 4, 6), (16, 4, 2), (32, 4, 2), (32, 4, 6))
+    for rows, ahead, nt in forms:
         fn = lambda d, s, r=rows, h=ahead, t=nt: k.stencil_lds_tune(d.data_ptr(), s.data_ptr(), g, g, xcfl, ycfl,  # noqa: E731
                                                                     r, h, t, st)
         out = run(fn)

@@ -185,7 +185,7 @@ __device__ __forceinline__ f32x4 ld4p(__amdgpu_buffer_rsrc_t r, int64_t elem) {
 // neighbouring workgroup is blockIdx + nbx: the same XCD whenever nbx % 8 == 0, e.g. 12288-wide grids).  The window
 // is indexed by grid offset (win[B + dir * k] is row center + k), so every output is the same sum in the same order:
 // bitwise the one-direction kernel.
-template <int ORDER, int ROWS, int AHEAD = kLdsAhead, int CP = 0, int DIR = 1>
+template <int ORDER, int ROWS, int AHEAD = kLdsAhead, int CP = 0, int DIR = 1, bool NTST = true>
 __device__ __forceinline__ void stencil_lds_walk(float* __restrict__ next, const float* __restrict__ curr, int gx,
                                                  int gy, int nx, int ny, float xcfl, float ycfl, int bx, int by,
                                                  f32x4 (*xrow)[66]) {
@@ -264,7 +264,8 @@ __device__ __forceinline__ void stencil_lds_walk(float* __restrict__ next, const
           ycfl);
     float* dst = next + rowc;
     if (x0 + 4 <= nx && (rowc & 3) == 0) {
-      __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(dst));
+      if constexpr (NTST) __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(dst));
+      else *reinterpret_cast<f32x4*>(dst) = o;
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -275,14 +276,14 @@ __device__ __forceinline__ void stencil_lds_walk(float* __restrict__ next, const
   }
 }
 
-template <int ORDER, int ROWS, int AHEAD = kLdsAhead, int CP = 0, bool ALT = false>
+template <int ORDER, int ROWS, int AHEAD = kLdsAhead, int CP = 0, bool ALT = false, bool NTST = true>
 __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const float* __restrict__ curr, int gx,
                                                  int gy, int nx, int ny, float xcfl, float ycfl, int bx, int by,
                                                  f32x4 (*xrow)[66]) {
   if (ALT && ((by * 4 + threadIdx.y) & 1))  // (wave-uniform)
-    stencil_lds_walk<ORDER, ROWS, AHEAD, CP, -1>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by, xrow);
+    stencil_lds_walk<ORDER, ROWS, AHEAD, CP, -1, NTST>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by, xrow);
   else
-    stencil_lds_walk<ORDER, ROWS, AHEAD, CP, 1>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by, xrow);
+    stencil_lds_walk<ORDER, ROWS, AHEAD, CP, 1, NTST>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by, xrow);
 }
 
 // border strips: rows [0,b) and [gy-b,gy) (full width), columns [0,b) and [gx-b,gx) of the middle rows;
@@ -362,22 +363,22 @@ void launch(float* next, const float* curr, int gx, int gy, float xcfl, float yc
 
 // the LDS variant's knobs, order 8, interior only (bench/stencil_tune.py): rows per wave, rows loaded ahead,
 // the streamed loads' cache policy
-template <int ROWS, int AHEAD, int CP, bool ALT>
+template <int ROWS, int AHEAD, int CP, bool ALT, bool NTST>
 __global__ __launch_bounds__(256) void stencil_lds_tune_kernel(float* __restrict__ next, const float* __restrict__ curr,
                                                                int gx, int gy, int nx, int ny, float xcfl, float ycfl,
                                                                int nbx) {
   __shared__ f32x4 xrow[4][2][66];
   const int id = blockIdx.x;
-  stencil_lds_body<8, ROWS, AHEAD, CP, ALT>(next, curr, gx, gy, nx, ny, xcfl, ycfl, id % nbx, id / nbx,
-                                            xrow[threadIdx.y]);
+  stencil_lds_body<8, ROWS, AHEAD, CP, ALT, NTST>(next, curr, gx, gy, nx, ny, xcfl, ycfl, id % nbx, id / nbx,
+                                                  xrow[threadIdx.y]);
 }
 
-template <int ROWS, int AHEAD, int CP, bool ALT = false>
+template <int ROWS, int AHEAD, int CP, bool ALT = false, bool NTST = true>
 void launch_lds_tune(float* next, const float* curr, int gx, int gy, float xcfl, float ycfl, hipStream_t s) {
   const int nx = gx - 8, ny = gy - 8;
   const int nbx = (nx + 255) / 256, nby = (ny + 4 * ROWS - 1) / (4 * ROWS);
-  stencil_lds_tune_kernel<ROWS, AHEAD, CP, ALT><<<nbx * nby, dim3(64, 4), 0, s>>>(next, curr, gx, gy, nx, ny, xcfl,
-                                                                                  ycfl, nbx);
+  stencil_lds_tune_kernel<ROWS, AHEAD, CP, ALT, NTST><<<nbx * nby, dim3(64, 4), 0, s>>>(next, curr, gx, gy, nx, ny,
+                                                                                        xcfl, ycfl, nbx);
 }
 
 }  // namespace
@@ -385,8 +386,14 @@ void launch_lds_tune(float* next, const float* curr, int gx, int gy, float xcfl,
 void stencil_lds_tune(float* next, const float* curr, int gx, int gy, float xcfl, float ycfl, int rows, int ahead,
                       int nt, hipStream_t s) {
   CME_REQUIRE((int64_t)gx * gy * 4 < (int64_t)0x7FFFFFF0, "stencil_lds_tune: grid too large for 32-bit offsets");
-  const int key = rows * 100 + ahead * 10 + (nt & 1) + (nt & 2 ? 100000 : 0);  // nt bit 1: alternate walk
+  // nt bit 0: non-temporal streamed loads, bit 1: alternate walk, bit 2: plain (not non-temporal) stores
+  const int key = rows * 100 + ahead * 10 + (nt & 1) + (nt & 2 ? 100000 : 0) + (nt & 4 ? 1000000 : 0);
   switch (key) {
+    case 1103240: launch_lds_tune<32, 4, 0, true, false>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 1103260: launch_lds_tune<32, 6, 0, true, false>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 1106440: launch_lds_tune<64, 4, 0, true, false>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 103260: launch_lds_tune<32, 6, 0, true>(next, curr, gx, gy, xcfl, ycfl, s); break;
+    case 101640: launch_lds_tune<16, 4, 0, true>(next, curr, gx, gy, xcfl, ycfl, s); break;
     case 103240: launch_lds_tune<32, 4, 0, true>(next, curr, gx, gy, xcfl, ycfl, s); break;
     case 103280: launch_lds_tune<32, 8, 0, true>(next, curr, gx, gy, xcfl, ycfl, s); break;
     case 106480: launch_lds_tune<64, 8, 0, true>(next, curr, gx, gy, xcfl, ycfl, s); break;
