@@ -112,7 +112,22 @@ def main(argv=None):
             lastpub = v[:, 1].max()
             lat += list((v[:, 2] - lastpub) / 100.0)
             first.append((v[:, 2].min() - lastpub) / 100.0)
-        print(json.dumps({"handoff_after_last_publish": pct(lat), "first_arrival_after_last_publish": pct(first)}),
+        # per row tile (= XCD under xcd_rows): when its workgroups published (GEMM + epilogue done)
+        byrt, byrt_e, byrt_k = {}, {}, {}
+        wall = wbuf.view(-1, 8, 4).cpu().numpy().astype(np.int64)
+        for b in range(allv.shape[0]):
+            if allv[b, 0] <= 0:
+                continue
+            xcd, slot = b & 7, b >> 3
+            rt = xcd if step.xcd_rows else slot % tm_
+            byrt.setdefault(rt, []).append((allv[b, 1] - t0) / 100.0)
+            byrt_e.setdefault(rt, []).append((allv[b, 0] - t0) / 100.0)
+            if b < wall.shape[0] and (wall[b, :, 1] > 0).all():
+                byrt_k.setdefault(rt, []).append((wall[b, :, 1].max() - t0) / 100.0)
+        print(json.dumps({"handoff_after_last_publish": pct(lat), "first_arrival_after_last_publish": pct(first),
+                          "published_by_row_tile": {str(k): pct(v) for k, v in sorted(byrt.items())},
+                          "entry_by_row_tile": {str(k): pct(v) for k, v in sorted(byrt_e.items())},
+                          "kloop_end_by_row_tile": {str(k): pct(v) for k, v in sorted(byrt_k.items())}}),
               flush=True)
         if rep == 3:  # per column tile (XCD-grouped grid: block b -> xcd b & 7, slot b >> 3, ct = xcd + 8 (slot // tm))
             tm = (a.hidden + 15) // 16
