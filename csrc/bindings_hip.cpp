@@ -79,6 +79,11 @@ struct MlpStep {
   // rows and dZ1 rows each launch writes are read back by the next one from the same XCD's L2 -- step 14.0 ->
   // 13.1-13.2 us at n = 800, 12.3 -> 11.7 us at n = 100, profiles/kbench_xcd_rows_r4.jsonl; 0 for A/B)
   int xcd_rows = 1;
+  // SplitStepArgs::xcd_rows == 2 for the forward + head when it fits (small batches): the first four XCDs start a
+  // launch up to ~1 us before the other four (profiles/r5/stamps_fha_per_xcd.jsonl), but two row tiles per XCD
+  // measured SLOWER, off: walking step +0.3-0.7 us at n = 100-512 (profiles/r5/kbench_xcd_pack.jsonl, alternated
+  // twice) -- each XCD then pulls twice the W1 rows and pixels through its L2
+  int xcd_pack = 0;
   // SplitStepArgs::pf_wgs, prefetch workgroups per XCD (0: off).  Walking-batch step (kbench step_walk_us, A/B twice):
   // 0 -> 4: 14.55-14.63 -> 14.11-14.14 us at n = 800, 13.0-13.1 -> 12.64-12.66 at n = 100; 2 and 6 slower at n = 800
   // (profiles/kbench_prefetch_wgs_r4.jsonl)
@@ -229,7 +234,8 @@ struct MlpStep {
     a.gstatus = P_<float>(gstatus);
     a.ag_wait_us = ag_wait_us;
     a.ag_test_skip = ag_test_skip;
-    a.xcd_rows = xcd_rows && cme::mlp_split_xcd_rows_ok(a);
+    a.xcd_rows = xcd_rows && cme::mlp_split_xcd_rows_ok(a) ? 1 : 0;
+    if (a.xcd_rows && xcd_pack && cme::mlp_split_xcd_rows_packed_ok(a)) a.xcd_rows = 2;
     a.pf_wgs = (a.xcd_rows && bias_col) ? prefetch : 0;
     a.pf_wgs_xt = (a.xcd_rows && bias_col) ? prefetch_xt : 0;
     a.wide_eng = wide_eng >= 0 ? wide_eng : (npw == 1 ? 1 : 0);
@@ -552,6 +558,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("store_a1", &MlpStep::store_a1)
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
       .def_readwrite("xcd_rows", &MlpStep::xcd_rows)
+      .def_readwrite("xcd_pack", &MlpStep::xcd_pack)
       .def_readwrite("prefetch", &MlpStep::prefetch)
       .def_readwrite("prefetch_xt", &MlpStep::prefetch_xt)
       .def_readwrite("wide_eng", &MlpStep::wide_eng)

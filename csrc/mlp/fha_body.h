@@ -62,8 +62,19 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   __shared__ int s_bad;
   __shared__ unsigned s_ep;
   const int xcd = blk & 7, slot = blk >> 3;
-  // column-tile grouping (the tm row tiles of a column tile on one XCD) or, xcd_rows, row tile rt on XCD rt
-  const int ct = f.xcd_rows ? slot : xcd + 8 * (slot / tm), rt = f.xcd_rows ? xcd : slot % tm;
+  // column-tile grouping (the tm row tiles of a column tile on one XCD) or, xcd_rows, row tile rt on XCD rt -- or,
+  // xcd_rows == 2 (the packed form for small batches), row tiles rt and rt + 4 on XCD rt < 4: the first four XCDs
+  // start a launch up to ~1 us before the others (bench/stamps_fha.py per row tile), and every column tile's
+  // all-gather waits for its last row tile
+  int ct, rt;
+  if (f.xcd_rows == 2) {
+    const int j = slot / tn;
+    ct = slot - j * tn;
+    rt = xcd < 4 ? xcd + 4 * j : tm;  // (XCDs 4-7: padding)
+  } else {
+    ct = f.xcd_rows ? slot : xcd + 8 * (slot / tm);
+    rt = f.xcd_rows ? xcd : slot % tm;
+  }
   if (ct >= tn || rt >= tm) return;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
   const int t = threadIdx.x, H = f.H, C = h.C, n = f.n;
   const int r0 = rt * 16, c0 = ct * kCols;

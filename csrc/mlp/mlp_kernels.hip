@@ -1111,7 +1111,10 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
                                         "last-arriver form, mlp_fwd1_head)");
   const bool af = mlp_split_fwd_fp32_w(f);
   const int vec = fha_vec(f);
-  const int nwg = f.xcd_rows ? 8 * tn + 8 * f.pf_wgs_xt : 8 * tm * cdiv(tn, 8);  // (prefetch workgroups last)
+  // (prefetch workgroups last; xcd_rows == 2: cdiv(tm, 4) slots of tn per XCD, XCDs 4-7 padding)
+  const int nwg = f.xcd_rows == 2 ? 8 * cdiv(tm, 4) * tn + 8 * f.pf_wgs_xt
+                  : f.xcd_rows    ? 8 * tn + 8 * f.pf_wgs_xt
+                                  : 8 * tm * cdiv(tn, 8);
 #define CME_FHA(np, af)                                                                                  \
   if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
   else if (vec == 1) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn); \

@@ -149,7 +149,8 @@ struct SplitStepArgs {
   // H <= 128 (at most 8 row tiles): the forward + head and the dW1 launches place the workgroups of row tile rt on
   // XCD rt (blockIdx % 8, speed only): the W1 rows the dW1 launch updates and the dZ1 rows the forward writes are
   // then read back by the next launch from the same XCD's L2 instead of the die-level cache.  Set by the launcher
-  // (mlp_split_xcd_rows_ok); 0: the column-tile grouping.
+  // (mlp_split_xcd_rows_ok); 0: the column-tile grouping; 2 (the forward + head launch only, small batches): row
+  // tiles rt and rt + 4 on XCD rt < 4 (mlp_split_xcd_rows_packed_ok; MlpStep.xcd_pack)
   int xcd_rows = 0;
   // H <= 128 under xcd_rows: pf_wgs extra workgroups per XCD in each launch pull the pixels that XCD's workgroups
   // read next into its L2, on CUs the step leaves idle: the forward + head launch this step's feature-major XT (for
@@ -182,6 +183,9 @@ bool mlp_split_wide_fwd_reads_planes(const SplitStepArgs& a, int ag, int allow64
 // the XCD-row placement (SplitStepArgs::xcd_rows) applies to this small-layer step: at most 8 row tiles of 16 and
 // at most one workgroup per CU of the XCD for each row tile's column tiles
 bool mlp_split_xcd_rows_ok(const SplitStepArgs& a);
+// ... and its packed form for the forward + head launch (xcd_rows == 2: row tiles rt and rt + 4 on XCD rt < 4, when
+// both fit the XCD's CUs: small batches)
+bool mlp_split_xcd_rows_packed_ok(const SplitStepArgs& a);
 
 
 // flag slots (workgroup tiles) of the fused-all-reduce wgrad launch for a P-H layer with the all-ones

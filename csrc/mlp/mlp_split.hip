@@ -1828,7 +1828,8 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   b.w2_ks = w2ks;
   b.w1_planes = mlp_split_w1_planes_read(a) ? 1 : 0;
   // the XCD-row placement only for the whole layer's dW1 (a bucketed row range keeps the plain order)
-  b.xcd_rows = a.xcd_rows && do_w1 && a.w1_row0 == 0 && a.w1_rows < 0 && cdiv(a.H, 16 * kWMB) <= 8;
+  // (the forward's packed form, xcd_rows == 2, is the forward's alone: 2 x 25 dW1 tiles would not fit 4 XCDs)
+  b.xcd_rows = a.xcd_rows && do_w1 && a.w1_row0 == 0 && a.w1_rows < 0 && cdiv(a.H, 16 * kWMB) <= 8 ? 1 : 0;
   b.pf_wgs = b.xcd_rows ? a.pf_wgs : 0;
   const dim3 grid((b.xcd_rows ? 8 * t1n : t1) + t2 + tb + 8 * b.pf_wgs);  // (prefetch workgroups last)
   const int fu = !fused ? 0 : a.xf_push ? 2 : 1;
@@ -1849,6 +1850,11 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
 #undef CME_WG
 #undef CME_WG3
   CME_LAUNCH_CHECK(s);
+}
+
+bool mlp_split_xcd_rows_packed_ok(const SplitStepArgs& a) {
+  const int tm = cdiv(a.H, 16), tn = cdiv(a.n, 32);
+  return mlp_split_xcd_rows_ok(a) && tm > 4 && tm <= 8 && cdiv(tm, 4) * tn <= device_cu_count() / 8;
 }
 
 bool mlp_split_xcd_rows_ok(const SplitStepArgs& a) {

@@ -840,3 +840,28 @@ def test_head_dw2_partials_match_the_role_gemm(n, store_a1):
     for a, b in zip(got[0][:2] + got[0][3:], got[1][:2] + got[1][3:]):
         assert torch.equal(a, b)
     assert not hipe.kernel_error()
+
+
+@pytest.mark.parametrize("H,n", [(100, 100), (100, 256), (100, 512), (128, 200), (100, 800), (64, 100)])
+def test_packed_xcd_rows_forward_is_bitwise_the_one_row_tile_per_xcd_form(H, n):
+    """The forward + head's packed placement for small batches (MlpStep.xcd_pack: row tiles rt and rt + 4 on XCD
+    rt < 4, the XCDs that start a launch first) against one row tile per XCD: the same tiles and sums, so the
+    parameters after several SGD steps and the last step's gradients are BITWISE equal (at n = 800 / H = 64 the
+    packed form does not apply and both runs are the same form)."""
+    x, y = synthetic_mnist(2 * n + 7, seed=H)
+    nn = NeuralNetwork([784, H, 10])
+    outs = []
+    for pack in (0, 1):
+        e = MlpEngine(nn.H, "f32", max_cols=n, device="cuda")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y, normalize=True)
+        e._hip_step().xcd_pack = pack
+        for off in (0, n, 7):
+            e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+        e.run(3, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
+        torch.cuda.synchronize()
+        assert not e.kernel_error()
+        outs.append([t.clone().cpu() for t in (e.D, e.params, e.grads)] + [e.loss_sum()])
+    for a, b in zip(outs[0][:-1], outs[1][:-1]):
+        assert torch.equal(a, b)
+    assert outs[0][-1] == outs[1][-1]
