@@ -82,7 +82,9 @@ def main(argv=None):
         hdw2 = int(m.group(1)) if m else None
         m = re.search(r"\+q(\d)", path)  # "+qK": the forward's packed XCD rows off / on (MlpStep.xcd_pack)
         xpack = int(m.group(1)) if m else None
-        path = re.sub(r"\+[sdxptglwhq]\d", "", path)
+        m = re.search(r"\+z(\d)", path)  # "+zK": the fragment-ordered W1 copy for the forward (MlpStep.w1_swz)
+        wswz = int(m.group(1)) if m else None
+        path = re.sub(r"\+[sdxptglwhqz]\d", "", path)
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -105,6 +107,8 @@ def main(argv=None):
                     step.head_dw2 = hdw2
                 if xpack is not None:
                     step.xcd_pack = xpack
+                if wswz is not None:
+                    step.w1_swz = wswz
                 if pref_xt is not None:
                     step.prefetch_xt = pref_xt
                 if no_a1:
@@ -116,7 +120,7 @@ def main(argv=None):
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else "") + (f"+g{weng}" if weng is not None else "") + (f"+l{gtouch}" if gtouch is not None else "") + (f"+w{w2ks}" if w2ks is not None else "") + (f"+h{hdw2}" if hdw2 is not None else "") + (f"+q{xpack}" if xpack is not None else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else "") + (f"+g{weng}" if weng is not None else "") + (f"+l{gtouch}" if gtouch is not None else "") + (f"+w{w2ks}" if w2ks is not None else "") + (f"+h{hdw2}" if hdw2 is not None else "") + (f"+q{xpack}" if xpack is not None else "") + (f"+z{wswz}" if wswz is not None else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(

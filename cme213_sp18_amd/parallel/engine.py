@@ -175,7 +175,7 @@ class MlpEngine:
         # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
         # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
         self.fh_counters = None
-        self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = self.w2g = None
+        self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = self.w2g = self.W1s = None
         if self.backend == "hip" and self.np and H <= 128 and C <= 16:
             tiles = (ld + 31) // 32
             self.fh_counters = torch.zeros(tiles, dtype=torch.int32, device=dev)
@@ -188,6 +188,8 @@ class MlpEngine:
             # counter (one 64-B line) and 7 x 256 partial-tile granules (tags only grow: never re-zeroed)
             t2 = (H + 15) // 16
             self.w2g = torch.zeros(t2 * 8 + t2 * 7 * 256, dtype=torch.int64, device=dev)
+            if self.np == 3:  # the forward's fragment-ordered fp32 copy of W1 (MlpStep.w1_swz)
+                self.W1s = torch.zeros(int(hip().mlp_split_w1s_floats(H, self.P)), dtype=torch.float32, device=dev)
         elif self.backend == "hip" and self.np and H >= 512 and C <= 16 and self.dw2buf is not None:
             # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_wide_ag) uses one
             # monotonic counter per column tile -- a separate array per tiling (128 x 128 / 64 x 64) -- and
@@ -254,9 +256,16 @@ class MlpEngine:
                 dst.copy_(torch.as_tensor(np.asarray(src)).to(dst.dtype))
             self.refresh_shadow()
 
+    def _w1_written(self) -> None:
+        """W1 changed outside the step's own in-place update: the forward's fragment-ordered copy (MlpStep.w1_swz)
+        is rebuilt before the next forward that reads it."""
+        if self._step is not None:
+            self._step.swz_stale = True
+
     def refresh_shadow(self):
         """Re-derive the low-precision copies of W1 (bf16 shadow or bf16 planes)."""
         self.join()
+        self._w1_written()
         with torch.no_grad():
             if self.np:
                 if self.backend == "hip":
@@ -350,6 +359,7 @@ class MlpEngine:
         reads the planes re-splits W1 first (MlpStep.lazy_planes: the wide in-place update skips the refresh)."""
         if self._step is not None and self.W1p is not None:
             self._step.planes_stale = True
+        self._w1_written()
 
     def _hip_step(self):
         if self._step is None:
@@ -370,7 +380,8 @@ class MlpEngine:
                          dZ1p=ptr(self.dZ1p))
             if self.fh_counters is not None:
                 b.update(fh_counters=ptr(self.fh_counters), fh_tiles=int(self.fh_counters.numel()),
-                         ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs), w2g=ptr(self.w2g))
+                         ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs), w2g=ptr(self.w2g),
+                         w1s=ptr(self.W1s))
             elif self.ag_gran is not None:  # the wide fused head
                 b.update(fh_tiles=int(self.ag_counters.numel()) // 64,  # [2 tilings][tiles][32]
                          ag_gran=ptr(self.ag_gran), ag_gran_count=int(self.ag_gran.numel()),
@@ -502,6 +513,7 @@ class MlpEngine:
     def sgd(self, lr: float):
         """params -= lr * grads over the whole flat arena (one fused kernel)."""
         self.join()
+        self._w1_written()
         if self.backend == "hip" and self.np:
             hip().split_sgd(self.params.data_ptr(), self.grads.data_ptr(), self.layout.total, float(lr),
                             self.W1p.data_ptr(), self.H * self.P, self.np,

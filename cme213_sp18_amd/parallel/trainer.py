@@ -475,6 +475,7 @@ class DataParallelTrainer:
         elif e.dtype == "bf16":  # bf16 path: single-rounded shadow of W1
             planes, np_ = e.W1g, 1
         self.xgmi.sgd_(e.grads, e.params, lr, planes, np_, e.H * e.P, status_index=e.status_index)
+        e._w1_written()
 
     # ---------------------------------------------------------------- data
     def load(self, x_train, y_train):

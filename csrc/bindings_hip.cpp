@@ -84,6 +84,18 @@ struct MlpStep {
   // measured SLOWER, off: walking step +0.3-0.7 us at n = 100-512 (profiles/r5/kbench_xcd_pack.jsonl, alternated
   // twice) -- each XCD then pulls twice the W1 rows and pixels through its L2
   int xcd_pack = 0;
+  // SplitStepArgs::w1_swz / W1s: the forward (H <= 128 split3, 16-byte pixel pairs) reads fp32 W1 from its
+  // fragment-ordered copy w1s; the in-place update keeps the copy fresh, every other W1 write marks it stale
+  // (swz_stale: MlpEngine.refresh_shadow / sgd / mark_planes_stale, run_wgrad with an update) and run() rebuilds it
+  // before the next forward that reads it
+  int w1_swz = 1;
+  uintptr_t w1s = 0;
+  bool swz_stale = true;
+  void refresh_swz(uintptr_t stream) {
+    if (!swz_stale || !w1s) return;
+    cme::mlp_split_w1s_refresh(P_<float>(W1), P_<float>(w1s), H, P, S(stream));
+    swz_stale = false;
+  }
   // SplitStepArgs::pf_wgs, prefetch workgroups per XCD (0: off).  Walking-batch step (kbench step_walk_us, A/B twice):
   // 0 -> 4: 14.55-14.63 -> 14.11-14.14 us at n = 800, 13.0-13.1 -> 12.64-12.66 at n = 100; 2 and 6 slower at n = 800
   // (profiles/kbench_prefetch_wgs_r4.jsonl)
@@ -197,6 +209,7 @@ struct MlpStep {
       else if (k == "ag_gran") ag_gran = u(); else if (k == "ag_gran_count") ag_gran_count = v.cast<int64_t>();
       else if (k == "kpart") kpart = u(); else if (k == "kpart_cap") kpart_cap = v.cast<int64_t>();
       else if (k == "w2g") w2g = u();
+      else if (k == "w1s") w1s = u();
       else throw std::invalid_argument("MlpStep.bind: unknown name '" + k + "'");
     }
   }
@@ -264,6 +277,12 @@ struct MlpStep {
       if (pf_next >= 0 && pf_next < N && a.pf_wgs) {
         a.pf_X = reinterpret_cast<const char*>(X) + (size_t)pf_next * P;
         a.pf_bytes = std::min<int64_t>(n, N - pf_next) * P;
+      }
+      // the forward reads the fragment-ordered W1 copy (rebuilt first if anything but this step's update wrote W1)
+      if (w1_swz && w1s && H <= 128 && npw == 3 && cme::mlp_split_fwd_fp32_w(a)) {
+        refresh_swz(stream);
+        a.w1_swz = 1;
+        a.W1s = P_<float>(w1s);
       }
       if (sgd == 2) {  // all-reduce + SGD inside the wgrad launch
         CME_REQUIRE(xf.world > 0 && xf_dev, "MlpStep.run(sgd=2): set_xgmi() first");
@@ -414,6 +433,7 @@ struct MlpStep {
     CME_REQUIRE(split, "MlpStep.run_wgrad: split (bf16-plane) paths only");
     CME_REQUIRE(n > 0 && n <= ld, "MlpStep.run_wgrad: 0 < n <= ld required");
     cme::SplitStepArgs a = split_args(off, n, scale, reg, lr, sgd, 0);
+    if (sgd) swz_stale = true;  // (an in-place update here does not maintain the forward's W1 copy)
     a.wg_parts = parts;
     a.w1_row0 = row0;
     a.w1_rows = rows;
@@ -559,6 +579,8 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("ag_tiles64", &MlpStep::ag_tiles64)
       .def_readwrite("xcd_rows", &MlpStep::xcd_rows)
       .def_readwrite("xcd_pack", &MlpStep::xcd_pack)
+      .def_readwrite("w1_swz", &MlpStep::w1_swz)
+      .def_readwrite("swz_stale", &MlpStep::swz_stale)
       .def_readwrite("prefetch", &MlpStep::prefetch)
       .def_readwrite("prefetch_xt", &MlpStep::prefetch_xt)
       .def_readwrite("wide_eng", &MlpStep::wide_eng)
@@ -620,6 +642,10 @@ PYBIND11_MODULE(_hip, m) {
         cme::occupy_cus(wgs, lds_bytes, ns, S(s), reinterpret_cast<int*>(running));
       },
       py::arg("wgs"), py::arg("lds_bytes"), py::arg("ns"), py::arg("stream"), py::arg("running") = 0);
+  m.def(
+      "mlp_split_w1s_floats", [](int H, int Pd) { return cme::mlp_split_w1s_floats(H, Pd); }, py::arg("H"),
+      py::arg("P"));
+
   m.def(
       "split_planes",
       [](uintptr_t W, uintptr_t planes, int64_t n, int np, uintptr_t s) {

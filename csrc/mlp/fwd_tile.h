@@ -15,6 +15,13 @@ __device__ __forceinline__ void fwd_tile(const SplitStepArgs& f, const TileGeom&
   const uint8_t* X = static_cast<const uint8_t*>(f.X);
   if constexpr (AF) {
     static_assert(NPW == 3, "fp32 W1 is split into three planes");
+    if constexpr (VEC == 3) {
+      if (f.w1_swz) {  // the fragment-ordered fp32 copy of W1 (SplitStepArgs::w1_swz)
+        wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t, float, true>(
+            f.W1s, (f.P + 63) / 64, X, f.P, g, epi, red, 0, stamps);
+        return;
+      }
+    }
     wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t>(f.W1, f.P, X, f.P, g, epi, red, 0, stamps);
   } else {
     wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, NPW, uint8_t>(

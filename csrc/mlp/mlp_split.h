@@ -96,6 +96,11 @@ struct SplitStepArgs {
   // the host on every launch: the native loop's host enqueue time per step is what that costs.)
   const XgmiFuse* xf = nullptr;
   int xf_world = 0, xf_push = 0;
+  // H <= 128 split3: the forward reads fp32 W1 from its fragment-ordered copy W1s (mma_tile.h ASWZ: every 16-byte
+  // load instruction of a wave reads 1 KB of contiguous memory instead of 16 rows x 64 B), and the weight-gradient
+  // launch's in-place update writes W1s next to W1 (w1s_off).  Set by MlpStep::run after refreshing a stale copy
+  int w1_swz = 0;
+  float* W1s = nullptr;
   // wide layers (LDS GEMM forward): when set, the forward GEMM's tile epilogue also leaves the head's
   // z2 partial sums, z2part[row tile][16][ld] = W2[:, tile rows] . a1[tile rows, :] (v_mfma_f32_16x16x4
   // on the activated accumulators), so the head never re-reads a1 for z2 (mlp_split_fwd1_z2_chunks)
@@ -186,6 +191,10 @@ bool mlp_split_xcd_rows_ok(const SplitStepArgs& a);
 // ... and its packed form for the forward + head launch (xcd_rows == 2: row tiles rt and rt + 4 on XCD rt < 4, when
 // both fit the XCD's CUs: small batches)
 bool mlp_split_xcd_rows_packed_ok(const SplitStepArgs& a);
+
+// the fragment-ordered fp32 copy of W1 (SplitStepArgs::W1s): floats for an H x P layer, and a full rebuild from W1
+int64_t mlp_split_w1s_floats(int H, int P);
+void mlp_split_w1s_refresh(const float* W1, float* W1s, int H, int P, hipStream_t s);
 
 
 // flag slots (workgroup tiles) of the fused-all-reduce wgrad launch for a P-H layer with the all-ones

@@ -329,6 +329,7 @@ struct EpiW1 {
   // into xo
   float *xs = nullptr, *xo = nullptr;
   int m0 = 0, n0 = 0;
+  float* W1s = nullptr;  // the fragment-ordered copy the forward reads (SplitStepArgs::W1s): updated with W1
   __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
     // (the all-ones feature column P: b1[row], so its update is not a dependent load after the K loop)
     if (col == P) pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
@@ -352,6 +353,7 @@ struct EpiW1 {
     if (upd) {
       const float nw = w - lr * g;
       W1[i] = nw;
+      if (W1s) W1s[w1s_off(row, col, (P + 63) >> 6)] = nw;
       if (npw == 3) split_store<3>(nw, W1p, plane, i);
       else if (npw == 1) split_store<1>(nw, W1p, plane, i);  // (0: no forward kernel reads the planes)
     } else if (sys == 2) {
@@ -423,6 +425,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     }
     EpiW1 epi{a.W1, gw, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, fused ? 0 : a.sgd, a.w1_planes ? a.npw : 0, reg, lr,
               a.xscale, {}, a.b1, gb, push ? 2 : (live ? 1 : 0), a.ag_err};
+    if (a.w1_swz) epi.W1s = a.W1s;
     XpWords xw;
     if (push) {
       epi.xs = xs;
@@ -457,6 +460,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
           ok && !(a.xp_dbg & 2)) {
         if (col < a.P) {
           a.W1[i] = nv;
+          if (a.w1_swz) a.W1s[w1s_off(row, col, (a.P + 63) >> 6)] = nv;
           if (a.w1_planes) {
             if (a.npw == 3) split_store<3>(nv, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
             else split_store<1>(nv, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
@@ -475,6 +479,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
           const int64_t i = (int64_t)row * a.P + col;
           const float w = a.W1[i] - lr * xf_sum(*a.xf, half + i);
           a.W1[i] = w;
+          if (a.w1_swz) a.W1s[w1s_off(row, col, (a.P + 63) >> 6)] = w;
           if (!a.w1_planes) continue;
           if (a.npw == 3) split_store<3>(w, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
           else split_store<1>(w, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, (size_t)i);
@@ -695,6 +700,19 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     const int r = first ? row : row - a.H;
     if (a.sgd && !poisoned(perr)) bp[r] = bpre - lr * s;
     else (first ? a.gb1 : a.gb2)[r] = s;
+  }
+}
+
+// the fragment-ordered copy of W1 rebuilt from W1 (padding slots: 0)
+__global__ __launch_bounds__(256) void w1s_kernel(const float* __restrict__ W, float* __restrict__ Ws, int H, int P,
+                                                  int64_t total) {
+  const int npair = (P + 63) >> 6;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int e = (int)(t & 3), lane = (int)((t >> 2) & 63), i = (int)((t >> 8) & 3);
+    const int64_t rp = t >> 10;  // rt * npair + p
+    const int p = (int)(rp % npair), rt = (int)(rp / npair);
+    const int row = rt * 16 + (lane & 15), col = p * 64 + (lane >> 4) * 16 + i * 4 + e;
+    Ws[t] = (row < H && col < P) ? W[(int64_t)row * P + col] : 0.f;
   }
 }
 
@@ -1865,6 +1883,15 @@ int mlp_split_fused_tiles(int P, int H, int cap) {
   // dW1 tiles, dW2 tiles, the db2 workgroup
   const int t = cdiv(P + 1, 16 * kWNB) * cdiv(H, 16 * kWMB) + cdiv(H, 16) + 1;
   return t <= cap ? t : -1;
+}
+
+int64_t mlp_split_w1s_floats(int H, int P) { return (int64_t)cdiv(H, 16) * 16 * cdiv(P, 64) * 64; }
+
+void mlp_split_w1s_refresh(const float* W1, float* W1s, int H, int P, hipStream_t s) {
+  const int64_t total = mlp_split_w1s_floats(H, P);
+  const int grid = (int)std::min<int64_t>(2048, (total + 255) / 256);
+  w1s_kernel<<<grid, 256, 0, s>>>(W1, W1s, H, P, total);
+  CME_LAUNCH_CHECK(s);
 }
 
 void mlp_split_planes(const float* W, void* planes, int64_t n, int np, hipStream_t s) {

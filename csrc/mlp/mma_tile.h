@@ -287,8 +287,19 @@ struct TileGeom {
 // TA = float (with T = bf16, NPA = 3, AK): A is the fp32 operand itself, 4 B per element pulled instead of
 // the 6 B of three stored planes, split into its exact planes in registers (split_trunc) while the MFMAs
 // of the previous unroll step run.
+//
+// ASWZ (fp32 A, VEC == 3, MB == 1): A is the fragment-ordered copy of the fp32 operand (SplitStepArgs::w1_swz): for
+// row tile rt, K pair p (64 k) and load i (0..3), lane l's 4 floats A(16 rt + (l & 15), 64 p + 16 (l >> 4) + 4 i ..
+// + 3) at float offset (((rt * lda + p) * 4 + i) * 64 + l) * 4, lda = the number of K pairs -- every 16-byte load
+// instruction of a wave reads 1 KB of contiguous memory instead of 16 rows x 64 B.
+// Float offset of A(row, col) in that copy (npair = cdiv(K, 64)).
+__host__ __device__ __forceinline__ int64_t w1s_off(int row, int col, int npair) {
+  const int rt = row >> 4, c = row & 15, p = col >> 6, w = col & 63;
+  const int lane = (w >> 4) * 16 + c, i = (w & 15) >> 2, e = w & 3;
+  return ((((int64_t)rt * npair + p) * 4 + i) * 64 + lane) * 4 + e;
+}
 template <typename T, int MB, int NB, int KS, bool AK, bool BK, int VEC, int U, int NPA = 1, typename TB = T,
-          typename TA = T, class Epi>
+          typename TA = T, bool ASWZ = false, class Epi>
 __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, const TB* __restrict__ B, int ldb,
                                          TileGeom g, Epi& epi,
                                          typename MmaTraits<T>::acc_t* __restrict__ red, int plane_bytes = 0,
@@ -372,7 +383,16 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = VEC == 3 ? kc + (u & ~1) * KC + 2 * V * grp + (u & 1) * V : kc + u * KC + V * grp;
-      if constexpr (AF32) {
+      if constexpr (AF32 && ASWZ) {
+        static_assert(MB == 1 && VEC == 3 && V == 8, "fragment-ordered A: one row block, chunk pairs");
+        const int kp = kc + (u & ~1) * KC;  // the pair's first k (a multiple of 64)
+        const bool ok = g.m0 + c < g.M && k < kend;
+        const int base = ((((g.m0 >> 4) * lda + (kp >> 6)) * 4 + 2 * (u & 1)) * 64 + lane) * 16;
+        const auto w0 = __builtin_amdgcn_raw_buffer_load_b128(rsA, ok ? base : kOOB, 0, 0);
+        const auto w1 = __builtin_amdgcn_raw_buffer_load_b128(rsA, ok ? base + 1024 : kOOB, 0, 0);
+        __builtin_memcpy(ar[u][0], &w0, 16);
+        __builtin_memcpy(reinterpret_cast<char*>(ar[u][0]) + 16, &w1, 16);
+      } else if constexpr (AF32) {
 #pragma unroll
         for (int i = 0; i < MB; ++i) load_frag<float, V, true, VA>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, ar[u][i]);
       } else {

@@ -865,3 +865,47 @@ def test_packed_xcd_rows_forward_is_bitwise_the_one_row_tile_per_xcd_form(H, n):
     for a, b in zip(outs[0][:-1], outs[1][:-1]):
         assert torch.equal(a, b)
     assert outs[0][-1] == outs[1][-1]
+
+
+@pytest.mark.parametrize("H,n", [(100, 800), (100, 100), (128, 513), (37, 48)])
+def test_fragment_ordered_w1_copy_is_bitwise_the_row_major_forward(H, n):
+    """The forward reading fp32 W1 from its fragment-ordered copy (MlpStep.w1_swz, mma_tile.h ASWZ) against the
+    row-major reads, through every way W1 changes: fused SGD steps (the copy maintained by the update), a gradient
+    step + the flat SGD kernel, an external overwrite + refresh_shadow(), mark_planes_stale() after a restore, and the
+    native step loop -- parameters bitwise equal after each."""
+    x, y = synthetic_mnist(4 * n + 7, seed=H)
+    nn = NeuralNetwork([784, H, 10])
+    engines = []
+    for swz in (0, 1):
+        e = MlpEngine(nn.H, "f32", max_cols=n, device="cuda", path="split3")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        e._hip_step().w1_swz = swz
+        engines.append(e)
+    p_init = engines[0].params.clone()
+
+    def both(fn):
+        for e in engines:
+            fn(e)
+        torch.cuda.synchronize()
+        assert torch.equal(engines[0].params, engines[1].params)
+
+    both(lambda e: [e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True) for off in (0, n, 7)])
+    both(lambda e: (e.run(3, n, 1.0 / n, 1e-4, 0.0, sgd=False), e.sgd(0.05), e.run(n, n, 1.0 / n, 1e-4, 0.05, sgd=True)))
+
+    def overwrite(e):
+        e.params.copy_(p_init)
+        e.refresh_shadow()
+        e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+    both(overwrite)
+
+    def restore(e):
+        e.params.copy_(p_init)
+        e.mark_planes_stale()
+        e.run(2 * n, n, 1.0 / n, 1e-4, 0.05, sgd=True)
+    both(restore)
+    N = engines[0].num_samples
+    both(lambda e: e._hip_step().run_steps(0, 5, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1,
+                                           torch.cuda.current_stream().cuda_stream))
+    for e in engines:
+        assert not e.kernel_error()
