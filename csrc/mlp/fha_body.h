@@ -49,7 +49,7 @@ struct EpiSigLds {
 
 // blk: the workgroup's slot in the XCD-grouped grid (the hardware XCD is blk & 7).  red: >= 8 * 2 * 4 * 64
 // floats of LDS.
-template <int NPW, int VEC, bool AF>
+template <int NPW, int VEC, bool AF, bool SWZ = false>
 __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs& h,
                                          unsigned long long* __restrict__ counters, gran_t* __restrict__ slabs,
                                          int* __restrict__ err, int tm, int tn, int blk, float* red) {
@@ -107,7 +107,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   const float b2v = buf_load1<float>(make_rsrc(h.b2), (t >= 256 && t < 256 + 16 && t - 256 < C) ? (t - 256) * 4 : kOOB);
   TileGeom g{H, n, f.P, r0, c0};
   EpiSigLds epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
-  fwd_tile<NPW, 2, VEC, 4, AF>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
+  fwd_tile<NPW, 2, VEC, 4, AF, SWZ>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
   // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
   // they are masked below.  w2s / b2s are complete after the barrier below.
   if (t < 256) w2s[wc][wr] = w2v;

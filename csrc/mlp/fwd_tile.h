@@ -9,18 +9,19 @@
 
 namespace cme {
 
-template <int NPW, int NB, int VEC, int U, bool AF, class Epi>
+// SWZ (AF, VEC == 3): read fp32 W1 from its fragment-ordered copy f.W1s (a template argument, not a runtime test:
+// the kernels that never read the copy carry none of its code)
+template <int NPW, int NB, int VEC, int U, bool AF, bool SWZ = false, class Epi>
 __device__ __forceinline__ void fwd_tile(const SplitStepArgs& f, const TileGeom& g, Epi& epi, float* red,
                                          unsigned long long* stamps = nullptr) {
   const uint8_t* X = static_cast<const uint8_t*>(f.X);
   if constexpr (AF) {
     static_assert(NPW == 3, "fp32 W1 is split into three planes");
-    if constexpr (VEC == 3) {
-      if (f.w1_swz) {  // the fragment-ordered fp32 copy of W1 (SplitStepArgs::w1_swz)
-        wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t, float, true>(
-            f.W1s, (f.P + 63) / 64, X, f.P, g, epi, red, 0, stamps);
-        return;
-      }
+    if constexpr (SWZ) {  // the fragment-ordered fp32 copy of W1 (SplitStepArgs::w1_swz)
+      static_assert(VEC == 3, "fragment-ordered W1: 16-byte pixel pairs");
+      wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t, float, true>(f.W1s, (f.P + 63) / 64, X, f.P,
+                                                                                       g, epi, red, 0, stamps);
+      return;
     }
     wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t>(f.W1, f.P, X, f.P, g, epi, red, 0, stamps);
   } else {

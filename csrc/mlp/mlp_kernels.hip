@@ -526,7 +526,7 @@ __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArg
 
 // ------------------------------------- forward GEMM + head in ONE launch, all-gather form (H <= 128)
 // (body: fha_body.h)
-template <int NPW, int VEC, bool AF>
+template <int NPW, int VEC, bool AF, bool SWZ = false>
 __global__ __launch_bounds__(512) void fwd1_head_ag_kernel(SplitStepArgs f, HeadArgs h,
                                                            unsigned long long* __restrict__ counters,
                                                            gran_t* __restrict__ slabs, int* __restrict__ err, int tm,
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(512) void fwd1_head_ag_kernel(SplitStepArgs f, Head
     if (xcd < tm) l2_touch(f.XT, 0, f.P + f.bias_col, f.ldxt, f.n, part, f.pf_wgs_xt, reinterpret_cast<char*>(red));
     return;
   }
-  fha_body<NPW, VEC, AF>(f, h, counters, slabs, err, tm, tn, blockIdx.x, red);
+  fha_body<NPW, VEC, AF, SWZ>(f, h, counters, slabs, err, tm, tn, blockIdx.x, red);
 }
 
 template <typename P, int NC>
@@ -1116,7 +1116,9 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
                   : f.xcd_rows    ? 8 * tn + 8 * f.pf_wgs_xt
                                   : 8 * tm * cdiv(tn, 8);
 #define CME_FHA(np, af)                                                                                  \
-  if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
+  if (vec == 3 && af && f.w1_swz)                                                                        \
+    fwd1_head_ag_kernel<3, 3, true, true><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);        \
+  else if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
   else if (vec == 1) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn); \
   else fwd1_head_ag_kernel<np, 0, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);
   if (af) { CME_FHA(3, true) } else if (f.npw == 3) { CME_FHA(3, false) } else { CME_FHA(1, false) }
