@@ -25,4 +25,4 @@ step wide4096_f32 180 python3 bench.py --gpus 1 --hidden 4096 --dtype f32 --step
 step wide4096_bf16 180 python3 bench.py --gpus 1 --hidden 4096 --dtype bf16 --steps 200 --warmup 20 &&
 step wide1024_bf16 180 python3 bench.py --gpus 1 --hidden 1024 --dtype bf16 --steps 400 --warmup 40 &&
 step headline_bf16 120 python3 bench.py --gpus 1 --dtype bf16 --steps 2000 --warmup 200 &&
-step rocprof 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o headline -- python3 bench.py --gpus 1 --steps 400 --warmup 40
+step rocprof 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o headline -- python3 bench.py --gpus 1 --steps 400 --warmup 40
