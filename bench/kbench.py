@@ -84,7 +84,9 @@ def main(argv=None):
         xpack = int(m.group(1)) if m else None
         m = re.search(r"\+z(\d)", path)  # "+zK": the fragment-ordered W1 copy for the forward (MlpStep.w1_swz)
         wswz = int(m.group(1)) if m else None
-        path = re.sub(r"\+[sdxptglwhqz]\d", "", path)
+        m = re.search(r"\+y(\d)", path)  # "+yK": the fragment-ordered pixel copy for the forward (MlpStep.x_swz)
+        xswz = int(m.group(1)) if m else None
+        path = re.sub(r"\+[sdxptglwhqzy]\d", "", path)
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -109,6 +111,8 @@ def main(argv=None):
                     step.xcd_pack = xpack
                 if wswz is not None:
                     step.w1_swz = wswz
+                if xswz is not None:
+                    step.x_swz = xswz
                 if pref_xt is not None:
                     step.prefetch_xt = pref_xt
                 if no_a1:

@@ -33,6 +33,16 @@ def _round_up(x: int, a: int) -> int:
     return (x + a - 1) // a * a
 
 
+def fragment_order_pixels(x: torch.Tensor) -> torch.Tensor:
+    """[N][P] uint8 -> the forward's fragment-ordered copy (csrc/mlp/mma_tile.h ``xs_off``): sample tile s // 16,
+    64-k pair k // 64, lane ((k % 64) // 16) * 16 + s % 16, byte k % 16; zero-padded to whole tiles and pairs."""
+    n, p = x.shape
+    ns, npair = _round_up(n, 16), (p + 63) // 64
+    xp = torch.zeros(ns, npair * 64, dtype=torch.uint8, device=x.device)
+    xp[:n, :p] = x
+    return xp.view(ns // 16, 16, npair, 4, 16).permute(0, 2, 3, 1, 4).contiguous().view(-1)
+
+
 def param_dtype(dtype: str) -> torch.dtype:
     return torch.float64 if dtype == "f64" else torch.float32
 
@@ -113,6 +123,7 @@ class MlpEngine:
         self.X = None
         self.Xw = self.XTw = None  # wide-layer bf16 copies (load_dataset)
         self.XT = None
+        self.Xs = None  # the pixels in the forward's fragment order (load_dataset)
         self.labels = None
         self._normalize = False
         self.xscale = 1.0
@@ -241,6 +252,12 @@ class MlpEngine:
         # (csrc/mlp/glds_gemm.h streams operands global -> LDS unconverted; 2 B/pixel, ~170 MB for the
         # 54k-image training split -- nothing next to 288 GB of HBM)
         self.Xw = self.XTw = None
+        # H <= 128 split3: the pixels again, in the forward's fragment order (MlpStep.x_swz; mma_tile.h xs_off):
+        # [cdiv(N, 16)][cdiv(P, 64)][4 lane groups][16 samples][16 B], zero-padded -- a wave's 16-byte load
+        # instruction reads 1 KB of contiguous memory instead of 16 rows x 64 B (~47 MB for 60k images)
+        self.Xs = None
+        if self.np == 3 and self.backend == "hip" and self.H <= 128 and self.XT is not None:
+            self.Xs = fragment_order_pixels(self.X)
         if self.np and self.backend == "hip" and self.H >= 512 and self.XT is not None:
             self.Xw = self.X.to(torch.bfloat16).contiguous()
             self.XTw = self.XT.to(torch.bfloat16).contiguous()
@@ -381,7 +398,7 @@ class MlpEngine:
             if self.fh_counters is not None:
                 b.update(fh_counters=ptr(self.fh_counters), fh_tiles=int(self.fh_counters.numel()),
                          ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs), w2g=ptr(self.w2g),
-                         w1s=ptr(self.W1s))
+                         w1s=ptr(self.W1s), xs=ptr(self.Xs))
             elif self.ag_gran is not None:  # the wide fused head
                 b.update(fh_tiles=int(self.ag_counters.numel()) // 64,  # [2 tilings][tiles][32]
                          ag_gran=ptr(self.ag_gran), ag_gran_count=int(self.ag_gran.numel()),

@@ -90,6 +90,10 @@ struct MlpStep {
   // before the next forward that reads it
   int w1_swz = 1;
   uintptr_t w1s = 0;
+  // SplitStepArgs::x_swz / Xs: with w1_swz, the forward also reads the pixels from their fragment-ordered copy xs
+  // (MlpEngine.load_dataset builds it once; a step whose first sample is not a multiple of 16 reads the row-major X)
+  int x_swz = 1;
+  uintptr_t xs = 0;
   bool swz_stale = true;
   void refresh_swz(uintptr_t stream) {
     if (!swz_stale || !w1s) return;
@@ -210,6 +214,7 @@ struct MlpStep {
       else if (k == "kpart") kpart = u(); else if (k == "kpart_cap") kpart_cap = v.cast<int64_t>();
       else if (k == "w2g") w2g = u();
       else if (k == "w1s") w1s = u();
+      else if (k == "xs") xs = u();
       else throw std::invalid_argument("MlpStep.bind: unknown name '" + k + "'");
     }
   }
@@ -274,15 +279,31 @@ struct MlpStep {
       // the next step's first sample (the native step loop knows it): its pixels are prefetched by this step's
       // weight-gradient launch (SplitStepArgs::pf_X)
       // (only the rows that exist: the next step's shard may be shorter than this one, or past the dataset's end)
-      if (pf_next >= 0 && pf_next < N && a.pf_wgs) {
-        a.pf_X = reinterpret_cast<const char*>(X) + (size_t)pf_next * P;
-        a.pf_bytes = std::min<int64_t>(n, N - pf_next) * P;
-      }
       // the forward reads the fragment-ordered W1 copy (rebuilt first if anything but this step's update wrote W1)
-      if (w1_swz && w1s && H <= 128 && npw == 3 && cme::mlp_split_fwd_fp32_w(a)) {
+      const bool swz = w1_swz && w1s && cme::mlp_fwd_swz_ok(a);
+      if (swz) {
         refresh_swz(stream);
         a.w1_swz = 1;
         a.W1s = P_<float>(w1s);
+      } else if (sgd) {
+        swz_stale = true;  // (this step's update does not write the copy)
+      }
+      // ... and the pixels from theirs when this step's samples start a 16-sample tile of it
+      const int64_t xs_tile = (int64_t)((P + 63) / 64) * 1024;  // bytes per 16 samples
+      const bool xsw = swz && x_swz && xs;
+      if (xsw && off % 16 == 0) {
+        a.x_swz = 1;
+        a.Xs = reinterpret_cast<const char*>(xs) + off / 16 * xs_tile;
+      }
+      if (pf_next >= 0 && pf_next < N && a.pf_wgs) {  // (the copy the next step's forward will read)
+        const int64_t rows = std::min<int64_t>(n, N - pf_next);
+        if (xsw && pf_next % 16 == 0) {
+          a.pf_X = reinterpret_cast<const char*>(xs) + pf_next / 16 * xs_tile;
+          a.pf_bytes = (rows + 15) / 16 * xs_tile;
+        } else {
+          a.pf_X = reinterpret_cast<const char*>(X) + (size_t)pf_next * P;
+          a.pf_bytes = rows * P;
+        }
       }
       if (sgd == 2) {  // all-reduce + SGD inside the wgrad launch
         CME_REQUIRE(xf.world > 0 && xf_dev, "MlpStep.run(sgd=2): set_xgmi() first");
@@ -580,6 +601,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("xcd_rows", &MlpStep::xcd_rows)
       .def_readwrite("xcd_pack", &MlpStep::xcd_pack)
       .def_readwrite("w1_swz", &MlpStep::w1_swz)
+      .def_readwrite("x_swz", &MlpStep::x_swz)
       .def_readwrite("swz_stale", &MlpStep::swz_stale)
       .def_readwrite("prefetch", &MlpStep::prefetch)
       .def_readwrite("prefetch_xt", &MlpStep::prefetch_xt)

@@ -49,7 +49,7 @@ struct EpiSigLds {
 
 // blk: the workgroup's slot in the XCD-grouped grid (the hardware XCD is blk & 7).  red: >= 8 * 2 * 4 * 64
 // floats of LDS.
-template <int NPW, int VEC, bool AF, bool SWZ = false>
+template <int NPW, int VEC, bool AF, int SWZ = 0>
 __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs& h,
                                          unsigned long long* __restrict__ counters, gran_t* __restrict__ slabs,
                                          int* __restrict__ err, int tm, int tn, int blk, float* red) {

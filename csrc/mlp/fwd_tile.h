@@ -9,18 +9,24 @@
 
 namespace cme {
 
-// SWZ (AF, VEC == 3): read fp32 W1 from its fragment-ordered copy f.W1s (a template argument, not a runtime test:
-// the kernels that never read the copy carry none of its code)
-template <int NPW, int NB, int VEC, int U, bool AF, bool SWZ = false, class Epi>
+// SWZ (AF, VEC == 3; a template argument, not a runtime test: the kernels that never read the copies carry none of
+// their code): bit0 reads fp32 W1 from its fragment-ordered copy f.W1s, bit1 also the pixels from theirs, f.Xs
+// (SplitStepArgs::w1_swz / x_swz; both need K pairs that start at multiples of 64: mlp_fwd_swz_ok)
+template <int NPW, int NB, int VEC, int U, bool AF, int SWZ = 0, class Epi>
 __device__ __forceinline__ void fwd_tile(const SplitStepArgs& f, const TileGeom& g, Epi& epi, float* red,
                                          unsigned long long* stamps = nullptr) {
   const uint8_t* X = static_cast<const uint8_t*>(f.X);
   if constexpr (AF) {
     static_assert(NPW == 3, "fp32 W1 is split into three planes");
-    if constexpr (SWZ) {  // the fragment-ordered fp32 copy of W1 (SplitStepArgs::w1_swz)
-      static_assert(VEC == 3, "fragment-ordered W1: 16-byte pixel pairs");
-      wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t, float, true>(f.W1s, (f.P + 63) / 64, X, f.P,
-                                                                                       g, epi, red, 0, stamps);
+    if constexpr (SWZ != 0) {  // the fragment-ordered fp32 copy of W1 (SplitStepArgs::w1_swz)
+      static_assert(VEC == 3 && (SWZ == 1 || SWZ == 3), "fragment-ordered W1 (+ pixels): 16-byte pixel pairs");
+      const int npair = (f.P + 63) / 64;
+      if constexpr (SWZ == 3)
+        wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t, float, true, true>(
+            f.W1s, npair, static_cast<const uint8_t*>(f.Xs), npair, g, epi, red, 0, stamps);
+      else
+        wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t, float, true>(f.W1s, npair, X, f.P, g, epi,
+                                                                                         red, 0, stamps);
       return;
     }
     wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t>(f.W1, f.P, X, f.P, g, epi, red, 0, stamps);

@@ -74,6 +74,9 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
 // the all-gather form's grid fits on the device at once (occupancy x CU count): every workgroup waits for the
 // others of its column tile, so a larger grid (a large per-GPU batch) must take the last-arriver form
 bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f);
+// its forward can read the fragment-ordered copies of W1 and of the pixels (SplitStepArgs::w1_swz / x_swz): fp32 W1,
+// 16-byte pixel pairs, and K ranges per wave that start on 64-k pair boundaries
+bool mlp_fwd_swz_ok(const SplitStepArgs& f);
 // TEST SUPPORT (occupy.hip): `wgs` workgroups of `lds_bytes` LDS each, sleeping for `ns` (bounded): keeps CUs busy;
 // `running` (host-pinned, may be null) is set to 1 once the first workgroup runs
 void occupy_cus(int wgs, int lds_bytes, int64_t ns, hipStream_t s, int* running = nullptr);

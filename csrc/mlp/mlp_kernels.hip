@@ -526,7 +526,7 @@ __global__ __launch_bounds__(512) void fwd1_head_kernel(SplitStepArgs f, HeadArg
 
 // ------------------------------------- forward GEMM + head in ONE launch, all-gather form (H <= 128)
 // (body: fha_body.h)
-template <int NPW, int VEC, bool AF, bool SWZ = false>
+template <int NPW, int VEC, bool AF, int SWZ = 0>
 __global__ __launch_bounds__(512) void fwd1_head_ag_kernel(SplitStepArgs f, HeadArgs h,
                                                            unsigned long long* __restrict__ counters,
                                                            gran_t* __restrict__ slabs, int* __restrict__ err, int tm,
@@ -1084,6 +1084,13 @@ static int fha_vec(const SplitStepArgs& f) {
   return x % 16 == 0 && f.P % 16 == 0 ? 3 : 1;
 }
 
+// the fragment-ordered operand copies (SplitStepArgs::w1_swz / x_swz) are laid out in 64-k pairs: the forward's
+// waves must start their K ranges on pair boundaries, i.e. an even number of 32-k chunks per wave (8 waves):
+// P = 784 / 800 / 1024 yes (4 chunks), P <= 256 or 513..768 no -- those take the row-major forms
+bool mlp_fwd_swz_ok(const SplitStepArgs& f) {
+  return f.H <= 128 && mlp_split_fwd_fp32_w(f) && fha_vec(f) == 3 && cdiv(cdiv(f.P, 32), 8) % 2 == 0;
+}
+
 bool mlp_fwd1_head_ag_fits(const SplitStepArgs& f) {
   if (f.n <= 0) return true;
   const int tm = cdiv(f.H, 16), tn = cdiv(f.n, 32), nwg = tm * tn;
@@ -1111,13 +1118,17 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
                                         "last-arriver form, mlp_fwd1_head)");
   const bool af = mlp_split_fwd_fp32_w(f);
   const int vec = fha_vec(f);
+  const bool swz = f.w1_swz && f.W1s && mlp_fwd_swz_ok(f);
+  CME_REQUIRE(!f.x_swz || (swz && f.Xs), "fwd1_head_ag: the fragment-ordered pixels need the W1 copy's form too");
   // (prefetch workgroups last; xcd_rows == 2: cdiv(tm, 4) slots of tn per XCD, XCDs 4-7 padding)
   const int nwg = f.xcd_rows == 2 ? 8 * cdiv(tm, 4) * tn + 8 * f.pf_wgs_xt
                   : f.xcd_rows    ? 8 * tn + 8 * f.pf_wgs_xt
                                   : 8 * tm * cdiv(tn, 8);
 #define CME_FHA(np, af)                                                                                  \
-  if (vec == 3 && af && f.w1_swz)                                                                        \
-    fwd1_head_ag_kernel<3, 3, true, true><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);        \
+  if (swz && f.x_swz)                                                                                   \
+    fwd1_head_ag_kernel<3, 3, true, 3><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);           \
+  else if (swz)                                                                                         \
+    fwd1_head_ag_kernel<3, 3, true, 1><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);           \
   else if (vec == 3) fwd1_head_ag_kernel<np, 3, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);  \
   else if (vec == 1) fwd1_head_ag_kernel<np, 1, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn); \
   else fwd1_head_ag_kernel<np, 0, af><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);

@@ -101,6 +101,10 @@ struct SplitStepArgs {
   // launch's in-place update writes W1s next to W1 (w1s_off).  Set by MlpStep::run after refreshing a stale copy
   int w1_swz = 0;
   float* W1s = nullptr;
+  // ... and (with w1_swz) the pixels from their fragment-ordered copy Xs: this step's first sample tile of the
+  // [cdiv(N, 16)][cdiv(P, 64)][64 lanes][16 B] copy (mma_tile.h BSWZ / xs_off; the step's first sample a multiple of 16)
+  int x_swz = 0;
+  const void* Xs = nullptr;
   // wide layers (LDS GEMM forward): when set, the forward GEMM's tile epilogue also leaves the head's
   // z2 partial sums, z2part[row tile][16][ld] = W2[:, tile rows] . a1[tile rows, :] (v_mfma_f32_16x16x4
   // on the activated accumulators), so the head never re-reads a1 for z2 (mlp_split_fwd1_z2_chunks)

@@ -298,8 +298,16 @@ __host__ __device__ __forceinline__ int64_t w1s_off(int row, int col, int npair)
   const int lane = (w >> 4) * 16 + c, i = (w & 15) >> 2, e = w & 3;
   return ((((int64_t)rt * npair + p) * 4 + i) * 64 + lane) * 4 + e;
 }
+// BSWZ (u8 B, VEC == 3): B is the fragment-ordered copy of the pixels (SplitStepArgs::x_swz), ldb = the number of K
+// pairs: sample tile st (16 samples), K pair p, lane l's 16 bytes at byte ((st * ldb + p) * 64 + l) * 16 (xs_off),
+// st counted from the tile geometry's n0 = 0 -- again 1 KB per wave load instruction.  Needs g.n0 % 16 == 0.
+__host__ __device__ __forceinline__ int64_t xs_off(int64_t s, int k, int npair) {
+  const int p = k >> 6, w = k & 63;
+  const int lane = (w >> 4) * 16 + (int)(s & 15);
+  return (((s >> 4) * npair + p) * 64 + lane) * 16 + (w & 15);
+}
 template <typename T, int MB, int NB, int KS, bool AK, bool BK, int VEC, int U, int NPA = 1, typename TB = T,
-          typename TA = T, bool ASWZ = false, class Epi>
+          typename TA = T, bool ASWZ = false, bool BSWZ = false, class Epi>
 __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, const TB* __restrict__ B, int ldb,
                                          TileGeom g, Epi& epi,
                                          typename MmaTraits<T>::acc_t* __restrict__ red, int plane_bytes = 0,
@@ -409,8 +417,9 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
           if constexpr (VEC == 3) {
             if ((u & 1) == 0) {  // the pair's 16 bytes: words 0-1 -> chunk u, words 2-3 -> chunk u + 1
               const int r = g.n0 + 16 * j + c;
-              const auto w = __builtin_amdgcn_raw_buffer_load_b128(
-                  rsB, (r < g.N && k + 16 <= kend) ? r * ldb + k : kOOB, 0, 0);
+              int off = r * ldb + k;
+              if constexpr (BSWZ) off = ((((g.n0 >> 4) + j) * ldb + ((kc + u * KC) >> 6)) * 64 + lane) * 16;
+              const auto w = __builtin_amdgcn_raw_buffer_load_b128(rsB, (r < g.N && k + 16 <= kend) ? off : kOOB, 0, 0);
               braw[u][j].w[0] = w[0];
               braw[u][j].w[1] = w[1];
               braw[u + 1][j].w[0] = w[2];

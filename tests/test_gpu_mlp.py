@@ -867,45 +867,55 @@ def test_packed_xcd_rows_forward_is_bitwise_the_one_row_tile_per_xcd_form(H, n):
     assert outs[0][-1] == outs[1][-1]
 
 
-@pytest.mark.parametrize("H,n", [(100, 800), (100, 100), (128, 513), (37, 48)])
-def test_fragment_ordered_w1_copy_is_bitwise_the_row_major_forward(H, n):
-    """The forward reading fp32 W1 from its fragment-ordered copy (MlpStep.w1_swz, mma_tile.h ASWZ) against the
-    row-major reads, through every way W1 changes: fused SGD steps (the copy maintained by the update), a gradient
-    step + the flat SGD kernel, an external overwrite + refresh_shadow(), mark_planes_stale() after a restore, and the
-    native step loop -- parameters bitwise equal after each."""
-    x, y = synthetic_mnist(4 * n + 7, seed=H)
-    nn = NeuralNetwork([784, H, 10])
+@pytest.mark.parametrize("P,H,n", [(784, 100, 800), (784, 100, 100), (784, 128, 513), (784, 37, 48), (800, 64, 96),
+                                   (208, 100, 128)])
+def test_fragment_ordered_copies_are_bitwise_the_row_major_forward(P, H, n):
+    """The forward reading fp32 W1 (MlpStep.w1_swz, mma_tile.h ASWZ) and the pixels (MlpStep.x_swz, BSWZ) from their
+    fragment-ordered copies against the row-major reads, through every way W1 changes: fused SGD steps (the copy
+    maintained by the update), a gradient step + the flat SGD kernel, an external overwrite + refresh_shadow(),
+    mark_planes_stale() after a restore, and the native step loop -- parameters bitwise equal after each.  Steps
+    start at multiples of 16 (the pixel copy read) and elsewhere (the row-major pixels); P = 208 has an odd number of
+    32-k chunks per wave, so neither copy may be read (mlp_fwd_swz_ok) -- the result must still match."""
+    g = torch.Generator().manual_seed(H + P)
+    x = torch.randint(0, 256, (4 * n + 7, P), generator=g, dtype=torch.uint8).numpy()
+    y = torch.randint(0, 10, (4 * n + 7,), generator=g).numpy()
+    nn = NeuralNetwork([P, H, 10])
     engines = []
-    for swz in (0, 1):
-        e = MlpEngine(nn.H, "f32", max_cols=n, device="cuda", path="split3")
+    for w1, xs in ((0, 0), (1, 0), (1, 1)):
+        e = MlpEngine((P, H, 10), "f32", max_cols=n, device="cuda", path="split3")
         e.set_params(*nn.params)
-        e.load_dataset(x, y)
-        e._hip_step().w1_swz = swz
+        e.load_dataset(x, y, normalize=True)
+        st = e._hip_step()
+        st.w1_swz, st.x_swz = w1, xs
         engines.append(e)
     p_init = engines[0].params.clone()
 
-    def both(fn):
+    def all_forms(fn):
         for e in engines:
             fn(e)
         torch.cuda.synchronize()
-        assert torch.equal(engines[0].params, engines[1].params)
+        for e in engines[1:]:
+            assert torch.equal(engines[0].params, e.params)
+            assert torch.equal(engines[0].D[:, :n], e.D[:, :n])
 
-    both(lambda e: [e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True) for off in (0, n, 7)])
-    both(lambda e: (e.run(3, n, 1.0 / n, 1e-4, 0.0, sgd=False), e.sgd(0.05), e.run(n, n, 1.0 / n, 1e-4, 0.05, sgd=True)))
+    all_forms(lambda e: [e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True) for off in (0, n, 7, 16, 32)])
+    all_forms(lambda e: (e.run(3, n, 1.0 / n, 1e-4, 0.0, sgd=False), e.sgd(0.05),
+                         e.run(n, n, 1.0 / n, 1e-4, 0.05, sgd=True)))
 
     def overwrite(e):
         e.params.copy_(p_init)
         e.refresh_shadow()
         e.run(0, n, 1.0 / n, 1e-4, 0.05, sgd=True)
-    both(overwrite)
+    all_forms(overwrite)
 
     def restore(e):
         e.params.copy_(p_init)
         e.mark_planes_stale()
         e.run(2 * n, n, 1.0 / n, 1e-4, 0.05, sgd=True)
-    both(restore)
+    all_forms(restore)
     N = engines[0].num_samples
-    both(lambda e: e._hip_step().run_steps(0, 5, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1,
-                                           torch.cuda.current_stream().cuda_stream))
+    # (the native loop walks batches of n from 0 and wraps; each step prefetches the tiles the next one reads)
+    all_forms(lambda e: e._hip_step().run_steps(0, 9, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1,
+                                                torch.cuda.current_stream().cuda_stream))
     for e in engines:
         assert not e.kernel_error()
