@@ -76,8 +76,6 @@ def main(argv=None):
         weng = int(m.group(1)) if m else None
         m = re.search(r"\+l(\d)", path)  # "+lK": the g64 engine's L2 pre-touch off / on (MlpStep.g64_touch)
         gtouch = int(m.group(1)) if m else None
-        m = re.search(r"\+w(\d)", path)  # "+wK": the dW2 role's workgroups per tile (MlpStep.w2_ks)
-        w2ks = int(m.group(1)) if m else None
         m = re.search(r"\+h(\d)", path)  # "+hK": the H <= 128 head's dW2 partials off / on (MlpStep.head_dw2)
         hdw2 = int(m.group(1)) if m else None
         m = re.search(r"\+q(\d)", path)  # "+qK": the forward's packed XCD rows off / on (MlpStep.xcd_pack)
@@ -103,8 +101,6 @@ def main(argv=None):
                     step.wide_eng = weng
                 if gtouch is not None:
                     step.g64_touch = gtouch
-                if w2ks is not None:
-                    step.w2_ks = w2ks
                 if hdw2 is not None:
                     step.head_dw2 = hdw2
                 if xpack is not None:
@@ -124,7 +120,7 @@ def main(argv=None):
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else "") + (f"+g{weng}" if weng is not None else "") + (f"+l{gtouch}" if gtouch is not None else "") + (f"+w{w2ks}" if w2ks is not None else "") + (f"+h{hdw2}" if hdw2 is not None else "") + (f"+q{xpack}" if xpack is not None else "") + (f"+z{wswz}" if wswz is not None else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else "") + (f"+g{weng}" if weng is not None else "") + (f"+l{gtouch}" if gtouch is not None else "") + (f"+h{hdw2}" if hdw2 is not None else "") + (f"+q{xpack}" if xpack is not None else "") + (f"+z{wswz}" if wswz is not None else "") + (f"+y{xswz}" if xswz is not None else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(

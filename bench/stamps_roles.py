@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """Timeline of the small-layer weight-gradient launch's ROLE workgroups (dW2 tiles / slices, db2 rows) from
 per-workgroup and per-wave s_memrealtime stamps (SplitStepArgs::wstamps: entry / end; SplitStepArgs::stamps inside
-wsk_tile: wave entry, K loop done, reduction barrier, epilogue done; 100 MHz), for MlpStep.w2_ks = 1 / 4 / 8 and
-the roles alone (run_wgrad parts = 2) or the whole launch (run parts = 2, SGD fused).  Diagnostic only.
+wsk_tile: wave entry, K loop done, reduction barrier, epilogue done; 100 MHz), with and without the head's dW2
+partials (MlpStep.head_dw2) and for the roles alone (run_wgrad parts = 2) or the whole launch (run parts = 2, SGD
+fused).  Diagnostic only.  (The dW2 role split over workgroups this script also timed, MlpStep.w2_ks, measured no
+faster and was removed: profiles/r5/stamps_roles_w2_split.jsonl.)
 
-    python bench/stamps_roles.py [--n 400 800] [--ks 1 4 8]
+    python bench/stamps_roles.py [--n 400 800]
 """
 from __future__ import annotations
 
@@ -19,7 +21,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, nargs="*", default=[400, 800])
-    ap.add_argument("--ks", type=int, nargs="*", default=[1, 4, 8])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--head-dw2", type=int, nargs="*", default=[0, 1])
     a = ap.parse_args(argv)
@@ -41,8 +42,7 @@ def main(argv=None):
         st = torch.cuda.current_stream().cuda_stream
         wbuf = torch.zeros(1024 * 8, dtype=torch.int64, device="cuda")
         sbuf = torch.zeros(1024 * 8 * 4, dtype=torch.int64, device="cuda")
-        for ks, hd in [(k, h) for h in a.head_dw2 for k in (a.ks if not h else [1])]:
-            step.w2_ks = ks
+        for hd in a.head_dw2:
             step.head_dw2 = hd
             for whole in (False, True):
                 rows = []
@@ -67,7 +67,7 @@ def main(argv=None):
                     us = lambda v: (v - t0) * 10.0 / 1000.0  # noqa: E731
                     nb = int(live.nonzero()[0].max()) + 1
                     first_role = 8 * 25 if whole else 0
-                    t2 = 7 * (ks if n >= 64 * ks and not hd else 1)
+                    t2 = 7
                     roles = [b for b in range(first_role, first_role + t2) if w[b, 0] > 0]
                     bias = [b for b in range(first_role + t2, nb) if w[b, 0] > 0 and w[b, 3] > 0 and b < first_role + t2 + 2]
                     kdone = [us(s[b, :, 1].max()) for b in roles if s[b, 0, 0] > 0]
@@ -80,7 +80,7 @@ def main(argv=None):
                 med = {k: [round(float(np.median([r[k][i] for r in rows if r[k]])), 3) for i in range(3)]
                        for k in rows[0] if k != "launch_end" and rows[0][k]}
                 med["launch_end"] = round(float(np.median([r["launch_end"] for r in rows])), 3)
-                print(json.dumps({"n": n, "w2_ks": ks, "head_dw2": hd, "launch": "whole" if whole else "roles", **med}), flush=True)
+                print(json.dumps({"n": n, "head_dw2": hd, "launch": "whole" if whole else "roles", **med}), flush=True)
 
 
 if __name__ == "__main__":

@@ -186,7 +186,7 @@ class MlpEngine:
         # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
         # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
         self.fh_counters = None
-        self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = self.w2g = self.W1s = None
+        self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = self.W1s = None
         if self.backend == "hip" and self.np and H <= 128 and C <= 16:
             tiles = (ld + 31) // 32
             self.fh_counters = torch.zeros(tiles, dtype=torch.int32, device=dev)
@@ -195,10 +195,6 @@ class MlpEngine:
             self.ag_counters = torch.zeros(tiles * 32, dtype=torch.int64, device=dev)  # one 256-B line each
             self.ag_slabs = torch.zeros(tiles * 8 * 16 * 32, dtype=torch.int64, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
-            # the dW2 role split over workgroups (SplitStepArgs::w2_ks <= 8): per 16-column tile a monotonic epoch
-            # counter (one 64-B line) and 7 x 256 partial-tile granules (tags only grow: never re-zeroed)
-            t2 = (H + 15) // 16
-            self.w2g = torch.zeros(t2 * 8 + t2 * 7 * 256, dtype=torch.int64, device=dev)
             if self.np == 3:  # the forward's fragment-ordered fp32 copy of W1 (MlpStep.w1_swz)
                 self.W1s = torch.zeros(int(hip().mlp_split_w1s_floats(H, self.P)), dtype=torch.float32, device=dev)
         elif self.backend == "hip" and self.np and H >= 512 and C <= 16 and self.dw2buf is not None:
@@ -397,7 +393,7 @@ class MlpEngine:
                          dZ1p=ptr(self.dZ1p))
             if self.fh_counters is not None:
                 b.update(fh_counters=ptr(self.fh_counters), fh_tiles=int(self.fh_counters.numel()),
-                         ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs), w2g=ptr(self.w2g),
+                         ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs),
                          w1s=ptr(self.W1s), xs=ptr(self.Xs))
             elif self.ag_gran is not None:  # the wide fused head
                 b.update(fh_tiles=int(self.ag_counters.numel()) // 64,  # [2 tilings][tiles][32]

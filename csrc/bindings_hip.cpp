@@ -108,12 +108,6 @@ struct MlpStep {
   int wide_eng = -1;    // SplitStepArgs::wide_eng: the 128 x 128 wide K loop's engine (0 rega, 1 g64; -1: g64 for bf16
                         // A, rega for fp32 -- 784-4096-10 step bf16 39.1 -> 38.1 us, fp32 55.4 -> 58.0 with g64,
                         // profiles/r5/kbench_wide_engines.jsonl)
-  // SplitStepArgs::w2_ks, the dW2 role's workgroups per tile (H <= 128 launches without the fused exchange or the
-  // head's dW2 partials; needs w2g).  Measured no faster, so off by default: 784-100-10 roles-only launch at n = 800
-  // 5.02 (1) / 4.98 (2) / 5.06 (4) / 5.21 us (8), and +0.7 us at n = 400 -- the granule hand-off to slice 0 costs
-  // what the shorter K loops save (profiles/r5/kbench_w2_split.jsonl, stamps_roles_w2_split.jsonl)
-  int w2_ks = 1;
-  uintptr_t w2g = 0;
   // H <= 128, the all-gather forward + head: it also leaves the dW2 partials per 32 columns (fha_body step 4a) for
   // the weight-gradient launch's dW2 role (needs dw2p); 0: the role forms D . a1^T over the batch itself; -1 (auto):
   // from n = 512 columns, where the role's GEMM is the weight-gradient launch's critical path
@@ -212,7 +206,6 @@ struct MlpStep {
       else if (k == "ag_counters") ag_counters = u(); else if (k == "ag_slabs") ag_slabs = u();
       else if (k == "ag_gran") ag_gran = u(); else if (k == "ag_gran_count") ag_gran_count = v.cast<int64_t>();
       else if (k == "kpart") kpart = u(); else if (k == "kpart_cap") kpart_cap = v.cast<int64_t>();
-      else if (k == "w2g") w2g = u();
       else if (k == "w1s") w1s = u();
       else if (k == "xs") xs = u();
       else throw std::invalid_argument("MlpStep.bind: unknown name '" + k + "'");
@@ -259,8 +252,6 @@ struct MlpStep {
     a.wide_eng = wide_eng >= 0 ? wide_eng : (npw == 1 ? 1 : 0);
     a.xp_dbg = xp_dbg;
     a.g64_touch = g64_touch;
-    a.w2g = P_<unsigned long long>(w2g);
-    a.w2_ks = (w2g && ag_err) ? w2_ks : 1;  // (a slice timeout reports through ag_err)
     return a;
   }
 
@@ -591,7 +582,6 @@ PYBIND11_MODULE(_hip, m) {
       .def_readonly("split", &MlpStep::split)
       .def_readwrite("shift", &MlpStep::shift)
       .def_readwrite("ag_err", &MlpStep::ag_err)
-      .def_readwrite("w2_ks", &MlpStep::w2_ks)
       .def_readwrite("head_dw2", &MlpStep::head_dw2)
       .def_readwrite("fh_allgather", &MlpStep::fh_allgather)
       .def_readwrite("ag_wait_us", &MlpStep::ag_wait_us)

@@ -131,13 +131,6 @@ struct SplitStepArgs {
   // them in column-tile order instead of forming D . a1^T from all of a1
   float* dw2part = nullptr;
   int dw2_cols = 32;  // columns per dW2 partial: 32 (head_wide_kernel), 128 (the fused all-gather head)
-  // small layers, no fused exchange, no dw2part: the dW2 role's K (= the batch) split over w2_ks in {2, 4, 8}
-  // workgroups per 16-column tile (1: one workgroup, the whole batch).  Slice s > 0 hands its partial tile to
-  // slice 0 as data-tagged granules; slice 0 sums the slices in slice order and applies reg + SGD.  w2g: per tile
-  // a monotonic epoch counter (8 x uint64, one line), then [tiles][w2_ks - 1][256] granules (never re-zeroed).
-  // Set by the launcher from the request (MlpStep.w2_ks); timeouts set *ag_err like the all-gather hand-offs.
-  int w2_ks = 1;
-  unsigned long long* w2g = nullptr;
   int w1_planes = 1;  // (set by mlp_split_wgrad) the small-layer W1 update refreshes the W1 planes
   // wide split3 layers: the A-in-registers dW1 launch's in-place update (sgd = 1) leaves the W1 planes alone (the
   // 128 x 128 forward reads fp32 W1); the caller marks them stale and refreshes them before a forward that reads them

@@ -367,7 +367,7 @@ struct EpiW1 {
   }
 };
 
-template <int FU>
+template <int FU, int PV = 32>
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
                                             uint32_t* s_xf, float* xs);
 
@@ -505,89 +505,18 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   }
 }
 
-// The dW2 role with its K (= the batch) split over a.w2_ks workgroups per 16-column tile (SplitStepArgs::w2_ks).
-// One workgroup per tile pulls its D rows and a1 rows over the whole batch (83 KB at n = 800) through ONE CU, and
-// at n = 800 that took longer than the dW1 tiles of the same launch (bench/kbench.py: wgrad_roles 5.02 us against
-// wgrad_w1 4.62): the roles were the launch's critical path.  Here slice s of tile tb forms the partial product
-// over batch columns [s * ks_cols, (s + 1) * ks_cols); slices s > 0 store it as data-tagged granules (granule.h: the
-// data is its own flag, no drain / counter / fence); slice 0 polls them after its own GEMM and sums the slices in
-// slice order (deterministic), then applies reg + SGD (or writes the gradient) as the unsplit role does.
-// The launch epoch: every slice adds kLcm / ks to the tile's counter at entry, so each launch adds exactly kLcm for
-// any ks in {2, 4, 8} and old / kLcm + 1 is the epoch on every slice (tags only grow across ks changes too).
-// Every slice workgroup is independent of the others but slice 0, which polls: no dispatch-order deadlock (the
-// pollers are at most cdiv(H, 16) <= 8 workgroups; the bounded poll sets *ag_err on a timeout).
-__device__ __forceinline__ void wgrad_w2_slices(const SplitStepArgs& a, int rid, float* red, uint32_t* s_xf,
-                                                float* xs) {
-  constexpr unsigned kLcm = 840;  // divisible by every w2_ks
-  const int ks = a.w2_ks, tb = rid / ks, s = rid % ks, tiles = (a.H + 15) / 16;
-  gran_t* cnt = a.w2g + (size_t)tb * 8;
-  gran_t* slab = a.w2g + (size_t)tiles * 8 + (size_t)tb * (ks - 1) * 256;
-  gran_t old = 0;
-  if (threadIdx.x == 0) old = gran_epoch_add(cnt, kLcm / ks);  // (waited for after the GEMM)
-  const int cols = ((a.n + ks - 1) / ks + 7) & ~7, k0 = min(a.n, s * cols), kn = min(cols, a.n - k0);
-  const int e = threadIdx.x, c = e >> 4, h = tb * 16 + (e & 15);
-  const bool ok = e < 256 && c < a.C && h < a.H;
-  // the reducer's epilogue operands, before the K loop
-  float w = 0.f;
-  int perr = 0;
-  if (s == 0) {
-    w = buf_load1<float>(make_rsrc(a.W2), ok ? (c * a.H + h) * 4 : kOOB);
-    perr = ag_err_load(a.ag_err);
-  }
-  struct EpiLds : EpiNoPrefetch {  // the partial tile into LDS xs[class * 16 + column - n0]
-    float* xs;
-    int n0;
-    __device__ __forceinline__ void operator()(int, int row, int col, float v) { xs[row * 16 + col - n0] = v; }
-  } epi;
-  epi.xs = xs;
-  epi.n0 = tb * 16;
-  const TileGeom g{a.C, a.H, kn, 0, tb * 16};
-  if (a.n % 4 == 0)
-    wsk_tile<float, 1, 1, kWKS, true, true, 1, 8>(a.D + k0, a.ld, a.a1 + k0, a.ld, g, epi, red, 0, a.stamps);
-  else
-    wsk_tile<float, 1, 1, kWKS, true, true, 0, 8>(a.D + k0, a.ld, a.a1 + k0, a.ld, g, epi, red, 0, a.stamps);
-  if (threadIdx.x == 0) {
-    gran_epoch_wait(old);
-    s_xf[0] = (unsigned)(old / kLcm) + 1u;
-  }
-  __syncthreads();  // xs complete; the epoch in LDS
-  const unsigned ep = s_xf[0];
-  if (s > 0) {
-    if (ok) gran_store(slab + (size_t)(s - 1) * 256 + e, xs[e], ep);
-    return;
-  }
-  if (e >= 256) return;  // (waves 4-7, uniform)
-  float v = ok ? xs[e] : 0.f;
-  auto add = [&](int, float p) { v += p; };
-  const uint32_t lim = (uint32_t)a.ag_wait_us;
-  const bool got = ks == 2   ? gran_poll<1>(slab, e, 256, 1, ok, ep, lim, add)
-                   : ks == 4 ? gran_poll<3>(slab, e, 256, 3, ok, ep, lim, add)
-                             : gran_poll<7>(slab, e, 256, 7, ok, ep, lim, add);
-  if (!got) {
-    if (e == 0 && a.ag_err) __hip_atomic_store(const_cast<int*>(a.ag_err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if (!ok) return;
-  const int i = c * a.H + h;
-  const float gr = v + (float)a.reg * w;
-  if (a.sgd && !poisoned(perr)) a.W2[i] = w - (float)a.lr * gr;
-  else a.gW2[i] = gr;
-}
-
 // The weight-gradient launch's workgroups past its t1 dW1 tiles: t2 dW2 tiles (+ the fused xGMI exchange)
 // followed by the bias-row workgroups.  `red`: kWKS * 4 * 64 floats of LDS, `s_xf`: 2 words of LDS.
 // Shared by wgrad_split_kernel and the wide engines' launches (their extra workgroups).
-template <int FU>
+// PV: dW2 partial loads in flight per lane (the small launch sums cdiv(n, 16) partials: 32; the wide launches' roles,
+// which share their CUs with the GEMM tiles, sum cdiv(n, 32 or 128): 8)
+template <int FU, int PV>
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
                                             uint32_t* s_xf, float* xs) {
   const float reg = (float)a.reg, lr = (float)a.lr;
   constexpr bool fused = FU > 0;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (bid < t1 + t2 && a.w2_ks > 1) {  // ---- dW2 with K split over workgroups (the launcher: no fused exchange)
-    wgrad_w2_slices(a, bid - t1, red, s_xf, xs);
-    return;
-  }
   if (bid < t1 + t2) {  // ---- dW2 = D a1^T on MFMA (exact f32 16x16x4): one 16x16 tile per workgroup,
     //                        the 8 waves split K = batch; fused reg + SGD (or gradient) epilogue
     const int tb = bid - t1;
@@ -611,13 +540,13 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
       epi.prefetch(0, c, h, ok);
       const __amdgpu_buffer_rsrc_t rp = make_rsrc(a.dw2part);
       float v = 0.f;
-      for (int k0 = 0; k0 < nct; k0 += 32) {  // (32 loads in flight per lane: n <= 1024 is one round trip)
-        float pv[32];
+      for (int k0 = 0; k0 < nct; k0 += PV) {  // (PV = 32 loads in flight per lane: n <= 1024 is one round trip)
+        float pv[PV];
 #pragma unroll
-        for (int u = 0; u < 32; ++u)
+        for (int u = 0; u < PV; ++u)
           pv[u] = buf_load1<float>(rp, (ok && k0 + u < nct) ? (((k0 + u) * 16 + c) * a.H + h) * 4 : kOOB);
 #pragma unroll
-        for (int u = 0; u < 32; ++u) v += pv[u];
+        for (int u = 0; u < PV; ++u) v += pv[u];
       }
       if (ok) epi(0, c, h, v);
     } else if (a.n % 4 == 0) {
@@ -1238,7 +1167,7 @@ template <int BM, int BN, int NPZ>
 __global__ __launch_bounds__(512) void wgrad_glds_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {  // the dW2 / db2 roles riding in this launch
-    wgrad_roles<0>(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
+    wgrad_roles<0, 8>(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
                 reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)),
                 reinterpret_cast<float*>(lds_dyn + kWKS * 4 * 64 * sizeof(float) + 16));  // (never fused: unused;
                                                                                             //  2 x kXpTile floats)
@@ -1421,7 +1350,7 @@ template <typename AT, int WC, int NKS, int ENG = 0>
 __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {
-    wgrad_roles<0>(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
+    wgrad_roles<0, 8>(a, (int)blockIdx.x - tbig, 0, t2, reinterpret_cast<float*>(lds_dyn),
                 reinterpret_cast<uint32_t*>(lds_dyn + kWKS * 4 * 64 * sizeof(float)),
                 reinterpret_cast<float*>(lds_dyn + kWKS * 4 * 64 * sizeof(float) + 16));  // (never fused: unused;
                                                                                             //  2 x kXpTile floats)
@@ -1796,18 +1725,11 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   const bool fused = a.xf_world > 0;
   const bool big = big_wgrad_ok(a) && !fused;
   const bool do_w1 = (a.wg_parts & 1) && a.w1_rows != 0, do_roles = (a.wg_parts & 2) != 0;
-  // the dW2 role's workgroup split (SplitStepArgs::w2_ks): the small-layer launch below only, without the fused
-  // exchange or the head's dW2 partials; a batch of fewer than 64 columns per slice keeps one workgroup
-  const int w2ks = (!big || !do_w1) && !fused && !a.dw2part && a.w2g &&
-                           (a.w2_ks == 2 || a.w2_ks == 4 || a.w2_ks == 8) && a.n >= 64 * a.w2_ks && a.C <= 16
-                       ? a.w2_ks
-                       : 1;
   if (big && do_w1) {  // dW1 as a blocked GEMM; the dW2 / db2 roles ride in the same launch as extra
     // workgroups: one launch and its boundary fewer, and they run on the CUs the dW1 tiles leave idle
     const int t2f = do_roles ? cdiv(a.H, 16) : 0;
     const int tbf = do_roles ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
-    SplitStepArgs c = a;
-    c.w2_ks = 1;  // (their roles: one workgroup per dW2 tile)
+    const SplitStepArgs& c = a;
     if (rega_wgrad_ok(c)) {
       if (c.npz == 3) launch_wgrad_rega<float>(c, t2f, tbf, s);
       else launch_wgrad_rega<bf16>(c, t2f, tbf, s);
@@ -1824,7 +1746,7 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   }
   const int w1rows = a.w1_rows < 0 ? a.H : a.w1_rows;
   const int t1n = cdiv(a.P + a.bias_col, 16 * kWNB), t1 = do_w1 ? cdiv(w1rows, 16 * kWMB) * t1n : 0;
-  const int t2 = do_roles ? cdiv(a.H, 16) * w2ks : 0;
+  const int t2 = do_roles ? cdiv(a.H, 16) : 0;
   if (fused)
     CME_REQUIRE(do_w1 && do_roles && a.bias_col && a.w1_row0 == 0 && a.w1_rows < 0 && a.C <= 16 &&
                     a.xf_world <= 8 && t1 + t2 + 1 <= mlp_split_fused_tiles(a.P, a.H, 1 << 30),
@@ -1843,7 +1765,6 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   const bool pairs = al16(a.XT) && a.ldxt % 16 == 0 && a.n % 16 == 0;
   const int vec = !base_ok ? 0 : (a.n % 8 == 0 ? (pairs ? 3 : 1) : (a.n % 4 == 0 ? 2 : 0));
   SplitStepArgs b = a;
-  b.w2_ks = w2ks;
   b.w1_planes = mlp_split_w1_planes_read(a) ? 1 : 0;
   // the XCD-row placement only for the whole layer's dW1 (a bucketed row range keeps the plain order)
   // (the forward's packed form, xcd_rows == 2, is the forward's alone: 2 x 25 dW1 tiles would not fit 4 XCDs)

@@ -780,44 +780,6 @@ def test_g64_wide_engine_is_bitwise_the_rega_engine(dt, path, H, n):
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]), fused
 
 
-@pytest.mark.parametrize("n", [800, 512, 256, 130])
-def test_dw2_workgroup_split_matches_one_workgroup(n):
-    """The dW2 role's batch split over 2 / 4 / 8 workgroups per 16-column tile (SplitStepArgs::w2_ks: slices
-    s > 0 hand their partial tile to slice 0 as tagged granules, slice 0 sums them in slice order): the gradient
-    within fp32 reassociation of the one-workgroup role and of PyTorch, each split bitwise repeatable, and the
-    fused SGD step the same.  Splits needing more than n / 64 slices fall back to one workgroup."""
-    hipe, te = _engine_pair("f32", n=n, path="split3")
-    step = hipe._hip_step()
-    step.head_dw2 = 0  # (the head's dW2 partials replace the role's GEMM altogether)
-    te.run(64, n, 1.0 / n, 1e-4, 0.0, sgd=False)
-    grads = {}
-    for ks in (1, 2, 4, 8, 4):
-        step.w2_ks = ks
-        hipe.run(64, n, 1.0 / n, 1e-4, 0.0, sgd=False)
-        torch.cuda.synchronize()
-        g = hipe.gW2.clone()
-        if ks in grads:
-            assert torch.equal(g, grads[ks]), ks
-        grads[ks] = g
-        assert _rel(g, te.gW2) < 2e-5, ks
-        assert _rel(g, grads[1]) < 2e-6, ks
-        assert _rel(hipe.gb2, te.gb2) < 2e-5
-    assert not hipe.kernel_error()
-    p0 = hipe.params.clone()
-    for ks in (1, 4):
-        hipe.params.copy_(p0)
-        hipe.refresh_shadow()
-        step.w2_ks = ks
-        for it in range(3):
-            hipe.run(n * (it % 2), n, 1.0 / n, 1e-4, 0.01, sgd=True)
-        torch.cuda.synchronize()
-        if ks == 1:
-            one = hipe.params.clone()
-        else:
-            assert _rel(hipe.params, one) < 1e-6
-    assert not hipe.kernel_error()
-
-
 @pytest.mark.parametrize("n", [800, 513, 100, 45])
 @pytest.mark.parametrize("store_a1", [True, False])
 def test_head_dw2_partials_match_the_role_gemm(n, store_a1):
