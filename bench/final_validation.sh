@@ -24,5 +24,9 @@ step pytest_gpu 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --time
 step wide4096_f32 180 python3 bench.py --gpus 1 --hidden 4096 --dtype f32 --steps 200 --warmup 20 &&
 step wide4096_bf16 180 python3 bench.py --gpus 1 --hidden 4096 --dtype bf16 --steps 200 --warmup 20 &&
 step wide1024_bf16 180 python3 bench.py --gpus 1 --hidden 1024 --dtype bf16 --steps 400 --warmup 40 &&
+# (the wide configs run 1.8-2.4 us/step slower for their first few hundred steps: the same runs after 600 warm-up steps)
+step wide4096_f32_warm 180 python3 bench.py --gpus 1 --hidden 4096 --dtype f32 --steps 400 --warmup 600 &&
+step wide4096_bf16_warm 180 python3 bench.py --gpus 1 --hidden 4096 --dtype bf16 --steps 400 --warmup 600 &&
+step wide1024_bf16_warm 180 python3 bench.py --gpus 1 --hidden 1024 --dtype bf16 --steps 400 --warmup 600 &&
 step headline_bf16 120 python3 bench.py --gpus 1 --dtype bf16 --steps 2000 --warmup 200 &&
 step rocprof 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o headline -- python3 bench.py --gpus 1 --steps 400 --warmup 40
