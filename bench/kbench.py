@@ -82,9 +82,13 @@ def main(argv=None):
         xpack = int(m.group(1)) if m else None
         m = re.search(r"\+z(\d)", path)  # "+zK": the fragment-ordered W1 copy for the forward (MlpStep.w1_swz)
         wswz = int(m.group(1)) if m else None
+        m = re.search(r"\+a(\d)", path)  # "+aK": SplitStepArgs::a_fp32 (bit0 fp32 W1, bit1 fp32 dZ1; MlpStep.a_fp32)
+        afp = int(m.group(1)) if m else None
+        m = re.search(r"\+v(\d)", path)  # "+vK": fp32 dZ1 in the dW1 GEMM's fragment order (MlpStep.dz_swz; needs +a3)
+        dzs = int(m.group(1)) if m else None
         m = re.search(r"\+y(\d)", path)  # "+yK": the fragment-ordered pixel copy for the forward (MlpStep.x_swz)
         xswz = int(m.group(1)) if m else None
-        path = re.sub(r"\+[sdxptglwhqzy]\d", "", path)
+        path = re.sub(r"\+[sdxptglwhqzyav]\d", "", path)
         for H in a.hidden:
             nn = NeuralNetwork([784, H, 10])
             for n in a.cols:
@@ -109,6 +113,10 @@ def main(argv=None):
                     step.w1_swz = wswz
                 if xswz is not None:
                     step.x_swz = xswz
+                if afp is not None:
+                    step.a_fp32 = afp
+                if dzs is not None:
+                    step.dz_swz = dzs
                 if pref_xt is not None:
                     step.prefetch_xt = pref_xt
                 if no_a1:
@@ -120,7 +128,7 @@ def main(argv=None):
                 def part(p, sgd=1):
                     return lambda: step.run(0, n, 1.0 / n, 1e-4, 0.0, sgd, 0, st(), p)
 
-                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else "") + (f"+g{weng}" if weng is not None else "") + (f"+l{gtouch}" if gtouch is not None else "") + (f"+h{hdw2}" if hdw2 is not None else "") + (f"+q{xpack}" if xpack is not None else "") + (f"+z{wswz}" if wswz is not None else "") + (f"+y{xswz}" if xswz is not None else ""), "H": H, "n": n}
+                row = {"dtype": dt, "path": e.path + ("+s0" if no_a1 else "") + ("+d0" if no_dw2 else "") + (f"+x{xrows}" if xrows is not None else "") + (f"+p{pref}" if pref is not None else "") + (f"+t{pref_xt}" if pref_xt is not None else "") + (f"+g{weng}" if weng is not None else "") + (f"+l{gtouch}" if gtouch is not None else "") + (f"+h{hdw2}" if hdw2 is not None else "") + (f"+q{xpack}" if xpack is not None else "") + (f"+z{wswz}" if wswz is not None else "") + (f"+y{xswz}" if xswz is not None else "") + (f"+a{afp}" if afp is not None else "") + (f"+v{dzs}" if dzs is not None else ""), "H": H, "n": n}
                 if e.np:  # split paths: the weight-gradient launch's two halves on their own
                     for name, prt in (("wgrad_w1", 1), ("wgrad_roles", 2)):
                         row[name + "_us"] = round(timeit(

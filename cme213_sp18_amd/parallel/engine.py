@@ -186,7 +186,7 @@ class MlpEngine:
         # split path, H <= 128: forward GEMM + head in one launch (mlp_fwd1_head); one uint32
         # counter per 32-column a1 tile tells the last row-tile workgroup to run the head
         self.fh_counters = None
-        self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = self.W1s = None
+        self.ag_counters = self.ag_slabs = self.ag_err = self.ag_gran = self.W1s = self.dZ1s = None
         if self.backend == "hip" and self.np and H <= 128 and C <= 16:
             tiles = (ld + 31) // 32
             self.fh_counters = torch.zeros(tiles, dtype=torch.int32, device=dev)
@@ -197,6 +197,8 @@ class MlpEngine:
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
             if self.np == 3:  # the forward's fragment-ordered fp32 copy of W1 (MlpStep.w1_swz)
                 self.W1s = torch.zeros(int(hip().mlp_split_w1s_floats(H, self.P)), dtype=torch.float32, device=dev)
+                # ... and dZ1 in the weight-gradient GEMM's fragment order (MlpStep.dz_swz)
+                self.dZ1s = torch.zeros(int(hip().mlp_split_w1s_floats(H, ld)), dtype=torch.float32, device=dev)
         elif self.backend == "hip" and self.np and H >= 512 and C <= 16 and self.dw2buf is not None:
             # wide layers: the all-gather head fused into the forward launch (mlp_fwd1_wide_ag) uses one
             # monotonic counter per column tile -- a separate array per tiling (128 x 128 / 64 x 64) -- and
@@ -268,6 +270,18 @@ class MlpEngine:
             for dst, src in ((self.W1, W1), (self.b1, b1), (self.W2, W2), (self.b2, b2)):
                 dst.copy_(torch.as_tensor(np.asarray(src)).to(dst.dtype))
             self.refresh_shadow()
+
+    def dz1(self) -> torch.Tensor:
+        """The last step's dZ1 as [H][ld] row-major.  A whole hip step with fp32 dZ1 leaves it only in the
+        weight-gradient GEMM's fragment order (MlpStep.dz_swz, csrc/mlp/mma_tile.h w1s_off over [H][ld]); this view
+        undoes that order (diagnostics and tests; the training step never reads dZ1 back)."""
+        st = self._step
+        if self.backend != "hip" or st is None or not st.dz_left_swz:
+            return self.dZ1
+        H, ld = self.H, self.ld
+        rt, npair = (H + 15) // 16, (ld + 63) // 64
+        v = self.dZ1s[: rt * 16 * npair * 64].view(rt, npair, 4, 4, 16, 4)  # [row tile][pair][i][lane group][c][e]
+        return v.permute(0, 4, 1, 3, 2, 5).reshape(rt * 16, npair * 64)[:H, :ld]
 
     def _w1_written(self) -> None:
         """W1 changed outside the step's own in-place update: the forward's fragment-ordered copy (MlpStep.w1_swz)
@@ -394,7 +408,7 @@ class MlpEngine:
             if self.fh_counters is not None:
                 b.update(fh_counters=ptr(self.fh_counters), fh_tiles=int(self.fh_counters.numel()),
                          ag_counters=ptr(self.ag_counters), ag_slabs=ptr(self.ag_slabs),
-                         w1s=ptr(self.W1s), xs=ptr(self.Xs))
+                         w1s=ptr(self.W1s), xs=ptr(self.Xs), dz1s=ptr(self.dZ1s))
             elif self.ag_gran is not None:  # the wide fused head
                 b.update(fh_tiles=int(self.ag_counters.numel()) // 64,  # [2 tilings][tiles][32]
                          ag_gran=ptr(self.ag_gran), ag_gran_count=int(self.ag_gran.numel()),

@@ -90,6 +90,13 @@ struct MlpStep {
   // before the next forward that reads it
   int w1_swz = 1;
   uintptr_t w1s = 0;
+  int a_fp32 = -1;  // SplitStepArgs::a_fp32 (-1: the measured policy in split_args; A/B knob)
+  // SplitStepArgs::dz_swz: with fp32 dZ1 (a_fp32 bit1) and the W1 copy's forward, the all-gather head writes dZ1 in
+  // the weight-gradient GEMM's fragment order into dz1s and that GEMM reads it from there (whole steps only: a
+  // bucketed run_wgrad reads the row-major dZ1)
+  int dz_swz = 1;
+  uintptr_t dz1s = 0;
+  int dz_left_swz = 0;  // the last forward + head left dZ1 in dz1s (fragment order), not in dZ1 (MlpEngine.dz1())
   // SplitStepArgs::x_swz / Xs: with w1_swz, the forward also reads the pixels from their fragment-ordered copy xs
   // (MlpEngine.load_dataset builds it once; a step whose first sample is not a multiple of 16 reads the row-major X)
   int x_swz = 1;
@@ -208,6 +215,7 @@ struct MlpStep {
       else if (k == "kpart") kpart = u(); else if (k == "kpart_cap") kpart_cap = v.cast<int64_t>();
       else if (k == "w1s") w1s = u();
       else if (k == "xs") xs = u();
+      else if (k == "dz1s") dz1s = u();
       else throw std::invalid_argument("MlpStep.bind: unknown name '" + k + "'");
     }
   }
@@ -234,10 +242,14 @@ struct MlpStep {
     a.wstamps = reinterpret_cast<unsigned long long*>(wstamps);
     a.bias_col = bias_col;
     // split3 small layers, measured (bench/kbench.py): fp32 W1 split in registers always (one split per weight
-    // per column tile is cheaper than pulling 6 B); fp32 dZ1 only above H = 128, where the separate head's plane
-    // stores cost ~2 us at H = 300 -- at H <= 128 the all-gather head stores planes cheaply and the 25-fold
-    // re-split of dZ1 in the dW1 tiles costs +0.5 us.  (The wide engines always split fp32 operands.)
-    a.a_fp32 = H <= 128 ? 1 : 3;
+    // per column tile is cheaper than pulling 6 B); fp32 dZ1 above H = 128, where the separate head's plane
+    // stores cost ~2 us at H = 300, and -- since round 5 (the head's dW2 partials, the fragment-ordered forward
+    // operands and dZ1, dz_swz) -- at H <= 128 from n = 200 columns: the head's three plane stores cost more than the
+    // dW1 tiles' re-split (walking step at n = 800 14.24 -> 14.02-14.07 us, n = 512 14.09-14.15 -> 13.33-13.36,
+    // n = 400 12.94-12.96 -> 12.67-12.76; n = 100 +0.04-0.16 us, so planes there: profiles/r5/kbench_dz_fp32_r5.jsonl).
+    // The decision depends only on the step's shape, so the head and every weight-gradient call of a step agree.
+    // (The wide engines always split fp32 operands.)
+    a.a_fp32 = a_fp32 >= 0 ? a_fp32 : (H <= 128 ? (n >= 200 ? 3 : 1) : 3);
     a.kpart = P_<float>(kpart);
     a.kpart_cap = kpart_cap;
     // a timed-out all-gather forward + head launch (sticky word) makes every later update a no-op
@@ -324,6 +336,16 @@ struct MlpStep {
             cme::HeadArgs hg = h;
             cme::SplitStepArgs fa = a;
             if (!store_a1 && bias_col && !dz32 && hg.dZ1_planes) hg.dZ1 = nullptr;
+            if (dz_swz && dz1s && dz32 && swz && (parts & 3) == 3 && !hg.dZ1_planes) {
+              cme::SplitStepArgs t = a;
+              t.dZ1 = P_<float>(dz1s);
+              if (cme::mlp_wgrad_dz_swz_ok(t)) {  // the head writes the fragment-ordered dZ1, the dW1 GEMM reads it
+                a.dZ1 = t.dZ1;
+                a.dz_swz = 1;
+                hg.dZ1 = a.dZ1;
+                hg.dz_swz = 1;
+              }
+            }
             if ((head_dw2 > 0 || (head_dw2 < 0 && n >= 512)) && dw2p && C <= 16) {  // the head leaves the dW2 partials (fha_body step 5); then
               // nothing after this launch reads a1: not stored in training (store_a1 off)
               hg.dw2part = P_<float>(dw2p);
@@ -367,6 +389,7 @@ struct MlpStep {
         }
         // what run_wgrad (the rest of this step's backward) reads: did this forward leave dW2 partials
         dw2_left = a.dw2part != nullptr;
+        dz_left_swz = a.dz_swz;
         dw2_cols_last = a.dw2_cols;
       } else if (dw2p && dw2_left) {  // the backward half alone (profiling): the partials of the last forward
         a.dw2part = P_<float>(dw2p);
@@ -592,6 +615,9 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("xcd_pack", &MlpStep::xcd_pack)
       .def_readwrite("w1_swz", &MlpStep::w1_swz)
       .def_readwrite("x_swz", &MlpStep::x_swz)
+      .def_readwrite("a_fp32", &MlpStep::a_fp32)
+      .def_readwrite("dz_swz", &MlpStep::dz_swz)
+      .def_readonly("dz_left_swz", &MlpStep::dz_left_swz)
       .def_readwrite("swz_stale", &MlpStep::swz_stale)
       .def_readwrite("prefetch", &MlpStep::prefetch)
       .def_readwrite("prefetch_xt", &MlpStep::prefetch_xt)

@@ -238,9 +238,11 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
       dz = da * x * (1.f - x);
     }
     const size_t zi = (size_t)row * h.ldz + gcol;
+    int zoff = (int)(zi * 4);
+    if constexpr ((SWZ & 4) != 0) zoff = (int)(w1s_off(row, gcol, (h.ldz + 63) >> 6) * 4);  // (HeadArgs::dz_swz)
     if (h.dZ1)
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dz), make_rsrc(h.dZ1),
-                                            ok ? (int)(zi * 4) : kOOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dz), make_rsrc(h.dZ1), ok ? zoff : kOOB, 0,
+                                            0);
     // the planes two columns per 4-byte word: lanes col and col ^ 1 (same row) both split both values;
     // the even lane stores the even planes' words, the odd lane the odd ones (the pair's second column
     // lies inside the ld padding when it is past n; the dW1 GEMM never reads past n)

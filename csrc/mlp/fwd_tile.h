@@ -19,9 +19,9 @@ __device__ __forceinline__ void fwd_tile(const SplitStepArgs& f, const TileGeom&
   if constexpr (AF) {
     static_assert(NPW == 3, "fp32 W1 is split into three planes");
     if constexpr (SWZ != 0) {  // the fragment-ordered fp32 copy of W1 (SplitStepArgs::w1_swz)
-      static_assert(VEC == 3 && (SWZ == 1 || SWZ == 3), "fragment-ordered W1 (+ pixels): 16-byte pixel pairs");
+      static_assert(VEC == 3 && (SWZ & 1), "fragment-ordered W1 (+ pixels): 16-byte pixel pairs");
       const int npair = (f.P + 63) / 64;
-      if constexpr (SWZ == 3)
+      if constexpr ((SWZ & 2) != 0)
         wsk_tile<__hip_bfloat16, 1, NB, 8, true, true, VEC, U, 3, uint8_t, float, true, true>(
             f.W1s, npair, static_cast<const uint8_t*>(f.Xs), npair, g, epi, red, 0, stamps);
       else

@@ -38,6 +38,9 @@ struct HeadArgs {
   void* dZ1_bf16;                 // optional bf16 shadow of dZ1 for the bf16 weight-gradient GEMM
   void* dZ1_planes = nullptr;     // optional exact bf16 planes of dZ1 ([npz][H][ldz]) for the split path
   int npz = 0;
+  // the H <= 128 all-gather head (fha_body SWZ & 4): dZ1 is stored in the weight-gradient GEMM's fragment order
+  // (mma_tile.h w1s_off over [H][cdiv(ldz, 64) pairs]) instead of row-major -- SplitStepArgs::dz_swz
+  int dz_swz = 0;
   float* loss_partial;            // optional: one sum of -log(yhat[label]) per workgroup
   int* pred;                      // predict mode: argmax labels [n]
   void* probs; int ldp;           // probs mode: [C][ldp]

@@ -1120,12 +1120,18 @@ void mlp_fwd1_head_ag(const SplitStepArgs& f, const HeadArgs& h, unsigned long l
   const int vec = fha_vec(f);
   const bool swz = f.w1_swz && f.W1s && mlp_fwd_swz_ok(f);
   CME_REQUIRE(!f.x_swz || (swz && f.Xs), "fwd1_head_ag: the fragment-ordered pixels need the W1 copy's form too");
+  CME_REQUIRE(!h.dz_swz || (swz && h.dZ1 && !h.dZ1_planes && mlp_wgrad_dz_swz_ok(f)),
+              "fwd1_head_ag: the fragment-ordered dZ1 needs the W1 copy's form, fp32 dZ1 and pair-aligned K ranges");
   // (prefetch workgroups last; xcd_rows == 2: cdiv(tm, 4) slots of tn per XCD, XCDs 4-7 padding)
   const int nwg = f.xcd_rows == 2 ? 8 * cdiv(tm, 4) * tn + 8 * f.pf_wgs_xt
                   : f.xcd_rows    ? 8 * tn + 8 * f.pf_wgs_xt
                                   : 8 * tm * cdiv(tn, 8);
 #define CME_FHA(np, af)                                                                                  \
-  if (swz && f.x_swz)                                                                                   \
+  if (swz && f.x_swz && h.dz_swz)                                                                       \
+    fwd1_head_ag_kernel<3, 3, true, 7><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);           \
+  else if (swz && h.dz_swz)                                                                             \
+    fwd1_head_ag_kernel<3, 3, true, 5><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);           \
+  else if (swz && f.x_swz)                                                                              \
     fwd1_head_ag_kernel<3, 3, true, 3><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);           \
   else if (swz)                                                                                         \
     fwd1_head_ag_kernel<3, 3, true, 1><<<nwg, 512, 0, s>>>(f, h, counters, slabs, err, tm, tn);           \

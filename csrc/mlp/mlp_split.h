@@ -105,6 +105,9 @@ struct SplitStepArgs {
   // [cdiv(N, 16)][cdiv(P, 64)][64 lanes][16 B] copy (mma_tile.h BSWZ / xs_off; the step's first sample a multiple of 16)
   int x_swz = 0;
   const void* Xs = nullptr;
+  // ... and (fp32 dZ1, a_fp32 bit1) the weight-gradient GEMM reads dZ1 from the fragment-ordered buffer the head
+  // wrote (a.dZ1 then points at it: [cdiv(H, 16)][cdiv(ld, 64)][4][64 lanes][4 floats], mma_tile.h w1s_off)
+  int dz_swz = 0;
   // wide layers (LDS GEMM forward): when set, the forward GEMM's tile epilogue also leaves the head's
   // z2 partial sums, z2part[row tile][16][ld] = W2[:, tile rows] . a1[tile rows, :] (v_mfma_f32_16x16x4
   // on the activated accumulators), so the head never re-reads a1 for z2 (mlp_split_fwd1_z2_chunks)
@@ -116,7 +119,7 @@ struct SplitStepArgs {
   // small layers (wave-split-K kernels), split3 only: bit0 = the forward GEMM reads fp32 W1, bit1 = the dW1
   // GEMM reads fp32 dZ1 (4 B per element, split into the exact bf16 planes in registers; the head then
   // writes no dZ1 planes); clear bits: the stored planes (6 B per element, split once by their writer).
-  // Policy (MlpStep::split_args, measured: bench/kbench.py): 1 at H <= 128, 3 above
+  // Policy (MlpStep::split_args, measured: bench/kbench.py): at H <= 128 1 below n = 200 columns, 3 from there; 3 above
   int a_fp32 = 1;
   // wide layers (the 128 x 128 A-in-registers tiling): the K loop's engine -- 0 rega_gemm.h (A fragments straight
   // into registers, 32-deep stages), 1 g64_gemm.h (both operands LDS-DMA'd in full rows, 64-deep steps); the same
@@ -170,6 +173,8 @@ bool mlp_split_w1_planes_read(const SplitStepArgs& a);
 
 // the small-layer forward GEMM reads fp32 W1 (split in registers) instead of the W1 planes
 bool mlp_split_fwd_fp32_w(const SplitStepArgs& a);
+// the weight-gradient GEMM can read fp32 dZ1 in fragment order (SplitStepArgs::dz_swz)
+bool mlp_wgrad_dz_swz_ok(const SplitStepArgs& a);
 
 // number of z2 row-tile partials mlp_split_fwd1 writes for `a` (0: the forward does not produce them)
 int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a);

@@ -376,7 +376,8 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
 // owner-tile push (SplitStepArgs::xf).  A template, not a runtime test: with the xGMI forms compiled into the one
 // kernel, the single-process step's weight-gradient launch ran 0.8 us longer (rocprofv3, 784-100-10 at n = 800:
 // 5.70 -> 6.51 us on one box, profiles/r5/regression_bisect.md) for code it never executes.
-template <int NPZ, int VEC, bool AF, int FU>
+// DSWZ (AF, VEC == 3): dZ1 is read from the fragment-ordered buffer the head wrote (SplitStepArgs::dz_swz)
+template <int NPZ, int VEC, bool AF, int FU, bool DSWZ = false>
 __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
   __shared__ uint32_t s_xf[2];
@@ -435,7 +436,10 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       if (threadIdx.x == 0) xw = xp_words_issue(*a.xf, bid, a.ag_err);
     }
     constexpr int U = 4;
-    if constexpr (AF)
+    if constexpr (AF && DSWZ)
+      wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, 3, uint8_t, float, true>(
+          a.dZ1, (a.ld + 63) / 64, static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi, red, 0, a.stamps);
+    else if constexpr (AF)
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, 3, uint8_t>(a.dZ1, a.ld, static_cast<const uint8_t*>(a.XT),
                                                                        a.ldxt, g, epi, red, 0, a.stamps);
     else
@@ -1585,6 +1589,14 @@ bool small_wgrad_fp32_ok(const SplitStepArgs& a) {
   return a.npz == 3 && (a.a_fp32 & 2) && a.dZ1 != nullptr && al16(a.dZ1) && a.ld % 4 == 0;
 }
 
+// the fragment-ordered fp32 dZ1 (SplitStepArgs::dz_swz): the wave-split-K dW1 GEMM over 16-byte pixel pairs whose
+// waves start their K (= batch) ranges on 64-column pairs: an even number of 32-column chunks per wave (n = 257-512,
+// 769-1024, ...)
+bool mlp_wgrad_dz_swz_ok(const SplitStepArgs& a) {
+  return a.H <= 128 && small_wgrad_fp32_ok(a) && a.n % 16 == 0 && al16(a.XT) && a.ldxt % 16 == 0 && a.ld % 8 == 0 &&
+         cdiv(cdiv(a.n, 32), kWKS) % 2 == 0;
+}
+
 // Decided on the whole step (not the row range of a bucketed call; the xGMI-fused launch always takes the
 // wave-split-K kernel) so that the head and every wgrad call of a step agree on what dZ1 form exists.
 bool mlp_split_wgrad_fp32_dz(const SplitStepArgs& a) {
@@ -1785,7 +1797,13 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   } else {                  \
     CME_WG3(npz, af, 0)     \
   }
-  if (af) { CME_WG(3, true) } else if (a.npz == 3) { CME_WG(3, false) } else { CME_WG(1, false) }
+  CME_REQUIRE(!a.dz_swz || (af && vec == 3 && do_w1 && mlp_wgrad_dz_swz_ok(a)),
+              "wgrad: the fragment-ordered dZ1 needs fp32 dZ1, 16-byte pixel pairs and pair-aligned K ranges");
+  if (a.dz_swz) {
+    if (fu == 2) wgrad_split_kernel<3, 3, true, 2, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
+    else if (fu == 1) wgrad_split_kernel<3, 3, true, 1, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
+    else wgrad_split_kernel<3, 3, true, 0, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
+  } else if (af) { CME_WG(3, true) } else if (a.npz == 3) { CME_WG(3, false) } else { CME_WG(1, false) }
 #undef CME_WG
 #undef CME_WG3
   CME_LAUNCH_CHECK(s);

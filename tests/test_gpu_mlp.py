@@ -113,7 +113,7 @@ def test_step_gradients_match_torch(dt, path, n, H):
         assert _rel(getattr(hipe, name), getattr(te, name)) < tol, name
     assert abs(hipe.loss_sum() - te.loss_sum()) / te.loss_sum() < 1e-4
     for name in ("a1", "dZ1", "D"):
-        a = getattr(hipe, name)[:, :n]
+        a = (hipe.dz1() if name == "dZ1" else getattr(hipe, name))[:, :n]
         b = getattr(te, name)[:, :n]
         assert _rel(a, b) < max(tol, 1e-5), name
 
@@ -292,7 +292,7 @@ def test_fwd1_head_single_launch_matches_two_launches(dtype, H, n):
         for step, off in enumerate((0, n, 7, 0)):
             e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True, with_loss=step == 3)
         torch.cuda.synchronize()
-        outs.append([t.clone().cpu() for t in (e.a1, e.D, e.dZ1, e.dZ1p, e.params)] + [e.loss_sum()])
+        outs.append([t.clone().cpu() for t in (e.a1, e.D, e.dz1(), e.dZ1p, e.params)] + [e.loss_sum()])
         if single:  # the last arriver of every tile re-arms its counter
             assert int(e.fh_counters.abs().sum()) == 0
     a, b = outs
@@ -351,7 +351,7 @@ def test_step_is_deterministic_on_fresh_engines(H, n):
         e.load_dataset(x, y)
         e.run(64, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
         torch.cuda.synchronize()
-        got = [e.a1[:, :n].clone(), e.D[:, :n].clone(), e.dZ1[:, :n].clone(), e.grads.clone()]
+        got = [e.a1[:, :n].clone(), e.D[:, :n].clone(), e.dz1()[:, :n].clone(), e.grads.clone()]
         if ref is None:
             ref = got
         for name, a, b in zip(("a1", "D", "dZ1", "grads"), got, ref):
@@ -472,7 +472,7 @@ def test_fwd1_head_allgather_matches_last_arriver(dtype, H, n):
         for step, off in enumerate(steps):
             e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True, with_loss=step == 3)
         torch.cuda.synchronize()
-        outs.append([t.clone().cpu() for t in (e.a1[:, :n], e.D[:, :n], e.dZ1[:, :n], e.params)] + [e.loss_sum()])
+        outs.append([t.clone().cpu() for t in (e.a1[:, :n], e.D[:, :n], e.dz1()[:, :n], e.params)] + [e.loss_sum()])
         if ag:
             tm, tn = (H + 15) // 16, (n + 31) // 32
             assert not e.kernel_error()
@@ -561,7 +561,7 @@ def test_fp32_operands_split_in_registers_match_torch(H, n):
             assert bool((e.W1p == 7.0).all())
             if H > 128:
                 assert bool((e.dZ1p == 7.0).all())
-        outs.append([t.clone().cpu() for t in (e.a1[:, :n], e.D[:, :n], e.dZ1[:, :n], e.params)])
+        outs.append([t.clone().cpu() for t in (e.a1[:, :n], e.D[:, :n], e.dz1()[:, :n], e.params)])
     for ta, tb in zip(*outs):
         assert _rel(ta, tb) < 2e-5
 
@@ -629,7 +629,7 @@ def test_wide_fused_allgather_head_matches_head_kernel(dt, path, H, n):
             e.a1.fill_(7.0)
         e.run(64, n, 1.0 / n, 1e-4, 0.0, sgd=False, with_loss=True)
         torch.cuda.synchronize()
-        first = [e.a1[:, :n].clone(), e.D[:, :n].clone(), e.dZ1[:, :n].clone(), e.dZ1p[:, :, :n].clone(),
+        first = [e.a1[:, :n].clone(), e.D[:, :n].clone(), e.dz1()[:, :n].clone(), e.dZ1p[:, :, :n].clone(),
                  e.gW1.clone(), e.gb1.clone(), e.gb2.clone(), e.gW2.clone(), e.loss_sum()]
         for off in (0, n, 32):
             e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True)
@@ -879,5 +879,50 @@ def test_fragment_ordered_copies_are_bitwise_the_row_major_forward(P, H, n):
     # (the native loop walks batches of n from 0 and wraps; each step prefetches the tiles the next one reads)
     all_forms(lambda e: e._hip_step().run_steps(0, 9, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1,
                                                 torch.cuda.current_stream().cuda_stream))
+    for e in engines:
+        assert not e.kernel_error()
+
+
+@pytest.mark.parametrize("n", [800, 512, 320, 100])
+def test_fragment_ordered_dz1_is_bitwise_the_row_major_dz1(n):
+    """fp32 dZ1 (a_fp32 = 3) written by the all-gather head in the weight-gradient GEMM's fragment order and read from
+    there (MlpStep.dz_swz) against the same step with row-major fp32 dZ1: parameters bitwise equal after fused SGD
+    steps, a gradient step and the native loop; n = 100 has one 32-column chunk per wave, so the fragment form must
+    not engage (mlp_wgrad_dz_swz_ok) and the result is the same either way.  The first gradient step of every form
+    (and of the default planes form) against the PyTorch backend."""
+    x, y = synthetic_mnist(4 * n + 32, seed=n)
+    nn = NeuralNetwork([784, 100, 10])
+    engines = []
+    for afp, dzs in ((3, 0), (3, 1), (-1, 0)):
+        e = MlpEngine(nn.H, "f32", max_cols=n, device="cuda", path="split3")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        e.set_store_a1(False)
+        st = e._hip_step()
+        st.a_fp32, st.dz_swz = afp, dzs
+        engines.append(e)
+    te = MlpEngine(nn.H, "f32", max_cols=n, device="cuda", backend="torch", path="split3")
+    te.set_params(*nn.params)
+    te.load_dataset(x, y)
+    te.run(0, n, 1.0 / n, 1e-4, 0.0, sgd=False)
+    for e in engines:
+        e.run(0, n, 1.0 / n, 1e-4, 0.0, sgd=False)
+    torch.cuda.synchronize()
+    for k, e in enumerate(engines):
+        for a, b in zip((e.gW1, e.gb1, e.gW2, e.gb2), (te.gW1, te.gb1, te.gW2, te.gb2)):
+            assert _rel(a, b) < 2e-5, k
+
+    def both(fn):
+        for e in engines[:2]:
+            fn(e)
+        torch.cuda.synchronize()
+        assert torch.equal(engines[0].params, engines[1].params)
+
+    both(lambda e: [e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True) for off in (0, n, 16, 2 * n)])
+    both(lambda e: (e.run(3 * n, n, 1.0 / n, 1e-4, 0.0, sgd=False), e.sgd(0.05)))
+    N = engines[0].num_samples
+    both(lambda e: e._hip_step().run_steps(0, 6, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1,
+                                           torch.cuda.current_stream().cuda_stream))
+    assert torch.equal(engines[0].grads, engines[1].grads)
     for e in engines:
         assert not e.kernel_error()
