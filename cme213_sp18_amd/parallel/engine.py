@@ -43,6 +43,14 @@ def fragment_order_pixels(x: torch.Tensor) -> torch.Tensor:
     return xp.view(ns // 16, 16, npair, 4, 16).permute(0, 2, 3, 1, 4).contiguous().view(-1)
 
 
+def fragment_rows_to_rowmajor(buf: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
+    """Inverse of the fp32 fragment order (csrc/mlp/mma_tile.h ``w1s_off``: row tile r // 16, 64-column pair c // 64,
+    load i = (c % 16) // 4, lane ((c % 64) // 16) * 16 + r % 16, element c % 4) -> a [rows][cols] view."""
+    rt, npair = (rows + 15) // 16, (cols + 63) // 64
+    v = buf[: rt * 16 * npair * 64].view(rt, npair, 4, 4, 16, 4)  # [row tile][pair][i][lane group][r % 16][e]
+    return v.permute(0, 4, 1, 3, 2, 5).reshape(rt * 16, npair * 64)[:rows, :cols]
+
+
 def param_dtype(dtype: str) -> torch.dtype:
     return torch.float64 if dtype == "f64" else torch.float32
 
@@ -278,10 +286,7 @@ class MlpEngine:
         st = self._step
         if self.backend != "hip" or st is None or not st.dz_left_swz:
             return self.dZ1
-        H, ld = self.H, self.ld
-        rt, npair = (H + 15) // 16, (ld + 63) // 64
-        v = self.dZ1s[: rt * 16 * npair * 64].view(rt, npair, 4, 4, 16, 4)  # [row tile][pair][i][lane group][c][e]
-        return v.permute(0, 4, 1, 3, 2, 5).reshape(rt * 16, npair * 64)[:H, :ld]
+        return fragment_rows_to_rowmajor(self.dZ1s, self.H, self.ld)
 
     def _w1_written(self) -> None:
         """W1 changed outside the step's own in-place update: the forward's fragment-ordered copy (MlpStep.w1_swz)

@@ -1,8 +1,8 @@
-"""The forward's fragment-ordered pixel copy (MlpEngine.load_dataset -> engine.fragment_order_pixels) holds every
+"""The fragment orders of the split kernels: the forward's pixel copy (MlpEngine.load_dataset -> engine.fragment_order_pixels) holds every
 pixel where the kernel's xs_off (csrc/mlp/mma_tile.h) looks for it, and zeros in the padding.  CPU only."""
 import torch
 
-from cme213_sp18_amd.parallel.engine import fragment_order_pixels
+from cme213_sp18_amd.parallel.engine import fragment_order_pixels, fragment_rows_to_rowmajor
 
 
 def xs_off(s, k, npair):  # mma_tile.h xs_off
@@ -24,3 +24,20 @@ def test_fragment_order_pixels_matches_the_kernel_offsets():
         pad = torch.ones_like(xs, dtype=torch.bool)
         pad[idx.reshape(-1)] = False
         assert int(xs[pad].count_nonzero()) == 0
+
+
+def w1s_off(row, col, npair):  # mma_tile.h w1s_off (fp32 W1 copy, fragment-ordered dZ1)
+    rt, c, p, w = row >> 4, row & 15, col >> 6, col & 63
+    lane, i, e = (w >> 4) * 16 + c, (w & 15) >> 2, w & 3
+    return (((rt * npair + p) * 4 + i) * 64 + lane) * 4 + e
+
+
+def test_fragment_rows_to_rowmajor_inverts_w1s_off():
+    for rows, cols in ((100, 800), (37, 96), (128, 784)):
+        npair = (cols + 63) // 64
+        src = torch.randn(rows, cols, dtype=torch.float64, generator=torch.Generator().manual_seed(rows))
+        buf = torch.zeros((rows + 15) // 16 * 16 * npair * 64, dtype=torch.float64)
+        r = torch.arange(rows).view(-1, 1).expand(rows, cols)
+        c = torch.arange(cols).view(1, -1).expand(rows, cols)
+        buf[w1s_off(r, c, npair).reshape(-1)] = src.reshape(-1)
+        assert torch.equal(fragment_rows_to_rowmajor(buf, rows, cols), src)
