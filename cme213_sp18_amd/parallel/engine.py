@@ -43,12 +43,14 @@ def fragment_order_pixels(x: torch.Tensor) -> torch.Tensor:
     return xp.view(ns // 16, 16, npair, 4, 16).permute(0, 2, 3, 1, 4).contiguous().view(-1)
 
 
-def fragment_rows_to_rowmajor(buf: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
-    """Inverse of the fp32 fragment order (csrc/mlp/mma_tile.h ``w1s_off``: row tile r // 16, 64-column pair c // 64,
-    load i = (c % 16) // 4, lane ((c % 64) // 16) * 16 + r % 16, element c % 4) -> a [rows][cols] view."""
-    rt, npair = (rows + 15) // 16, (cols + 63) // 64
-    v = buf[: rt * 16 * npair * 64].view(rt, npair, 4, 4, 16, 4)  # [row tile][pair][i][lane group][r % 16][e]
-    return v.permute(0, 4, 1, 3, 2, 5).reshape(rt * 16, npair * 64)[:rows, :cols]
+def fragment_rows_to_rowmajor(buf: torch.Tensor, rows: int, cols: int, kblock: int = 64) -> torch.Tensor:
+    """Inverse of the fp32 fragment orders -> a [rows][cols] view.  kblock 64: csrc/mlp/mma_tile.h ``w1s_off`` (row
+    tile r // 16, 64-column pair c // 64, load i = (c % 16) // 4, lane ((c % 64) // 16) * 16 + r % 16, element c % 4);
+    kblock 32: csrc/mlp/rega_gemm.h ``dzr_off`` (32-column stage c // 32, load h = (c % 8) // 4, lane
+    ((c % 32) // 8) * 16 + r % 16, element c % 4)."""
+    rt, nb = (rows + 15) // 16, (cols + kblock - 1) // kblock
+    v = buf[: rt * 16 * nb * kblock].view(rt, nb, kblock // 16, 4, 16, 4)  # [row tile][block][load][lane grp][r][e]
+    return v.permute(0, 4, 1, 3, 2, 5).reshape(rt * 16, nb * kblock)[:rows, :cols]
 
 
 def param_dtype(dtype: str) -> torch.dtype:
@@ -212,6 +214,8 @@ class MlpEngine:
             # monotonic counter per column tile -- a separate array per tiling (128 x 128 / 64 x 64) -- and
             # the timed-out-wait word
             tiles = (ld + 31) // 32
+            if self.np == 3:  # fp32 dZ1 in the A-in-registers dW1 K loop's fragment order (MlpStep.dz_swz)
+                self.dZ1s = torch.zeros((H + 15) // 16 * 16 * ((ld + 31) // 32 * 32), dtype=torch.float32, device=dev)
             self.ag_counters = torch.zeros(2 * tiles * 32, dtype=torch.int64, device=dev)
             self.ag_err = torch.zeros(1, dtype=torch.int32, device=dev)
             # its hand-off granules: 8-byte {value, epoch} z2 partials [H/64][16][ld] and D [16][ld] (tags only
@@ -286,7 +290,7 @@ class MlpEngine:
         st = self._step
         if self.backend != "hip" or st is None or not st.dz_left_swz:
             return self.dZ1
-        return fragment_rows_to_rowmajor(self.dZ1s, self.H, self.ld)
+        return fragment_rows_to_rowmajor(self.dZ1s, self.H, self.ld, 64 if st.dz_left_swz == 1 else 32)
 
     def _w1_written(self) -> None:
         """W1 changed outside the step's own in-place update: the forward's fragment-ordered copy (MlpStep.w1_swz)
@@ -417,7 +421,7 @@ class MlpEngine:
             elif self.ag_gran is not None:  # the wide fused head
                 b.update(fh_tiles=int(self.ag_counters.numel()) // 64,  # [2 tilings][tiles][32]
                          ag_gran=ptr(self.ag_gran), ag_gran_count=int(self.ag_gran.numel()),
-                         ag_counters=ptr(self.ag_counters))
+                         ag_counters=ptr(self.ag_counters), dz1s=ptr(self.dZ1s))
             if self.kpart is not None:
                 b.update(kpart=ptr(self.kpart), kpart_cap=int(self.kpart.numel()))
             bias_col = bool(self.np and self.XT is not None and self.XT.shape[0] == self.P + 1)

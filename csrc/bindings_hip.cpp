@@ -377,6 +377,16 @@ struct MlpStep {
             const bool ag = fh_allgather && ag_counters && ag_err && ag_gran && h.dw2part && !(parts & 12) &&
                             cme::mlp_fwd1_wide_ag_ok(f, h, ag64());
             if (!(parts & 8) && cme::mlp_split_wide_fwd_reads_planes(f, ag, ag64())) refresh_planes(stream);
+            if (ag && dz_swz && dz1s && dz32 && h.dZ1 && (parts & 3) == 3) {
+              cme::SplitStepArgs t = a;
+              t.dZ1 = P_<float>(dz1s);
+              if (cme::mlp_wgrad_dzr_ok(t)) {  // the wide head writes dZ1 in the dW1 K loop's fragment order
+                a.dZ1 = t.dZ1;
+                a.dz_swz = 2;
+                h.dZ1 = a.dZ1;
+                h.dz_swz = 2;
+              }
+            }
             if (ag) {  // one launch: forward GEMM + the all-gather head
               a.dw2_cols = cme::mlp_fwd1_wide_ag(f, h, P_<unsigned long long>(ag_counters), fh_tiles,
                                                  P_<unsigned long long>(ag_gran), ag_gran_count, P_<int>(ag_err),

@@ -106,7 +106,8 @@ struct SplitStepArgs {
   int x_swz = 0;
   const void* Xs = nullptr;
   // ... and (fp32 dZ1, a_fp32 bit1) the weight-gradient GEMM reads dZ1 from the fragment-ordered buffer the head
-  // wrote (a.dZ1 then points at it: [cdiv(H, 16)][cdiv(ld, 64)][4][64 lanes][4 floats], mma_tile.h w1s_off)
+  // wrote (a.dZ1 then points at it).  1: H <= 128, [cdiv(H, 16)][cdiv(ld, 64)][4][64 lanes][4 floats] (mma_tile.h
+  // w1s_off); 2: the wide A-in-registers engine, [cdiv(H, 16)][cdiv(ld, 32)][2][64 lanes][4 floats] (rega_gemm.h dzr_off)
   int dz_swz = 0;
   // wide layers (LDS GEMM forward): when set, the forward GEMM's tile epilogue also leaves the head's
   // z2 partial sums, z2part[row tile][16][ld] = W2[:, tile rows] . a1[tile rows, :] (v_mfma_f32_16x16x4
@@ -175,6 +176,8 @@ bool mlp_split_w1_planes_read(const SplitStepArgs& a);
 bool mlp_split_fwd_fp32_w(const SplitStepArgs& a);
 // the weight-gradient GEMM can read fp32 dZ1 in fragment order (SplitStepArgs::dz_swz)
 bool mlp_wgrad_dz_swz_ok(const SplitStepArgs& a);
+// ... and the wide A-in-registers dW1 in its own fragment order (SplitStepArgs::dz_swz == 2, rega_gemm.h dzr_off)
+bool mlp_wgrad_dzr_ok(const SplitStepArgs& a);
 
 // number of z2 row-tile partials mlp_split_fwd1 writes for `a` (0: the forward does not produce them)
 int mlp_split_fwd1_z2_chunks(const SplitStepArgs& a);

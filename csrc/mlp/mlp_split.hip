@@ -935,16 +935,20 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
     const int row = rw + rr, col = cw + c4;
     const f32x4 v = *reinterpret_cast<const f32x4*>(ts + (rw - m0 + rr) * LD + cw - n0 + c4);
     const bool rok = row < H, full = rok && col + 4 <= n;
-    if (h.dZ1) {
+    if (h.dZ1) {  // (dz_swz == 2: in the weight-gradient K loop's fragment order, rega_gemm.h dzr_off; the 4 columns
+      //            col .. col + 3 stay one 16-byte group there)
+      const int nst = (h.ldz + 31) >> 5;
       if (full) {
         __attribute__((ext_vector_type(4))) unsigned w;
         __builtin_memcpy(&w, &v, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(w, rdz, (row * h.ldz + col) * 4, 0, 0);
+        const int off = h.dz_swz == 2 ? (int)dzr_off(row, col, nst) : row * h.ldz + col;
+        __builtin_amdgcn_raw_buffer_store_b128(w, rdz, off * 4, 0, 0);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float ve = v[e];
-          st_f32(rdz, (rok && col + e < n) ? (row * h.ldz + col + e) * 4 : kOOB, ve);
+          const int off = h.dz_swz == 2 ? (int)dzr_off(row, col + e, nst) : row * h.ldz + col + e;
+          st_f32(rdz, (rok && col + e < n) ? off * 4 : kOOB, ve);
         }
       }
     }
@@ -1350,7 +1354,9 @@ __global__ __launch_bounds__(512) void fwd1_rega_kernel(SplitStepArgs a, int tn,
 // dW1 = dZ1 XT on the A-in-registers engine: dZ1 read as fp32 (AT = float; the head writes it instead of
 // the three bf16 planes: 4 B per element stored and loaded instead of 6) or as its one bf16 plane (split1),
 // with wgrad_glds_kernel's fused reg + SGD + plane-refresh epilogue; the dW2 / db2 roles ride along
-template <typename AT, int WC, int NKS, int ENG = 0>
+// DSWZ (fp32, rega engine): dZ1 is read in the K loop's fragment order from the buffer the wide head wrote
+// (SplitStepArgs::dz_swz == 2, rega_gemm.h dzr_off)
+template <typename AT, int WC, int NKS, int ENG = 0, bool DSWZ = false>
 __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn, int tbig, int t2) {
   extern __shared__ __attribute__((aligned(16))) char lds_dyn[];
   if ((int)blockIdx.x >= tbig) {
@@ -1381,6 +1387,10 @@ __global__ __launch_bounds__(512) void wgrad_rega_kernel(SplitStepArgs a, int tn
     g64_gemm_mainloop<AT, (NKS > 0 ? (NKS * 32 + 63) / 64 : 0)>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M,
                                                                P + a.bias_col, a.n, m0, n0, lds_dyn, acc,
                                                                g64_touch(a, id, tbig, tn));
+  } else if constexpr (DSWZ) {
+    static_assert(sizeof(AT) == 4, "fragment-ordered dZ1: fp32");
+    rega_gemm_mainloop<AT, 128, WC, NKS, 0, true>(A, (a.ld + 31) / 32, static_cast<const bf16*>(a.XTw), a.ldxt, M,
+                                                  P + a.bias_col, a.n, m0, n0, lds_dyn, acc);
   } else {
     rega_gemm_mainloop<AT, 128, WC, NKS>(A, a.ld, static_cast<const bf16*>(a.XTw), a.ldxt, M, P + a.bias_col, a.n, m0,
                                          n0, lds_dyn, acc);
@@ -1492,6 +1502,15 @@ void launch_wgrad_rega_k(const SplitStepArgs& a, int t2, int tb, hipStream_t s) 
   // (the K-loop ring, the epilogue's transposed 128 x (128 + 4) fp32 tile, the role workgroups' scratch)
   constexpr int L = std::max({ra::lds_bytes<128>(), g64::lds_bytes<AT>(), W1Chunks<128, 128>::kLdsBytes,
                               kWKS * 4 * 64 * (int)sizeof(float) + 16 + 2 * kXpTile * (int)sizeof(float)});
+  if constexpr (sizeof(AT) == 4) {
+    if (a.dz_swz == 2) {
+      CME_REQUIRE(a.wide_eng == 0, "wgrad_rega: the fragment-ordered dZ1 is read by the A-in-registers engine");
+      set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS, 0, true>>(L);
+      wgrad_rega_kernel<AT, kRegaWC, NKS, 0, true><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
+      return;
+    }
+  }
+  CME_REQUIRE(a.dz_swz == 0, "wgrad_rega: fragment-ordered dZ1 with bf16 planes");
   if (a.wide_eng == 1) {
     set_lds_limit<wgrad_rega_kernel<AT, kRegaWC, NKS, 1>>(L);
     wgrad_rega_kernel<AT, kRegaWC, NKS, 1><<<tbig + t2 + tb, 512, L, s>>>(a, tn, tbig, t2);
@@ -1589,12 +1608,20 @@ bool small_wgrad_fp32_ok(const SplitStepArgs& a) {
   return a.npz == 3 && (a.a_fp32 & 2) && a.dZ1 != nullptr && al16(a.dZ1) && a.ld % 4 == 0;
 }
 
+// the wide form (SplitStepArgs::dz_swz == 2): the whole layer's dW1 on the A-in-registers engine reading fp32 dZ1, no
+// fused exchange, db1 from the all-ones XT row
+bool mlp_wgrad_dzr_ok(const SplitStepArgs& a) {
+  return a.npz == 3 && a.xf_world == 0 && big_wgrad_ok(a) && rega_wgrad_ok(a) && a.wide_eng == 0 && a.bias_col &&
+         a.w1_row0 == 0 && a.w1_rows < 0 && a.dZ1 != nullptr && al16(a.dZ1);
+}
+
 // the fragment-ordered fp32 dZ1 (SplitStepArgs::dz_swz): the wave-split-K dW1 GEMM over 16-byte pixel pairs whose
 // waves start their K (= batch) ranges on 64-column pairs: an even number of 32-column chunks per wave (n = 257-512,
 // 769-1024, ...)
 bool mlp_wgrad_dz_swz_ok(const SplitStepArgs& a) {
-  return a.H <= 128 && small_wgrad_fp32_ok(a) && a.n % 16 == 0 && al16(a.XT) && a.ldxt % 16 == 0 && a.ld % 8 == 0 &&
-         cdiv(cdiv(a.n, 32), kWKS) % 2 == 0;
+  // (bias_col: db1 comes out of the dW1 GEMM; without the all-ones XT row a bias role would read dZ1 row-major)
+  return a.H <= 128 && a.bias_col && small_wgrad_fp32_ok(a) && a.n % 16 == 0 && al16(a.XT) && a.ldxt % 16 == 0 &&
+         a.ld % 8 == 0 && cdiv(cdiv(a.n, 32), kWKS) % 2 == 0;
 }
 
 // Decided on the whole step (not the row range of a bucketed call; the xGMI-fused launch always takes the
@@ -1748,6 +1775,7 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
       CME_LAUNCH_CHECK(s);
       return;
     }
+    CME_REQUIRE(c.dz_swz == 0, "wgrad: fragment-ordered dZ1 outside the A-in-registers engine");
     if (glds_wgrad_ok(c)) {
       if (c.npz == 3) launch_wgrad_glds<3>(c, t2f, tbf, s);
       else launch_wgrad_glds<1>(c, t2f, tbf, s);

@@ -106,7 +106,15 @@ struct RegaGeom {
 // per trip before the A registers are used.
 // ABLATE (bench/micro/rega_ablate.hip only): 1 = no MFMA (fragments still read and split, kept live),
 // 2 = no loads after the prologue (the MFMAs run on whatever the ring holds)
-template <typename AT, int BN, int WC = 1, int NKS = 0, int ABLATE = 0>
+// ASWZ (fp32 A): A is in the K loop's fragment order (dzr_off; the wide head's dZ1, SplitStepArgs::dz_swz == 2) and
+// lda is the number of 32-k stages per 16-row block: each 16-byte load instruction of a wave reads 1 KB of contiguous
+// memory instead of 16 rows x 64 B.
+// Float offset of A(row, col) in that order (nst = stages per row block = cdiv(row length, 32)).
+__host__ __device__ __forceinline__ int64_t dzr_off(int row, int col, int nst) {
+  const int kt = col >> 5, w = col & 31, lane = (w >> 3) * 16 + (row & 15);
+  return (((((int64_t)(row >> 4) * nst + kt) * 2 + ((w >> 2) & 1)) * 64 + lane) * 4) + (w & 3);
+}
+template <typename AT, int BN, int WC = 1, int NKS = 0, int ABLATE = 0, bool ASWZ = false>
 __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int lda,
                                                    const __hip_bfloat16* __restrict__ B, int ldb, int M, int N,
                                                    int K, int m0, int n0, char* __restrict__ lds,
@@ -133,7 +141,12 @@ __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int arow = m0 + 16 * (MB * wr + mb) + fr;
-    abase[mb] = arow < M ? (arow * lda + 8 * fg) * (int)sizeof(AT) : -1;
+    if constexpr (ASWZ) {
+      static_assert(F32, "fragment-ordered A: fp32");
+      abase[mb] = arow < M ? (((m0 >> 4) + MB * wr + mb) * lda * 2 * 64 + lane) * 16 : -1;
+    } else {
+      abase[mb] = arow < M ? (arow * lda + 8 * fg) * (int)sizeof(AT) : -1;
+    }
   }
   // B DMA: chunk c = wave + 8 j of 16 rows; lane -> row lane >> 2, physical slot lane & 3 holding logical
   // k-chunk slot ^ gl::swz(row)
@@ -156,8 +169,11 @@ __device__ __forceinline__ void rega_gemm_mainloop(const AT* __restrict__ A, int
     const bool ak = k0 + 8 * fg < K;
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
-      const int ao = (abase[mb] >= 0 && ak) ? abase[mb] + k0 * (int)sizeof(AT) : kOOB;
-      if constexpr (F32) {
+      const int ao = (abase[mb] >= 0 && ak) ? abase[mb] + (ASWZ ? kt * 2048 : k0 * (int)sizeof(AT)) : kOOB;
+      if constexpr (ASWZ) {
+        fa.v[2 * mb] = load16_asm<0>(rsa, ao);
+        fa.v[2 * mb + 1] = load16_asm<1024>(rsa, ao);
+      } else if constexpr (F32) {
         fa.v[2 * mb] = load16_asm<0>(rsa, ao);
         fa.v[2 * mb + 1] = load16_asm<16>(rsa, ao);
       } else {

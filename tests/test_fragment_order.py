@@ -41,3 +41,20 @@ def test_fragment_rows_to_rowmajor_inverts_w1s_off():
         c = torch.arange(cols).view(1, -1).expand(rows, cols)
         buf[w1s_off(r, c, npair).reshape(-1)] = src.reshape(-1)
         assert torch.equal(fragment_rows_to_rowmajor(buf, rows, cols), src)
+
+
+def dzr_off(row, col, nst):  # rega_gemm.h dzr_off (the wide fp32 dZ1 in the A-in-registers K loop's order)
+    kt, w = col >> 5, col & 31
+    lane = (w >> 3) * 16 + (row & 15)
+    return ((((row >> 4) * nst + kt) * 2 + ((w >> 2) & 1)) * 64 + lane) * 4 + (w & 3)
+
+
+def test_fragment_rows_to_rowmajor_inverts_dzr_off():
+    for rows, cols in ((512, 800), (37, 96), (100, 40)):
+        nst = (cols + 31) // 32
+        src = torch.randn(rows, cols, dtype=torch.float64, generator=torch.Generator().manual_seed(cols))
+        buf = torch.zeros((rows + 15) // 16 * 16 * nst * 32, dtype=torch.float64)
+        r = torch.arange(rows).view(-1, 1).expand(rows, cols)
+        c = torch.arange(cols).view(1, -1).expand(rows, cols)
+        buf[dzr_off(r, c, nst).reshape(-1)] = src.reshape(-1)
+        assert torch.equal(fragment_rows_to_rowmajor(buf, rows, cols, 32), src)

@@ -926,3 +926,38 @@ def test_fragment_ordered_dz1_is_bitwise_the_row_major_dz1(n):
     assert torch.equal(engines[0].grads, engines[1].grads)
     for e in engines:
         assert not e.kernel_error()
+
+
+@pytest.mark.parametrize("H,n", [(1024, 800), (512, 256), (4096, 800)])
+def test_wide_fragment_ordered_dz1_is_bitwise_the_row_major_dz1(H, n):
+    """Wide split3 layers: the fused head writing fp32 dZ1 in the A-in-registers dW1 K loop's fragment order
+    (MlpStep.dz_swz -> SplitStepArgs::dz_swz == 2, rega_gemm.h dzr_off) against row-major dZ1: parameters and
+    gradients bitwise equal over fused SGD steps, a gradient step and the native loop; dz1() is the same view."""
+    x, y = synthetic_mnist(3 * n + 16, seed=H)
+    nn = NeuralNetwork([784, H, 10])
+    engines = []
+    for dzs in (0, 1):
+        e = MlpEngine(nn.H, "f32", max_cols=n, device="cuda", path="split3")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        e.set_store_a1(False)
+        e._hip_step().dz_swz = dzs
+        engines.append(e)
+
+    def both(fn):
+        for e in engines:
+            fn(e)
+        torch.cuda.synchronize()
+        assert torch.equal(engines[0].params, engines[1].params)
+
+    both(lambda e: [e.run(off, n, 1.0 / n, 1e-4, 0.05, sgd=True) for off in (0, n, 16)])
+    both(lambda e: e.run(2 * n, n, 1.0 / n, 1e-4, 0.0, sgd=False))
+    assert torch.equal(engines[0].grads, engines[1].grads)
+    # (the A-in-registers dW1 takes layers with >= 192 of its 128 x 128 tiles: H = 4096 here, not 512 / 1024)
+    assert engines[1]._hip_step().dz_left_swz == (2 if (H + 127) // 128 * ((784 + 1 + 127) // 128) >= 192 else 0)
+    assert torch.equal(engines[0].dz1()[:, :n], engines[1].dz1()[:, :n])
+    N = engines[0].num_samples
+    both(lambda e: e._hip_step().run_steps(0, 4, n, 0, n, N, 1.0 / n, 1e-4, 0.05, 1,
+                                           torch.cuda.current_stream().cuda_stream))
+    for e in engines:
+        assert not e.kernel_error()
