@@ -111,7 +111,11 @@ struct MlpStep {
   // 0 -> 4: 14.55-14.63 -> 14.11-14.14 us at n = 800, 13.0-13.1 -> 12.64-12.66 at n = 100; 2 and 6 slower at n = 800
   // (profiles/kbench_prefetch_wgs_r4.jsonl)
   int prefetch = 4;
-  int prefetch_xt = 4;  // SplitStepArgs::pf_wgs_xt
+  // SplitStepArgs::pf_wgs_xt (this step's XT pulled by extra workgroups of the forward + head launch): on in round 4,
+  // OFF since the end of round 5 -- with the fragment-ordered forward operands and fp32 dZ1 they cost the forward more
+  // than they save the weight-gradient launch: walking step 14.01-14.06 -> 13.73-13.85 us at n = 800, -0.13 at 512,
+  // -0.15 at 400, -0.03 to -0.1 at 100-200 (profiles/r5/kbench_prefetch_xt_r5.jsonl, alternated three times)
+  int prefetch_xt = 0;
   int wide_eng = -1;    // SplitStepArgs::wide_eng: the 128 x 128 wide K loop's engine (0 rega, 1 g64; -1: g64 for bf16
                         // A, rega for fp32 -- 784-4096-10 step bf16 39.1 -> 38.1 us, fp32 55.4 -> 58.0 with g64,
                         // profiles/r5/kbench_wide_engines.jsonl)
