@@ -333,7 +333,7 @@ class MlpEngine:
     def set_store_a1(self, on: bool) -> None:
         """Split layers with the head fused into the forward launch: False skips the a1 store whenever that launch
         also leaves the dW2 partials (no kernel of the training step reads a1 then: dZ1 and the partials come out
-        of the same launch).  Wide layers: always; H <= 128: from n = 512 columns (MlpStep.head_dw2 auto), where
+        of the same launch).  Wide layers: always; H <= 128: from n = 768 columns (MlpStep.head_dw2 auto), where
         the weight-gradient launch's dW2 GEMM over the whole batch was that launch's critical path
         (bench/stamps_roles.py: roles end 5.99 -> 3.74 us at n = 800; below, the partials cost the forward more
         than they save -- profiles/r5/)."""

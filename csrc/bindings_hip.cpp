@@ -121,7 +121,8 @@ struct MlpStep {
                         // profiles/r5/kbench_wide_engines.jsonl)
   // H <= 128, the all-gather forward + head: it also leaves the dW2 partials per 32 columns (fha_body step 4a) for
   // the weight-gradient launch's dW2 role (needs dw2p); 0: the role forms D . a1^T over the batch itself; -1 (auto):
-  // from n = 512 columns, where the role's GEMM is the weight-gradient launch's critical path
+  // from n = 768 columns (it was 512 when it went in; re-measured on the final round-5 forms, walking step: n = 512
+  // h0 12.90-13.04 vs h1 13.24-13.25 us, n = 800 equal, 13.76-13.91 either way -- profiles/r5/kbench_head_dw2_r5end.jsonl)
   int head_dw2 = -1;
   int xp_dbg = 0;       // SplitStepArgs::xp_dbg (diagnostics)
   int g64_touch = 0;    // SplitStepArgs::g64_touch (measured slower: 784-4096-10 bf16 38.1 -> 41.7 us,
@@ -350,7 +351,7 @@ struct MlpStep {
                 hg.dz_swz = 1;
               }
             }
-            if ((head_dw2 > 0 || (head_dw2 < 0 && n >= 512)) && dw2p && C <= 16) {  // the head leaves the dW2 partials (fha_body step 5); then
+            if ((head_dw2 > 0 || (head_dw2 < 0 && n >= 768)) && dw2p && C <= 16) {  // the head leaves the dW2 partials (fha_body step 5); then
               // nothing after this launch reads a1: not stored in training (store_a1 off)
               hg.dw2part = P_<float>(dw2p);
               a.dw2part = hg.dw2part;
