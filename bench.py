@@ -146,15 +146,19 @@ def timed(ctx, runners) -> float:
 
 # ------------------------------------------------------------------------------------------ data parallel
 def dp_prepare(ctx, global_batch: int, allreduce: str, warmup: int, extra_plans: int = 0):
-    """Trainer + captured graphs + ``warmup`` warm-up steps.  Returns (trainer, full-batch list)."""
+    """Trainer + captured graphs + ``warmup`` warm-up steps.  Returns (trainer, full-batch list).  ``allreduce``:
+    an --allreduce value, or "xgmi-push" (the xGMI all-reduce fused into the weight-gradient launch in its
+    owner-tile push form; "xgmi" / "auto" fuse the one-shot pull)."""
     from cme213_sp18_amd.models.mlp import NeuralNetwork
     from cme213_sp18_amd.parallel.trainer import DataParallelTrainer
 
     a = ctx.a
     nn = NeuralNetwork([784, a.hidden, 10])
+    form = "push" if allreduce == "xgmi-push" else "auto"
     tr = DataParallelTrainer(nn, comm=ctx.comm, device=ctx.device, dtype=a.dtype, batch_size=global_batch,
-                             backend=a.backend, use_graphs=not a.no_graphs, allreduce=allreduce,
-                             grad_wire=a.grad_wire, executor="eager" if a.no_graphs else a.executor)
+                             backend=a.backend, use_graphs=not a.no_graphs,
+                             allreduce="xgmi" if allreduce == "xgmi-push" else allreduce, grad_wire=a.grad_wire,
+                             executor="eager" if a.no_graphs else a.executor, fused_form=form)
     tr.load(ctx.x, ctx.y)
     full = [(s, ln) for s, ln in tr.epoch_plan().steps if ln == global_batch]
     if not full:
@@ -193,9 +197,11 @@ def dp_probe(ctx, tr, full, steps: int) -> float:
 
 def dp_tune_allreduce(ctx, global_batch: int, tune: dict) -> str:
     """The gradient sync mode to time (an --allreduce value), chosen by measurement when N > 1 and
-    --allreduce auto: the cost model's pick, the xGMI two-shot (N >= 3) and RCCL each run --tune-steps steps
-    from the initial weights (the fastest wins; identical floats on every rank: one decision).  Results go into
-    ``tune`` (impl name -> us/step, 'failed', 'unavailable' or 'skipped: budget')."""
+    --allreduce auto: the cost model's pick, the other form of the fused xGMI all-reduce (the owner-tile push next
+    to the one-shot pull: which is faster rests on a hop latency only the node can tell), the xGMI two-shot
+    (N >= 3) and RCCL each run --tune-steps steps from the initial weights (the fastest wins; identical floats on
+    every rank: one decision).  Results go into ``tune`` (impl name -> us/step, 'failed', 'unavailable' or
+    'skipped: budget')."""
     a = ctx.a
     if not (ctx.R > 1 and a.allreduce == "auto" and a.backend == "hip" and a.tune_allreduce == "on"):
         return a.allreduce
@@ -210,10 +216,11 @@ def dp_tune_allreduce(ctx, global_batch: int, tune: dict) -> str:
     else:
         tune[pick] = dp_probe(ctx, tr, full, a.tune_steps)
     tr.close()
-    others = (["xgmi2"] if ctx.R >= 3 and pick != "xgmi-2shot" else []) + (["rccl"] if pick.startswith("xgmi") else [])
+    others = ((["xgmi-push"] if pick == "xgmi-fused" else []) + (["xgmi2"] if ctx.R >= 3 and pick != "xgmi-2shot" else [])
+              + (["rccl"] if pick.startswith("xgmi") else []))
     for mode in others:
         if not ctx.budget_left():
-            tune[{"xgmi2": "xgmi-2shot", "rccl": ctx.comm.name}[mode]] = "skipped: budget"
+            tune[{"xgmi-push": "xgmi-push", "xgmi2": "xgmi-2shot", "rccl": ctx.comm.name}[mode]] = "skipped: budget"
             continue
         try:
             tr, full = dp_prepare(ctx, global_batch, mode, a.warmup, a.tune_steps)
@@ -241,11 +248,14 @@ PROBE_FACTOR = 3.0  # a timed run this many times slower per step than its probe
 
 
 def guard_probe(res: dict, steps: int, probe_us, retime=None) -> dict:
-    """First-contact guard: the timed run's us/step against the probe that chose its configuration (max over
-    ranks on both sides, so every rank decides alike).  More than PROBE_FACTOR x off: re-time once on the next
-    candidate (``retime() -> (result, its own probe us/step or None)``); still off (or nothing to fall back on):
-    the record is marked ``"invalid": "timed run inconsistent with probe"`` instead of reported clean.  The
-    decision and both timings go into ``config.probe_guard``."""
+    """First-contact guard: the timed us/step against the probe that chose its configuration (max over
+    ranks on both sides, so every rank decides alike).  More than PROBE_FACTOR x off: re-timed on the next
+    candidate -- ``retime`` is one callable or a fallback CHAIN of them, tried in order (the owner-tile push form:
+    push -> the one-shot pull -> RCCL), each ``() -> (result, its own probe us/step or None)``; the first re-timed run
+    that agrees with its probe is reported.  None agrees (or nothing to fall back on): the record is marked
+    ``"invalid": "timed run inconsistent with probe"`` instead of reported clean.  The decision and every timing go
+    into ``config.probe_guard`` ("first", "retimed" = the last re-time, "chain" = all of them when more than one; a
+    re-timed run's own guard record is kept under "inner")."""
     if not isinstance(probe_us, (int, float)) or not probe_us or probe_us == float("inf") or not res.get("ok"):
         return res
     us = 1e6 * res["dt"] / steps
@@ -255,20 +265,26 @@ def guard_probe(res: dict, steps: int, probe_us, retime=None) -> dict:
     if us <= PROBE_FACTOR * probe_us:
         res["config"]["probe_guard"] = {"consistent": True, **first}
         return res
-    if retime is not None:
-        res2, probe2 = retime()
+    chain = [] if retime is None else (list(retime) if isinstance(retime, (list, tuple)) else [retime])
+    if not chain:
+        res["config"]["probe_guard"] = {"consistent": False, "first": first}
+    done = []
+    for k, fn in enumerate(chain):
+        res2, probe2 = fn()
         us2 = 1e6 * res2["dt"] / steps
         ref = probe2 if isinstance(probe2, (int, float)) and probe2 and probe2 != float("inf") else probe_us
         second = {"timed_us_per_step": round(us2, 3), "probe_us_per_step": round(ref, 3),
                   "what": res2["config"].get("allreduce") if res2.get("parallelism", "").startswith("dp")
                   else res2.get("parallelism")}
-        res2["config"]["probe_guard"] = {"consistent": bool(res2.get("ok")) and us2 <= PROBE_FACTOR * ref,
-                                         "first": first, "retimed": second}
-        if res2["config"]["probe_guard"]["consistent"]:
-            return res2
+        done.append(second)
+        inner = res2["config"].get("probe_guard")  # the re-timed run's own guard (run_dp), kept, not overwritten
+        ok2 = bool(res2.get("ok")) and us2 <= PROBE_FACTOR * ref
+        res2["config"]["probe_guard"] = {"consistent": ok2, "first": first, "retimed": second,
+                                         **({"chain": list(done)} if len(chain) > 1 else {}),
+                                         **({"inner": inner} if inner else {})}
         res = res2
-    else:
-        res["config"]["probe_guard"] = {"consistent": False, "first": first}
+        if ok2:
+            return res2
     res["ok"] = False
     res["invalid"] = "timed run inconsistent with probe"
     return res
@@ -284,14 +300,26 @@ def run_dp(ctx, global_batch: int, allreduce: str | None = None, tune: dict | No
     mode = allreduce if allreduce is not None else dp_tune_allreduce(ctx, global_batch, tune)
     res = _run_dp_timed(ctx, global_batch, mode, tune)
     impl = res["config"]["allreduce"]
-    retime = None
-    if ctx.R > 1 and impl != ctx.comm.name:
+    return guard_probe(res, a.steps, tune.get(impl), dp_fallbacks(ctx, global_batch, impl, tune))
+
+
+def dp_fallbacks(ctx, global_batch: int, impl: str, tune: dict) -> list:
+    """The first-contact guard's re-time chain for a data-parallel run on ``impl`` (each entry probes its candidate,
+    then times it): the owner-tile push form falls back to the one-shot pull and then RCCL, every other xGMI form
+    to RCCL; RCCL itself (and one rank) to nothing."""
+    a = ctx.a
+    if ctx.R <= 1 or impl == ctx.comm.name:
+        return []
+
+    def on(mode):
         def retime():
-            tr, full = dp_prepare(ctx, global_batch, "rccl", a.warmup, a.tune_steps)
+            tr, full = dp_prepare(ctx, global_batch, mode, a.warmup, a.tune_steps)
             probe = dp_probe(ctx, tr, full, a.tune_steps)
             tr.close()
-            return _run_dp_timed(ctx, global_batch, "rccl", tune), probe
-    return guard_probe(res, a.steps, tune.get(impl), retime)
+            return _run_dp_timed(ctx, global_batch, mode, tune), probe
+        retime.mode = mode
+        return retime
+    return ([on("xgmi")] if impl == "xgmi-push" else []) + [on("rccl")]
 
 
 def _run_dp_timed(ctx, global_batch: int, mode: str, tune: dict) -> dict:
@@ -487,8 +515,10 @@ def measure(ctx, scaling: str, parallel: str | None = None, allreduce: str | Non
     if parallel == "tp":
         res = run_tp(ctx, gb)
         if ptune:  # chosen by probing: a timed run far off its probe is re-timed once on data parallel
+            # (the fallback runs the configuration choose_parallel probed -- the all-reduce policy's pick -- without
+            # a second all-reduce sweep; its guard is the outer one, against that probe)
             res = guard_probe(res, a.steps, ptune.get(res["parallelism"]),
-                              lambda: (run_dp(ctx, gb), ptune.get(f"dp{ctx.R}")))
+                              lambda: (run_dp(ctx, gb, allreduce="auto", tune={}), ptune.get(f"dp{ctx.R}")))
             if res["parallelism"].startswith("dp"):
                 parallel = "dp"
                 res["allreduce_mode"] = _mode_of(res["config"]["allreduce"], ctx)
@@ -507,7 +537,7 @@ def _mode_of(impl: str, ctx) -> str:
     """The --allreduce value that reproduces an implementation name (for the secondary run)."""
     if ctx.R == 1:
         return "auto"
-    return {"xgmi": "xgmi", "xgmi-fused": "xgmi", "xgmi-push": "xgmi", "xgmi-2shot": "xgmi2", "xgmi-bf16wire": "xgmi",
+    return {"xgmi": "xgmi", "xgmi-fused": "xgmi", "xgmi-push": "xgmi-push", "xgmi-2shot": "xgmi2", "xgmi-bf16wire": "xgmi",
             "host-gloo": "host"}.get(impl, "rccl")
 
 

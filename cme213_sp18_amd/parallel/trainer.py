@@ -99,8 +99,11 @@ def fused_exchange_us(R: int, wire_bytes: int, form: str, model: CostModel | Non
 
 
 def auto_fused_form(R: int, wire_bytes: int, model: CostModel | None = None) -> str:
-    """The fused all-reduce's form by the cost model: the owner-tile push once its 4 S / R bytes per link and
-    one hop fewer beat the one-shot's S (R >= 4 at 784-100-10 with the planning constants), else the pull."""
+    """The fused all-reduce's form the cost model PREDICTS faster: the owner-tile push once its 4 S / R bytes per
+    link and one hop fewer beat the one-shot's S (R >= 4 at 784-100-10 with the planning constants), else the pull.
+    A prediction only (bench/predict_scaling.py): the hop latency is a planning constant nobody has measured across
+    GPUs, so the trainer's "auto" form is the pull, and bench.py times the push next to it (dp_tune_allreduce) --
+    the faster measured form is the one it runs."""
     return "push" if fused_exchange_us(R, wire_bytes, "push", model) < fused_exchange_us(R, wire_bytes, "pull",
                                                                                           model) else "pull"
 
@@ -146,13 +149,19 @@ def measure_cost_model(comm, device, small: int = 1024, large: int = 1 << 20, it
         return comm.allreduce_scalar(1e6 * (time.perf_counter() - t0) / iters, op="max")
 
     m = CostModel(measured=True)
+    plan = CostModel()
     t = {}
     for numel in (small, large):
         buf = torch.zeros(numel, dtype=torch.float32, device=dev)
-        t[("rccl", numel)] = timed(lambda: comm.allreduce_(buf))
+        t[("rccl", numel)] = min(timed(lambda: comm.allreduce_(buf)) for _ in range(3))
     ds = 4 * (large - small)
-    m.rccl_us = t[("rccl", small)]
-    m.rccl_gbps = 2 * (R - 1) / R * ds / max(t[("rccl", large)] - t[("rccl", small)], 1e-3) / 1e3
+    fixed, slope = _fit_bounded(t[("rccl", small)], t[("rccl", large)], 2 * (R - 1) / R * ds, plan.rccl_us,
+                                plan.rccl_gbps)
+    if fixed is None:
+        m.rccl_us, m.rccl_gbps = plan.rccl_us, plan.rccl_gbps
+        m.measured = False
+    else:
+        m.rccl_us, m.rccl_gbps = fixed, slope
     from .xgmi import XgmiBucket
 
     try:
@@ -160,14 +169,32 @@ def measure_cost_model(comm, device, small: int = 1024, large: int = 1 << 20, it
             xb = XgmiBucket(comm.group, comm.rank, R, numel, torch.float32, dev, self_test=False)
             buf = torch.zeros(numel, dtype=torch.float32, device=dev)
             try:
-                t[("xgmi", numel)] = timed(lambda: xb.allreduce_(buf))
+                t[("xgmi", numel)] = min(timed(lambda: xb.allreduce_(buf)) for _ in range(3))
             finally:
                 xb.close()
-        m.kernel_us = t[("xgmi", small)]
-        m.link_gbps = ds / max(t[("xgmi", large)] - t[("xgmi", small)], 1e-3) / 1e3
+        fixed, slope = _fit_bounded(t[("xgmi", small)], t[("xgmi", large)], ds, plan.kernel_us, plan.link_gbps)
+        if fixed is None:
+            m.measured = False
+        else:
+            m.kernel_us, m.link_gbps = fixed, slope
     except RuntimeError:  # IPC unavailable: raised on every rank together (XgmiBucket's collective setup)
         pass
     return m
+
+
+def _fit_bounded(t_small: float, t_large: float, bytes_moved: float, plan_fixed_us: float, plan_gbps: float):
+    """(fixed cost in us, rate in GB/s) from two timings (the min of 3 probes each, max over ranks), or (None, None)
+    when the fit is not plausible -- a non-positive slope, a fixed cost outside [0.05, 20] x the planning one, or a
+    rate outside [0.05, 20] x the planning one -- so a noisy probe never replaces the planning constants with
+    millions of GB/s (the caller keeps the planning numbers and records measured = False).  The same bounds for
+    every rank: the timings are max-reduced before this is called."""
+    dt = t_large - t_small
+    if not (dt > 0 and t_small > 0):
+        return None, None
+    gbps = bytes_moved / dt / 1e3
+    if not (0.05 * plan_fixed_us <= t_small <= 20 * plan_fixed_us and 0.05 * plan_gbps <= gbps <= 20 * plan_gbps):
+        return None, None
+    return t_small, gbps
 
 
 class FaultInjected(RuntimeError):
@@ -222,8 +249,9 @@ class DataParallelTrainer:
         self.grad_wire = grad_wire
         # the all-reduce fused into the weight-gradient launch (H <= 128): "push" = the owner-tile form (each tile
         # reduced by one rank, pushed both ways as tagged granules: 2 one-way hops, 2 S / R payload per link),
-        # "pull" = the one-shot (every rank reads every peer's tile after its flag: S per link), "auto" = the cost
-        # model's pick (auto_fused_form: push from 4 ranks at 784-100-10)
+        # "pull" = the one-shot (every rank reads every peer's tile after its flag: S per link), "auto" = the pull:
+        # the push is predicted faster from 4 ranks (auto_fused_form) but has not run across GPUs, and its pick
+        # would rest on an unmeasured hop latency -- bench.py measures both forms on the node and runs the faster
         if fused_form not in ("push", "pull", "auto"):
             raise ValueError("fused_form must be push, pull or auto")
         self.fused_form = fused_form
@@ -273,7 +301,7 @@ class DataParallelTrainer:
                 and self.xgmi.shots == 1):
             slots = self.engine.fused_allreduce_slots()
             if self.fused_form == "auto":
-                self.fused_form = auto_fused_form(self.R, self.engine.params.numel() * 4)
+                self.fused_form = "pull"
             if slots and self.engine.params.dtype == torch.float32 and self._fused_fits(slots):
                 from .xgmi import XgmiBucket
 
@@ -520,6 +548,7 @@ class DataParallelTrainer:
         self._restore(snap)
         torch.cuda.synchronize(e.device)
         ok = self._all_true(ok)
+        self._graphs.clear()  # (graphs captured against another attachment must not be replayed: MlpStep.set_xgmi)
         if not ok:
             e.attach_xgmi(None)
             self._xgmi_fused.close()  # collective; also drops its error flag
@@ -757,6 +786,7 @@ class DataParallelTrainer:
         after a timed-out peer wait) and use the communicator's all-reduce (RCCL on GPUs), bucketed and overlapped
         where the gradient spans several buckets -- the same choice __init__ makes with allreduce="rccl"."""
         self.engine.attach_xgmi(None)
+        self._graphs.clear()
         for name in ("_xgmi_fused", "xgmi"):
             b = getattr(self, name)
             if b is not None:

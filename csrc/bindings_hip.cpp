@@ -132,12 +132,25 @@ struct MlpStep {
   cme::XgmiFuse xf;
   // push != 0: the owner-tile push form (XgmiFuse::push; the bucket must have slab_tiles >= the launch's tiles)
   cme::XgmiFuse* xf_dev = nullptr;  // its device copy (SplitStepArgs::xf): allocated once, so captured graphs stay valid
+  // The XCD-local step pipeline (mlp_xstep, csrc/mlp/xstep.hip): run_steps runs the whole plan in ONE persistent
+  // launch when the plan's step has the pipeline's shape (H <= 128 split3, fragment-ordered operands, the head's dW2
+  // partials, fused SGD, one process, steps on the 16-sample grid); -1 auto (on), 0 off, 1 required (an error if
+  // the plan does not qualify).  xstep_pf: prefetch workgroups per XCD (the pixels each XCD reads next).
+  int xstep = -1, xstep_pf = 0, xstep_pfm = 0;  // xstep_pfm: XStepPlan::pf_mode
+  int xstep_used = 0;     // the last run_steps ran as one xstep launch (tests, bench records)
+  unsigned xs_ep = 1, xs_launch = 0;  // the next step's granule tag; launches so far (control bank)
+  unsigned long long *xs_gran = nullptr, *xs_ctl = nullptr;
+  float *xs_dx = nullptr, *xs_b2x = nullptr;
+  uintptr_t xs_stamps = 0;  // diagnostics: [xs_stamp_steps][8][32][4] uint64 (bench/stamps_xstep.py)
+  int xs_stamp_steps = 0;
   ~MlpStep() {
     if (xf_dev) (void)hipFree(xf_dev);
+    for (void* q : {(void*)xs_gran, (void*)xs_ctl, (void*)xs_dx, (void*)xs_b2x})
+      if (q) (void)hipFree(q);
   }
   void set_xgmi(uintptr_t desc, int64_t slots, int64_t off_b1, int64_t off_W2, int64_t off_b2, int push = 0) {
     if (!desc) {
-      xf = cme::XgmiFuse{};
+      xf = cme::XgmiFuse{};  // (the device copy is read only by sgd = 2 launches, which now refuse to run)
       return;
     }
     CME_REQUIRE(split && bias_col && XT, "MlpStep.set_xgmi: split path with the all-ones XT feature only");
@@ -175,6 +188,10 @@ struct MlpStep {
     }
     xf = f;
     if (!xf_dev) HIP_CHECK(hipMalloc(&xf_dev, sizeof(cme::XgmiFuse)));
+    // every launch already enqueued (on any stream, or replayed from a graph) reads the device copy: it finishes
+    // before the copy changes under it.  A graph captured against the old bucket must not be replayed afterwards --
+    // DataParallelTrainer drops its captured graphs wherever it attaches or detaches a bucket.
+    HIP_CHECK(hipDeviceSynchronize());
     HIP_CHECK(hipMemcpy(xf_dev, &xf, sizeof(cme::XgmiFuse), hipMemcpyHostToDevice));
   }
   float xscale = 1.f;    // split path: inputs are uint8 * xscale
@@ -455,6 +472,98 @@ struct MlpStep {
     if (parts & 2) cme::mlp_wgrad(d, w, S(stream));
   }
 
+  // The plan's step as the two-launch form would run it (run(): the all-gather forward + head with the fragment-ordered
+  // operands, fp32 dZ1 in fragment order, the head's dW2 partials, SGD fused into the weight-gradient launch), or false
+  // when any of those choices would differ -- the XCD-local pipeline then does not apply and run_steps launches per step.
+  const char* xstep_args(int64_t off, int n, double scale, double reg, double lr, uintptr_t stream,
+                         cme::SplitStepArgs& a, cme::HeadArgs& h) {
+    if (!split || !XT || !W1p || !dZ1p || !w1s || !xs || !dz1s || !dw2p || !bias_col) return "not the split3 H <= 128 "
+                                                                                               "layout";
+    if (!fh_allgather || !ag_counters || !ag_slabs || !ag_err) return "the all-gather forward + head is off";
+    if (!w1_swz || !x_swz || !dz_swz) return "a fragment-ordered operand is off";
+    if (off % 16 != 0) return "a step off the 16-sample grid";
+    if (C > 16 || head_dw2 == 0 || (head_dw2 < 0 && n < 768)) return "the head leaves no dW2 partials";
+    a = split_args(off, n, scale, reg, lr, 1, 0);
+    if (!cme::mlp_fwd_swz_ok(a) || cme::mlp_split_w1_planes_read(a) || !cme::mlp_split_wgrad_fp32_dz(a))
+      return "the forward / weight gradient would not read fp32 operands";
+    a.w1_swz = 1;
+    a.W1s = P_<float>(w1s);
+    a.x_swz = 1;
+    a.Xs = reinterpret_cast<const char*>(xs) + off / 16 * ((int64_t)((P + 63) / 64) * 1024);
+    h = cme::HeadArgs{};
+    h.a1 = a.a1; h.lda = ld; h.W2 = a.W2; h.b2 = a.b2; h.labels = a.labels; h.H = H; h.C = C;
+    h.n = n; h.scale = scale; h.D = a.D; h.ldd = ld; h.dZ1 = a.dZ1; h.ldz = ld; h.dZ1_bf16 = nullptr;
+    h.dZ1_planes = nullptr; h.npz = npz; h.loss_partial = nullptr; h.shift = shift; h.mode = cme::HEAD_TRAIN;
+    h.z2part = P_<float>(z2p);
+    h.stamps = hstamps ? reinterpret_cast<unsigned long long*>(hstamps) : nullptr;  // (diagnostics)
+    if (!cme::mlp_fwd1_head_ok(a, h) || !cme::mlp_fwd1_head_ag_fits(a)) return "the all-gather head does not fit";
+    a.dZ1 = P_<float>(dz1s);
+    if (!cme::mlp_wgrad_dz_swz_ok(a)) return "dZ1 cannot be read in fragment order";
+    a.dz_swz = 1;
+    h.dZ1 = a.dZ1;
+    h.dz_swz = 1;
+    h.dw2part = P_<float>(dw2p);
+    a.dw2part = h.dw2part;
+    a.dw2_cols = 16;
+    if (!store_a1) {  // (run(): nothing after the forward reads a1 once the head leaves the dW2 partials)
+      a.a1 = nullptr;
+      h.a1 = nullptr;
+    }
+    if (!cme::mlp_xstep_ok(a, h)) return "mlp_xstep_ok";
+    refresh_swz(stream);
+    return nullptr;
+  }
+  std::string xstep_reason = "";  // why the last run_steps did not take the pipeline ("" when it did)
+
+  // the whole plan as one XCD-local pipeline launch; false (nothing enqueued) when the plan does not qualify
+  bool run_xstep(int64_t gstart0, int64_t count, int64_t B, int64_t shard_off, int n, int64_t N_end, double scale,
+                 double reg, double lr, uintptr_t stream) {
+    xstep_reason = "off";
+    if (xstep == 0) return false;
+    xstep_reason = "the plan's steps are off the 16-sample grid";
+    if (count <= 0 || count > (1 << 30) || gstart0 % 16 || B % 16 || shard_off % 16) return false;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_CHECK(hipStreamIsCapturing(S(stream), &cap));
+    xstep_reason = "the stream is capturing a graph";
+    if (cap != hipStreamCaptureStatusNone) return false;  // (granule tags come from the host: never replayed)
+    int64_t g0 = gstart0 + B > N_end ? 0 : gstart0;
+    cme::SplitStepArgs a;
+    cme::HeadArgs h;
+    if (const char* why = xstep_args(g0 + shard_off, n, scale, reg, lr, stream, a, h)) {
+      xstep_reason = why;
+      return false;
+    }
+    xstep_reason.clear();
+    if (!xs_gran) {
+      HIP_CHECK(hipMalloc(&xs_gran, cme::kXstepGranules * 8));
+      HIP_CHECK(hipMemset(xs_gran, 0, cme::kXstepGranules * 8));
+      HIP_CHECK(hipMalloc(&xs_ctl, cme::kXstepCtlWords * 8));
+      HIP_CHECK(hipMemset(xs_ctl, 0, cme::kXstepCtlWords * 8));
+      HIP_CHECK(hipMalloc(&xs_dx, (size_t)8 * 16 * ld * 4));
+      HIP_CHECK(hipMalloc(&xs_b2x, (size_t)8 * 16 * 4));
+      HIP_CHECK(hipDeviceSynchronize());
+    }
+    cme::XStepPlan p;
+    p.gstart0 = gstart0; p.B = B; p.shard_off = shard_off; p.N_end = N_end; p.count = (int)count;
+    p.X0 = P_<const uint8_t>(X); p.XT0 = P_<const uint8_t>(XT); p.Xs0 = P_<const uint8_t>(xs);
+    p.lab0 = P_<const int>(labels);
+    p.xs_tile = (int64_t)((P + 63) / 64) * 1024;
+    p.ep0 = xs_ep; p.launch = xs_launch;
+    p.gran = xs_gran; p.ctl = xs_ctl; p.Dx = xs_dx; p.b2x = xs_b2x; p.err = P_<int>(ag_err);
+    p.nw = cme::mlp_xstep_workers(a);
+    p.npf = std::max(0, std::min(xstep_pf, 32 - p.nw - 1));
+    p.pf_mode = xstep_pfm;
+    p.stamps = reinterpret_cast<unsigned long long*>(xs_stamps);
+    p.stamp_steps = xs_stamps ? xs_stamp_steps : 0;
+    cme::mlp_xstep(a, h, p, S(stream));
+    xs_ep += (unsigned)count;
+    xs_launch += 1;
+    dw2_left = 1;
+    dz_left_swz = 1;
+    dw2_cols_last = 16;
+    return true;
+  }
+
   // Native step loop: `count` consecutive global batches of B samples starting at gstart0 (wrapping to 0
   // when a batch would pass N_end), this rank's shard [gstart + shard_off, +n) of each, every kernel
   // launched from here with no Python between steps.  sgd = 1: single process, SGD fused into wgrad;
@@ -466,6 +575,10 @@ struct MlpStep {
     CME_REQUIRE(count >= 0 && n > 0 && n <= ld && B >= n && N_end >= B && (sgd == 1 || sgd == 2),
                 "MlpStep.run_steps: bad step plan");
     if (count == 0) return;
+    xstep_used = sgd == 1 && run_xstep(gstart0, count, B, shard_off, n, N_end, scale, reg, lr, stream) ? 1 : 0;
+    CME_REQUIRE(xstep_used || xstep != 1 || sgd != 1,
+                "MlpStep.run_steps: xstep = 1 but the plan's step does not qualify: " + xstep_reason);
+    if (xstep_used) return;
     int64_t gs = gstart0;
     for (int64_t i = 0; i < count; ++i) {
       if (gs + B > N_end) gs = 0;
@@ -639,6 +752,13 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("wide_eng", &MlpStep::wide_eng)
       .def_readwrite("xp_dbg", &MlpStep::xp_dbg)
       .def_readwrite("g64_touch", &MlpStep::g64_touch)
+      .def_readwrite("xstep", &MlpStep::xstep)
+      .def_readwrite("xstep_pf", &MlpStep::xstep_pf)
+      .def_readwrite("xstep_pfm", &MlpStep::xstep_pfm)
+      .def_readonly("xstep_used", &MlpStep::xstep_used)
+      .def_readonly("xstep_reason", &MlpStep::xstep_reason)
+      .def_readwrite("xs_stamps", &MlpStep::xs_stamps)
+      .def_readwrite("xs_stamp_steps", &MlpStep::xs_stamp_steps)
       .def_readwrite("lazy_planes", &MlpStep::lazy_planes)
       .def_readwrite("planes_stale", &MlpStep::planes_stale)
       .def_readwrite("dw2p", &MlpStep::dw2p)

@@ -13,6 +13,11 @@
 // Requires every workgroup of the launch to be resident at once (mlp_fwd1_head_ag_fits); a poll that outlasts
 // ag_wait_us of wall time sets *err: the launch's results are not trusted, and the weight-gradient launch that
 // follows reads *err and applies nothing (SplitStepArgs::ag_err; MlpEngine.kernel_error(), KernelHandoffTimeout).
+//
+// PS (the XCD-local step pipeline, xstep.hip): the same body as one phase of a persistent multi-step launch -- the
+// caller names the tile (rt, ct) and the step's granule tag, and the operands other workgroups of that launch rewrite
+// between steps (b1, W2, b2; W1s in the K loop) are read with sc1 (L1-bypassing) loads; every row tile stores D
+// (h.D: its own XCD's copy).  Returns false when a hand-off wait timed out (nothing after it was written).
 #pragma once
 
 #include "fwd_tile.h"
@@ -29,7 +34,8 @@ constexpr int kAgCounterStride = 32;  // uint64 words: one 256-byte line per til
 
 __device__ __forceinline__ float ag_sigmoid(float x) { return sigmoid_f32(x); }  // (head_math.h)
 
-struct EpiSigLds {
+template <int CP = 0>  // CP: the b1 load's cache policy (kSc1 under PS)
+struct EpiSigLdsT {
   const float* b1;
   float* a1;
   float (*a1s)[33];  // [16][32 + 1] this workgroup's a1 tile
@@ -37,7 +43,7 @@ struct EpiSigLds {
   float xscale;
   float pre[kEpiMaxQ];
   __device__ __forceinline__ void prefetch(int q, int row, int, bool ok) {
-    pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
+    pre[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(b1), ok ? row * 4 : kOOB, 0, CP));
   }
   __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
     const float s = ag_sigmoid(v * xscale + pre[q]);
@@ -49,10 +55,12 @@ struct EpiSigLds {
 
 // blk: the workgroup's slot in the XCD-grouped grid (the hardware XCD is blk & 7).  red: >= 8 * 2 * 4 * 64
 // floats of LDS.
-template <int NPW, int VEC, bool AF, int SWZ = 0>
-__device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs& h,
+template <int NPW, int VEC, bool AF, int SWZ = 0, bool PS = false>
+__device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs& h,
                                          unsigned long long* __restrict__ counters, gran_t* __restrict__ slabs,
-                                         int* __restrict__ err, int tm, int tn, int blk, float* red) {
+                                         int* __restrict__ err, int tm, int tn, int blk, float* red, int ps_rt = 0,
+                                         int ps_ct = 0, unsigned ps_ep = 0) {
+  constexpr int CP = PS ? kSc1 : 0;
   constexpr int kCols = 32;
   __shared__ float a1s[16][kCols + 1];
   __shared__ float w2s[16][17];        // W2[class][row of this tile], zero past C / H
@@ -67,7 +75,10 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   // start a launch up to ~1 us before the others (bench/stamps_fha.py per row tile), and every column tile's
   // all-gather waits for its last row tile
   int ct, rt;
-  if (f.xcd_rows == 2) {
+  if constexpr (PS) {
+    ct = ps_ct;
+    rt = ps_rt;
+  } else if (f.xcd_rows == 2) {
     const int j = slot / tn;
     ct = slot - j * tn;
     rt = xcd < 4 ? xcd + 4 * j : tm;  // (XCDs 4-7: padding)
@@ -75,7 +86,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     ct = f.xcd_rows ? slot : xcd + 8 * (slot / tm);
     rt = f.xcd_rows ? xcd : slot % tm;
   }
-  if (ct >= tn || rt >= tm) return;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
+  if (ct >= tn || rt >= tm) return true;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
   const int t = threadIdx.x, H = f.H, C = h.C, n = f.n;
   const int r0 = rt * 16, c0 = ct * kCols;
   unsigned long long* st = f.stamps ? f.stamps + (size_t)blk * 4 : nullptr;  // diagnostics only
@@ -89,9 +100,13 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   // stores: a store round trip in front of the z2 publication of every workgroup, bench/stamps_fha.py.)
   constexpr int kEpochThread = 448;
   if (t == kEpochThread) {
-    gran_t ep_old = gran_epoch_add(counters + (size_t)ct * kAgCounterStride);
-    gran_epoch_wait(ep_old);
-    s_ep = (unsigned)(ep_old / (unsigned)tm) + 1u;
+    if constexpr (PS) {
+      s_ep = ps_ep;
+    } else {
+      gran_t ep_old = gran_epoch_add(counters + (size_t)ct * kAgCounterStride);
+      gran_epoch_wait(ep_old);
+      s_ep = (unsigned)(ep_old / (unsigned)tm) + 1u;
+    }
     s_bad = 0;
   }
   // the label of this thread's softmax column (t >> 4), fetched now: loaded where the softmax uses it, it was
@@ -102,12 +117,13 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
   // the GEMM (written here, each wave waited for its W2 load before its K-loop burst: a dependent memory round
   // trip in front of the GEMM, ~0.5 us of the launch per bench/stamps_fha.py)
   const int wc = t >> 4, wr = t & 15;
-  const float w2v = buf_load1<float>(
-      make_rsrc(h.W2), (t < 256 && wc < C && r0 + wr < H) ? (wc * H + r0 + wr) * 4 : kOOB);
-  const float b2v = buf_load1<float>(make_rsrc(h.b2), (t >= 256 && t < 256 + 16 && t - 256 < C) ? (t - 256) * 4 : kOOB);
+  const float w2v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+      make_rsrc(h.W2), (t < 256 && wc < C && r0 + wr < H) ? (wc * H + r0 + wr) * 4 : kOOB, 0, CP));
+  const float b2v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+      make_rsrc(h.b2), (t >= 256 && t < 256 + 16 && t - 256 < C) ? (t - 256) * 4 : kOOB, 0, CP));
   TileGeom g{H, n, f.P, r0, c0};
-  EpiSigLds epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
-  fwd_tile<NPW, 2, VEC, 4, AF, SWZ>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
+  EpiSigLdsT<CP> epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
+  fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
   // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
   // they are masked below.  w2s / b2s are complete after the barrier below.
   if (t < 256) w2s[wc][wr] = w2v;
@@ -171,7 +187,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     const float d = (cval && cls < C) ? (yh - (hit ? 1.f : 0.f)) * (float)h.scale : 0.f;
     __syncthreads();  // every lane has read zs before it is overwritten with D
     zs[cls][col2] = d;
-    if (rt == 0)
+    if (PS || rt == 0)
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, d), make_rsrc(h.D),
                                             (cval && cls < C) ? (cls * h.ldd + gcol) * 4 : kOOB, 0, 0);
     if (rt == 0 && h.loss_partial) {
@@ -190,7 +206,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
       h.loss_partial[vb] = sl;
     }
   }
-  if (s_bad) return;  // (zs holds D) a timed-out wait: nothing more is written
+  if (s_bad) return false;  // (zs holds D) a timed-out wait: nothing more is written
   // ---- 4a. (h.dw2part) this tile's dW2 partials D[:, 16 columns] . a1[tile rows, 16 columns]^T into
   // dw2part[16-column block][16 classes][H] (SplitStepArgs::dw2part, dw2_cols = 16): the weight-gradient launch's
   // dW2 role then sums cdiv(n, 16) partials per element (32 KB per 16-row tile at n = 800) instead of pulling D and
@@ -270,6 +286,7 @@ __device__ __forceinline__ void fha_body(const SplitStepArgs& f, const HeadArgs&
     __syncthreads();
     stamp(3);
   }
+  return true;
 }
 
 }  // namespace cme

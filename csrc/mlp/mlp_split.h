@@ -223,6 +223,38 @@ int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long lo
                      hipStream_t s);
 void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s);
 
+// The XCD-local step pipeline (xstep.hip): every step of a native step-loop plan (MlpStep::run_steps) in ONE
+// persistent launch -- row tile rt's forward + head, dW1 tiles and W2 rows on XCD rt, two XCD-local barriers per step,
+// the z2 all-gather the only cross-XCD hand-off.  `a` / `h` are the plan's step as the two-launch form would run it
+// (fragment-ordered W1, pixels and dZ1, the head's dW2 partials, fused SGD; their pixel / label pointers are
+// re-based per step from the plan's bases).
+struct XStepPlan {
+  int64_t gstart0 = 0, B = 0, shard_off = 0, N_end = 0;  // MlpStep::run_steps's walk over the dataset
+  int count = 0;
+  const uint8_t* X0 = nullptr;   // row-major pixels [N][P]
+  const uint8_t* XT0 = nullptr;  // feature-major pixels [P + 1][ldxt] (the all-ones row last)
+  const uint8_t* Xs0 = nullptr;  // fragment-ordered pixels (mma_tile.h xs_off), xs_tile bytes per 16 samples
+  const int* lab0 = nullptr;
+  int64_t xs_tile = 0;
+  unsigned ep0 = 1;        // the first step's granule tag; step s uses ep0 + s (tags never repeat over a buffer's life)
+  unsigned launch = 0;     // launches so far: control bank launch & 1
+  unsigned long long* gran = nullptr;  // z2 partial granules [2 step parities][32][8][16][32]
+  unsigned long long* ctl = nullptr;   // [2 banks][8 XCDs][64] ticket / barrier words, zeroed once at allocation
+  float* Dx = nullptr;     // [8 XCDs][16][ld]: each XCD's copy of D (its role workgroup's db2 reads it)
+  float* b2x = nullptr;    // [8 XCDs][16]: each XCD's copy of b2 (updated in the same order on every XCD)
+  int* err = nullptr;      // the sticky timed-out word (MlpEngine.ag_err)
+  int nw = 0, npf = 0;     // workers per XCD (mlp_xstep_workers), prefetch workgroups per XCD
+  int pf_mode = 0;         // the workers' own L2 prefetch during the z2 all-gather wait: bit0 this step's dW1 pixels
+                           // (XT), bit1 the next step's forward pixels (fragment-ordered X)
+  unsigned long long* stamps = nullptr;  // diagnostics: [stamp_steps][8][32][4] s_memrealtime per workgroup
+  int stamp_steps = 0;
+};
+bool mlp_xstep_ok(const SplitStepArgs& a, const HeadArgs& h);
+int mlp_xstep_workers(const SplitStepArgs& a);
+void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hipStream_t s);
+constexpr int64_t kXstepGranules = 2 * 32 * 8 * 16 * 32;
+constexpr int64_t kXstepCtlWords = 2 * 8 * 64;
+
 // planes[p][i] for i < n: exact np-way bf16 split of W[i] (np = 1: plain rounding).
 void mlp_split_planes(const float* W, void* planes, int64_t n, int np, hipStream_t s);
 // params[i] -= lr * grads[i]; then refresh the W1 planes (first w1_count params).

@@ -12,26 +12,17 @@
 #include "g64_gemm.h"
 #include "mma_tile.h"
 #include "fwd_tile.h"
+#include "wgrad_epi.h"
 
 namespace cme {
 
 namespace {
 
 using bf16 = __hip_bfloat16;
+using namespace wg;  // (wgrad_epi.h: split_store, kXfSys, ag_err_load, poisoned, xf_store, row_sum, EpiW1, EpiW2)
 
 __device__ __forceinline__ float sigm(float x) { return sigmoid_f32(x); }  // (head_math.h)
 
-// exact np-way split of an fp32 value into bf16 planes (np = 1: plain rounding)
-template <int NP>
-__device__ __forceinline__ void split_store(float v, bf16* base, size_t plane_stride, size_t idx) {
-  float r = v;
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const bf16 h = __float2bfloat16(r);
-    base[p * plane_stride + idx] = h;
-    r -= __bfloat162float(h);
-  }
-}
 
 // Kernel A1 (tiled): a1 = sigmoid(W1 X + b1) on 16x32 tiles, K split over 8 waves, W1 as fp32 split in
 // registers or NPW exact bf16 planes; with the separate head kernel where the fused forward + head launch does
@@ -69,16 +60,8 @@ __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a,
 // system-scope release flag store into every peer's slot [tile][rank]; bounded wait for every peer's
 // flag; rank-order sum with system-coherent loads (bit-identical on every rank).  Double
 // buffering + per-tile epochs: half e&1 of a tile is rewritten only after every peer passed e-1.
-constexpr int kXfSys = 1 | 16;  // cache policy sc0 | sc1: system coherent
 constexpr uint64_t kXfWaitTicks = kPeerWaitUs * kTicksPerUs;  // 2 s of wall time (hip_common.h)
 
-// The forward + head launch of this step timed out (SplitStepArgs::ag_err): the word is loaded (a vector
-// atomic load from L2) BEFORE the K loop, like the epilogue's other operands, and tested only by the epilogue
-// (poisoned()), so its latency hides behind the loop.
-__device__ __forceinline__ int ag_err_load(const int* e) {
-  return e ? __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-}
-__device__ __forceinline__ bool poisoned(int v) { return __builtin_amdgcn_readfirstlane(v) != 0; }
 
 // sgd = 0: the dW1 launch marks the gradient bucket's status element (one lane of workgroup 0, after its
 // epilogue): 1.f when this rank's step is untrusted
@@ -86,9 +69,6 @@ __device__ __forceinline__ void mark_status(const SplitStepArgs& a, int err) {
   if (a.gstatus && blockIdx.x == 0 && threadIdx.x == 0) *a.gstatus = poisoned(err) ? 1.f : 0.f;
 }
 
-__device__ __forceinline__ void xf_store(float* base, int64_t idx, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), make_rsrc(base), (int)(idx * 4), 0, kXfSys);
-}
 
 __device__ __forceinline__ float xf_load(const void* base, int64_t idx) {
   const auto w = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(base), (int)(idx * 4), 0, kXfSys);
@@ -265,109 +245,8 @@ __device__ __forceinline__ bool xp_exchange(const XgmiFuse& x, int tile, uint32_
 // ======================================================================
 constexpr int kWMB = 1, kWNB = 2, kWKS = 8, kWT = 64 * kWKS;
 
-// this lane's share of sum(src[0:n]) (combine with wave_sum)
-__device__ __forceinline__ float row_sum(const float* src, int n, int lane) {
-  const __amdgpu_buffer_rsrc_t rs = make_rsrc(src);
-  float s = 0.f;
-  for (int j0 = 0; j0 < n; j0 += 64 * 16) {
-    float v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int j = j0 + u * 64 + lane;
-      v[u] = buf_load1<float>(rs, j < n ? j * 4 : kOOB);
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) s += v[u];
-  }
-  return s;
-}
 
-struct EpiW2 {
-  float* W2;
-  float* gW2;
-  int H, sgd;
-  int sys;  // gradients into a peer-visible IPC buffer (write-through)
-  float reg, lr;
-  float pre[kEpiMaxQ];
-  const int* ag_err;  // the step's forward timed out: no update (the gradient goes to gW2, unused)
-  int perr = 0;
-  // sys == 2 (the push form): gradient / current weight into LDS xs / xo[class * 16 + column - n0]
-  float *xs = nullptr, *xo = nullptr;
-  int n0 = 0;
-  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
-    pre[q] = buf_load1<float>(make_rsrc(W2), ok ? (row * H + col) * 4 : kOOB);
-    if (q == 0) perr = ag_err_load(ag_err);
-  }
-  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
-    const size_t i = (size_t)row * H + col;
-    const float w = pre[q];
-    const float g = v + reg * w;
-    if (sgd && !poisoned(perr)) W2[i] = w - lr * g;
-    else if (sys == 2) {
-      xs[row * 16 + col - n0] = g;
-      xo[row * 16 + col - n0] = w;
-    }
-    else if (sys) xf_store(gW2, (int64_t)i, g);
-    else gW2[i] = g;
-  }
-};
-
-struct EpiW1 {
-  float* W1;
-  float* gW1;
-  bf16* W1p;
-  size_t plane;  // H*P
-  int P, sgd, npw;
-  float reg, lr, xscale;
-  float pre[kEpiMaxQ];
-  float* b1;
-  float* gb1;
-  int sys;  // gradients into a peer-visible IPC buffer (write-through)
-  const int* ag_err;  // the step's forward timed out: no update (the gradient goes to gW1, unused)
-  int perr = 0;
-  // sys == 2 (the push form): the gradient into LDS xs[(row - m0) * 32 + col - n0] and the current weight (or b1)
-  // into xo
-  float *xs = nullptr, *xo = nullptr;
-  int m0 = 0, n0 = 0;
-  float* W1s = nullptr;  // the fragment-ordered copy the forward reads (SplitStepArgs::W1s): updated with W1
-  __device__ __forceinline__ void prefetch(int q, int row, int col, bool ok) {
-    // (the all-ones feature column P: b1[row], so its update is not a dependent load after the K loop)
-    if (col == P) pre[q] = buf_load1<float>(make_rsrc(b1), ok ? row * 4 : kOOB);
-    else pre[q] = buf_load1<float>(make_rsrc(W1), (ok && col < P) ? (row * P + col) * 4 : kOOB);
-    if (q == 0) perr = ag_err_load(ag_err);
-  }
-  __device__ __forceinline__ void operator()(int q, int row, int col, float v) {
-    const bool upd = sgd && !poisoned(perr);
-    if (col == P) {  // the all-ones feature: db1[row] (no input scale, no regulariser)
-      if (upd) b1[row] = pre[q] - lr * v;
-      else if (sys == 2) {
-        xs[(row - m0) * 32 + col - n0] = v;
-        xo[(row - m0) * 32 + col - n0] = pre[q];
-      } else if (sys) xf_store(gb1, row, v);
-      else gb1[row] = v;
-      return;
-    }
-    const size_t i = (size_t)row * P + col;
-    const float w = pre[q];
-    const float g = v * xscale + reg * w;
-    if (upd) {
-      const float nw = w - lr * g;
-      W1[i] = nw;
-      if (W1s) W1s[w1s_off(row, col, (P + 63) >> 6)] = nw;
-      if (npw == 3) split_store<3>(nw, W1p, plane, i);
-      else if (npw == 1) split_store<1>(nw, W1p, plane, i);  // (0: no forward kernel reads the planes)
-    } else if (sys == 2) {
-      xs[(row - m0) * 32 + col - n0] = g;
-      xo[(row - m0) * 32 + col - n0] = w;
-    } else if (sys) {
-      xf_store(gW1, (int64_t)i, g);
-    } else {
-      gW1[i] = g;
-    }
-  }
-};
-
-template <int FU, int PV = 32>
+template <int FU, int PV = 32, bool XPD = false>
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
                                             uint32_t* s_xf, float* xs);
 
@@ -377,8 +256,13 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
 // kernel, the single-process step's weight-gradient launch ran 0.8 us longer (rocprofv3, 784-100-10 at n = 800:
 // 5.70 -> 6.51 us on one box, profiles/r5/regression_bisect.md) for code it never executes.
 // DSWZ (AF, VEC == 3): dZ1 is read from the fragment-ordered buffer the head wrote (SplitStepArgs::dz_swz)
-template <int NPZ, int VEC, bool AF, int FU, bool DSWZ = false>
+// XPD (FU == 2 only): the diagnostics instantiation that honours SplitStepArgs::xp_dbg (bench/kbench.py's push-form
+// ablations).  Every production instantiation has XPD = false: the ablation tests fold away and the multi-GPU kernel
+// carries none of them (a runtime branch of this kind cost a launch 0.8 us, profiles/r5/regression_bisect.md).
+template <int NPZ, int VEC, bool AF, int FU, bool DSWZ = false, bool XPD = false>
 __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t1, int t1n, int t2) {
+  static_assert(!XPD || FU == 2, "the push-form ablations exist only in the push form");
+  const int xdbg = XPD ? a.xp_dbg : 0;
   __shared__ __attribute__((aligned(16))) float red[kWKS * kWMB * kWNB * 4 * 64];
   __shared__ uint32_t s_xf[2];
   // the push form's staged gradient tile, then the current values (FU = 2); otherwise xs is the upper half of
@@ -447,7 +331,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
                                                                 static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
                                                                 red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
     wstamp(1);
-    if (push && (a.xp_dbg & 16)) return;  // (diagnostics: no exchange work at all after the tile)
+    if (push && (xdbg & 16)) return;  // (diagnostics: no exchange work at all after the tile)
     if (push) {  // the owner-tile exchange: thread e holds element (e / 32, e % 32) of the tile
       const int e = threadIdx.x, row = g.m0 + e / 32, col = g.n0 + e % 32;
       const bool ok = e < 512 && row < g.M && col < g.N;
@@ -460,8 +344,8 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
       __syncthreads();  // xs / xo complete
       wstamp(4);
       float nv = ok ? xo[e] - lr * xs[e] : 0.f;
-      if (!s_xf[1] && ((a.xp_dbg & 1) || xp_exchange(*a.xf, bid, s_xf, xs, 512, ok, ok ? xo[e] : 0.f, lr, &nv, wst)) &&
-          ok && !(a.xp_dbg & 2)) {
+      if (!s_xf[1] && ((xdbg & 1) || xp_exchange(*a.xf, bid, s_xf, xs, 512, ok, ok ? xo[e] : 0.f, lr, &nv, wst)) &&
+          ok && !(xdbg & 2)) {
         if (col < a.P) {
           a.W1[i] = nv;
           if (a.w1_swz) a.W1s[w1s_off(row, col, (a.P + 63) >> 6)] = nv;
@@ -502,7 +386,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     }
     return;
   }
-  wgrad_roles<FU>(a, bid, t1, t2, red, s_xf, xs);
+  wgrad_roles<FU, 32, XPD>(a, bid, t1, t2, red, s_xf, xs);
   if (wst) {  // (no barrier: the roles' returns are not block-uniform)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wstamp(3);
@@ -514,10 +398,11 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
 // Shared by wgrad_split_kernel and the wide engines' launches (their extra workgroups).
 // PV: dW2 partial loads in flight per lane (the small launch sums cdiv(n, 16) partials: 32; the wide launches' roles,
 // which share their CUs with the GEMM tiles, sum cdiv(n, 32 or 128): 8)
-template <int FU, int PV>
+template <int FU, int PV, bool XPD>
 __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int t1, int t2, float* red,
                                             uint32_t* s_xf, float* xs) {
   const float reg = (float)a.reg, lr = (float)a.lr;
+  const int xdbg = XPD ? a.xp_dbg : 0;  // (diagnostics instantiation only: wgrad_split_kernel XPD)
   constexpr bool fused = FU > 0;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -558,7 +443,7 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
     } else {
       wsk_tile<float, 1, 1, kWKS, true, true, 0, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red, 0, a.stamps);
     }
-    if (!live || (push && (a.xp_dbg & 32))) return;  // (xp_dbg 32: diagnostics, the roles stop after the GEMM)
+    if (!live || (push && (xdbg & 32))) return;  // (xp_dbg 32: diagnostics, the roles stop after the GEMM)
     if (push) {  // the owner-tile exchange: element e < 256 is W2[e / 16][tb * 16 + e % 16]
       const int e = threadIdx.x, c = e / 16, h = tb * 16 + e % 16;
       const bool ok = e < 256 && c < a.C && h < a.H;
@@ -571,7 +456,7 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
       __syncthreads();  // xs / xo complete
       const float old = ok ? xs[kXpTile + e] : 0.f;
       float nv = ok ? old - lr * xs[e] : 0.f;  // (xp_dbg 4: diagnostics, no exchange -- world 1's own value)
-      if (!s_xf[1] && ((a.xp_dbg & 4) || xp_exchange(*a.xf, bid, s_xf, xs, 256, ok, old, lr, &nv)) && ok) a.W2[i] = nv;
+      if (!s_xf[1] && ((xdbg & 4) || xp_exchange(*a.xf, bid, s_xf, xs, 256, ok, old, lr, &nv)) && ok) a.W2[i] = nv;
       return;
     }
     if (!xf_exchange(*a.xf, bid, s_xf)) return;
@@ -612,7 +497,7 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
       }
       __syncthreads();  // xs complete
       float nv = ok ? bold - lr * xs[e] : 0.f;
-      if (!s_xf[1] && ((a.xp_dbg & 8) || xp_exchange(*a.xf, bid, s_xf, xs, a.C, ok, bold, lr, &nv)) && ok) a.b2[e] = nv;
+      if (!s_xf[1] && ((xdbg & 8) || xp_exchange(*a.xf, bid, s_xf, xs, a.C, ok, bold, lr, &nv)) && ok) a.b2[e] = nv;
       return;
     }
     if (!xf_exchange(*a.xf, bid, s_xf)) return;
@@ -1827,7 +1712,13 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   }
   CME_REQUIRE(!a.dz_swz || (af && vec == 3 && do_w1 && mlp_wgrad_dz_swz_ok(a)),
               "wgrad: the fragment-ordered dZ1 needs fp32 dZ1, 16-byte pixel pairs and pair-aligned K ranges");
-  if (a.dz_swz) {
+  if (a.xp_dbg) {  // diagnostics (bench/kbench.py xp rows): the push form's two headline shapes only
+    CME_REQUIRE(fu == 2 && vec == 3 && (a.dz_swz || (!af && a.npz == 3)),
+                "wgrad: xp_dbg ablations exist for the push form at 16-byte pixel pairs, fragment-ordered fp32 dZ1 "
+                "(n = 800) or the three dZ1 planes (n = 100)");
+    if (a.dz_swz) wgrad_split_kernel<3, 3, true, 2, true, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
+    else wgrad_split_kernel<3, 3, false, 2, false, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
+  } else if (a.dz_swz) {
     if (fu == 2) wgrad_split_kernel<3, 3, true, 2, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
     else if (fu == 1) wgrad_split_kernel<3, 3, true, 1, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
     else wgrad_split_kernel<3, 3, true, 0, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);

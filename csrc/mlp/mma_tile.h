@@ -306,8 +306,12 @@ __host__ __device__ __forceinline__ int64_t xs_off(int64_t s, int k, int npair) 
   const int lane = (w >> 4) * 16 + (int)(s & 15);
   return (((s >> 4) * npair + p) * 64 + lane) * 16 + (w & 15);
 }
+//
+// CPA (fp32 fragment-ordered A only): the A loads' cache policy -- kSc1 for an operand another workgroup of the same
+// launch rewrote since this CU last read it (the XCD-local step pipeline, xstep.hip: W1s and dZ1 are read with
+// L1-bypassing, L2-served loads; a plain load could return this CU's stale L1 line)
 template <typename T, int MB, int NB, int KS, bool AK, bool BK, int VEC, int U, int NPA = 1, typename TB = T,
-          typename TA = T, bool ASWZ = false, bool BSWZ = false, class Epi>
+          typename TA = T, bool ASWZ = false, bool BSWZ = false, int CPA = 0, class Epi>
 __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, const TB* __restrict__ B, int ldb,
                                          TileGeom g, Epi& epi,
                                          typename MmaTraits<T>::acc_t* __restrict__ red, int plane_bytes = 0,
@@ -374,6 +378,7 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
   constexpr bool AF32 = std::is_same_v<TA, float> && !std::is_same_v<T, float>;
   static_assert(!AF32 || (std::is_same_v<T, __hip_bfloat16> && NPA == 3 && AK), "fp32 A: split3 bf16, K-contiguous");
   constexpr bool BU8 = std::is_same_v<TB, uint8_t>;
+  static_assert(CPA == 0 || (AF32 && ASWZ), "an A cache policy only on the fragment-ordered fp32 A loads");
   // VEC == 3 (u8 B only): chunks go in PAIRS.  Lane group grp of chunk pair (u, u + 1) covers the 16 k
   // kp + 16 grp .. kp + 16 grp + 15 (kp = the pair's first k): chunk u takes the first 8, chunk u + 1 the
   // last 8 (the MFMA sums over its chunk, so any bijection of k onto (lane group, element) that A and B
@@ -396,8 +401,8 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
         const int kp = kc + (u & ~1) * KC;  // the pair's first k (a multiple of 64)
         const bool ok = g.m0 + c < g.M && k < kend;
         const int base = ((((g.m0 >> 4) * lda + (kp >> 6)) * 4 + 2 * (u & 1)) * 64 + lane) * 16;
-        const auto w0 = __builtin_amdgcn_raw_buffer_load_b128(rsA, ok ? base : kOOB, 0, 0);
-        const auto w1 = __builtin_amdgcn_raw_buffer_load_b128(rsA, ok ? base + 1024 : kOOB, 0, 0);
+        const auto w0 = __builtin_amdgcn_raw_buffer_load_b128(rsA, ok ? base : kOOB, 0, CPA);
+        const auto w1 = __builtin_amdgcn_raw_buffer_load_b128(rsA, ok ? base + 1024 : kOOB, 0, CPA);
         __builtin_memcpy(ar[u][0], &w0, 16);
         __builtin_memcpy(reinterpret_cast<char*>(ar[u][0]) + 16, &w1, 16);
       } else if constexpr (AF32) {

@@ -1,0 +1,318 @@
+// The XCD-local step pipeline (H <= 128, split3, one process): every step of a native step-loop plan in ONE
+// persistent launch, with no grid-wide seam anywhere.
+//
+// The two-launch step (forward + head, then weight gradient) pays at both kernel boundaries of every step: the XCDs
+// start a launch 0.6-1.5 us apart and every z2 all-gather waits for the last one (profiles/r5/stamps_fha_per_xcd.jsonl),
+// and whatever the previous launch WROTE -- the updated W1, dZ1, the dW2 partials -- is read back at the die-level
+// cache's rate, 2.44 us against 0.92 us for an L2-resident 2 MiB (docs/PERFORMANCE.md "Data written by one kernel is
+// cold for the next").  Under the XCD-row placement, row tile rt of W1 is both forward-read and updated on XCD rt,
+// dZ1 rows rt are written and read there, and so are W2[:, rt rows] and their dW2 partials.  The only cross-XCD
+// dependency of a step is the z2 all-gather of the head, already an in-launch hand-off.  So here:
+//
+//   * every workgroup reads its XCD from HW_REG_XCC_ID and takes a ticket on that XCD's counter: row tile rt = XCD,
+//     slot j = ticket (placement decides only which XCD serves which row tile: every hand-off below is between
+//     workgroups that read the same XCC id, i.e. that share one L2);
+//   * slot j < nw is a worker: the forward + head of tile (rt, column tile j) -- fha_body, the two-launch forward's
+//     own body, in its PS form: z2 partials out as data-tagged granules (tag = the plan's step number, slab by step
+//     parity), the all-gather, softmax, D, the dW2 partials and dZ1 -- then, after the XCD's first barrier, the dW1
+//     tile (rt, feature tile j) over the whole batch with the fused reg + SGD update of W1 / W1s / b1 (EpiW1, the
+//     two-launch epilogue);
+//   * slot nw is the XCD's role workgroup: after the first barrier it sums the dW2 partials of W2[:, rt rows] (EpiW2)
+//     and reduces D into db2 -- redundantly on every XCD, in the same order, into that XCD's own copy of b2 (XCD 0
+//     also writes the master b2 at the plan's last step);
+//   * slots past nw pull the pixels the XCD reads next into its L2 (l2_touch: this step's XT, the next step's
+//     fragment-ordered X).
+//
+// The two barriers per step are XCD-local: each participant drains its stores (s_waitcnt vmcnt(0) + workgroup
+// barrier), adds one to its XCD's counter (an agent-scope atomic) and lane 0 polls it with sc1 loads; every read of
+// data another workgroup of the launch wrote goes through sc1 (L1-bypassing, L2-served) loads, so a CU never reuses a
+// stale L1 line, and the producer's plain stores stay in the XCD's L2 (bench/micro/xcd_barrier.hip prices the
+// barrier at 0.64-0.83 us and the same-XCD read-back at 1.1 us for 50 KB per workgroup, profiles/r6/).  Arithmetic
+// and summation orders are those of the two-launch step, so the parameters are bitwise equal to it
+// (tests/test_gpu_xstep.py).
+//
+// Failure semantics: a z2 hand-off wait that outlasts SplitStepArgs::ag_wait_us sets *err and makes its workgroup
+// arrive "bad" at the first barrier; every XCD's workgroup of that column tile waits for the same missing granule,
+// so every XCD stops there and the step applies nothing (the launch ends; the steps before it stay applied).  A
+// barrier wait that times out (a workgroup that never arrives) sets *err and stops the launch.
+// Reference: the hot loop of fpcode/neural_network.cpp:449-555 (forward/backward :281-394) -- here one launch.
+#include "mlp_split.h"
+#include "mlp_kernels.h"
+
+#include "fha_body.h"
+#include "granule.h"
+#include "l2_touch.h"
+#include "mma_tile.h"
+#include "wgrad_epi.h"
+
+namespace cme {
+
+namespace {
+
+using bf16 = __hip_bfloat16;
+using namespace wg;
+
+constexpr int kXsWgsPerXcd = 32;                 // 256 CUs / 8 XCDs: one workgroup per CU
+constexpr unsigned long long kXsBad = 1ull << 40;  // a barrier arrival that stops the XCD (added to the count)
+constexpr int kXsCols = 32;                      // the forward's column tile (fha_body)
+
+inline int xs_cdiv(int a, int b) { return (a + b - 1) / b; }
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 15u;
+}
+
+// control words: [2 banks][8 XCDs][64] uint64 -- ticket at [0], barrier counter at [32] (separate 256-byte lines)
+__device__ __forceinline__ unsigned long long* xs_ticket(unsigned long long* ctl, int bank, int x) {
+  return ctl + ((size_t)bank * 8 + x) * 64;
+}
+__device__ __forceinline__ unsigned long long* xs_counter(unsigned long long* ctl, int bank, int x) {
+  return ctl + ((size_t)bank * 8 + x) * 64 + 32;
+}
+
+// XCD-local barrier: this workgroup's stores are drained by every wave, then one agent-scope add (1, or 1 + kXsBad
+// when its step is bad) and lane 0 polls the counter with sc1 loads until `target` arrivals.  False (block-uniform)
+// when the XCD must stop: a bad arrival, or a wait past `limit_us` (then *err is set and kXsBad added, so every other
+// waiter -- the prefetch workgroups too -- stops as well).
+__device__ __forceinline__ bool xs_barrier(unsigned long long* cnt, unsigned long long target, bool bad, int* err,
+                                           uint32_t limit_us, int* s_stop) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(cnt, bad ? 1ull + kXsBad : 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t t0 = 0;
+    const uint64_t limit = (uint64_t)limit_us * kTicksPerUs;
+    for (uint32_t pass = 1;; ++pass) {
+      const unsigned long long v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v >= kXsBad) {
+        *s_stop = 1;
+        break;
+      }
+      if (v >= target) break;
+      if (pass == 1) t0 = wall_ticks();
+      else if ((pass & 7) == 0 && wall_ticks() - t0 > limit) {
+        atomicExch(err, 1);
+        __hip_atomic_fetch_add(cnt, kXsBad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_stop = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  return *s_stop == 0;
+}
+
+// The samples of a run_steps plan's steps: consecutive global batches of B from gstart0, wrapping to 0 when one
+// would pass N_end (MlpStep::run_steps), this rank's shard at +shard_off.  off() is the current step's first sample,
+// next() the following step's; advance() moves on by one step.
+struct XsWalk {
+  int64_t gs;
+  const XStepPlan& p;
+  __device__ explicit XsWalk(const XStepPlan& q) : gs(q.gstart0 + q.B > q.N_end ? 0 : q.gstart0), p(q) {}
+  __device__ int64_t off() const { return gs + p.shard_off; }
+  __device__ int64_t next() const { return (gs + 2 * p.B > p.N_end ? 0 : gs + p.B) + p.shard_off; }
+  __device__ void advance() { gs = gs + 2 * p.B > p.N_end ? 0 : gs + p.B; }
+};
+
+__global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h, XStepPlan p, int tm, int tn,
+                                                    int t1n) {
+  __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];  // both GEMM tiles' K reductions
+  __shared__ int s_slot, s_stop;
+  __shared__ unsigned s_x;
+  const int t = threadIdx.x;
+  const int bank = (int)(p.launch & 1u);
+  if (t == 0) {
+    const unsigned x = xcc_id();
+    int slot = -1;
+    if (x < 8) {
+      slot = (int)__hip_atomic_fetch_add(xs_ticket(p.ctl, bank, (int)x), 1ull, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+      if (slot == 0) {  // the other bank, for the next launch (the previous launch that used it has ended)
+        __hip_atomic_store(xs_ticket(p.ctl, bank ^ 1, (int)x), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(xs_counter(p.ctl, bank ^ 1, (int)x), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    s_x = x;
+    s_slot = slot;
+    s_stop = 0;
+  }
+  __syncthreads();
+  const int x = (int)s_x, slot = s_slot;
+  if (x >= tm || slot < 0 || slot > p.nw + p.npf) return;  // (uniform) XCDs past the last row tile, spare CUs
+  unsigned long long* cnt = xs_counter(p.ctl, bank, x);
+  const unsigned long long np = (unsigned long long)p.nw + 1;  // barrier participants: the workers + the role
+  const uint32_t limit_us = (uint32_t)a.ag_wait_us;
+  const int n = a.n, ld = a.ld;
+  const float reg = (float)a.reg, lr = (float)a.lr;
+  unsigned long long* st = p.stamps;  // diagnostics: [step][8][32][4]
+  auto stamp = [&](int s, int i) {
+    if (st && t == 0 && s < p.stamp_steps)
+      st[(((size_t)s * 8 + x) * kXsWgsPerXcd + slot) * 4 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+
+  if (slot > p.nw) {  // ---- prefetch: this step's XT, then the next step's fragment-ordered pixels, into this L2
+    const int part = slot - p.nw - 1;
+    XsWalk w(p);
+    for (int s = 0; s < p.count; ++s, w.advance()) {
+      if (t == 0) {  // the step has started on this XCD: its previous step's second barrier is complete
+        const unsigned long long target = 2ull * (unsigned long long)s * np;
+        const uint64_t t0 = wall_ticks();
+        for (;;) {
+          const unsigned long long v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (v >= kXsBad || (wall_ticks() - t0 > (uint64_t)limit_us * kTicksPerUs)) {
+            s_stop = 1;
+            break;
+          }
+          if (v >= target) break;
+          __builtin_amdgcn_s_sleep(8);
+        }
+      }
+      __syncthreads();
+      if (s_stop) return;
+      l2_touch(p.XT0, w.off(), a.P + a.bias_col, a.ldxt, n, part, p.npf, reinterpret_cast<char*>(red));
+      if (s + 1 < p.count) {
+        const int64_t nx = w.next();
+        l2_touch(p.Xs0, nx / 16 * p.xs_tile, 1, 0, (int64_t)((n + 15) / 16) * p.xs_tile, part, p.npf,
+                 reinterpret_cast<char*>(red));
+      }
+      __syncthreads();
+    }
+    return;
+  }
+
+  XsWalk w(p);
+  for (int s = 0; s < p.count; ++s, w.advance()) {
+    const int64_t off = w.off();
+    stamp(s, 0);
+    // ---- forward + head of tile (x, slot)
+    bool bad = false;
+    if (slot < p.nw && slot < tn) {
+      SplitStepArgs f = a;
+      f.X = p.X0 + off * a.P;
+      f.Xs = p.Xs0 + off / 16 * p.xs_tile;
+      f.XT = p.XT0 + off;
+      HeadArgs hh = h;
+      hh.labels = p.lab0 + off;
+      hh.D = p.Dx + (size_t)x * 16 * ld;  // this XCD's copy of D (the role's db2 reads it)
+      hh.b2 = s == 0 ? (const void*)a.b2 : (const void*)(p.b2x + x * 16);
+      gran_t* slabs = p.gran + (size_t)(s & 1) * 32 * 8 * 16 * kXsCols;
+      bad = !fha_body<3, 3, true, 7, true>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red, x, slot,
+                                           p.ep0 + (unsigned)s);
+    }
+    stamp(s, 1);
+    if (!xs_barrier(cnt, (2ull * s + 1) * np, bad, p.err, limit_us, &s_stop)) return;
+    stamp(s, 2);
+    if (slot < p.nw) {
+      if (slot < t1n) {  // ---- dW1 tile (x, slot) over the whole batch + reg + SGD (W1, W1s, b1)
+        TileGeom g{a.H, a.P + a.bias_col, n, x * 16, slot * 32};
+        EpiW1 epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, 1, 0, reg, lr, a.xscale, {}, a.b1,
+                  a.gb1, 0, nullptr};
+        epi.W1s = a.W1s;
+        wsk_tile<bf16, 1, 2, 8, true, true, 3, 4, 3, uint8_t, float, true, false, kSc1>(
+            a.dZ1, (ld + 63) / 64, static_cast<const uint8_t*>(p.XT0) + off, a.ldxt, g, epi, red, 0, nullptr);
+      }
+    } else {  // ---- the role: W2[:, x rows] from the dW2 partials and db2 into this XCD's b2 copy, side by side
+      // (waves [0, dw): dW2, one element per lane; waves [dw, 8): db2, up to 4 classes per wave with every row's
+      // loads in flight at once -- one after the other they were this workgroup's 4.2 us critical path,
+      // profiles/r6/xstep_ab_r6a.jsonl)
+      const int lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+      const int dw = (16 * a.C + 63) / 64;
+      if (wv < dw) {
+        const int nct = (n + 15) / 16, e = t, c = e >> 4, hr = x * 16 + (e & 15);
+        const bool ok = c < a.C && hr < a.H;
+        EpiW2 epi{a.W2, a.gW2, a.H, 1, 0, reg, lr, {}, nullptr};
+        epi.prefetch(0, c, hr, ok);
+        const __amdgpu_buffer_rsrc_t rp = make_rsrc(a.dw2part);
+        float v = 0.f;
+        for (int k0 = 0; k0 < nct; k0 += 32) {  // (the two-launch role's summation order: k ascending)
+          float pv[32];
+#pragma unroll
+          for (int u = 0; u < 32; ++u)
+            pv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rp, (ok && k0 + u < nct) ? (((k0 + u) * 16 + c) * a.H + hr) * 4 : kOOB,
+                                                  0, kSc1));
+#pragma unroll
+          for (int u = 0; u < 32; ++u) v += pv[u];
+        }
+        if (ok) epi(0, c, hr, v);
+      } else {
+        // db2 as the two-launch step's bias-row workgroups compute it (row_sum's lane-strided order, then wave_sum)
+        const int nd = 8 - dw, c0 = wv - dw;
+        const float* b2src = s == 0 ? a.b2 : p.b2x + x * 16;
+        const __amdgpu_buffer_rsrc_t rb = make_rsrc(b2src);
+        float bpre[4], acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cc = c0 + k * nd;
+          bpre[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, cc < a.C ? cc * 4 : kOOB, 0,
+                                                                                   kSc1));
+        }
+        for (int j0 = 0; j0 < n; j0 += 64 * 16) {
+          float v[4][16];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int cc = c0 + k * nd;
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.Dx + ((size_t)x * 16 + (cc < a.C ? cc : 0)) * ld);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int jj = j0 + u * 64 + lane;
+              v[k][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                      rs, (cc < a.C && jj < n) ? jj * 4 : kOOB, 0, kSc1));
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int u = 0; u < 16; ++u) acc[k] += v[k][u];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cc = c0 + k * nd;
+          const float sum = wave_sum(acc[k]);
+          if (cc < a.C && lane == 0) {
+            const float nb = bpre[k] - lr * sum;
+            p.b2x[x * 16 + cc] = nb;
+            if (x == 0 && s + 1 == p.count) a.b2[cc] = nb;
+          }
+        }
+      }
+    }
+    stamp(s, 3);
+    if (!xs_barrier(cnt, (2ull * s + 2) * np, false, p.err, limit_us, &s_stop)) return;
+  }
+}
+
+}  // namespace
+
+bool mlp_xstep_ok(const SplitStepArgs& a, const HeadArgs& h) {
+  const int tm = xs_cdiv(a.H, 16), tn = xs_cdiv(a.n, kXsCols), t1n = xs_cdiv(a.P + a.bias_col, 32);
+  const int nw = std::max(tn, t1n);
+  return a.H <= 128 && tm <= 8 && a.C <= 16 && a.bias_col && a.sgd == 1 && a.xf_world == 0 && a.npw == 3 &&
+         a.npz == 3 && a.w1_swz && a.W1s && a.x_swz && a.Xs && a.dz_swz == 1 && a.dZ1 && h.dz_swz == 1 &&
+         h.dZ1 == a.dZ1 && !h.dZ1_planes && a.dw2part && h.dw2part == a.dw2part && a.dw2_cols == 16 && !h.a1 &&
+         !h.loss_partial && a.n > 0 && a.n % 16 == 0 && nw + 1 <= kXsWgsPerXcd &&
+         device_cu_count() == 8 * kXsWgsPerXcd && mlp_wgrad_dz_swz_ok(a) &&
+         (int64_t)a.P * a.ldxt < (int64_t)kOOB && (int64_t)xs_cdiv(a.H, 16) * 16 * a.ld < (int64_t)kOOB / 4;
+}
+
+int mlp_xstep_workers(const SplitStepArgs& a) { return std::max(xs_cdiv(a.n, kXsCols), xs_cdiv(a.P + a.bias_col, 32)); }
+
+void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hipStream_t s) {
+  if (p.count <= 0) return;
+  CME_REQUIRE(mlp_xstep_ok(a, h), "xstep: the plan's step is not the XCD-local pipeline's shape");
+  const int tm = xs_cdiv(a.H, 16), tn = xs_cdiv(a.n, kXsCols), t1n = xs_cdiv(a.P + a.bias_col, 32);
+  CME_REQUIRE(p.nw == mlp_xstep_workers(a) && p.npf >= 0 && p.nw + 1 + p.npf <= kXsWgsPerXcd,
+              "xstep: workers + role + prefetch workgroups must fit one XCD's CUs");
+  CME_REQUIRE(p.gran && p.ctl && p.Dx && p.b2x && p.err && p.X0 && p.XT0 && p.Xs0 && p.lab0 && p.xs_tile > 0,
+              "xstep: scratch buffers missing");
+  CME_REQUIRE(p.gstart0 % 16 == 0 && p.B % 16 == 0 && p.shard_off % 16 == 0 && p.B >= a.n && p.N_end >= p.B,
+              "xstep: every step must start a 16-sample tile of the fragment-ordered pixels");
+  CME_REQUIRE(a.ld >= a.n && a.ld % 16 == 0, "xstep: activation pitch");
+  xstep_kernel<<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  CME_LAUNCH_CHECK(s);
+}
+
+}  // namespace cme

@@ -1,0 +1,125 @@
+"""The XCD-local step pipeline (csrc/mlp/xstep.hip: a whole native-loop plan in ONE persistent launch, XCD-local
+barriers, the z2 all-gather the only cross-XCD hand-off) against the two-launch step it replaces: parameters
+BITWISE equal over whole epochs (the same arithmetic and summation orders), across launches (the control banks
+alternate, the granule tags continue), mixed with two-launch steps, and a forced hand-off timeout that applies
+nothing.  The reference's hot loop: fpcode/neural_network.cpp:449-555."""
+import pytest
+import torch
+
+from cme213_sp18_amd.models.mlp import NeuralNetwork
+from cme213_sp18_amd.parallel.engine import MlpEngine
+from cme213_sp18_amd.utils.data import synthetic_mnist
+
+pytestmark = pytest.mark.gpu
+
+LR, REG = 0.05, 1e-4
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _pair(H, n, N, seed):
+    """Two engines with the same weights and data: [0] the two-launch step (xstep = 0), [1] the pipeline (auto)."""
+    x, y = synthetic_mnist(N, seed=seed)
+    nn = NeuralNetwork([784, H, 10])
+    out = []
+    for xs in (0, -1):
+        e = MlpEngine(nn.H, "f32", max_cols=n, device="cuda", path="split3")
+        e.set_params(*nn.params)
+        e.load_dataset(x, y)
+        e.set_store_a1(False)
+        e._hip_step().xstep = xs
+        out.append(e)
+    return out
+
+
+def _plan(e, g0, count, n, N):
+    e._hip_step().run_steps(g0, count, n, 0, n, N, 1.0 / n, REG, LR, 1, _stream())
+
+
+@pytest.mark.parametrize("H,n", [(100, 800), (128, 800), (64, 960), (100, 784)])
+def test_xstep_is_bitwise_the_two_launch_step(H, n):
+    """Two epochs (with the wrap to sample 0) as one plan, then plans from other start batches (the other control
+    bank, then the first again), then a two-launch step and a plan again: parameters bitwise equal throughout."""
+    N = 5 * n + 48  # (a partial batch at the end: the walk wraps before it)
+    engines = _pair(H, n, N, seed=H + n)
+
+    def both(fn):
+        for e in engines:
+            fn(e)
+        torch.cuda.synchronize()
+        assert torch.equal(engines[0].params, engines[1].params)
+
+    both(lambda e: _plan(e, 0, 2 * (N // n), n, N))
+    assert engines[1]._hip_step().xstep_used == 1, engines[1]._hip_step().xstep_reason
+    assert engines[0]._hip_step().xstep_used == 0
+    both(lambda e: _plan(e, 2 * n, 3, n, N))
+    both(lambda e: _plan(e, n, 7, n, N))
+    both(lambda e: e.run(16, n, 1.0 / n, REG, LR, sgd=True))  # a two-launch step between plans
+    both(lambda e: _plan(e, 3 * n, 1, n, N))
+    both(lambda e: _plan(e, 0, 4, n, N))
+    assert torch.equal(engines[0].dz1()[:, :n], engines[1].dz1()[:, :n])
+    for e in engines:
+        assert not e.kernel_error()
+
+
+def test_xstep_falls_back_where_it_does_not_apply():
+    """Plans the pipeline does not take run the two-launch loop (bitwise the same as xstep = 0): steps off the
+    16-sample grid, a batch below the head's dW2 threshold; xstep = 1 (required) then raises."""
+    n, N = 800, 3 * 800 + 48
+    engines = _pair(100, n, N, seed=7)
+    for e in engines:
+        _plan(e, 8, 2, n, N)  # (first sample 8: off the fragment-ordered pixels' 16-sample grid)
+    torch.cuda.synchronize()
+    assert engines[1]._hip_step().xstep_used == 0
+    assert "16-sample grid" in engines[1]._hip_step().xstep_reason
+    assert torch.equal(engines[0].params, engines[1].params)
+    st = engines[1]._hip_step()
+    st.xstep = 1
+    with pytest.raises(ValueError, match="xstep"):
+        _plan(engines[1], 8, 1, n, N)
+    small = _pair(100, 400, 2000, seed=8)
+    for e in small:
+        _plan(e, 0, 3, 400, 2000)
+    torch.cuda.synchronize()
+    assert small[1]._hip_step().xstep_used == 0
+    assert "dW2 partials" in small[1]._hip_step().xstep_reason
+    assert torch.equal(small[0].params, small[1].params)
+
+
+def test_xstep_prefetch_workgroups_do_not_change_results():
+    """The prefetch workgroups (MlpStep.xstep_pf) only move bytes into L2: 0 and 6 per XCD give the same bits."""
+    n, N = 800, 4 * 800
+    engines = _pair(100, n, N, seed=11)
+    engines[0]._hip_step().xstep = -1
+    engines[0]._hip_step().xstep_pf = 0
+    for e in engines:
+        _plan(e, 0, 9, n, N)
+    torch.cuda.synchronize()
+    assert all(e._hip_step().xstep_used for e in engines), [e._hip_step().xstep_reason for e in engines]
+    assert torch.equal(engines[0].params, engines[1].params)
+
+
+def test_xstep_handoff_timeout_applies_nothing():
+    """A z2 hand-off that never completes (row tile 3 of column tile 0 withholds its granules): every XCD's
+    workgroup of that column tile times out, arrives 'bad' at the first barrier, and the launch stops before any
+    update -- the parameters are bitwise those before the plan and the sticky error word is set."""
+    n, N = 800, 4 * 800
+    x, y = synthetic_mnist(N, seed=3)
+    nn = NeuralNetwork([784, 100, 10])
+    e = MlpEngine(nn.H, "f32", max_cols=n, device="cuda", path="split3")
+    e.set_params(*nn.params)
+    e.load_dataset(x, y)
+    e.set_store_a1(False)
+    _plan(e, 0, 2, n, N)  # a good plan first (launch 0)
+    torch.cuda.synchronize()
+    assert e._hip_step().xstep_used == 1, e._hip_step().xstep_reason
+    assert not e.kernel_error()
+    before = e.params.clone()
+    e.inject_handoff_timeout(row_tile=3, wait_us=2000)
+    _plan(e, 0, 3, n, N)
+    torch.cuda.synchronize()
+    assert e._hip_step().xstep_used == 1
+    assert e.kernel_error()
+    assert torch.equal(e.params, before)

@@ -121,3 +121,68 @@ def test_fused_form_policy_pushes_from_four_ranks():
     assert T.auto_fused_form(2, s) == "pull"
     assert T.auto_fused_form(4, s) == "push" and T.auto_fused_form(8, s) == "push"
     assert T.fused_exchange_us(8, s, "push") < T.fused_exchange_us(8, s, "pull")
+
+
+def test_push_form_falls_back_to_pull_then_rccl():
+    """An owner-tile push run far off its probe is re-timed on the one-shot pull first; when that is off too, on
+    RCCL; every timing is in the record's chain."""
+    order = []
+
+    def pull():
+        order.append("pull")
+        return fake_dp(500.0, "xgmi-fused"), 40.0
+
+    def rccl():
+        order.append("rccl")
+        return fake_dp(60.0, "nccl"), 55.0
+
+    res = bench.guard_probe(fake_dp(360.0, "xgmi-push"), STEPS, 36.0, [pull, rccl])
+    assert order == ["pull", "rccl"]
+    assert res["ok"] and res["config"]["allreduce"] == "nccl"
+    g = res["config"]["probe_guard"]
+    assert g["first"]["what"] == "xgmi-push"
+    assert [c["what"] for c in g["chain"]] == ["xgmi-fused", "nccl"]
+    # the pull agrees with its probe: RCCL is never timed
+    order.clear()
+    res = bench.guard_probe(fake_dp(360.0, "xgmi-push"), STEPS, 36.0, [lambda: (fake_dp(41.0, "xgmi-fused"), 40.0),
+                                                                       rccl])
+    assert order == [] and res["ok"] and res["config"]["allreduce"] == "xgmi-fused"
+
+
+def test_fallback_chain_order_by_implementation():
+    """bench.dp_fallbacks: push -> pull -> RCCL; any other xGMI form -> RCCL; RCCL and one rank -> nothing (the
+    chain is built, nothing is run)."""
+    from types import SimpleNamespace as NS
+
+    class Comm:
+        name = "nccl"
+
+    ctx = NS(R=4, comm=Comm(), a=NS(warmup=1, tune_steps=1))
+    assert [f.mode for f in bench.dp_fallbacks(ctx, 800, "xgmi-push", {})] == ["xgmi", "rccl"]
+    assert [f.mode for f in bench.dp_fallbacks(ctx, 800, "xgmi-fused", {})] == ["rccl"]
+    assert [f.mode for f in bench.dp_fallbacks(ctx, 800, "xgmi-2shot", {})] == ["rccl"]
+    assert bench.dp_fallbacks(ctx, 800, "nccl", {}) == []
+    assert bench.dp_fallbacks(NS(R=1, comm=Comm(), a=ctx.a), 800, "xgmi-push", {}) == []
+
+
+def test_retime_keeps_the_inner_guard_record():
+    inner = {"consistent": True, "timed_us_per_step": 150.0}
+
+    def retime():
+        r = fake_dp(150.0, "nccl")
+        r["config"]["probe_guard"] = dict(inner)
+        return r, 140.0
+    tp = {"ok": True, "dt": 1000e-6 * STEPS, "images": 0, "global_batch": 6400, "per_gpu_batch": 6400,
+          "parallelism": "tp4", "checks": {}, "config": {"allreduce": "xgmi"}}
+    res = bench.guard_probe(tp, STEPS, 119.0, retime)
+    assert res["config"]["probe_guard"]["inner"] == inner
+
+
+def test_cost_model_fit_is_bounded():
+    """measure_cost_model's fit: a noisy (non-positive or absurd) slope keeps the planning constants."""
+    plan = T.CostModel()
+    fixed, gbps = T._fit_bounded(10.0, 30.0, 4 * (1 << 20), plan.kernel_us, plan.link_gbps)
+    assert fixed == 10.0 and abs(gbps - 4 * (1 << 20) / 20.0 / 1e3) < 1e-9
+    assert T._fit_bounded(10.0, 9.0, 4e6, plan.kernel_us, plan.link_gbps) == (None, None)       # slope < 0
+    assert T._fit_bounded(10.0, 10.0001, 4e6, plan.kernel_us, plan.link_gbps) == (None, None)   # 40 TB/s
+    assert T._fit_bounded(1e4, 2e4, 4e6, plan.kernel_us, plan.link_gbps) == (None, None)        # 10 ms fixed
