@@ -3,11 +3,11 @@
 
 For each batch size: the walking native loop (``MlpStep.run_steps`` over consecutive batches, as bench.py's timed
 region runs it) with ``xstep = 0`` (two launches per step) and ``xstep = -1`` (the whole plan in one persistent
-launch; prefetch workgroups per XCD from --pf), ``--rounds`` times alternated; us/step = best of 5 event-timed plans
+launch; its XCD-local barrier's form from --bar), ``--rounds`` times alternated; us/step = best of 5 event-timed plans
 of --reps steps.  With --stamps K, the pipeline also records per-workgroup phase stamps of its first K steps
 (s_memrealtime): forward + head, first barrier, dW1 / role, second barrier -- medians per XCD.
 
-    python bench/xstep_ab.py [--cols 800] [--reps 200] [--rounds 2] [--pf 6 0] [--stamps 40] [--json out.jsonl]
+    python bench/xstep_ab.py [--cols 800] [--reps 200] [--rounds 2] [--bar 0 1] [--stamps 40] [--fha-stamps 30]
 """
 from __future__ import annotations
 
@@ -25,8 +25,7 @@ def main(argv=None):
     ap.add_argument("--cols", type=int, nargs="*", default=[800])
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--pf", type=int, nargs="*", default=[0])
-    ap.add_argument("--pfm", type=int, nargs="*", default=[0], help="MlpStep.xstep_pfm values (XStepPlan::pf_mode)")
+    ap.add_argument("--bar", type=int, nargs="*", default=[1], help="MlpStep.xstep_bar values (XStepPlan::bar)")
     ap.add_argument("--stamps", type=int, default=0)
     ap.add_argument("--fha-stamps", type=int, default=0, help="forward + head body stamps of the last of K steps")
     ap.add_argument("--json", default=None)
@@ -60,10 +59,10 @@ def main(argv=None):
         def walk(count, g0=0):
             st.run_steps(g0, count, n, 0, n, N, 1.0 / n, 1e-4, 1e-3, 1, stream)
 
-        forms = [("two_launch", 0, 0, 0)] + [(f"xstep_pf{p}_pfm{m}", -1, p, m) for p in a.pf for m in a.pfm]
+        forms = [("two_launch", 0, 1)] + [(f"xstep_bar{b}", -1, b) for b in a.bar]
         for rnd in range(a.rounds):
-            for name, xs, pf, pfm in forms:
-                st.xstep, st.xstep_pf, st.xstep_pfm = xs, pf, pfm
+            for name, xs, b in forms:
+                st.xstep, st.xstep_bar = xs, b
                 walk(20)
                 torch.cuda.synchronize()
                 best = float("inf")
@@ -76,12 +75,12 @@ def main(argv=None):
                     best = min(best, s0.elapsed_time(s1) * 1e3 / a.reps)
                 emit({"n": n, "H": a.hidden, "form": name, "round": rnd, "reps": a.reps, "us_per_step": round(best, 3),
                       "xstep_used": int(st.xstep_used), "kernel_error": bool(e.kernel_error())})
-        if a.stamps and a.pf:
+        if a.stamps:
             # phase stamps of the first K steps, relative to each step's GLOBAL start (the earliest workgroup entry
             # into the step on any XCD): per XCD, medians over its workers (and the role workgroup)
             k = a.stamps
             buf = torch.zeros(k * 8 * 32 * 4, dtype=torch.int64, device="cuda")
-            st.xstep, st.xstep_pf, st.xstep_pfm = -1, a.pf[0], a.pfm[-1]
+            st.xstep, st.xstep_bar = -1, a.bar[-1]
             st.xs_stamps, st.xs_stamp_steps = buf.data_ptr(), k
             walk(k)
             torch.cuda.synchronize()
@@ -100,7 +99,7 @@ def main(argv=None):
                            "dw1_done_last": np.median(w[:, :, 3].max(axis=1)), "role_done": np.median(r[:, 3])}
                 rows[x] = {kk: round(float(v) / 100, 3) for kk, v in rows[x].items()}
             per = np.diff(g0[:, 0]) / 100
-            emit({"n": n, "H": a.hidden, "pf": a.pf[0], "pfm": a.pfm[-1], "stamps_steps": k, "step_period_median_us": round(float(np.median(per)), 3),
+            emit({"n": n, "H": a.hidden, "bar": a.bar[-1], "stamps_steps": k, "step_period_median_us": round(float(np.median(per)), 3),
                   "per_xcd_median_us_from_step_start": rows})
         if a.fha_stamps:
             # the forward + head body's own stamps (fha_body: entry, z2 partial published, all partials gathered,
@@ -109,7 +108,7 @@ def main(argv=None):
             k = a.fha_stamps
             fst = torch.zeros(256 * 4, dtype=torch.int64, device="cuda")
             hst = torch.zeros(256 * 8 * 4, dtype=torch.int64, device="cuda")
-            st.xstep, st.xstep_pf, st.xstep_pfm = -1, a.pf[0] if a.pf else 0, a.pfm[-1]
+            st.xstep, st.xstep_bar = -1, a.bar[-1]
             st.stamps, st.hstamps = fst.data_ptr(), hst.data_ptr()
             walk(k)
             torch.cuda.synchronize()
@@ -132,7 +131,7 @@ def main(argv=None):
                                   "published": round(float(np.median(f4[m, 1] - t0)) / 100, 3),
                                   "gathered": round(float(np.median(f4[m, 2] - t0)) / 100, 3),
                                   "end": round(float(np.median(f4[m, 3] - t0)) / 100, 3)}
-            emit({"n": n, "H": a.hidden, "pf": st.xstep_pf, "pfm": st.xstep_pfm, "fha_stamps_last_of": k,
+            emit({"n": n, "H": a.hidden, "bar": st.xstep_bar, "fha_stamps_last_of": k,
                   "fha_median_us": {kk: (round(float(v) / 100, 3) if v is not None else None) for kk, v in rows.items()},
                   "fha_per_xcd_median_us": per_xcd})
     if out:

@@ -135,8 +135,8 @@ struct MlpStep {
   // The XCD-local step pipeline (mlp_xstep, csrc/mlp/xstep.hip): run_steps runs the whole plan in ONE persistent
   // launch when the plan's step has the pipeline's shape (H <= 128 split3, fragment-ordered operands, the head's dW2
   // partials, fused SGD, one process, steps on the 16-sample grid); -1 auto (on), 0 off, 1 required (an error if
-  // the plan does not qualify).  xstep_pf: prefetch workgroups per XCD (the pixels each XCD reads next).
-  int xstep = -1, xstep_pf = 0, xstep_pfm = 0;  // xstep_pfm: XStepPlan::pf_mode
+  // the plan does not qualify).  xstep_bar: XStepPlan::bar (the XCD-local barrier's form).
+  int xstep = -1, xstep_bar = 1;
   int xstep_used = 0;     // the last run_steps ran as one xstep launch (tests, bench records)
   unsigned xs_ep = 1, xs_launch = 0;  // the next step's granule tag; launches so far (control bank)
   unsigned long long *xs_gran = nullptr, *xs_ctl = nullptr;
@@ -551,8 +551,7 @@ struct MlpStep {
     p.ep0 = xs_ep; p.launch = xs_launch;
     p.gran = xs_gran; p.ctl = xs_ctl; p.Dx = xs_dx; p.b2x = xs_b2x; p.err = P_<int>(ag_err);
     p.nw = cme::mlp_xstep_workers(a);
-    p.npf = std::max(0, std::min(xstep_pf, 32 - p.nw - 1));
-    p.pf_mode = xstep_pfm;
+    p.bar = xstep_bar;
     p.stamps = reinterpret_cast<unsigned long long*>(xs_stamps);
     p.stamp_steps = xs_stamps ? xs_stamp_steps : 0;
     cme::mlp_xstep(a, h, p, S(stream));
@@ -753,8 +752,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("xp_dbg", &MlpStep::xp_dbg)
       .def_readwrite("g64_touch", &MlpStep::g64_touch)
       .def_readwrite("xstep", &MlpStep::xstep)
-      .def_readwrite("xstep_pf", &MlpStep::xstep_pf)
-      .def_readwrite("xstep_pfm", &MlpStep::xstep_pfm)
+      .def_readwrite("xstep_bar", &MlpStep::xstep_bar)
       .def_readonly("xstep_used", &MlpStep::xstep_used)
       .def_readonly("xstep_reason", &MlpStep::xstep_reason)
       .def_readwrite("xs_stamps", &MlpStep::xs_stamps)

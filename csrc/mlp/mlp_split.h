@@ -243,9 +243,8 @@ struct XStepPlan {
   float* Dx = nullptr;     // [8 XCDs][16][ld]: each XCD's copy of D (its role workgroup's db2 reads it)
   float* b2x = nullptr;    // [8 XCDs][16]: each XCD's copy of b2 (updated in the same order on every XCD)
   int* err = nullptr;      // the sticky timed-out word (MlpEngine.ag_err)
-  int nw = 0, npf = 0;     // workers per XCD (mlp_xstep_workers), prefetch workgroups per XCD
-  int pf_mode = 0;         // the workers' own L2 prefetch during the z2 all-gather wait: bit0 this step's dW1 pixels
-                           // (XT), bit1 the next step's forward pixels (fragment-ordered X)
+  int nw = 0;              // workers per XCD (mlp_xstep_workers)
+  int bar = 1;             // the XCD-local barrier: 0 an atomic counter, 1 a flag line in the XCD's L2 (xstep.hip XsBar)
   unsigned long long* stamps = nullptr;  // diagnostics: [stamp_steps][8][32][4] s_memrealtime per workgroup
   int stamp_steps = 0;
 };
@@ -253,7 +252,7 @@ bool mlp_xstep_ok(const SplitStepArgs& a, const HeadArgs& h);
 int mlp_xstep_workers(const SplitStepArgs& a);
 void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hipStream_t s);
 constexpr int64_t kXstepGranules = 2 * 32 * 8 * 16 * 32;
-constexpr int64_t kXstepCtlWords = 2 * 8 * 64;
+constexpr int64_t kXstepCtlWords = 2 * 8 * 64 + 8 * 16;
 
 // planes[p][i] for i < n: exact np-way bf16 split of W[i] (np = 1: plain rounding).
 void mlp_split_planes(const float* W, void* planes, int64_t n, int np, hipStream_t s);

@@ -20,14 +20,15 @@
 //   * slot nw is the XCD's role workgroup: after the first barrier it sums the dW2 partials of W2[:, rt rows] (EpiW2)
 //     and reduces D into db2 -- redundantly on every XCD, in the same order, into that XCD's own copy of b2 (XCD 0
 //     also writes the master b2 at the plan's last step);
-//   * slots past nw pull the pixels the XCD reads next into its L2 (l2_touch: this step's XT, the next step's
-//     fragment-ordered X).
+//   * the other slots idle.  (Extra workgroups pulling the pixels each XCD reads next into its L2 -- this step's XT,
+//     the next step's X -- measured slower, +1.5 us per step, and so did the workers' own LDS-DMA pull during the z2
+//     wait: profiles/r6/xstep_ab_r6b.jsonl, xstep_ab_r6c_prefetch_rejected.jsonl.)
 //
-// The two barriers per step are XCD-local: each participant drains its stores (s_waitcnt vmcnt(0) + workgroup
-// barrier), adds one to its XCD's counter (an agent-scope atomic) and lane 0 polls it with sc1 loads; every read of
-// data another workgroup of the launch wrote goes through sc1 (L1-bypassing, L2-served) loads, so a CU never reuses a
-// stale L1 line, and the producer's plain stores stay in the XCD's L2 (bench/micro/xcd_barrier.hip prices the
-// barrier at 0.64-0.83 us and the same-XCD read-back at 1.1 us for 50 KB per workgroup, profiles/r6/).  Arithmetic
+// The two barriers per step are XCD-local (XsBar): each participant drains its stores (s_waitcnt vmcnt(0) + workgroup
+// barrier) and signals on its XCD's flag line (or counter); every read of data another workgroup of the launch wrote
+// goes through sc1 (L1-bypassing, L2-served) loads, so a CU never reuses a stale L1 line, and the producer's plain
+// stores stay in the XCD's L2 (bench/micro/xcd_barrier.hip: the same-XCD read-back checked word by word, and priced,
+// profiles/r6/xcd_barrier_micro*.jsonl).  Arithmetic
 // and summation orders are those of the two-launch step, so the parameters are bitwise equal to it
 // (tests/test_gpu_xstep.py).
 //
@@ -41,7 +42,6 @@
 
 #include "fha_body.h"
 #include "granule.h"
-#include "l2_touch.h"
 #include "mma_tile.h"
 #include "wgrad_epi.h"
 
@@ -71,39 +71,95 @@ __device__ __forceinline__ unsigned long long* xs_ticket(unsigned long long* ctl
 __device__ __forceinline__ unsigned long long* xs_counter(unsigned long long* ctl, int bank, int x) {
   return ctl + ((size_t)bank * 8 + x) * 64 + 32;
 }
-
-// XCD-local barrier: this workgroup's stores are drained by every wave, then one agent-scope add (1, or 1 + kXsBad
-// when its step is bad) and lane 0 polls the counter with sc1 loads until `target` arrivals.  False (block-uniform)
-// when the XCD must stop: a bad arrival, or a wait past `limit_us` (then *err is set and kXsBad added, so every other
-// waiter -- the prefetch workgroups too -- stops as well).
-__device__ __forceinline__ bool xs_barrier(unsigned long long* cnt, unsigned long long target, bool bad, int* err,
-                                           uint32_t limit_us, int* s_stop) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(cnt, bad ? 1ull + kXsBad : 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t t0 = 0;
-    const uint64_t limit = (uint64_t)limit_us * kTicksPerUs;
-    for (uint32_t pass = 1;; ++pass) {
-      const unsigned long long v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (v >= kXsBad) {
-        *s_stop = 1;
-        break;
-      }
-      if (v >= target) break;
-      if (pass == 1) t0 = wall_ticks();
-      else if ((pass & 7) == 0 && wall_ticks() - t0 > limit) {
-        atomicExch(err, 1);
-        __hip_atomic_fetch_add(cnt, kXsBad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_stop = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-  return *s_stop == 0;
+// ... then [8 XCDs][16] uint64: one 128-byte flag line per XCD (XsBar<1>), never reset
+__device__ __forceinline__ unsigned* xs_flags(unsigned long long* ctl, int x) {
+  return reinterpret_cast<unsigned*>(ctl + 2 * 8 * 64 + (size_t)x * 16);
 }
+
+// The XCD-local barriers.  Every participant first drains its stores (s_waitcnt vmcnt(0) in every wave, then a
+// workgroup barrier); lane 0 then signals and wave 0 waits; the other waves wait at a workgroup barrier.  sync(q, bad)
+// is the plan's q-th barrier (two per step: q = 2 s + b); false (block-uniform) when the XCD must stop -- a bad
+// arrival (a timed-out z2 hand-off upstream) or a wait past `limit_us` (then *err is set and the stop is signalled
+// to every other waiter).
+//
+// BAR 0: one monotonic 64-bit counter per XCD (ctl bank launch & 1), an agent-scope atomic add per arrival, lane 0
+//        polling it with sc1 loads (bench/micro/xcd_barrier.hip mode 2: 0.64 us from arrival to release); a stop
+//        adds kXsBad.
+// BAR 1: a FLAG LINE per XCD: one 32-bit word per participant in a single 128-byte line, written with a PLAIN
+//        store -- the line stays in this XCD's L2, no trip to the memory-side atomic unit -- holding the barrier's tag
+//        2 (ep0 + s) + b (tags only grow over the buffer's life, so nothing is ever reset); lanes 0-31 of wave 0 poll
+//        the whole line with sc1 (L2-served) loads.  Word 31 is the stop word: launch + 1 when this launch stopped.
+//        Valid because every participant of a line is on the XCD whose L2 holds it (they all read the same XCC id).
+template <int BAR>
+struct XsBar {
+  unsigned long long* cnt;  // BAR 0
+  unsigned* line;           // BAR 1: 32 words
+  unsigned long long np;    // participants
+  unsigned ep0, stop_tag;   // BAR 1: the first step's granule tag, this launch's stop value
+  int slot;
+  int* err;
+  uint32_t limit_us;
+  int* s_stop;
+  __device__ bool sync(int q, bool bad) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int t = threadIdx.x;
+    const uint64_t limit = (uint64_t)limit_us * kTicksPerUs;
+    if constexpr (BAR == 0) {
+      if (t == 0) {
+        const unsigned long long target = (unsigned long long)(q + 1) * np;
+        __hip_atomic_fetch_add(cnt, bad ? 1ull + kXsBad : 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t t0 = 0;
+        for (uint32_t pass = 1;; ++pass) {
+          const unsigned long long v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (v >= kXsBad) {
+            *s_stop = 1;
+            break;
+          }
+          if (v >= target) break;
+          if (pass == 1) t0 = wall_ticks();
+          else if ((pass & 7) == 0 && wall_ticks() - t0 > limit) {
+            atomicExch(err, 1);
+            __hip_atomic_fetch_add(cnt, kXsBad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *s_stop = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    } else {
+      const unsigned tag = 2u * (ep0 + (unsigned)(q >> 1)) + (unsigned)(q & 1);
+      if (t == 0) {
+        if (bad) line[31] = stop_tag;
+        line[slot] = tag;
+      }
+      if (t < 64) {
+        const __amdgpu_buffer_rsrc_t rl = make_rsrc(line);
+        uint64_t t0 = 0;
+        for (uint32_t pass = 1;; ++pass) {
+          const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(rl, t < 32 ? t * 4 : kOOB, 0, kSc1);
+          if (__any(t == 31 && v == stop_tag)) {
+            if (t == 0) *s_stop = 1;
+            break;
+          }
+          if (__all(t >= (int)np || v - tag < 0x80000000u)) break;  // (wrap-safe v >= tag)
+          if (pass == 1) t0 = wall_ticks();
+          else if ((pass & 7) == 0 && wall_ticks() - t0 > limit) {
+            if (t == 0) {
+              atomicExch(err, 1);
+              line[31] = stop_tag;
+              *s_stop = 1;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    }
+    __syncthreads();
+    return *s_stop == 0;
+  }
+};
 
 // The samples of a run_steps plan's steps: consecutive global batches of B from gstart0, wrapping to 0 when one
 // would pass N_end (MlpStep::run_steps), this rank's shard at +shard_off.  off() is the current step's first sample,
@@ -117,6 +173,7 @@ struct XsWalk {
   __device__ void advance() { gs = gs + 2 * p.B > p.N_end ? 0 : gs + p.B; }
 };
 
+template <int BAR>
 __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h, XStepPlan p, int tm, int tn,
                                                     int t1n) {
   __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];  // both GEMM tiles' K reductions
@@ -141,10 +198,11 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
   }
   __syncthreads();
   const int x = (int)s_x, slot = s_slot;
-  if (x >= tm || slot < 0 || slot > p.nw + p.npf) return;  // (uniform) XCDs past the last row tile, spare CUs
-  unsigned long long* cnt = xs_counter(p.ctl, bank, x);
-  const unsigned long long np = (unsigned long long)p.nw + 1;  // barrier participants: the workers + the role
+  if (x >= tm || slot < 0 || slot > p.nw) return;  // (uniform) XCDs past the last row tile, spare CUs
   const uint32_t limit_us = (uint32_t)a.ag_wait_us;
+  // barrier participants: the workers + the role
+  XsBar<BAR> bar{xs_counter(p.ctl, bank, x), xs_flags(p.ctl, x), (unsigned long long)p.nw + 1, p.ep0, p.launch + 1u,
+                 slot, p.err, limit_us, &s_stop};
   const int n = a.n, ld = a.ld;
   const float reg = (float)a.reg, lr = (float)a.lr;
   unsigned long long* st = p.stamps;  // diagnostics: [step][8][32][4]
@@ -152,36 +210,6 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
     if (st && t == 0 && s < p.stamp_steps)
       st[(((size_t)s * 8 + x) * kXsWgsPerXcd + slot) * 4 + i] = __builtin_amdgcn_s_memrealtime();
   };
-
-  if (slot > p.nw) {  // ---- prefetch: this step's XT, then the next step's fragment-ordered pixels, into this L2
-    const int part = slot - p.nw - 1;
-    XsWalk w(p);
-    for (int s = 0; s < p.count; ++s, w.advance()) {
-      if (t == 0) {  // the step has started on this XCD: its previous step's second barrier is complete
-        const unsigned long long target = 2ull * (unsigned long long)s * np;
-        const uint64_t t0 = wall_ticks();
-        for (;;) {
-          const unsigned long long v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (v >= kXsBad || (wall_ticks() - t0 > (uint64_t)limit_us * kTicksPerUs)) {
-            s_stop = 1;
-            break;
-          }
-          if (v >= target) break;
-          __builtin_amdgcn_s_sleep(8);
-        }
-      }
-      __syncthreads();
-      if (s_stop) return;
-      l2_touch(p.XT0, w.off(), a.P + a.bias_col, a.ldxt, n, part, p.npf, reinterpret_cast<char*>(red));
-      if (s + 1 < p.count) {
-        const int64_t nx = w.next();
-        l2_touch(p.Xs0, nx / 16 * p.xs_tile, 1, 0, (int64_t)((n + 15) / 16) * p.xs_tile, part, p.npf,
-                 reinterpret_cast<char*>(red));
-      }
-      __syncthreads();
-    }
-    return;
-  }
 
   XsWalk w(p);
   for (int s = 0; s < p.count; ++s, w.advance()) {
@@ -203,7 +231,7 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
                                            p.ep0 + (unsigned)s);
     }
     stamp(s, 1);
-    if (!xs_barrier(cnt, (2ull * s + 1) * np, bad, p.err, limit_us, &s_stop)) return;
+    if (!bar.sync(2 * s, bad)) return;
     stamp(s, 2);
     if (slot < p.nw) {
       if (slot < t1n) {  // ---- dW1 tile (x, slot) over the whole batch + reg + SGD (W1, W1s, b1)
@@ -281,7 +309,7 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
       }
     }
     stamp(s, 3);
-    if (!xs_barrier(cnt, (2ull * s + 2) * np, false, p.err, limit_us, &s_stop)) return;
+    if (!bar.sync(2 * s + 1, false)) return;
   }
 }
 
@@ -293,7 +321,7 @@ bool mlp_xstep_ok(const SplitStepArgs& a, const HeadArgs& h) {
   return a.H <= 128 && tm <= 8 && a.C <= 16 && a.bias_col && a.sgd == 1 && a.xf_world == 0 && a.npw == 3 &&
          a.npz == 3 && a.w1_swz && a.W1s && a.x_swz && a.Xs && a.dz_swz == 1 && a.dZ1 && h.dz_swz == 1 &&
          h.dZ1 == a.dZ1 && !h.dZ1_planes && a.dw2part && h.dw2part == a.dw2part && a.dw2_cols == 16 && !h.a1 &&
-         !h.loss_partial && a.n > 0 && a.n % 16 == 0 && nw + 1 <= kXsWgsPerXcd &&
+         !h.loss_partial && a.n > 0 && a.n % 16 == 0 && nw + 1 <= kXsWgsPerXcd && nw + 1 <= 31 &&
          device_cu_count() == 8 * kXsWgsPerXcd && mlp_wgrad_dz_swz_ok(a) &&
          (int64_t)a.P * a.ldxt < (int64_t)kOOB && (int64_t)xs_cdiv(a.H, 16) * 16 * a.ld < (int64_t)kOOB / 4;
 }
@@ -304,14 +332,15 @@ void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hi
   if (p.count <= 0) return;
   CME_REQUIRE(mlp_xstep_ok(a, h), "xstep: the plan's step is not the XCD-local pipeline's shape");
   const int tm = xs_cdiv(a.H, 16), tn = xs_cdiv(a.n, kXsCols), t1n = xs_cdiv(a.P + a.bias_col, 32);
-  CME_REQUIRE(p.nw == mlp_xstep_workers(a) && p.npf >= 0 && p.nw + 1 + p.npf <= kXsWgsPerXcd,
-              "xstep: workers + role + prefetch workgroups must fit one XCD's CUs");
+  CME_REQUIRE(p.nw == mlp_xstep_workers(a) && p.nw + 1 <= kXsWgsPerXcd && p.nw + 1 <= 31,
+              "xstep: the workers + the role must fit one XCD's CUs and its flag line");
   CME_REQUIRE(p.gran && p.ctl && p.Dx && p.b2x && p.err && p.X0 && p.XT0 && p.Xs0 && p.lab0 && p.xs_tile > 0,
               "xstep: scratch buffers missing");
   CME_REQUIRE(p.gstart0 % 16 == 0 && p.B % 16 == 0 && p.shard_off % 16 == 0 && p.B >= a.n && p.N_end >= p.B,
               "xstep: every step must start a 16-sample tile of the fragment-ordered pixels");
   CME_REQUIRE(a.ld >= a.n && a.ld % 16 == 0, "xstep: activation pitch");
-  xstep_kernel<<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  if (p.bar == 1) xstep_kernel<1><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  else xstep_kernel<0><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   CME_LAUNCH_CHECK(s);
 }
 

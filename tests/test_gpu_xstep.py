@@ -88,17 +88,19 @@ def test_xstep_falls_back_where_it_does_not_apply():
     assert torch.equal(small[0].params, small[1].params)
 
 
-def test_xstep_prefetch_workgroups_do_not_change_results():
-    """The prefetch workgroups (MlpStep.xstep_pf) only move bytes into L2: 0 and 6 per XCD give the same bits."""
+def test_xstep_barrier_forms_give_the_same_bits():
+    """The two XCD-local barrier forms (MlpStep.xstep_bar: 0 an atomic counter, 1 a flag line in the XCD's L2) order
+    the same work: the same bits, over launches that alternate the control banks."""
     n, N = 800, 4 * 800
     engines = _pair(100, n, N, seed=11)
     engines[0]._hip_step().xstep = -1
-    engines[0]._hip_step().xstep_pf = 0
-    for e in engines:
-        _plan(e, 0, 9, n, N)
-    torch.cuda.synchronize()
-    assert all(e._hip_step().xstep_used for e in engines), [e._hip_step().xstep_reason for e in engines]
-    assert torch.equal(engines[0].params, engines[1].params)
+    engines[0]._hip_step().xstep_bar = 0
+    for g0, k in ((0, 9), (n, 3), (2 * n, 5)):
+        for e in engines:
+            _plan(e, g0, k, n, N)
+        torch.cuda.synchronize()
+        assert all(e._hip_step().xstep_used for e in engines), [e._hip_step().xstep_reason for e in engines]
+        assert torch.equal(engines[0].params, engines[1].params)
 
 
 def test_xstep_handoff_timeout_applies_nothing():
