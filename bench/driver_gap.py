@@ -66,6 +66,10 @@ def run(a):
 
 
 def analyse(d):
+    """Per timed region: host start -> first kernel start, last kernel end -> host stop, the kernels' durations and
+    gaps (two-launch form: F/W per step; the XCD-local pipeline: ONE kernel per region), and -- with
+    ``--hip-runtime-trace`` in the rocprofv3 run -- every HIP API call inside the region (start / end relative to the
+    timer start): which part of the first-kernel gap is the host's launch path and which the device's."""
     import csv
 
     reg = json.load(open(glob.glob(os.path.join(d, "**", "regions.json"), recursive=True)[0]))
@@ -73,27 +77,42 @@ def analyse(d):
     ks = []
     for row in csv.DictReader(open(trace)):
         name = row.get("Kernel_Name", "")
-        if "fwd1_head" in name or "wgrad" in name:
-            ks.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), "F" if "fwd1" in name else "W"))
+        if "fwd1_head" in name or "wgrad" in name or "xstep_kernel" in name:
+            ks.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]),
+                       "X" if "xstep" in name else "F" if "fwd1" in name else "W"))
     ks.sort()
+    api = []
+    for f in glob.glob(os.path.join(d, "**", "*hip_api_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            api.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), row.get("Function", row.get("Name", ""))))
+    api.sort()
     K = reg["steps"]
     for r in reg["regions"]:
         inr = [k for k in ks if r["t0"] <= k[0] <= r["t1"]]
-        if len(inr) != 2 * K:
-            print(json.dumps({"warning": f"{len(inr)} kernels in region, expected {2 * K}"}))
+        calls = [(round((a0 - r["t0"]) / 1e3, 2), round((a1 - r["t0"]) / 1e3, 2), nm) for a0, a1, nm in api
+                 if r["t0"] <= a0 <= r["t1"]]
+        if not inr or (inr[0][2] != "X" and len(inr) != 2 * K):
+            print(json.dumps({"warning": f"{len(inr)} kernels in region, expected {2 * K} (or one xstep launch)"}))
             continue
         first, last = inr[0], inr[-1]
         dur = [round((k[1] - k[0]) / 1e3, 2) for k in inr]
         gaps = [round((inr[i + 1][0] - inr[i][1]) / 1e3, 2) for i in range(len(inr) - 1)]
-        print(json.dumps({
+        rec = {
             "region_us": round((r["t1"] - r["t0"]) / 1e3, 2),
             "host_start_to_first_kernel_us": round((first[0] - r["t0"]) / 1e3, 2),
             "last_kernel_end_to_host_stop_us": round((r["t1"] - last[1]) / 1e3, 2),
             "kernels_span_us": round((last[1] - first[0]) / 1e3, 2),
-            "fwd_us_first3": dur[0:6:2], "wgrad_us_first3": dur[1:6:2],
-            "fwd_us_median": sorted(dur[0::2])[K // 2], "wgrad_us_median": sorted(dur[1::2])[K // 2],
-            "gaps_us_first6": gaps[:6], "gap_us_median": sorted(gaps)[len(gaps) // 2],
-        }))
+            "host_enqueue_us": round(r.get("host_enqueue_us", 0.0), 2),
+        }
+        if first[2] == "X":
+            rec.update(kernels=len(inr), xstep_kernel_us=dur, xstep_us_per_step=round(dur[0] / K, 3))
+        else:
+            rec.update({"fwd_us_first3": dur[0:6:2], "wgrad_us_first3": dur[1:6:2],
+                        "fwd_us_median": sorted(dur[0::2])[K // 2], "wgrad_us_median": sorted(dur[1::2])[K // 2],
+                        "gaps_us_first6": gaps[:6], "gap_us_median": sorted(gaps)[len(gaps) // 2]})
+        if calls:
+            rec["hip_api_calls_us"] = calls[:12]
+        print(json.dumps(rec))
 
 
 def main(argv=None):

@@ -26,8 +26,11 @@ def main(argv=None):
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--bar", type=int, nargs="*", default=[1], help="MlpStep.xstep_bar values (XStepPlan::bar)")
+    ap.add_argument("--pf", type=int, nargs="*", default=[0], help="MlpStep.xstep_pf values (XStepPlan::npf)")
     ap.add_argument("--stamps", type=int, default=0)
     ap.add_argument("--fha-stamps", type=int, default=0, help="forward + head body stamps of the last of K steps")
+    ap.add_argument("--gemm-stamps", action="store_true",
+                    help="with --fha-stamps: also the forward K loop's per-wave stamps (stored mid-body: they perturb)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args(argv)
     import numpy as np
@@ -59,10 +62,11 @@ def main(argv=None):
         def walk(count, g0=0):
             st.run_steps(g0, count, n, 0, n, N, 1.0 / n, 1e-4, 1e-3, 1, stream)
 
-        forms = [("two_launch", 0, 1)] + [(f"xstep_bar{b}", -1, b) for b in a.bar]
+        forms = [("two_launch", 0, 1, 0)] + [(f"xstep_bar{b}_pf{q}", -1, b, q) for b in a.bar for q in a.pf
+                                             if b == 1 or q == 0]
         for rnd in range(a.rounds):
-            for name, xs, b in forms:
-                st.xstep, st.xstep_bar = xs, b
+            for name, xs, b, q in forms:
+                st.xstep, st.xstep_bar, st.xstep_pf = xs, b, q
                 walk(20)
                 torch.cuda.synchronize()
                 best = float("inf")
@@ -80,7 +84,7 @@ def main(argv=None):
             # into the step on any XCD): per XCD, medians over its workers (and the role workgroup)
             k = a.stamps
             buf = torch.zeros(k * 8 * 32 * 4, dtype=torch.int64, device="cuda")
-            st.xstep, st.xstep_bar = -1, a.bar[-1]
+            st.xstep, st.xstep_bar, st.xstep_pf = -1, a.bar[-1], a.pf[-1]
             st.xs_stamps, st.xs_stamp_steps = buf.data_ptr(), k
             walk(k)
             torch.cuda.synchronize()
@@ -106,20 +110,25 @@ def main(argv=None):
             # end) and the K loop's per-wave stamps (wsk_tile) for the LAST step of a K-step plan, relative to the
             # earliest entry
             k = a.fha_stamps
-            fst = torch.zeros(256 * 4, dtype=torch.int64, device="cuda")
+            fst = torch.zeros(2 * 256 * 4, dtype=torch.int64, device="cuda")
             hst = torch.zeros(256 * 8 * 4, dtype=torch.int64, device="cuda")
-            st.xstep, st.xstep_bar = -1, a.bar[-1]
-            st.stamps, st.hstamps = fst.data_ptr(), hst.data_ptr()
+            st.xstep, st.xstep_bar, st.xstep_pf = -1, a.bar[-1], a.pf[-1]
+            st.stamps, st.hstamps = fst.data_ptr(), hst.data_ptr() if a.gemm_stamps else 0
             walk(k)
             torch.cuda.synchronize()
             st.stamps, st.hstamps = 0, 0
-            f4 = fst.view(256, 4).cpu().numpy().astype(np.int64)  # [slot * 8 + xcd]
+            f8 = fst.view(2, 256, 4).cpu().numpy().astype(np.int64)
+            f4, f4b = f8[0], f8[1]  # [slot * 8 + xcd]: fha_body's four stamps, then its PS extras
             h4 = hst.view(256, 8, 4).cpu().numpy().astype(np.int64)  # [blockIdx][wave] (physical block)
             used = f4[:, 0] > 0
             t0 = f4[used, 0].min()
-            kl = h4[:, :, 1].max(axis=1)  # the workgroup's K loops done (slowest wave)
-            kl = kl[kl > 0]
-            rows = {"entry": np.median(f4[used, 0] - t0), "kloop_done_med": np.median(kl - t0) if len(kl) else None,
+            hb = h4[h4[:, 0, 0] > 0]  # the forward K loop's per-wave stamps: entry, K loop done, reduced, epilogue done
+            kst = {f"gemm_{nm}": np.median(hb[:, :, i].max(axis=1) - t0) if len(hb) else None
+                   for i, nm in enumerate(("entry", "kloop_done", "reduced", "epilogue_done"))}
+            kst["gemm_kloop_done_first_wave"] = np.median(hb[:, :, 1].min(axis=1) - t0) if len(hb) else None
+            rows = {"entry": np.median(f4[used, 0] - t0), **kst,
+                    "fwd_tile_returned": np.median(f4b[used, 0] - t0), "w2_staged": np.median(f4b[used, 1] - t0),
+                    "z2_partial_formed": np.median(f4b[used & (f4b[:, 2] > 0), 2] - t0),
                     "z2_published": np.median(f4[used, 1] - t0), "z2_published_last": (f4[used, 1] - t0).max(),
                     "gathered": np.median(f4[used, 2] - t0), "end": np.median(f4[used, 3] - t0),
                     "end_last": (f4[used, 3] - t0).max()}

@@ -136,7 +136,7 @@ struct MlpStep {
   // launch when the plan's step has the pipeline's shape (H <= 128 split3, fragment-ordered operands, the head's dW2
   // partials, fused SGD, one process, steps on the 16-sample grid); -1 auto (on), 0 off, 1 required (an error if
   // the plan does not qualify).  xstep_bar: XStepPlan::bar (the XCD-local barrier's form).
-  int xstep = -1, xstep_bar = 1;
+  int xstep = -1, xstep_bar = 1, xstep_pf = 0;  // xstep_pf: XStepPlan::npf
   int xstep_used = 0;     // the last run_steps ran as one xstep launch (tests, bench records)
   unsigned xs_ep = 1, xs_launch = 0;  // the next step's granule tag; launches so far (control bank)
   unsigned long long *xs_gran = nullptr, *xs_ctl = nullptr;
@@ -552,6 +552,7 @@ struct MlpStep {
     p.gran = xs_gran; p.ctl = xs_ctl; p.Dx = xs_dx; p.b2x = xs_b2x; p.err = P_<int>(ag_err);
     p.nw = cme::mlp_xstep_workers(a);
     p.bar = xstep_bar;
+    p.npf = std::max(0, std::min(xstep_pf, 32 - p.nw - 1));
     p.stamps = reinterpret_cast<unsigned long long*>(xs_stamps);
     p.stamp_steps = xs_stamps ? xs_stamp_steps : 0;
     cme::mlp_xstep(a, h, p, S(stream));
@@ -753,6 +754,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_readwrite("g64_touch", &MlpStep::g64_touch)
       .def_readwrite("xstep", &MlpStep::xstep)
       .def_readwrite("xstep_bar", &MlpStep::xstep_bar)
+      .def_readwrite("xstep_pf", &MlpStep::xstep_pf)
       .def_readonly("xstep_used", &MlpStep::xstep_used)
       .def_readonly("xstep_reason", &MlpStep::xstep_reason)
       .def_readwrite("xs_stamps", &MlpStep::xs_stamps)

@@ -90,8 +90,30 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
   const int t = threadIdx.x, H = f.H, C = h.C, n = f.n;
   const int r0 = rt * 16, c0 = ct * kCols;
   unsigned long long* st = f.stamps ? f.stamps + (size_t)blk * 4 : nullptr;  // diagnostics only
+  // (PS: the stamps are held in registers and stored at the end -- a store in the middle of the body puts its
+  // completion in front of the next vmcnt wait -- with three more per workgroup after the first 256 x 4: the GEMM
+  // returned, W2 staged, z2 partial formed)
+  unsigned long long ts[8] = {};
   auto stamp = [&](int i) {
-    if (st && t == 0) st[i] = __builtin_amdgcn_s_memrealtime();
+    if constexpr (PS) {
+      if (st && t == 0) ts[i] = __builtin_amdgcn_s_memrealtime();
+    } else {
+      if (st && t == 0) st[i] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  auto stamp2 = [&](int i) {
+    if constexpr (PS) {
+      if (st && t == 0) ts[4 + i] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  auto stamps_out = [&]() {
+    if constexpr (PS) {
+      if (st && t == 0)
+        for (int i = 0; i < 4; ++i) {
+          st[i] = ts[i];
+          st[1024 + i] = ts[4 + i];
+        }
+    }
   };
   stamp(0);
   // the launch epoch: one add per workgroup now, by wave 7, which has no K range at K = 784 or 800 -- so it also
@@ -124,11 +146,13 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
   TileGeom g{H, n, f.P, r0, c0};
   EpiSigLdsT<CP> epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
   fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
+  stamp2(0);
   // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
   // they are masked below.  w2s / b2s are complete after the barrier below.
   if (t < 256) w2s[wc][wr] = w2v;
   else if (t < 256 + 16) b2s[t - 256] = b2v;
   __syncthreads();
+  stamp2(1);
   const unsigned ep = s_ep;
   // ---- 1. z2 partial W2[:, tile rows] . a1[tile rows, 32 columns] on MFMA (waves 0 and 1: 16 columns each,
   // 4 x v_mfma_f32_16x16x4_f32 over the 16 rows), published as tagged granules (lane: classes 4 g + i of
@@ -142,6 +166,13 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
     for (int s = 0; s < 4; ++s) {
       const int r = 4 * s + kg;
       p = __builtin_amdgcn_mfma_f32_16x16x4f32(w2s[l16][r], (colok && r0 + r < H) ? a1s[r][zc] : 0.f, p, 0, 0, 0);
+    }
+    if constexpr (PS) {
+      if (st) {  // (diagnostics: the partial is formed)
+        float sink = p[0];
+        asm volatile("" ::"v"(sink));
+        stamp2(2);
+      }
     }
     // (test hook: one workgroup of column tile 0 never publishes, so that tile's polls time out)
     if (!(f.ag_test_skip == rt && ct == 0)) {
@@ -206,7 +237,10 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
       h.loss_partial[vb] = sl;
     }
   }
-  if (s_bad) return false;  // (zs holds D) a timed-out wait: nothing more is written
+  if (s_bad) {  // (zs holds D) a timed-out wait: nothing more is written
+    stamps_out();
+    return false;
+  }
   // ---- 4a. (h.dw2part) this tile's dW2 partials D[:, 16 columns] . a1[tile rows, 16 columns]^T into
   // dw2part[16-column block][16 classes][H] (SplitStepArgs::dw2part, dw2_cols = 16): the weight-gradient launch's
   // dW2 role then sums cdiv(n, 16) partials per element (32 KB per 16-row tile at n = 800) instead of pulling D and
@@ -285,6 +319,7 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     stamp(3);
+    stamps_out();
   }
   return true;
 }

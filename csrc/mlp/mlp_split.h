@@ -244,6 +244,7 @@ struct XStepPlan {
   float* b2x = nullptr;    // [8 XCDs][16]: each XCD's copy of b2 (updated in the same order on every XCD)
   int* err = nullptr;      // the sticky timed-out word (MlpEngine.ag_err)
   int nw = 0;              // workers per XCD (mlp_xstep_workers)
+  int npf = 0;             // prefetch workgroups per XCD (idle CUs pulling the pixels the XCD reads next into its L2)
   int bar = 1;             // the XCD-local barrier: 0 an atomic counter, 1 a flag line in the XCD's L2 (xstep.hip XsBar)
   unsigned long long* stamps = nullptr;  // diagnostics: [stamp_steps][8][32][4] s_memrealtime per workgroup
   int stamp_steps = 0;

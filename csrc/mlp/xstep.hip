@@ -42,6 +42,7 @@
 
 #include "fha_body.h"
 #include "granule.h"
+#include "l2_touch.h"
 #include "mma_tile.h"
 #include "wgrad_epi.h"
 
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
   }
   __syncthreads();
   const int x = (int)s_x, slot = s_slot;
-  if (x >= tm || slot < 0 || slot > p.nw) return;  // (uniform) XCDs past the last row tile, spare CUs
+  if (x >= tm || slot < 0 || slot > p.nw + p.npf) return;  // (uniform) XCDs past the last row tile, spare CUs
   const uint32_t limit_us = (uint32_t)a.ag_wait_us;
   // barrier participants: the workers + the role
   XsBar<BAR> bar{xs_counter(p.ctl, bank, x), xs_flags(p.ctl, x), (unsigned long long)p.nw + 1, p.ep0, p.launch + 1u,
@@ -210,6 +211,39 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
     if (st && t == 0 && s < p.stamp_steps)
       st[(((size_t)s * 8 + x) * kXsWgsPerXcd + slot) * 4 + i] = __builtin_amdgcn_s_memrealtime();
   };
+
+  if (slot > p.nw) {  // ---- prefetch (BAR 1): the pixels this XCD reads next, pulled into its L2 by idle CUs
+    if constexpr (BAR == 1) {
+      // at the start of step s (the flag line says the previous step's second barrier is complete): this step's XT
+      // (the dW1 tiles read it after the first barrier) and the next step's fragment-ordered X (the next forward)
+      const int part = slot - p.nw - 1;
+      const unsigned* line = xs_flags(p.ctl, x);
+      XsWalk w(p);
+      for (int s = 0; s < p.count; ++s, w.advance()) {
+        if (s > 0 && t < 64) {
+          const unsigned tag = 2u * (p.ep0 + (unsigned)(s - 1)) + 1u, stop = p.launch + 1u;
+          const __amdgpu_buffer_rsrc_t rl = make_rsrc(line);
+          const uint64_t t0 = wall_ticks();
+          for (;;) {
+            const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(rl, t < 32 ? t * 4 : kOOB, 0, kSc1);
+            if (__any(t == 31 && v == stop) || wall_ticks() - t0 > (uint64_t)limit_us * kTicksPerUs) {
+              if (t == 0) s_stop = 1;
+              break;
+            }
+            if (__all(t > p.nw || v - tag < 0x80000000u)) break;
+            __builtin_amdgcn_s_sleep(4);
+          }
+        }
+        __syncthreads();
+        if (s_stop) return;
+        l2_touch(p.XT0, w.off(), a.P + a.bias_col, a.ldxt, n, part, p.npf, reinterpret_cast<char*>(red));
+        if (s + 1 < p.count)
+          l2_touch(p.Xs0, w.next() / 16 * p.xs_tile, 1, 0, (int64_t)((n + 15) / 16) * p.xs_tile, part, p.npf,
+                   reinterpret_cast<char*>(red));
+      }
+    }
+    return;
+  }
 
   XsWalk w(p);
   for (int s = 0; s < p.count; ++s, w.advance()) {
@@ -332,8 +366,9 @@ void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hi
   if (p.count <= 0) return;
   CME_REQUIRE(mlp_xstep_ok(a, h), "xstep: the plan's step is not the XCD-local pipeline's shape");
   const int tm = xs_cdiv(a.H, 16), tn = xs_cdiv(a.n, kXsCols), t1n = xs_cdiv(a.P + a.bias_col, 32);
-  CME_REQUIRE(p.nw == mlp_xstep_workers(a) && p.nw + 1 <= kXsWgsPerXcd && p.nw + 1 <= 31,
-              "xstep: the workers + the role must fit one XCD's CUs and its flag line");
+  CME_REQUIRE(p.nw == mlp_xstep_workers(a) && p.nw + 1 + p.npf <= kXsWgsPerXcd && p.nw + 1 <= 31 && p.npf >= 0 &&
+                  (p.npf == 0 || p.bar == 1),
+              "xstep: the workers + the role (+ prefetch workgroups, flag-line barrier only) must fit one XCD's CUs");
   CME_REQUIRE(p.gran && p.ctl && p.Dx && p.b2x && p.err && p.X0 && p.XT0 && p.Xs0 && p.lab0 && p.xs_tile > 0,
               "xstep: scratch buffers missing");
   CME_REQUIRE(p.gstart0 % 16 == 0 && p.B % 16 == 0 && p.shard_off % 16 == 0 && p.B >= a.n && p.N_end >= p.B,

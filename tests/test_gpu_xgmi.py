@@ -179,7 +179,8 @@ def test_tensor_parallel_xgmi_z2_allreduce(tmp_path, world, H):
 @pytest.mark.parametrize("gpus", [2, 4])
 def test_bench_tunes_allreduce_shared_gpu(gpus):
     """bench.py --gpus N (self-launched, N ranks on GPU 0): the gradient sync is chosen by measurement -- the
-    policy's xGMI pick, the xGMI two-shot (N >= 3) and the communicator's all-reduce each run the probe, every
+    policy's xGMI pick (the fused pull), the fused owner-tile push, the xGMI two-shot (N >= 3) and the communicator's
+    all-reduce each run the probe, every
     timing is in the record, the fastest ran the timed region, and the record is valid (replicas bitwise equal)."""
     import json
 
@@ -192,7 +193,8 @@ def test_bench_tunes_allreduce_shared_gpu(gpus):
     cfg = rec["config"]
     tune = cfg["allreduce_tuning_us_per_step"]
     assert rec["n_gpus"] == gpus and cfg["ranks_seen"] == gpus and cfg["replicas_bitwise_equal"], rec
-    assert len(tune) == (2 if gpus == 2 else 3) and any(k.startswith("xgmi") for k in tune), tune
+    # (the policy's pick -- the fused one-shot pull --, the fused owner-tile push, the two-shot at N >= 3, RCCL)
+    assert len(tune) == (3 if gpus == 2 else 4) and "xgmi-fused" in tune and "xgmi-push" in tune, tune
     nums = {k: v for k, v in tune.items() if isinstance(v, (int, float))}
     assert nums and cfg["allreduce"] == min(nums, key=nums.get), (cfg["allreduce"], tune)
 
