@@ -193,8 +193,11 @@ def test_bench_tunes_allreduce_shared_gpu(gpus):
     cfg = rec["config"]
     tune = cfg["allreduce_tuning_us_per_step"]
     assert rec["n_gpus"] == gpus and cfg["ranks_seen"] == gpus and cfg["replicas_bitwise_equal"], rec
-    # (the policy's pick -- the fused one-shot pull --, the fused owner-tile push, the two-shot at N >= 3, RCCL)
-    assert len(tune) == (3 if gpus == 2 else 4) and "xgmi-fused" in tune and "xgmi-push" in tune, tune
+    # (the policy's pick, the two-shot at N >= 3, RCCL; and where the pick is the fused one-shot pull, the fused
+    # owner-tile push too -- four ranks on one GPU do not get the fused form: its launch needs the whole GPU)
+    fused = "xgmi-fused" in tune
+    assert len(tune) == (2 if gpus == 2 else 3) + fused and any(k.startswith("xgmi") for k in tune), tune
+    assert fused == ("xgmi-push" in tune), tune
     nums = {k: v for k, v in tune.items() if isinstance(v, (int, float))}
     assert nums and cfg["allreduce"] == min(nums, key=nums.get), (cfg["allreduce"], tune)
 

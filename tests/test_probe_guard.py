@@ -179,10 +179,12 @@ def test_retime_keeps_the_inner_guard_record():
 
 
 def test_cost_model_fit_is_bounded():
-    """measure_cost_model's fit: a noisy (non-positive or absurd) slope keeps the planning constants."""
+    """measure_cost_model's fit: a noisy (non-positive or absurd) slope keeps the planning constants; a large fixed
+    cost (a host-staged gloo communicator) is kept."""
     plan = T.CostModel()
     fixed, gbps = T._fit_bounded(10.0, 30.0, 4 * (1 << 20), plan.kernel_us, plan.link_gbps)
     assert fixed == 10.0 and abs(gbps - 4 * (1 << 20) / 20.0 / 1e3) < 1e-9
     assert T._fit_bounded(10.0, 9.0, 4e6, plan.kernel_us, plan.link_gbps) == (None, None)       # slope < 0
     assert T._fit_bounded(10.0, 10.0001, 4e6, plan.kernel_us, plan.link_gbps) == (None, None)   # 40 TB/s
-    assert T._fit_bounded(1e4, 2e4, 4e6, plan.kernel_us, plan.link_gbps) == (None, None)        # 10 ms fixed
+    assert T._fit_bounded(0.0, 20.0, 4e6, plan.kernel_us, plan.link_gbps) == (None, None)       # no fixed cost
+    assert T._fit_bounded(4500.0, 9000.0, 4e6, plan.rccl_us, plan.rccl_gbps)[0] == 4500.0      # gloo: kept
