@@ -25,7 +25,7 @@ def main(argv=None):
     ap.add_argument("--cols", type=int, nargs="*", default=[800])
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--bar", type=int, nargs="*", default=[1], help="MlpStep.xstep_bar values (XStepPlan::bar)")
+    ap.add_argument("--bar", type=int, nargs="*", default=[3], help="MlpStep.xstep_bar values (XStepPlan::bar)")
     ap.add_argument("--pf", type=int, nargs="*", default=[0], help="MlpStep.xstep_pf values (XStepPlan::npf)")
     ap.add_argument("--stamps", type=int, default=0)
     ap.add_argument("--fha-stamps", type=int, default=0, help="forward + head body stamps of the last of K steps")

@@ -136,7 +136,7 @@ struct MlpStep {
   // launch when the plan's step has the pipeline's shape (H <= 128 split3, fragment-ordered operands, the head's dW2
   // partials, fused SGD, one process, steps on the 16-sample grid); -1 auto (on), 0 off, 1 required (an error if
   // the plan does not qualify).  xstep_bar: XStepPlan::bar (the XCD-local barrier's form).
-  int xstep = -1, xstep_bar = 1, xstep_pf = 0;  // xstep_pf: XStepPlan::npf
+  int xstep = -1, xstep_bar = 3, xstep_pf = 0;  // xstep_pf: XStepPlan::npf
   int xstep_used = 0;     // the last run_steps ran as one xstep launch (tests, bench records)
   unsigned xs_ep = 1, xs_launch = 0;  // the next step's granule tag; launches so far (control bank)
   unsigned long long *xs_gran = nullptr, *xs_ctl = nullptr;

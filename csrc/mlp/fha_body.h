@@ -53,13 +53,100 @@ struct EpiSigLdsT {
   }
 };
 
+// ---- the XCD-local step pipeline's flag line (xstep.hip XsBar): one 32-bit word per participant of an XCD in one
+// 128-byte line of that XCD's L2, word 31 the launch's stop word.  ONE WAVE (every lane) waits until the words of
+// participants [lo, hi) -- and `extra` when >= 0 -- carry `tag` (wrap-safe >=).  False when the launch stops: the
+// stop word, or a wait past limit_us (then *err is set and the stop word written); *s_stop (LDS) is set either way.
+__device__ __forceinline__ bool xcd_flags_wait(unsigned* line, unsigned tag, unsigned stop_tag, int lo, int hi,
+                                               int extra, int* s_stop, int* err, uint32_t limit_us) {
+  const int l = threadIdx.x & 63;
+  const __amdgpu_buffer_rsrc_t rl = make_rsrc(line);
+  const uint64_t limit = (uint64_t)limit_us * kTicksPerUs;
+  uint64_t t0 = 0;
+  for (uint32_t pass = 1;; ++pass) {
+    const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(rl, l < 32 ? l * 4 : kOOB, 0, kSc1);
+    if (__any(l == 31 && v == stop_tag)) {
+      if (l == 0) *s_stop = 1;
+      return false;
+    }
+    if (__all(!((l >= lo && l < hi) || l == extra) || v - tag < 0x80000000u)) return true;
+    if (pass == 1) t0 = wall_ticks();
+    else if ((pass & 7) == 0 && wall_ticks() - t0 > limit) {
+      if (l == 0) {
+        atomicExch(err, 1);
+        line[31] = stop_tag;
+        *s_stop = 1;
+      }
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// PS with a gate (PSG): instead of a barrier between the previous step's weight update and this forward, each wave
+// of the forward GEMM waits for the flags of the dW1 tiles that wrote the W1 columns of its K range (dW1 feature tile
+// j = features [32 j, 32 j + 32)); the wave with no K range (wave 7) waits for every dW1 tile and the role workgroup
+// -- this step's head then overwrites what they read (dZ1, D, the dW2 partials) -- and then stages b1 (this tile's
+// rows), W2[:, rows] and b2 into LDS for the epilogue and the head (nobody else loads them).  line == nullptr: the
+// plan's first step, nothing to wait for.
+struct PsGate {
+  unsigned* line = nullptr;
+  unsigned tag = 0, stop_tag = 0;  // the previous step's second-barrier tag, this launch's stop value
+  int ntiles = 0, role = 0;        // dW1 tiles of the XCD (slots [0, ntiles)), the role's slot
+  int* s_stop = nullptr;
+  int* err = nullptr;
+  uint32_t limit_us = 0;
+};
+
+template <int CP>
+struct EpiSigGate {  // (EpiSigLdsT's arithmetic; b1 from LDS, staged by wave 7)
+  float* a1;
+  float (*a1s)[33];
+  int ld, r0, c0;
+  float xscale;
+  const PsGate* gate;
+  float* b1s;                      // [16]
+  float (*w2s)[17];                // [16][17]
+  float* b2s;                      // [16]
+  const float *b1, *W2, *b2;
+  int H, C;
+  __device__ __forceinline__ void prefetch(int, int, int, bool) {}
+  __device__ void before_kloop(int kbeg, int kend) {
+    const PsGate& g = *gate;
+    if (kend > kbeg) {
+      if (g.line) xcd_flags_wait(g.line, g.tag, g.stop_tag, kbeg / 32, min(g.ntiles, (kend + 31) / 32), -1, g.s_stop,
+                                 g.err, g.limit_us);
+      return;
+    }
+    if (g.line) xcd_flags_wait(g.line, g.tag, g.stop_tag, 0, g.ntiles, g.role, g.s_stop, g.err, g.limit_us);
+    const int l = threadIdx.x & 63;
+    if (l < 16)
+      b1s[l] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(b1), r0 + l < H ? (r0 + l) * 4 : kOOB,
+                                                                              0, CP));
+    for (int e = l; e < 256; e += 64) {  // W2[class][tile row], zero past C / H
+      const int c = e >> 4, r = e & 15;
+      w2s[c][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                make_rsrc(W2), (c < C && r0 + r < H) ? (c * H + r0 + r) * 4 : kOOB, 0, CP));
+    }
+    if (l < 16)
+      b2s[l] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(b2), l < C ? l * 4 : kOOB, 0,
+                                                                              CP));
+  }
+  __device__ __forceinline__ void operator()(int, int row, int col, float v) {
+    const float s = ag_sigmoid(v * xscale + b1s[row - r0]);
+    a1s[row - r0][col - c0] = s;
+    if (a1) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), make_rsrc(a1), (row * ld + col) * 4, 0, 0);
+  }
+};
+
 // blk: the workgroup's slot in the XCD-grouped grid (the hardware XCD is blk & 7).  red: >= 8 * 2 * 4 * 64
 // floats of LDS.
-template <int NPW, int VEC, bool AF, int SWZ = 0, bool PS = false>
+template <int NPW, int VEC, bool AF, int SWZ = 0, bool PS = false, bool PSG = false>
 __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs& h,
                                          unsigned long long* __restrict__ counters, gran_t* __restrict__ slabs,
                                          int* __restrict__ err, int tm, int tn, int blk, float* red, int ps_rt = 0,
-                                         int ps_ct = 0, unsigned ps_ep = 0) {
+                                         int ps_ct = 0, unsigned ps_ep = 0, const PsGate* ps_gate = nullptr) {
+  static_assert(!PSG || PS, "the gate is a persistent-pipeline form");
   constexpr int CP = PS ? kSc1 : 0;
   constexpr int kCols = 32;
   __shared__ float a1s[16][kCols + 1];
@@ -139,18 +226,30 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
   // the GEMM (written here, each wave waited for its W2 load before its K-loop burst: a dependent memory round
   // trip in front of the GEMM, ~0.5 us of the launch per bench/stamps_fha.py)
   const int wc = t >> 4, wr = t & 15;
-  const float w2v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-      make_rsrc(h.W2), (t < 256 && wc < C && r0 + wr < H) ? (wc * H + r0 + wr) * 4 : kOOB, 0, CP));
-  const float b2v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-      make_rsrc(h.b2), (t >= 256 && t < 256 + 16 && t - 256 < C) ? (t - 256) * 4 : kOOB, 0, CP));
   TileGeom g{H, n, f.P, r0, c0};
-  EpiSigLdsT<CP> epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
-  fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
-  stamp2(0);
-  // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
-  // they are masked below.  w2s / b2s are complete after the barrier below.
-  if (t < 256) w2s[wc][wr] = w2v;
-  else if (t < 256 + 16) b2s[t - 256] = b2v;
+  if constexpr (PSG) {  // (wave 7 stages b1, W2 and b2 into LDS inside the GEMM, after its wait: EpiSigGate)
+    __shared__ float b1s[16];
+    EpiSigGate<CP> epi{f.a1, a1s, f.ld, r0, c0, f.xscale, ps_gate, b1s, w2s, b2s, f.b1, static_cast<const float*>(h.W2),
+                       static_cast<const float*>(h.b2), H, C};
+    fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, h.stamps);
+    stamp2(0);
+    if (*ps_gate->s_stop) {  // (a wait of this step's gate saw the launch stop: nothing is written)
+      stamps_out();
+      return false;
+    }
+  } else {
+    const float w2v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+        make_rsrc(h.W2), (t < 256 && wc < C && r0 + wr < H) ? (wc * H + r0 + wr) * 4 : kOOB, 0, CP));
+    const float b2v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+        make_rsrc(h.b2), (t >= 256 && t < 256 + 16 && t - 256 < C) ? (t - 256) * 4 : kOOB, 0, CP));
+    EpiSigLdsT<CP> epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
+    fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
+    stamp2(0);
+    // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
+    // they are masked below.  w2s / b2s are complete after the barrier below.
+    if (t < 256) w2s[wc][wr] = w2v;
+    else if (t < 256 + 16) b2s[t - 256] = b2v;
+  }
   __syncthreads();
   stamp2(1);
   const unsigned ep = s_ep;

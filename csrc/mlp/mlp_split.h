@@ -245,7 +245,11 @@ struct XStepPlan {
   int* err = nullptr;      // the sticky timed-out word (MlpEngine.ag_err)
   int nw = 0;              // workers per XCD (mlp_xstep_workers)
   int npf = 0;             // prefetch workgroups per XCD (idle CUs pulling the pixels the XCD reads next into its L2)
-  int bar = 1;             // the XCD-local barrier: 0 an atomic counter, 1 a flag line in the XCD's L2 (xstep.hip XsBar)
+  int bar = 3;             // the XCD-local barriers: 0 an atomic counter, 1 a flag line in the XCD's L2 (xstep.hip XsBar),
+                           // 2 the flag line with the first barrier fine-grained (each dW1 wave waits for its own
+                           // column tiles' dZ1: EpiW1Gate), 3 both fine-grained (the next step's forward waves wait
+                           // for their own dW1 tiles, wave 7 for all of them and the role: fha_body PsGate)
+                           // -- n = 800 walking step: 0 ~14, 1 11.0, 2 10.8, 3 9.85 us (profiles/r6/xstep_ab_r6i.jsonl)
   unsigned long long* stamps = nullptr;  // diagnostics: [stamp_steps][8][32][4] s_memrealtime per workgroup
   int stamp_steps = 0;
 };

@@ -27,6 +27,7 @@
 #include "../common/hip_common.h"
 
 #include <type_traits>
+#include <utility>
 
 namespace cme {
 
@@ -270,6 +271,14 @@ struct TileGeom {
   int m0, n0;
 };
 
+// An epilogue may also gate the K loop: epi.before_kloop(kbeg, kend) -- this wave's K range -- is called by every wave
+// right before its first K-loop load, after the epilogue prefetch (the XCD-local step pipeline's dW1 waves wait there
+// for the dZ1 column tiles their range reads, xstep.hip).  Epilogues without it compile to the plain loop.
+template <class E, class = void>
+struct HasBeforeKloop : std::false_type {};
+template <class E>
+struct HasBeforeKloop<E, std::void_t<decltype(std::declval<E&>().before_kloop(0, 0))>> : std::true_type {};
+
 // One workgroup = KS waves computing the (16*MB) x (16*NB) tile at (m0, n0)
 // of C = A * B with K split across the waves.  On return, `epi(row, col, v)`
 // has been called exactly once for every in-bounds element of the tile.
@@ -375,6 +384,7 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
   const int kbeg = wave * cpw * KC;
   const int kend = min(g.K, (wave + 1) * cpw * KC);
 
+  if constexpr (HasBeforeKloop<Epi>::value) epi.before_kloop(kbeg, kend);
   constexpr bool AF32 = std::is_same_v<TA, float> && !std::is_same_v<T, float>;
   static_assert(!AF32 || (std::is_same_v<T, __hip_bfloat16> && NPA == 3 && AK), "fp32 A: split3 bf16, K-contiguous");
   constexpr bool BU8 = std::is_same_v<TB, uint8_t>;

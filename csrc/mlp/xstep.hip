@@ -101,12 +101,52 @@ struct XsBar {
   int* err;
   uint32_t limit_us;
   int* s_stop;
-  __device__ bool sync(int q, bool bad) {
+  __device__ unsigned tag_of(int q) const { return 2u * (ep0 + (unsigned)(q >> 1)) + (unsigned)(q & 1); }
+  // BAR 1: this workgroup's stores drained (every wave), then lane 0 publishes its flag (and the stop word first when
+  // its step is bad).  Returns after the workgroup barrier that follows the drain: the flag may still be in flight.
+  __device__ void arrive(int q, bool bad) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int t = threadIdx.x;
+    if (threadIdx.x == 0) {
+      if (bad) line[31] = stop_tag;
+      line[slot] = tag_of(q);
+    }
+  }
+  // BAR 1, one WAVE (all its lanes): wait until the flags of participants [lo, hi) carry barrier q's tag.  False when
+  // the launch stops (the stop word, or a wait past limit_us: then *err is set and the stop word written); *s_stop is
+  // then set for the workgroup (read after its next workgroup barrier).
+  __device__ bool poll(int q, int lo, int hi) {
+    const int l = threadIdx.x & 63;
+    const unsigned tag = tag_of(q);
+    const __amdgpu_buffer_rsrc_t rl = make_rsrc(line);
     const uint64_t limit = (uint64_t)limit_us * kTicksPerUs;
+    uint64_t t0 = 0;
+    for (uint32_t pass = 1;; ++pass) {
+      const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(rl, l < 32 ? l * 4 : kOOB, 0, kSc1);
+      if (__any(l == 31 && v == stop_tag)) {
+        if (l == 0) *s_stop = 1;
+        return false;
+      }
+      if (__all(l < lo || l >= hi || v - tag < 0x80000000u)) return true;  // (wrap-safe v >= tag)
+      if (pass == 1) t0 = wall_ticks();
+      else if ((pass & 7) == 0 && wall_ticks() - t0 > limit) {
+        if (l == 0) {
+          atomicExch(err, 1);
+          line[31] = stop_tag;
+          *s_stop = 1;
+        }
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  // the whole barrier: arrive, wave 0 waits for every participant, the workgroup joins it
+  __device__ bool sync(int q, bool bad) {
+    const int t = threadIdx.x;
     if constexpr (BAR == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const uint64_t limit = (uint64_t)limit_us * kTicksPerUs;
       if (t == 0) {
         const unsigned long long target = (unsigned long long)(q + 1) * np;
         __hip_atomic_fetch_add(cnt, bad ? 1ull + kXsBad : 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -129,36 +169,27 @@ struct XsBar {
         }
       }
     } else {
-      const unsigned tag = 2u * (ep0 + (unsigned)(q >> 1)) + (unsigned)(q & 1);
-      if (t == 0) {
-        if (bad) line[31] = stop_tag;
-        line[slot] = tag;
-      }
-      if (t < 64) {
-        const __amdgpu_buffer_rsrc_t rl = make_rsrc(line);
-        uint64_t t0 = 0;
-        for (uint32_t pass = 1;; ++pass) {
-          const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(rl, t < 32 ? t * 4 : kOOB, 0, kSc1);
-          if (__any(t == 31 && v == stop_tag)) {
-            if (t == 0) *s_stop = 1;
-            break;
-          }
-          if (__all(t >= (int)np || v - tag < 0x80000000u)) break;  // (wrap-safe v >= tag)
-          if (pass == 1) t0 = wall_ticks();
-          else if ((pass & 7) == 0 && wall_ticks() - t0 > limit) {
-            if (t == 0) {
-              atomicExch(err, 1);
-              line[31] = stop_tag;
-              *s_stop = 1;
-            }
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
+      arrive(q, bad);
+      if (t < 64) poll(q, 0, (int)np);
     }
     __syncthreads();
     return *s_stop == 0;
+  }
+};
+
+// FG (fine-grained first barrier, BAR 1): the dW1 tile's epilogue, gated.  Each wave of the tile waits only for the
+// forward + head workgroups whose dZ1 column tiles its K range reads (samples [kbeg, kend) = column tiles
+// [kbeg / 32, ceil(kend / 32))), instead of the whole XCD; a wave that sees the launch stop marks the workgroup and
+// the update is then not applied (the K loop's reduction barrier orders that mark before the epilogue).
+struct EpiW1Gate : EpiW1 {
+  XsBar<1>* bar;
+  int q, tn;
+  const int* s_stop;
+  __device__ void before_kloop(int kbeg, int kend) {
+    if (kend > kbeg) bar->poll(q, kbeg / kXsCols, min(tn, (kend + kXsCols - 1) / kXsCols));
+  }
+  __device__ __forceinline__ void operator()(int qq, int row, int col, float v) {
+    if (!*s_stop) EpiW1::operator()(qq, row, col, v);
   }
 };
 
@@ -174,9 +205,12 @@ struct XsWalk {
   __device__ void advance() { gs = gs + 2 * p.B > p.N_end ? 0 : gs + p.B; }
 };
 
-template <int BAR>
+// FG: 0 two full XCD barriers per step; 1 the first fine-grained (EpiW1Gate); 2 both (the forward's waves wait for
+// their own dW1 tiles: fha_body's PsGate) -- no full barrier left, only flags.
+template <int BAR, int FG>
 __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h, XStepPlan p, int tm, int tn,
                                                     int t1n) {
+  static_assert(FG == 0 || BAR == 1, "the fine-grained barriers need the flag line");
   __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];  // both GEMM tiles' K reductions
   __shared__ int s_slot, s_stop;
   __shared__ unsigned s_x;
@@ -213,7 +247,7 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
   };
 
   if (slot > p.nw) {  // ---- prefetch (BAR 1): the pixels this XCD reads next, pulled into its L2 by idle CUs
-    if constexpr (BAR == 1) {
+    if constexpr (BAR == 1 && FG == 0) {
       // at the start of step s (the flag line says the previous step's second barrier is complete): this step's XT
       // (the dW1 tiles read it after the first barrier) and the next step's fragment-ordered X (the next forward)
       const int part = slot - p.nw - 1;
@@ -261,22 +295,55 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
       hh.D = p.Dx + (size_t)x * 16 * ld;  // this XCD's copy of D (the role's db2 reads it)
       hh.b2 = s == 0 ? (const void*)a.b2 : (const void*)(p.b2x + x * 16);
       gran_t* slabs = p.gran + (size_t)(s & 1) * 32 * 8 * 16 * kXsCols;
-      bad = !fha_body<3, 3, true, 7, true>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red, x, slot,
-                                           p.ep0 + (unsigned)s);
-    }
+      if constexpr (FG == 2) {  // (the previous step's dW1 tiles and role, waited for per wave inside the GEMM)
+        PsGate gate;
+        gate.line = s > 0 ? xs_flags(p.ctl, x) : nullptr;
+        gate.tag = bar.tag_of(2 * s - 1);
+        gate.stop_tag = p.launch + 1u;
+        gate.ntiles = t1n;
+        gate.role = p.nw;
+        gate.s_stop = &s_stop;
+        gate.err = p.err;
+        gate.limit_us = limit_us;
+        bad = !fha_body<3, 3, true, 7, true, true>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red, x, slot,
+                                                   p.ep0 + (unsigned)s, &gate);
+      } else {
+        bad = !fha_body<3, 3, true, 7, true>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red, x, slot,
+                                             p.ep0 + (unsigned)s);
+      }
+    }  // (FG 2, a worker without a forward tile: the heads that overwrite what its dW1 tile read waited for it)
     stamp(s, 1);
-    if (!bar.sync(2 * s, bad)) return;
+    if constexpr (FG > 0) {
+      bar.arrive(2 * s, bad);  // (the dW1 waves wait for their own column tiles, the role for all of them)
+    } else {
+      if (!bar.sync(2 * s, bad)) return;
+    }
     stamp(s, 2);
     if (slot < p.nw) {
       if (slot < t1n) {  // ---- dW1 tile (x, slot) over the whole batch + reg + SGD (W1, W1s, b1)
         TileGeom g{a.H, a.P + a.bias_col, n, x * 16, slot * 32};
-        EpiW1 epi{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, 1, 0, reg, lr, a.xscale, {}, a.b1,
-                  a.gb1, 0, nullptr};
-        epi.W1s = a.W1s;
-        wsk_tile<bf16, 1, 2, 8, true, true, 3, 4, 3, uint8_t, float, true, false, kSc1>(
-            a.dZ1, (ld + 63) / 64, static_cast<const uint8_t*>(p.XT0) + off, a.ldxt, g, epi, red, 0, nullptr);
+        const EpiW1 e1{a.W1, a.gW1, static_cast<bf16*>(a.W1p), (size_t)a.H * a.P, a.P, 1, 0, reg, lr, a.xscale, {},
+                       a.b1, a.gb1, 0, nullptr};
+        if constexpr (FG > 0) {
+          EpiW1Gate epi{e1, &bar, 2 * s, tn, &s_stop};
+          epi.W1s = a.W1s;
+          wsk_tile<bf16, 1, 2, 8, true, true, 3, 4, 3, uint8_t, float, true, false, kSc1>(
+              a.dZ1, (ld + 63) / 64, static_cast<const uint8_t*>(p.XT0) + off, a.ldxt, g, epi, red, 0, nullptr);
+        } else {
+          EpiW1 epi = e1;
+          epi.W1s = a.W1s;
+          wsk_tile<bf16, 1, 2, 8, true, true, 3, 4, 3, uint8_t, float, true, false, kSc1>(
+              a.dZ1, (ld + 63) / 64, static_cast<const uint8_t*>(p.XT0) + off, a.ldxt, g, epi, red, 0, nullptr);
+        }
       }
-    } else {  // ---- the role: W2[:, x rows] from the dW2 partials and db2 into this XCD's b2 copy, side by side
+    } else {
+      if constexpr (FG > 0) {  // (the role reads every column tile's dW2 partials and D: it waits for all of them)
+        if (t < 64) bar.poll(2 * s, 0, tn);
+        __syncthreads();
+      }
+    }
+    if (slot == p.nw && !s_stop) {  // ---- the role: W2[:, x rows] from the dW2 partials and db2 into this XCD's b2
+      // copy, side by side
       // (waves [0, dw): dW2, one element per lane; waves [dw, 8): db2, up to 4 classes per wave with every row's
       // loads in flight at once -- one after the other they were this workgroup's 4.2 us critical path,
       // profiles/r6/xstep_ab_r6a.jsonl)
@@ -343,7 +410,12 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
       }
     }
     stamp(s, 3);
-    if (!bar.sync(2 * s + 1, false)) return;
+    if constexpr (FG == 2) {
+      bar.arrive(2 * s + 1, s_stop != 0);  // (the next forward's waves wait for the flags they need)
+      if (s_stop) return;
+    } else {
+      if (!bar.sync(2 * s + 1, s_stop != 0)) return;
+    }
   }
 }
 
@@ -357,6 +429,8 @@ bool mlp_xstep_ok(const SplitStepArgs& a, const HeadArgs& h) {
          h.dZ1 == a.dZ1 && !h.dZ1_planes && a.dw2part && h.dw2part == a.dw2part && a.dw2_cols == 16 && !h.a1 &&
          !h.loss_partial && a.n > 0 && a.n % 16 == 0 && nw + 1 <= kXsWgsPerXcd && nw + 1 <= 31 &&
          device_cu_count() == 8 * kXsWgsPerXcd && mlp_wgrad_dz_swz_ok(a) &&
+         // (the forward GEMM's wave 7 has no K range: the gated forward stages b1 / W2 / b2 there, fha_body PsGate)
+         xs_cdiv(xs_cdiv(a.P, 32), 8) * 7 * 32 >= a.P &&
          (int64_t)a.P * a.ldxt < (int64_t)kOOB && (int64_t)xs_cdiv(a.H, 16) * 16 * a.ld < (int64_t)kOOB / 4;
 }
 
@@ -367,15 +441,17 @@ void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hi
   CME_REQUIRE(mlp_xstep_ok(a, h), "xstep: the plan's step is not the XCD-local pipeline's shape");
   const int tm = xs_cdiv(a.H, 16), tn = xs_cdiv(a.n, kXsCols), t1n = xs_cdiv(a.P + a.bias_col, 32);
   CME_REQUIRE(p.nw == mlp_xstep_workers(a) && p.nw + 1 + p.npf <= kXsWgsPerXcd && p.nw + 1 <= 31 && p.npf >= 0 &&
-                  (p.npf == 0 || p.bar == 1),
+                  (p.npf == 0 || p.bar == 1) && p.bar >= 0 && p.bar <= 3,
               "xstep: the workers + the role (+ prefetch workgroups, flag-line barrier only) must fit one XCD's CUs");
   CME_REQUIRE(p.gran && p.ctl && p.Dx && p.b2x && p.err && p.X0 && p.XT0 && p.Xs0 && p.lab0 && p.xs_tile > 0,
               "xstep: scratch buffers missing");
   CME_REQUIRE(p.gstart0 % 16 == 0 && p.B % 16 == 0 && p.shard_off % 16 == 0 && p.B >= a.n && p.N_end >= p.B,
               "xstep: every step must start a 16-sample tile of the fragment-ordered pixels");
   CME_REQUIRE(a.ld >= a.n && a.ld % 16 == 0, "xstep: activation pitch");
-  if (p.bar == 1) xstep_kernel<1><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
-  else xstep_kernel<0><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  if (p.bar == 3) xstep_kernel<1, 2><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  else if (p.bar == 2) xstep_kernel<1, 1><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  else if (p.bar == 1) xstep_kernel<1, 0><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  else xstep_kernel<0, 0><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   CME_LAUNCH_CHECK(s);
 }
 

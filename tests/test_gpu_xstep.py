@@ -88,13 +88,16 @@ def test_xstep_falls_back_where_it_does_not_apply():
     assert torch.equal(small[0].params, small[1].params)
 
 
-def test_xstep_barrier_forms_give_the_same_bits():
-    """The two XCD-local barrier forms (MlpStep.xstep_bar: 0 an atomic counter, 1 a flag line in the XCD's L2) order
-    the same work: the same bits, over launches that alternate the control banks."""
+@pytest.mark.parametrize("bar", [0, 1, 2])
+def test_xstep_barrier_forms_give_the_same_bits(bar):
+    """The XCD-local barrier forms (MlpStep.xstep_bar: 0 an atomic counter, 1 a flag line in the XCD's L2, 2 the flag
+    line with the first barrier fine-grained per dW1 wave, 3 both barriers fine-grained -- the forward's waves wait
+    for their own dW1 tiles, the default) order the same work: the same bits as the default form, over launches that
+    alternate the control banks."""
     n, N = 800, 4 * 800
     engines = _pair(100, n, N, seed=11)
     engines[0]._hip_step().xstep = -1
-    engines[0]._hip_step().xstep_bar = 0
+    engines[0]._hip_step().xstep_bar = bar
     for g0, k in ((0, 9), (n, 3), (2 * n, 5)):
         for e in engines:
             _plan(e, g0, k, n, N)
@@ -103,7 +106,8 @@ def test_xstep_barrier_forms_give_the_same_bits():
         assert torch.equal(engines[0].params, engines[1].params)
 
 
-def test_xstep_handoff_timeout_applies_nothing():
+@pytest.mark.parametrize("bar", [1, 2, 3])
+def test_xstep_handoff_timeout_applies_nothing(bar):
     """A z2 hand-off that never completes (row tile 3 of column tile 0 withholds its granules): every XCD's
     workgroup of that column tile times out, arrives 'bad' at the first barrier, and the launch stops before any
     update -- the parameters are bitwise those before the plan and the sticky error word is set."""
@@ -114,6 +118,7 @@ def test_xstep_handoff_timeout_applies_nothing():
     e.set_params(*nn.params)
     e.load_dataset(x, y)
     e.set_store_a1(False)
+    e._hip_step().xstep_bar = bar
     _plan(e, 0, 2, n, N)  # a good plan first (launch 0)
     torch.cuda.synchronize()
     assert e._hip_step().xstep_used == 1, e._hip_step().xstep_reason
