@@ -482,7 +482,9 @@ struct MlpStep {
     if (!fh_allgather || !ag_counters || !ag_slabs || !ag_err) return "the all-gather forward + head is off";
     if (!w1_swz || !x_swz || !dz_swz) return "a fragment-ordered operand is off";
     if (off % 16 != 0) return "a step off the 16-sample grid";
-    if (C > 16 || head_dw2 == 0 || (head_dw2 < 0 && n < 768)) return "the head leaves no dW2 partials";
+    // (head_dw2 auto: the pipeline always takes the head's dW2 partials -- its role workgroup sums them; below 768
+    // columns the two-launch form forms dW2 in its own role instead, so the bits there match head_dw2 = 1)
+    if (C > 16 || head_dw2 == 0) return "the head leaves no dW2 partials";
     a = split_args(off, n, scale, reg, lr, 1, 0);
     if (!cme::mlp_fwd_swz_ok(a) || cme::mlp_split_w1_planes_read(a) || !cme::mlp_split_wgrad_fp32_dz(a))
       return "the forward / weight gradient would not read fp32 operands";

@@ -20,7 +20,9 @@ def _stream():
 
 
 def _pair(H, n, N, seed):
-    """Two engines with the same weights and data: [0] the two-launch step (xstep = 0), [1] the pipeline (auto)."""
+    """Two engines with the same weights and data: [0] the two-launch step (xstep = 0), [1] the pipeline
+    (auto); the head's dW2 partials on below 768 columns too (the pipeline always takes them, and [1]'s own
+    two-launch steps must then match [0]'s)."""
     x, y = synthetic_mnist(N, seed=seed)
     nn = NeuralNetwork([784, H, 10])
     out = []
@@ -30,6 +32,7 @@ def _pair(H, n, N, seed):
         e.load_dataset(x, y)
         e.set_store_a1(False)
         e._hip_step().xstep = xs
+        e._hip_step().head_dw2 = 1
         out.append(e)
     return out
 
@@ -38,7 +41,7 @@ def _plan(e, g0, count, n, N):
     e._hip_step().run_steps(g0, count, n, 0, n, N, 1.0 / n, REG, LR, 1, _stream())
 
 
-@pytest.mark.parametrize("H,n", [(100, 800), (128, 800), (64, 960), (100, 784)])
+@pytest.mark.parametrize("H,n", [(100, 800), (128, 800), (64, 960), (100, 784), (100, 400), (128, 512)])
 def test_xstep_is_bitwise_the_two_launch_step(H, n):
     """Two epochs (with the wrap to sample 0) as one plan, then plans from other start batches (the other control
     bank, then the first again), then a two-launch step and a plan again: parameters bitwise equal throughout."""
@@ -66,7 +69,7 @@ def test_xstep_is_bitwise_the_two_launch_step(H, n):
 
 def test_xstep_falls_back_where_it_does_not_apply():
     """Plans the pipeline does not take run the two-launch loop (bitwise the same as xstep = 0): steps off the
-    16-sample grid, a batch below the head's dW2 threshold; xstep = 1 (required) then raises."""
+    16-sample grid, the head's dW2 partials off; xstep = 1 (required) then raises."""
     n, N = 800, 3 * 800 + 48
     engines = _pair(100, n, N, seed=7)
     for e in engines:
@@ -81,6 +84,7 @@ def test_xstep_falls_back_where_it_does_not_apply():
         _plan(engines[1], 8, 1, n, N)
     small = _pair(100, 400, 2000, seed=8)
     for e in small:
+        e._hip_step().head_dw2 = 0
         _plan(e, 0, 3, 400, 2000)
     torch.cuda.synchronize()
     assert small[1]._hip_step().xstep_used == 0
