@@ -1713,10 +1713,11 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
   CME_REQUIRE(!a.dz_swz || (af && vec == 3 && do_w1 && mlp_wgrad_dz_swz_ok(a)),
               "wgrad: the fragment-ordered dZ1 needs fp32 dZ1, 16-byte pixel pairs and pair-aligned K ranges");
   if (a.xp_dbg) {  // diagnostics (bench/kbench.py xp rows): the push form's two headline shapes only
-    CME_REQUIRE(fu == 2 && vec == 3 && (a.dz_swz || (!af && a.npz == 3)),
-                "wgrad: xp_dbg ablations exist for the push form at 16-byte pixel pairs, fragment-ordered fp32 dZ1 "
-                "(n = 800) or the three dZ1 planes (n = 100)");
+    CME_REQUIRE(fu == 2 && vec == 3 && (a.dz_swz || af || a.npz == 3),
+                "wgrad: xp_dbg ablations exist for the push form at 16-byte pixel pairs with fp32 dZ1 (fragment-ordered "
+                "or row-major: n = 800) or the three dZ1 planes (n = 100)");
     if (a.dz_swz) wgrad_split_kernel<3, 3, true, 2, true, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
+    else if (af) wgrad_split_kernel<3, 3, true, 2, false, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
     else wgrad_split_kernel<3, 3, false, 2, false, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
   } else if (a.dz_swz) {
     if (fu == 2) wgrad_split_kernel<3, 3, true, 2, true><<<grid, kWT, 0, s>>>(b, t1, t1n, t2);
