@@ -21,7 +21,7 @@ def main(argv=None):
     ap.add_argument("--n", type=int, default=12288)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--forms", default="all", choices=["all", "stores"])
+    ap.add_argument("--forms", default="all", choices=["all", "stores", "two_step"])
     a = ap.parse_args(argv)
     import torch
 
@@ -64,6 +64,29 @@ def main(argv=None):
 
     nx = g - 8
     comp = a.iters * (g * g + nx * nx) * 4  # read the grid, write the interior
+    if a.forms == "two_step":
+        # the temporal-blocked walk (two time steps per sweep, stencil_step2_bc) against two one-step LDS launches,
+        # both with the boundary condition; --iters counts time steps (even)
+        scale = 0.999
+        steps = a.iters // 2
+        one = lambda d, s: k.stencil_step_bc(d.data_ptr(), s.data_ptr(), g, g, 8, xcfl, ycfl, 2, scale, st)  # noqa: E731
+        it0 = a.iters
+        ref = run(one).clone()
+        ms = timeit(one)
+        print(json.dumps({"form": "one-step lds + bc, per time step", "ms": round(ms, 3),
+                          "compulsory_GBps": round(comp / (ms * 1e-3) / 1e9, 1)}), flush=True)
+        a.iters = steps
+        for rows, ahead in ((64, 4), (64, 2), (32, 4), (96, 4), (128, 4), (128, 2), (32, 2), (64, 3), (64, 1), (96, 2),
+                            (64, 2), (32, 2), (64, 4)):
+            fn = lambda d, s, r=rows, h=ahead: k.stencil_step2_bc(d.data_ptr(), s.data_ptr(), g, g, 8, xcfl, ycfl,  # noqa: E731
+                                                                  scale, st, r, h)
+            out = run(fn)
+            same = bool(torch.equal(out, ref))
+            ms = timeit(fn)
+            print(json.dumps({"two_step_rows": rows, "ahead": ahead, "time_steps": it0, "ms": round(ms, 3),
+                              "bitwise_equal": same, "compulsory_GBps": round(comp / (ms * 1e-3) / 1e9, 1)}),
+                  flush=True)
+        return
     prod = lambda d, s: k.stencil_step(d.data_ptr(), s.data_ptr(), g, g, 8, xcfl, ycfl, 2, st)  # noqa: E731
     ref = run(prod).clone()
     ms = timeit(prod)

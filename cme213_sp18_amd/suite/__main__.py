@@ -163,8 +163,8 @@ def cmd_stencil(a):
 
     _cuda()
     p = hw3.SimParams.from_file(a.params) if a.params else hw3.SimParams(a.nx, a.ny, 1.0, 1.0, a.iters, a.order)
-    chosen = ([v for v, f in (("global", a.g), ("block", a.b), ("shared", a.s), ("vec", a.v)) if f]
-              or ["global", "block", "shared", "vec"])
+    chosen = ([v for v, f in (("global", a.g), ("block", a.b), ("shared", a.s), ("vec", a.v), ("shared2", a.t)) if f]
+              or ["global", "block", "shared", "vec", "shared2"])
     g0 = hw3.init_grid(p)
     t0 = time.perf_counter()
     ref = hw3.cpu_computation(g0, p)
@@ -249,6 +249,8 @@ def main(argv=None) -> int:
     s.add_argument("-b", action="store_true", help="register-blocked (loop) kernel")
     s.add_argument("-s", action="store_true", help="LDS-tiled kernel")
     s.add_argument("-v", action="store_true", help="16-byte-vector register-window kernel")
+    s.add_argument("-t", action="store_true",
+                   help="LDS-tiled kernel with temporal blocking: two time steps per sweep of the grid (order 8)")
     s.add_argument("--params")
     s.add_argument("--nx", type=int, default=4096)
     s.add_argument("--ny", type=int, default=4096)

@@ -26,7 +26,7 @@ import torch
 from ..utils.common import ulp_distance
 from ._dev import EventTimer, host, kernels, require_cuda, stream_handle
 
-VARIANTS = {"global": 0, "block": 1, "shared": 2, "vec": 3}
+VARIANTS = {"global": 0, "block": 1, "shared": 2, "vec": 3, "shared2": 4}  # shared2: LDS walk, 2 steps per sweep
 MAX_ULPS = 512  # main.cu:229
 
 
@@ -151,15 +151,31 @@ def gpu_step(grid: Grid, p: SimParams, variant: int, fused: bool = True) -> None
     grid.swap()
 
 
+def gpu_step2(grid: Grid, p: SimParams) -> None:
+    """TWO time steps in one sweep (the temporal-blocked LDS walk, order 8): bitwise two ``gpu_step`` calls."""
+    kernels().stencil_step2_bc(grid.next.data_ptr(), grid.curr.data_ptr(), p.gx, p.gy, p.order, p.xcfl, p.ycfl,
+                               p.bc_scale, stream_handle())
+    grid.swap()
+
+
 def gpu_computation(host_grid: np.ndarray, p: SimParams, variant: str | int = "shared",
                     fused: bool = True) -> tuple[np.ndarray, float]:
-    """Run ``iters`` steps on the GPU; returns (final grid, milliseconds)."""
+    """Run ``iters`` steps on the GPU; returns (final grid, milliseconds).  ``shared2`` (order 8): pairs of steps
+    per sweep, an odd last step by the one-step LDS walk."""
     v = VARIANTS[variant] if isinstance(variant, str) else int(variant)
+    if v == 4 and p.order != 8:
+        v = VARIANTS["shared"]
     g = Grid(host_grid)
     require_cuda(g.curr)
     with EventTimer() as t:
-        for _ in range(p.iters):
-            gpu_step(g, p, v, fused)
+        if v == 4:
+            for _ in range(p.iters // 2):
+                gpu_step2(g, p)
+            if p.iters % 2:
+                gpu_step(g, p, VARIANTS["shared"], fused)
+        else:
+            for _ in range(p.iters):
+                gpu_step(g, p, v, fused)
     return g.to_host(), t.ms
 
 

@@ -40,17 +40,19 @@ struct Coef<8> {
   }
 };
 
-// value at (x, y) given accessors for the x-line and the y-column
+// value at (x, y) given accessors for the x-line and the y-column.  Explicit FMAs: every kernel that inlines this
+// (one-step, two-step, any walk direction) evaluates the same chain -- with contraction left to the compiler the
+// one- and two-step walks differed by 1-3 ULP at scattered points (bench/dbg/stencil2_diag.py)
 template <int ORDER, class FX, class FY>
 __device__ __forceinline__ float apply_stencil(float center, FX fx, FY fy, float xcfl, float ycfl) {
   constexpr int B = Coef<ORDER>::B;
   float sx = 0.f, sy = 0.f;
 #pragma unroll
   for (int k = -B; k <= B; ++k) {
-    sx += Coef<ORDER>::c(k) * fx(k);
-    sy += Coef<ORDER>::c(k) * fy(k);
+    sx = __builtin_fmaf(Coef<ORDER>::c(k), fx(k), sx);
+    sy = __builtin_fmaf(Coef<ORDER>::c(k), fy(k), sy);
   }
-  return center + xcfl * sx + ycfl * sy;
+  return __builtin_fmaf(ycfl, sy, __builtin_fmaf(xcfl, sx, center));
 }
 
 template <int ORDER>
@@ -286,6 +288,151 @@ __device__ __forceinline__ void stencil_lds_body(float* __restrict__ next, const
     stencil_lds_walk<ORDER, ROWS, AHEAD, CP, 1, NTST>(next, curr, gx, gy, nx, ny, xcfl, ycfl, bx, by, xrow);
 }
 
+// variant 4 "lds2" (order 8): TWO time steps per sweep of the grid -- temporal blocking on the LDS walk above, so
+// the grid crosses HBM once per two iterations instead of once per iteration.  A wave owns a 256-column strip of the
+// INTERMEDIATE grid u1 (4 columns per lane) and writes u2 for the inner 248 columns (lanes 1..62); lanes 0 and 63
+// carry u1 only, as the x-halo of the second step (strips overlap by 8 columns: 3 % of the work done twice).  Walking
+// down, each new u0 row (loaded kLdsAhead rows ahead) completes a 9-row u0 window: stage 1 forms u1 of its centre
+// row -- the stencil, or the boundary condition u0 * scale on the border rows / columns, exactly as the one-step
+// launch forms them -- and pushes it into a 9-row u1 window; once that is full, stage 2 forms u2 of ITS centre row.
+// The x-neighbours of both stages come from the wave's LDS rows (u0 with the strip's halo float4s; u1 needs none).
+// A block of ROWS output rows reads ROWS + 16 u0 rows (the halo of both steps).  Every value is the same expression
+// on the same operands as in two one-step launches: bitwise those (tests/test_gpu_suite.py).
+template <int ORDER, int ROWS, int AHEAD = kLdsAhead>
+__device__ __forceinline__ void stencil_lds2_walk(float* __restrict__ next, const float* __restrict__ curr, int gx,
+                                                  int gy, int nx, int ny, float xcfl, float ycfl, float scale, int bx,
+                                                  int by, f32x4 (*xr0)[66], f32x4 (*xr1)[66]) {
+  constexpr int B = Coef<ORDER>::B;
+  static_assert(B == 4, "the two-step walk's strip geometry is order 8's (a float4 of halo per side and step)");
+  constexpr int WIN = 2 * B + 1;
+  constexpr int OUTW = 256 - 2 * B * 1;  // u2 columns per strip (lanes 1..62)
+  const int lane = threadIdx.x, w = threadIdx.y;
+  const int s0 = B + OUTW * bx;          // first u2 column of the strip (grid coordinates)
+  const int colL = s0 - 4 + 4 * lane;    // this lane's 4 grid columns [colL, colL + 4) of u0 / u1
+  const int yo0 = B + (by * 4 + w) * ROWS;
+  if (yo0 >= B + ny) return;  // wave-uniform (no workgroup barrier below)
+  const int nout = min(ROWS, B + ny - yo0);
+  const int g0 = yo0 - 2 * B, nin = nout + 4 * B;  // u0 rows [g0, g0 + nin)
+  const __amdgpu_buffer_rsrc_t rc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(curr), (short)0, (int)((int64_t)gx * gy * 4), 0x00020000);
+  constexpr int64_t kOffOOB = (int64_t)0x7FFFFFF0 / 4;
+  auto at = [&](int g, int col) -> int64_t {
+    return (g >= 0 && g < gy && col >= 0) ? (int64_t)g * gx + col : kOffOOB;
+  };
+  auto centre = [&](int i) { return ld4p<0>(rc, i < nin ? at(g0 + i, colL) : kOffOOB); };
+  // the strip's halo float4s (lane 0 the one left of the strip, lane 63 the one right of it) of the u0 window's
+  // CENTRE row at iteration i (row g0 + i - B, where stage 1 uses them), queued with the window's new rows
+  auto halo = [&](int i) {
+    const int g = g0 + i - B;
+    return ld4p<0>(rc, i < nin ? (lane == 0 ? at(g, colL - 4) : (lane == 63 ? at(g, colL + 4) : kOffOOB)) : kOffOOB);
+  };
+  f32x4 q[AHEAD], hq[AHEAD];
+#pragma unroll
+  for (int i = 0; i < AHEAD; ++i) {
+    q[i] = centre(i);
+    hq[i] = halo(i);
+  }
+  f32x4 w0[WIN], w1[WIN];  // w0[k] = u0 row (a - B + k), w1[k] = u1 row (o - B + k)
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  for (int i = 0; i < nin; ++i) {
+#pragma unroll
+    for (int k = 0; k < WIN - 1; ++k) w0[k] = w0[k + 1];
+    w0[WIN - 1] = q[0];
+    const f32x4 hv = hq[0];
+#pragma unroll
+    for (int k = 0; k < AHEAD - 1; ++k) {
+      q[k] = q[k + 1];
+      hq[k] = hq[k + 1];
+    }
+    q[AHEAD - 1] = centre(i + AHEAD);
+    hq[AHEAD - 1] = halo(i + AHEAD);
+    if (i < 2 * B) continue;  // (uniform) the u0 window is not full yet
+    // ---- stage 1: u1 of row a
+    const int a = g0 + i - B;
+    f32x4* r0 = xr0[i & 1];
+    r0[1 + lane] = w0[B];
+    if (lane == 0) r0[0] = hv;
+    if (lane == 63) r0[65] = hv;
+    wave_sync();
+    const f32x4 lf = r0[lane], rt = r0[lane + 2];
+    const bool brow = a < B || a >= gy - B;
+    float line[12];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      line[j] = lf[j];
+      line[4 + j] = w0[B][j];
+      line[8 + j] = rt[j];
+    }
+    f32x4 u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = colL + j;
+      u[j] = (brow || c < B || c >= gx - B)
+                 ? w0[B][j] * scale
+                 : apply_stencil<ORDER>(
+                       line[4 + j], [&](int k) { return line[4 + j + k]; }, [&](int k) { return w0[B + k][j]; },
+                       xcfl, ycfl);
+    }
+#pragma unroll
+    for (int k = 0; k < WIN - 1; ++k) w1[k] = w1[k + 1];
+    w1[WIN - 1] = u;
+    if (i < 4 * B) continue;  // (uniform) the u1 window is not full yet
+    // ---- stage 2: u2 of row o (an interior row of this block)
+    const int o = a - B;
+    f32x4* r1 = xr1[i & 1];
+    r1[1 + lane] = w1[B];
+    wave_sync();
+    const f32x4 lf1 = r1[lane], rt1 = r1[lane + 2];
+    if (lane >= 1 && lane <= 62) {
+      float l1[12];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        l1[j] = lf1[j];
+        l1[4 + j] = w1[B][j];
+        l1[8 + j] = rt1[j];
+      }
+      f32x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v[j] = apply_stencil<ORDER>(
+            l1[4 + j], [&](int k) { return l1[4 + j + k]; }, [&](int k) { return w1[B + k][j]; }, xcfl, ycfl);
+      const int64_t rowc = (int64_t)o * gx + colL;
+      float* dst = next + rowc;
+      if (colL + 4 <= B + nx && (rowc & 3) == 0) {
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (colL + j < B + nx) dst[j] = v[j];
+      }
+    }
+  }
+}
+
+// the border of u2: next = (curr * scale) * scale -- the boundary condition applied twice, as two one-step launches
+// apply it (two roundings)
+__device__ __forceinline__ void bc2_cells(float* __restrict__ next, const float* __restrict__ curr, int gx, int gy,
+                                          int b, float scale, int64_t first, int64_t stride);
+
+template <int ORDER, int ROWS, int AHEAD = kLdsAhead>
+__global__ __launch_bounds__(256) void stencil_lds2_fused(float* __restrict__ next, const float* __restrict__ curr,
+                                                          int gx, int gy, int nx, int ny, float xcfl, float ycfl,
+                                                          int nbx, int nint, float scale) {
+  const int id = blockIdx.x;
+  if (id >= nint) {
+    const int64_t tid = (int64_t)(id - nint) * 256 + threadIdx.y * 64 + threadIdx.x;
+    bc2_cells(next, curr, gx, gy, Coef<ORDER>::B, scale, tid, (int64_t)(gridDim.x - nint) * 256);
+    return;
+  }
+  __shared__ f32x4 x0[4][2][66], x1[4][2][66];
+  stencil_lds2_walk<ORDER, ROWS, AHEAD>(next, curr, gx, gy, nx, ny, xcfl, ycfl, scale, id % nbx, id / nbx,
+                                        x0[threadIdx.y], x1[threadIdx.y]);
+}
+
 // border strips: rows [0,b) and [gy-b,gy) (full width), columns [0,b) and [gx-b,gx) of the middle rows;
 // `first`/`stride` enumerate the border cells over the calling threads
 __device__ __forceinline__ void bc_cells(float* __restrict__ next, const float* __restrict__ curr, int gx, int gy,
@@ -305,6 +452,27 @@ __device__ __forceinline__ void bc_cells(float* __restrict__ next, const float* 
       idx = (left ? i : i + (gx - b)) + (int64_t)gx * (b + j);
     }
     next[idx] = curr[idx] * scale;
+  }
+}
+
+__device__ __forceinline__ void bc2_cells(float* __restrict__ next, const float* __restrict__ curr, int gx, int gy,
+                                          int b, float scale, int64_t first, int64_t stride) {
+  const int64_t n_top = (int64_t)gx * b;
+  const int64_t n_side = (int64_t)(gy - 2 * b) * b;
+  const int64_t total = 2 * n_top + 2 * n_side;
+  for (int64_t t = first; t < total; t += stride) {
+    int64_t idx;
+    if (t < n_top) idx = t;
+    else if (t < 2 * n_top) idx = (t - n_top) + (int64_t)gx * (gy - b);
+    else {
+      const int64_t u = t - 2 * n_top;
+      const bool left = u < n_side;
+      const int64_t v = left ? u : u - n_side;
+      const int64_t j = v / b, i = v % b;
+      idx = (left ? i : i + (gx - b)) + (int64_t)gx * (b + j);
+    }
+    const float u1 = curr[idx] * scale;
+    next[idx] = u1 * scale;
   }
 }
 
@@ -426,6 +594,55 @@ void stencil_step_bc(float* next, const float* curr, int gx, int gy, int order, 
     case 4: launch<4>(next, curr, gx, gy, xcfl, ycfl, variant, scale, with_bc, s); break;
     case 8: launch<8>(next, curr, gx, gy, xcfl, ycfl, variant, scale, with_bc, s); break;
     default: CME_REQUIRE(false, "stencil_step: order must be 2, 4 or 8");
+  }
+  CME_LAUNCH_CHECK(s);
+}
+
+namespace {
+template <int ROWS, int AHEAD>
+void launch_lds2(float* next, const float* curr, int gx, int gy, float xcfl, float ycfl, float scale, hipStream_t s) {
+  constexpr int B = 4;
+  const int nx = gx - 2 * B, ny = gy - 2 * B;
+  const int nbx = (nx + 247) / 248, nby = (ny + 4 * ROWS - 1) / (4 * ROWS);
+  const int nint = nbx * nby;
+  const int64_t bc_cells_total = 2 * ((int64_t)gx * B + (int64_t)(gy - 2 * B) * B);
+  const int nbc = (int)std::min<int64_t>((bc_cells_total + 255) / 256, 1024);
+  stencil_lds2_fused<8, ROWS, AHEAD><<<nint + nbc, dim3(64, 4), 0, s>>>(next, curr, gx, gy, nx, ny, xcfl, ycfl, nbx,
+                                                                        nint, scale);
+}
+}  // namespace
+
+void stencil_step2_bc(float* next, const float* curr, int gx, int gy, int order, float xcfl, float ycfl, float scale,
+                      hipStream_t s, int rows, int ahead) {
+  CME_REQUIRE(order == 8, "stencil_step2_bc: the two-step LDS walk is built for order 8");
+  CME_REQUIRE((int64_t)gx * gy * 4 < (int64_t)0x7FFFFFF0, "stencil_step2_bc: grid too large for 32-bit buffer offsets");
+  CME_REQUIRE(gx > 8 && gy > 8, "stencil_step2_bc: grid smaller than its border");
+  if (rows <= 0) {  // rows per wave: one round of resident workgroups (~4 per CU) with >= 2 per CU if any does
+    // (bench/stencil_tune.py --forms two_step, profiles/r6/stencil/: 4096^2 -> 32, 8192^2 -> 96, 12288^2 -> 64)
+    const int nbx = (gx - 8 + 247) / 248;
+    auto wgs = [&](int r) { return nbx * ((gy - 8 + 4 * r - 1) / (4 * r)); };
+    rows = 64;
+    for (int r : {96, 64, 32})
+      if (wgs(r) >= 512 && wgs(r) <= 1024) {
+        rows = r;
+        break;
+      }
+    if (wgs(32) < 512) rows = 32;
+  }
+  if (ahead <= 0) ahead = 2;  // (2 rows of loads ahead: fewer registers, more waves -- faster than 4 at every size)
+  // (rows, ahead): the production choice and the tuning grid of bench/stencil_tune.py --two-step
+  switch (rows * 10 + ahead) {
+    case 644: launch_lds2<64, 4>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    case 642: launch_lds2<64, 2>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    case 324: launch_lds2<32, 4>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    case 964: launch_lds2<96, 4>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    case 1284: launch_lds2<128, 4>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    case 1282: launch_lds2<128, 2>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    case 322: launch_lds2<32, 2>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    case 643: launch_lds2<64, 3>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    case 641: launch_lds2<64, 1>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    case 962: launch_lds2<96, 2>(next, curr, gx, gy, xcfl, ycfl, scale, s); break;
+    default: CME_REQUIRE(false, "stencil_step2_bc: (rows, ahead) not instantiated");
   }
   CME_LAUNCH_CHECK(s);
 }

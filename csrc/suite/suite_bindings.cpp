@@ -49,6 +49,11 @@ void bind_suite(py::module_& m) {
     stencil_step_bc(P<float>(next), P<const float>(curr), gx, gy, order, xcfl, ycfl, variant, scale, true, S(s));
   }, py::arg("next"), py::arg("curr"), py::arg("gx"), py::arg("gy"), py::arg("order"), py::arg("xcfl"),
      py::arg("ycfl"), py::arg("variant"), py::arg("scale"), py::arg("stream") = 0);
+  sm.def("stencil_step2_bc", [](uintptr_t next, uintptr_t curr, int gx, int gy, int order, float xcfl, float ycfl,
+                                float scale, uintptr_t s, int rows, int ahead) {
+    stencil_step2_bc(P<float>(next), P<const float>(curr), gx, gy, order, xcfl, ycfl, scale, S(s), rows, ahead);
+  }, py::arg("next"), py::arg("curr"), py::arg("gx"), py::arg("gy"), py::arg("order"), py::arg("xcfl"),
+     py::arg("ycfl"), py::arg("scale"), py::arg("stream") = 0, py::arg("rows") = 0, py::arg("ahead") = 0);
   sm.def("stencil_bc", [](uintptr_t next, uintptr_t curr, int gx, int gy, int b, float scale, uintptr_t s) {
     stencil_bc(P<float>(next), P<const float>(curr), gx, gy, b, scale, S(s));
   }, py::arg("next"), py::arg("curr"), py::arg("gx"), py::arg("gy"), py::arg("b"), py::arg("scale"),

@@ -48,6 +48,11 @@ void stencil_lds_tune(float* next, const float* curr, int gx, int gy, float xcfl
                       int nt, hipStream_t s);
 // next(border) = curr(border) * scale  (border width b)
 void stencil_bc(float* next, const float* curr, int gx, int gy, int b, float scale, hipStream_t s);
+// TWO time steps (each: interior stencil + border * scale) in one sweep of the grid: the LDS walk with temporal
+// blocking (order 8); bitwise two stencil_step_bc launches
+// (rows, ahead <= 0: the production walk -- 64 rows per wave, 4 rows of loads ahead; others: tuning)
+void stencil_step2_bc(float* next, const float* curr, int gx, int gy, int order, float xcfl, float ycfl, float scale,
+                      hipStream_t s, int rows = 0, int ahead = 0);
 
 // -------------------------------------------------------------- hw1 sums
 // sums[0] = sum of even values, sums[1] = sum of odd values (64-bit, device)

@@ -75,7 +75,7 @@ def test_pagerank_gpu(variant, nodes, edges):
 
 
 # ------------------------------------------------------------------ hw3
-@pytest.mark.parametrize("variant", ["global", "block", "shared", "vec"])
+@pytest.mark.parametrize("variant", ["global", "block", "shared", "vec", "shared2"])
 @pytest.mark.parametrize("order", [2, 4, 8])
 @pytest.mark.parametrize("shape", [(64, 64), (257, 131), (1000, 77), (1023, 5)])
 def test_stencil_gpu(variant, order, shape):
@@ -142,4 +142,17 @@ def test_stencil_fused_bc_equals_two_launches(variant, order):
     g0 = hw3.init_grid(p)
     a, _ = hw3.gpu_computation(g0, p, variant, fused=True)
     b, _ = hw3.gpu_computation(g0, p, variant, fused=False)
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("iters", [1, 2, 7, 8])
+@pytest.mark.parametrize("shape", [(9, 9), (248, 256), (249, 257), (1000, 77), (600, 600), (2100, 530)])
+def test_stencil_two_steps_per_sweep_is_bitwise_two_launches(shape, iters):
+    """The temporal-blocked LDS walk (two time steps per sweep, order 8: strips of 248 output columns over 256 of
+    the intermediate grid, 64-row blocks reading 16 rows of halo) against the one-step LDS walk: the same bits,
+    across strip and block edges, grids narrower than one strip, and an odd last step."""
+    p = hw3.SimParams(shape[0], shape[1], 1.0, 1.0, iters, 8)
+    g0 = hw3.init_grid(p)
+    a, _ = hw3.gpu_computation(g0, p, "shared")
+    b, _ = hw3.gpu_computation(g0, p, "shared2")
     assert np.array_equal(a, b)
