@@ -207,7 +207,10 @@ struct XsWalk {
 
 // FG: 0 two full XCD barriers per step; 1 the first fine-grained (EpiW1Gate); 2 both (the forward's waves wait for
 // their own dW1 tiles: fha_body's PsGate) -- no full barrier left, only flags.
-template <int BAR, int FG>
+// DIAG: the diagnostics instantiation that honours the stamp buffers (XStepPlan::stamps, SplitStepArgs::stamps,
+// HeadArgs::stamps); the production one has none of their branches (a runtime diagnostics branch in a production
+// kernel cost a launch 0.8 us in round 5, profiles/r5/regression_bisect.md).
+template <int BAR, int FG, bool DIAG = false>
 __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h, XStepPlan p, int tm, int tn,
                                                     int t1n) {
   static_assert(FG == 0 || BAR == 1, "the fine-grained barriers need the flag line");
@@ -240,7 +243,7 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
                  slot, p.err, limit_us, &s_stop};
   const int n = a.n, ld = a.ld;
   const float reg = (float)a.reg, lr = (float)a.lr;
-  unsigned long long* st = p.stamps;  // diagnostics: [step][8][32][4]
+  unsigned long long* st = DIAG ? p.stamps : nullptr;  // diagnostics: [step][8][32][4]
   auto stamp = [&](int s, int i) {
     if (st && t == 0 && s < p.stamp_steps)
       st[(((size_t)s * 8 + x) * kXsWgsPerXcd + slot) * 4 + i] = __builtin_amdgcn_s_memrealtime();
@@ -287,10 +290,12 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
     bool bad = false;
     if (slot < p.nw && slot < tn) {
       SplitStepArgs f = a;
+      if constexpr (!DIAG) f.stamps = nullptr;  // (fha_body's per-workgroup stamps)
       f.X = p.X0 + off * a.P;
       f.Xs = p.Xs0 + off / 16 * p.xs_tile;
       f.XT = p.XT0 + off;
       HeadArgs hh = h;
+      if constexpr (!DIAG) hh.stamps = nullptr;  // (the forward K loop's per-wave stamps)
       hh.labels = p.lab0 + off;
       hh.D = p.Dx + (size_t)x * 16 * ld;  // this XCD's copy of D (the role's db2 reads it)
       hh.b2 = s == 0 ? (const void*)a.b2 : (const void*)(p.b2x + x * 16);
@@ -448,7 +453,11 @@ void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hi
   CME_REQUIRE(p.gstart0 % 16 == 0 && p.B % 16 == 0 && p.shard_off % 16 == 0 && p.B >= a.n && p.N_end >= p.B,
               "xstep: every step must start a 16-sample tile of the fragment-ordered pixels");
   CME_REQUIRE(a.ld >= a.n && a.ld % 16 == 0, "xstep: activation pitch");
-  if (p.bar == 3) xstep_kernel<1, 2><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  const bool diag = p.stamps || a.stamps || h.stamps;
+  CME_REQUIRE(!diag || p.bar == 3 || p.bar == 1, "xstep: the stamps exist in the diagnostics builds of barrier forms 1 and 3");
+  if (diag && p.bar == 3) xstep_kernel<1, 2, true><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  else if (diag) xstep_kernel<1, 0, true><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  else if (p.bar == 3) xstep_kernel<1, 2><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   else if (p.bar == 2) xstep_kernel<1, 1><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   else if (p.bar == 1) xstep_kernel<1, 0><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   else xstep_kernel<0, 0><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
