@@ -98,8 +98,8 @@ struct PsGate {
   uint32_t limit_us = 0;
 };
 
-template <int CP>
-struct EpiSigGate {  // (EpiSigLdsT's arithmetic; b1 from LDS, staged by wave 7)
+template <int CP, bool A1 = false>
+struct EpiSigGate {  // (EpiSigLdsT's arithmetic; b1 from LDS, staged by wave 7; A1: the a1 store's test compiled in)
   float* a1;
   float (*a1s)[33];
   int ld, r0, c0;
@@ -135,13 +135,20 @@ struct EpiSigGate {  // (EpiSigLdsT's arithmetic; b1 from LDS, staged by wave 7)
   __device__ __forceinline__ void operator()(int, int row, int col, float v) {
     const float s = ag_sigmoid(v * xscale + b1s[row - r0]);
     a1s[row - r0][col - c0] = s;
-    if (a1) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), make_rsrc(a1), (row * ld + col) * 4, 0, 0);
+    if constexpr (A1) {
+      if (a1) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s), make_rsrc(a1), (row * ld + col) * 4, 0, 0);
+    }
   }
 };
 
 // blk: the workgroup's slot in the XCD-grouped grid (the hardware XCD is blk & 7).  red: >= 8 * 2 * 4 * 64
 // floats of LDS.
-template <int NPW, int VEC, bool AF, int SWZ = 0, bool PS = false, bool PSG = false>
+// DG (PS only): the diagnostics build -- the stamps and the hand-off test hook (SplitStepArgs::ag_test_skip); a
+// production PS body compiles neither, nor the a1 store and the loss partials (the pipeline takes neither: mlp_xstep_ok)
+// HK (PS only): the non-PS body's runtime tests kept in the build -- bit 0 the hand-off hook, bit 1 the loss
+// partials, bit 2 the a1 store; each is a no-op in the pipeline (mlp_xstep_ok), but with all three the compiler's
+// schedule of the body is 0.25 us faster per step (xstep.hip's launcher, profiles/r6/hk/)
+template <int NPW, int VEC, bool AF, int SWZ = 0, bool PS = false, bool PSG = false, bool DG = !PS, int HK = 0>
 __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs& h,
                                          unsigned long long* __restrict__ counters, gran_t* __restrict__ slabs,
                                          int* __restrict__ err, int tm, int tn, int blk, float* red, int ps_rt = 0,
@@ -176,7 +183,7 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
   if (ct >= tn || rt >= tm) return true;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
   const int t = threadIdx.x, H = f.H, C = h.C, n = f.n;
   const int r0 = rt * 16, c0 = ct * kCols;
-  unsigned long long* st = f.stamps ? f.stamps + (size_t)blk * 4 : nullptr;  // diagnostics only
+  unsigned long long* st = (DG && f.stamps) ? f.stamps + (size_t)blk * 4 : nullptr;  // diagnostics only
   // (PS: the stamps are held in registers and stored at the end -- a store in the middle of the body puts its
   // completion in front of the next vmcnt wait -- with three more per workgroup after the first 256 x 4: the GEMM
   // returned, W2 staged, z2 partial formed)
@@ -229,7 +236,7 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
   TileGeom g{H, n, f.P, r0, c0};
   if constexpr (PSG) {  // (wave 7 stages b1, W2 and b2 into LDS inside the GEMM, after its wait: EpiSigGate)
     __shared__ float b1s[16];
-    EpiSigGate<CP> epi{f.a1, a1s, f.ld, r0, c0, f.xscale, ps_gate, b1s, w2s, b2s, f.b1, static_cast<const float*>(h.W2),
+    EpiSigGate<CP, (HK & 4) != 0> epi{f.a1, a1s, f.ld, r0, c0, f.xscale, ps_gate, b1s, w2s, b2s, f.b1, static_cast<const float*>(h.W2),
                        static_cast<const float*>(h.b2), H, C};
     fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, h.stamps);
     stamp2(0);
@@ -274,7 +281,7 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
       }
     }
     // (test hook: one workgroup of column tile 0 never publishes, so that tile's polls time out)
-    if (!(f.ag_test_skip == rt && ct == 0)) {
+    if (!((DG || (HK & 1)) && f.ag_test_skip == rt && ct == 0)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (4 * kg + i < C) gran_store(slabs + (size_t)(ct * tm + rt) * 16 * kCols + (4 * kg + i) * kCols + zc, p[i], ep);
@@ -320,7 +327,7 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
     if (PS || rt == 0)
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, d), make_rsrc(h.D),
                                             (cval && cls < C) ? (cls * h.ldd + gcol) * 4 : kOOB, 0, 0);
-    if (rt == 0 && h.loss_partial) {
+    if ((!PS || (HK & 2)) && rt == 0 && h.loss_partial) {
       float lp = (cval && hit) ? -__logf(yh) : 0.f;
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) lp += __shfl_xor(lp, o, 64);
@@ -328,7 +335,7 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
     }
   }
   __syncthreads();
-  if (rt == 0 && h.loss_partial && t < 2) {  // one partial per 16 columns (the column head's layout)
+  if ((!PS || (HK & 2)) && rt == 0 && h.loss_partial && t < 2) {  // one partial per 16 columns (the column head's layout)
     const int vb = ct * 2 + t;
     if (vb * 16 < n) {
       float sl = 0.f;

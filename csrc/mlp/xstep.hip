@@ -208,9 +208,10 @@ struct XsWalk {
 // FG: 0 two full XCD barriers per step; 1 the first fine-grained (EpiW1Gate); 2 both (the forward's waves wait for
 // their own dW1 tiles: fha_body's PsGate) -- no full barrier left, only flags.
 // DIAG: the diagnostics instantiation that honours the stamp buffers (XStepPlan::stamps, SplitStepArgs::stamps,
-// HeadArgs::stamps); the production one has none of their branches (a runtime diagnostics branch in a production
+// HeadArgs::stamps) and the hand-off test hook (SplitStepArgs::ag_test_skip); the production one has none of their
+// branches (dropping the stamps' took the walking step 9.86 -> 9.55 us, profiles/r6/xstep_ab_r6k_diag_templated.jsonl) (a runtime diagnostics branch in a production
 // kernel cost a launch 0.8 us in round 5, profiles/r5/regression_bisect.md).
-template <int BAR, int FG, bool DIAG = false>
+template <int BAR, int FG, bool DIAG = false, int HK = 0>
 __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h, XStepPlan p, int tm, int tn,
                                                     int t1n) {
   static_assert(FG == 0 || BAR == 1, "the fine-grained barriers need the flag line");
@@ -310,11 +311,11 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
         gate.s_stop = &s_stop;
         gate.err = p.err;
         gate.limit_us = limit_us;
-        bad = !fha_body<3, 3, true, 7, true, true>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red, x, slot,
-                                                   p.ep0 + (unsigned)s, &gate);
+        bad = !fha_body<3, 3, true, 7, true, true, DIAG, HK>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red,
+                                                             x, slot, p.ep0 + (unsigned)s, &gate);
       } else {
-        bad = !fha_body<3, 3, true, 7, true>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red, x, slot,
-                                             p.ep0 + (unsigned)s);
+        bad = !fha_body<3, 3, true, 7, true, false, DIAG>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red, x,
+                                                          slot, p.ep0 + (unsigned)s);
       }
     }  // (FG 2, a worker without a forward tile: the heads that overwrite what its dW1 tile read waited for it)
     stamp(s, 1);
@@ -431,7 +432,7 @@ bool mlp_xstep_ok(const SplitStepArgs& a, const HeadArgs& h) {
   const int nw = std::max(tn, t1n);
   return a.H <= 128 && tm <= 8 && a.C <= 16 && a.bias_col && a.sgd == 1 && a.xf_world == 0 && a.npw == 3 &&
          a.npz == 3 && a.w1_swz && a.W1s && a.x_swz && a.Xs && a.dz_swz == 1 && a.dZ1 && h.dz_swz == 1 &&
-         h.dZ1 == a.dZ1 && !h.dZ1_planes && a.dw2part && h.dw2part == a.dw2part && a.dw2_cols == 16 && !h.a1 &&
+         h.dZ1 == a.dZ1 && !h.dZ1_planes && a.dw2part && h.dw2part == a.dw2part && a.dw2_cols == 16 && !h.a1 && !a.a1 &&
          !h.loss_partial && a.n > 0 && a.n % 16 == 0 && nw + 1 <= kXsWgsPerXcd && nw + 1 <= 31 &&
          device_cu_count() == 8 * kXsWgsPerXcd && mlp_wgrad_dz_swz_ok(a) &&
          // (the forward GEMM's wave 7 has no K range: the gated forward stages b1 / W2 / b2 there, fha_body PsGate)
@@ -453,11 +454,15 @@ void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hi
   CME_REQUIRE(p.gstart0 % 16 == 0 && p.B % 16 == 0 && p.shard_off % 16 == 0 && p.B >= a.n && p.N_end >= p.B,
               "xstep: every step must start a 16-sample tile of the fragment-ordered pixels");
   CME_REQUIRE(a.ld >= a.n && a.ld % 16 == 0, "xstep: activation pitch");
-  const bool diag = p.stamps || a.stamps || h.stamps;
-  CME_REQUIRE(!diag || p.bar == 3 || p.bar == 1, "xstep: the stamps exist in the diagnostics builds of barrier forms 1 and 3");
+  const bool diag = p.stamps || a.stamps || h.stamps || a.ag_test_skip >= 0;
+  CME_REQUIRE(!diag || p.bar == 3 || p.bar == 1,
+              "xstep: the stamps and the hand-off test hook exist in the diagnostics builds of barrier forms 1 and 3");
   if (diag && p.bar == 3) xstep_kernel<1, 2, true><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   else if (diag) xstep_kernel<1, 0, true><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
-  else if (p.bar == 3) xstep_kernel<1, 2><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  // (the production form keeps fha_body's three no-op runtime tests, HK = 7: measured 9.55-9.61 us against 9.81-9.86
+  // without them and 9.62-9.94 with any one or two -- the compiler schedules the body differently; alternated four
+  // and three times on two boxes, profiles/r6/hk/)
+  else if (p.bar == 3) xstep_kernel<1, 2, false, 7><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   else if (p.bar == 2) xstep_kernel<1, 1><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   else if (p.bar == 1) xstep_kernel<1, 0><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   else xstep_kernel<0, 0><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);

@@ -110,11 +110,13 @@ def test_xstep_barrier_forms_give_the_same_bits(bar):
         assert torch.equal(engines[0].params, engines[1].params)
 
 
-@pytest.mark.parametrize("bar", [1, 2, 3])
+@pytest.mark.parametrize("bar", [1, 3])
 def test_xstep_handoff_timeout_applies_nothing(bar):
     """A z2 hand-off that never completes (row tile 3 of column tile 0 withholds its granules): every XCD's
     workgroup of that column tile times out, arrives 'bad' at the first barrier, and the launch stops before any
-    update -- the parameters are bitwise those before the plan and the sticky error word is set."""
+    update -- the parameters are bitwise those before the plan and the sticky error word is set.  (The withholding
+    hook exists only in the diagnostics build of the kernel, barrier forms 1 and 3; the waits, bad arrivals and stop
+    are the production code.)"""
     n, N = 800, 4 * 800
     x, y = synthetic_mnist(N, seed=3)
     nn = NeuralNetwork([784, 100, 10])
