@@ -900,6 +900,7 @@ def test_fragment_ordered_dz1_is_bitwise_the_row_major_dz1(n):
         e.set_store_a1(False)
         st = e._hip_step()
         st.a_fp32, st.dz_swz = afp, dzs
+        st.xstep = 0  # (the two-launch step's forms; the XCD-local pipeline has its own tests: test_gpu_xstep.py)
         engines.append(e)
     te = MlpEngine(nn.H, "f32", max_cols=n, device="cuda", backend="torch", path="split3")
     te.set_params(*nn.params)
