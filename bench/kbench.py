@@ -16,7 +16,8 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# (CME_PKG_ROOT: a variant copy of the package, bench/flags_ab_build.py)
+sys.path.insert(0, os.environ.get("CME_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main(argv=None):

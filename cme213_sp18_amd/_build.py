@@ -56,7 +56,8 @@ def _stale(src: Path, obj: Path, hdr_mtime: float) -> bool:
     if not obj.exists():
         return True
     om = obj.stat().st_mtime
-    return om < src.stat().st_mtime or om < hdr_mtime
+    deps = [CSRC / d for d in UNIT_DEPS.get(src.name, [])]
+    return om < src.stat().st_mtime or om < hdr_mtime or any(om < d.stat().st_mtime for d in deps)
 
 
 def _run(cmd: list[str]) -> None:
@@ -65,9 +66,24 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build command failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
 
 
+# per-translation-unit code-generation flags, each measured (process-alternated A/B of whole libraries that differ
+# only in that unit's flags: bench/flags_ab_build.py + bench/flags_ab_run.sh)
+UNIT_FLAGS = {
+    # the XCD-local pipeline: the machine scheduler's memory-clause strategy, walking step 9.55-9.58 -> 9.46-9.50 us
+    # (max-ilp 9.54-9.59, iterative-ilp 10.2-10.4, -O2 9.64-9.66; profiles/r6/flags/)
+    "xstep.hip": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
+    # the wide fp32 A-in-registers engine (mlp_split.hip's fp32 launchers, compiled apart): max-ILP, 784-4096-10 fp32
+    # walking step 57.4-58.0 -> 55.4-55.5 us; the same strategy on the whole of mlp_split.hip made the bf16 wide step
+    # +3.3 us and the n = 100 two-launch step +0.4 us (profiles/r6/flags_split/)
+    "mlp_wide_f32.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+}
+# sources a unit includes besides the headers (its object is stale when they change)
+UNIT_DEPS = {"mlp_wide_f32.hip": ["mlp/mlp_split.hip"]}
+
+
 def _hip_compile_cmd(src: Path, obj: Path) -> list[str]:
     return [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", str(src), "-o",
-            str(obj), f"-I{CSRC}", "-Wno-unused-result", *_pybind_includes()]
+            str(obj), f"-I{CSRC}", "-Wno-unused-result", *_pybind_includes(), *UNIT_FLAGS.get(src.name, [])]
 
 
 def _cpu_compile_cmd(src: Path, obj: Path) -> list[str]:

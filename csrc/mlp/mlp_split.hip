@@ -587,6 +587,8 @@ __device__ __forceinline__ void st_bf16(__amdgpu_buffer_rsrc_t r, int off, bf16 
 // Every workgroup must be resident at once (one per CU: the launcher's LDS request and tm * tn <= CUs).  A poll
 // that outlasts ag_wait_us of wall time sets *err (MlpEngine.kernel_error()) and the workgroup writes nothing
 // more; the weight-gradient launch that follows applies nothing (SplitStepArgs::ag_err).
+}  // namespace
+// (outside the anonymous namespace: the fp32 launchers of mlp_wide_f32.hip, the same source compiled apart, take it)
 struct RegaAgArgs {
   HeadArgs h{};
   unsigned long long* counters = nullptr;  // [column tile * kRegaAgCounterStride], monotonic: the launch epoch
@@ -598,6 +600,7 @@ struct RegaAgArgs {
   int ep_off = 0;    // LDS byte offset of the epoch + 2 flag words (past every other LDS use of the launch)
   int tiling = 0;    // 0: 128 x 128, 1: 64 x 64 -- the low bit of every tag (both tilings share the granules)
 };
+namespace {
 constexpr int kRegaAgCounterStride = 32;  // uint64 words: one 256-byte line per column-tile counter
 // LDS of the fused head for a BM x BN tile: the D tile [16][BN + 4], the a1 tile [BM][BN + 4] (row pitch BN + 4:
 // conflict-free MFMA-layout reads), z2 [16][17], loss [16]
@@ -1488,6 +1491,27 @@ void launch_wgrad_glds(const SplitStepArgs& a, int t2, int tb, hipStream_t s) {
 
 }  // namespace
 
+// The fp32 (split3) launches of the A-in-registers engine are compiled in their own translation unit,
+// mlp_wide_f32.hip (this file again under CME_WIDE_F32_TU), with the machine scheduler's max-ILP strategy: its
+// K loops (MFMA + the in-register split VALU) run 784-4096-10 fp32 2.2 us per step faster that way, while the same
+// strategy makes the bf16 engines and the small-layer kernels of this file slower (profiles/r6/flags_split/).
+namespace wide_f32 {
+void fwd1_rega(const SplitStepArgs& a, hipStream_t s);
+void fwd1_rega_ag(const SplitStepArgs& a, RegaAgArgs g, hipStream_t s);
+void wgrad_rega(const SplitStepArgs& a, int t2, int tb, hipStream_t s);
+}  // namespace wide_f32
+
+#ifdef CME_WIDE_F32_TU
+namespace wide_f32 {
+void fwd1_rega(const SplitStepArgs& a, hipStream_t s) { launch_fwd1_rega<float>(a, s); }
+void fwd1_rega_ag(const SplitStepArgs& a, RegaAgArgs g, hipStream_t s) {
+  if (cdiv(a.P, ra::kBK) == 25) launch_fwd1_rega_ag_k<float, 25>(a, g, s);
+  else launch_fwd1_rega_ag_k<float, 0>(a, g, s);
+}
+void wgrad_rega(const SplitStepArgs& a, int t2, int tb, hipStream_t s) { launch_wgrad_rega<float>(a, t2, tb, s); }
+}  // namespace wide_f32
+#else
+
 // the wave-split-K dW1 reads fp32 dZ1 (split3, a_fp32, 16-byte rows)
 bool small_wgrad_fp32_ok(const SplitStepArgs& a) {
   return a.npz == 3 && (a.a_fp32 & 2) && a.dZ1 != nullptr && al16(a.dZ1) && a.ld % 4 == 0;
@@ -1597,8 +1621,7 @@ int mlp_fwd1_wide_ag(const SplitStepArgs& a, const HeadArgs& h, unsigned long lo
   if (bm == 128) {
     const bool k25 = cdiv(a.P, ra::kBK) == 25;
     if (a.npw == 3) {
-      if (k25) launch_fwd1_rega_ag_k<float, 25>(a, g, s);
-      else launch_fwd1_rega_ag_k<float, 0>(a, g, s);
+      wide_f32::fwd1_rega_ag(a, g, s);
     } else {
       if (k25) launch_fwd1_rega_ag_k<bf16, 25>(a, g, s);
       else launch_fwd1_rega_ag_k<bf16, 0>(a, g, s);
@@ -1618,7 +1641,7 @@ void mlp_split_fwd1(const SplitStepArgs& a, hipStream_t s) {
               "split path: operand too large for 32-bit buffer offsets");
   CME_REQUIRE(a.ld >= a.n, "split path: ld >= n");
   if (rega_fwd_ok(a)) {
-    if (a.npw == 3) launch_fwd1_rega<float>(a, s);
+    if (a.npw == 3) wide_f32::fwd1_rega(a, s);
     else launch_fwd1_rega<bf16>(a, s);
     CME_LAUNCH_CHECK(s);
     return;
@@ -1655,7 +1678,7 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s) {
     const int tbf = do_roles ? cdiv((a.bias_col ? 0 : a.H) + a.C, kWKS) : 0;
     const SplitStepArgs& c = a;
     if (rega_wgrad_ok(c)) {
-      if (c.npz == 3) launch_wgrad_rega<float>(c, t2f, tbf, s);
+      if (c.npz == 3) wide_f32::wgrad_rega(c, t2f, tbf, s);
       else launch_wgrad_rega<bf16>(c, t2f, tbf, s);
       CME_LAUNCH_CHECK(s);
       return;
@@ -1771,5 +1794,7 @@ void mlp_split_sgd(float* params, const float* grads, int64_t count, double lr, 
     sgd_planes_kernel<1><<<grid, 256, 0, s>>>(params, grads, count, (float)lr, (bf16*)W1p, w1_count, status);
   CME_LAUNCH_CHECK(s);
 }
+
+#endif  // CME_WIDE_F32_TU
 
 }  // namespace cme
