@@ -19,11 +19,11 @@ from cme213_sp18_amd import _build as B  # noqa: E402
 
 
 def main(argv):
-    unit = ROOT / "csrc" / "mlp" / "xstep.hip"
+    units = [ROOT / "csrc" / "mlp" / "xstep.hip"]
     specs = []
     for a in argv:
-        if a.startswith("--unit="):
-            unit = ROOT / a.split("=", 1)[1]
+        if a.startswith("--unit="):  # (comma-separated: every listed unit gets the variant's flags)
+            units = [ROOT / u for u in a.split("=", 1)[1].split(",")]
             continue
         name, flags = a.split("=", 1)
         specs.append((name, shlex.split(flags)))
@@ -36,12 +36,15 @@ def main(argv):
         pkg = d / "cme213_sp18_amd"
         shutil.copytree(ROOT / "cme213_sp18_amd", pkg, ignore=shutil.ignore_patterns("__pycache__", "*.so", "*.tmp"))
         shutil.copy2(B.PKG / f"_cpu{B.EXT}", pkg / f"_cpu{B.EXT}")
-        obj = d / f"hip_{unit.stem}.o"
-        subprocess.run(B._hip_compile_cmd(unit, obj) + flags, check=True)
-        mine = [obj if o.name == f"hip_{unit.stem}.o" else o for o in objs]
+        mine = list(objs)
+        for unit in units:
+            obj = d / f"hip_{unit.stem}.o"
+            subprocess.run(B._hip_compile_cmd(unit, obj) + flags, check=True)
+            mine = [obj if o.name == obj.name else o for o in mine]
         subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", *map(str, mine), "-o",
                         str(pkg / f"_hip{B.EXT}")], check=True)
-        os.remove(obj)
+        for unit in units:
+            os.remove(d / f"hip_{unit.stem}.o")
         print(f"built {name}: {' '.join(flags)}", flush=True)
 
 

@@ -91,19 +91,29 @@ def _cpu_compile_cmd(src: Path, obj: Path) -> list[str]:
             f"-I{CSRC}", "-Wall", "-Wextra", "-Wno-unused-parameter", *_pybind_includes()]
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> dict[str, Path]:
-    OBJ.mkdir(parents=True, exist_ok=True)
+# the diagnostics library (build(diag=True), `--diag`): the same kernels with the two-launch kernels' stamps compiled
+# in, as module _hip_diag (loaded instead of _hip when CME_DIAG=1: cme213_sp18_amd/_native.py; bench/stamps_*.py)
+DIAG_FLAGS = ["-DCME_DIAG_STAMPS=1", "-DCME_HIP_MODULE=_hip_diag"]
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True, diag: bool = False) -> dict[str, Path]:
+    obj_dir = OBJ.parent / "obj_diag" if diag else OBJ
+    obj_dir.mkdir(parents=True, exist_ok=True)
     hdr = _headers_mtime()
     jobs = jobs or min(8, os.cpu_count() or 4)
     out: dict[str, Path] = {}
 
+    def hip_cmd(src, obj):
+        return _hip_compile_cmd(src, obj) + (DIAG_FLAGS if diag else [])
+
     plans = {
-        "_hip": ([(s, OBJ / f"hip_{s.stem}.o") for s in _hip_sources()], _hip_compile_cmd,
-                 lambda objs, so: [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o",
-                                   str(so)]),
-        "_cpu": ([(s, OBJ / f"cpu_{s.stem}.o") for s in _cpu_sources()], _cpu_compile_cmd,
-                 lambda objs, so: [CXX, "-shared", "-fPIC", "-fopenmp", *map(str, objs), "-o", str(so)]),
+        "_hip_diag" if diag else "_hip": (
+            [(s, obj_dir / f"hip_{s.stem}.o") for s in _hip_sources()], hip_cmd,
+            lambda objs, so: [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(so)]),
     }
+    if not diag:
+        plans["_cpu"] = ([(s, OBJ / f"cpu_{s.stem}.o") for s in _cpu_sources()], _cpu_compile_cmd,
+                         lambda objs, so: [CXX, "-shared", "-fPIC", "-fopenmp", *map(str, objs), "-o", str(so)])
     todo = []
     for name, (pairs, mk, _) in plans.items():
         for src, obj in pairs:
@@ -136,8 +146,9 @@ def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--diag", action="store_true", help="the diagnostics library _hip_diag (stamps compiled in)")
     a = ap.parse_args(argv)
-    build(force=a.force, jobs=a.jobs)
+    build(force=a.force, jobs=a.jobs, diag=a.diag)
     return 0
 
 

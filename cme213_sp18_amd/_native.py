@@ -9,6 +9,7 @@ raises.
 from __future__ import annotations
 
 import importlib
+import os
 import threading
 
 _lock = threading.Lock()
@@ -31,7 +32,7 @@ def _load(name: str):
             from . import _build
 
             try:
-                _build.build(verbose=True)
+                _build.build(verbose=True, diag=name == "_hip_diag")
             except Exception as e:  # pragma: no cover - surfaced to the caller
                 raise NativeExtensionError(f"could not build native extension {name}: {e}") from e
             importlib.invalidate_caches()
@@ -44,8 +45,9 @@ def _load(name: str):
 
 
 def hip():
-    """The gfx950 kernel module (``cme213_sp18_amd._hip``)."""
-    return _load("_hip")
+    """The gfx950 kernel module (``cme213_sp18_amd._hip``; with ``CME_DIAG=1`` the diagnostics build
+    ``_hip_diag`` -- the same kernels with the two-launch kernels' timing stamps compiled in)."""
+    return _load("_hip_diag" if os.environ.get("CME_DIAG") == "1" else "_hip")
 
 
 def cpu():

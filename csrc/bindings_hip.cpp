@@ -644,7 +644,11 @@ struct MlpStep {
 void bind_suite(py::module_& m);  // suite_bindings.cpp
 void bind_comm(py::module_& m);   // comm/comm_bindings.cpp
 
-PYBIND11_MODULE(_hip, m) {
+#ifndef CME_HIP_MODULE
+#define CME_HIP_MODULE _hip  // (_hip_diag: the diagnostics library, cme213_sp18_amd/_build.py --diag)
+#endif
+PYBIND11_MODULE(CME_HIP_MODULE, m) {
+  m.attr("diag_stamps") = CME_DIAG_STAMPS;
   m.doc() = "cme213_sp18_amd gfx950 HIP kernels (MFMA MLP engine + homework kernel suite)";
 
   m.def(

@@ -183,7 +183,8 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
   if (ct >= tn || rt >= tm) return true;  // padding workgroup of the XCD-grouped grid (uniform: no barrier reached)
   const int t = threadIdx.x, H = f.H, C = h.C, n = f.n;
   const int r0 = rt * 16, c0 = ct * kCols;
-  unsigned long long* st = (DG && f.stamps) ? f.stamps + (size_t)blk * 4 : nullptr;  // diagnostics only
+  constexpr bool kStamps = PS ? DG : (CME_DIAG_STAMPS != 0);  // (PS: the pipeline's DIAG build; else the diag library)
+  unsigned long long* st = (kStamps && f.stamps) ? f.stamps + (size_t)blk * 4 : nullptr;  // diagnostics
   // (PS: the stamps are held in registers and stored at the end -- a store in the middle of the body puts its
   // completion in front of the next vmcnt wait -- with three more per workgroup after the first 256 x 4: the GEMM
   // returned, W2 staged, z2 partial formed)
@@ -238,7 +239,7 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
     __shared__ float b1s[16];
     EpiSigGate<CP, (HK & 4) != 0> epi{f.a1, a1s, f.ld, r0, c0, f.xscale, ps_gate, b1s, w2s, b2s, f.b1, static_cast<const float*>(h.W2),
                        static_cast<const float*>(h.b2), H, C};
-    fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, h.stamps);
+    fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, kStamps ? h.stamps : nullptr);
     stamp2(0);
     if (*ps_gate->s_stop) {  // (a wait of this step's gate saw the launch stop: nothing is written)
       stamps_out();
@@ -250,7 +251,7 @@ __device__ __forceinline__ bool fha_body(const SplitStepArgs& f, const HeadArgs&
     const float b2v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
         make_rsrc(h.b2), (t >= 256 && t < 256 + 16 && t - 256 < C) ? (t - 256) * 4 : kOOB, 0, CP));
     EpiSigLdsT<CP> epi{f.b1, f.a1, a1s, f.ld, r0, c0, f.xscale, {}};
-    fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, h.stamps);  // (h.stamps: per-wave GEMM timeline, diagnostics)
+    fwd_tile<NPW, 2, VEC, 4, AF, SWZ, CP>(f, g, epi, red, kStamps ? h.stamps : nullptr);  // (per-wave GEMM timeline)
     stamp2(0);
     // wsk_tile ends with a barrier: a1s is complete.  Rows past H / columns past n: a1s holds stale LDS, so
     // they are masked below.  w2s / b2s are complete after the barrier below.

@@ -25,6 +25,14 @@
 
 #include "../common/hip_common.h"
 
+// The two-launch kernels' per-wave / per-workgroup s_memrealtime stamps (SplitStepArgs::stamps / wstamps,
+// HeadArgs::stamps; bench/stamps_*.py) exist only in the diagnostics library (`python -m cme213_sp18_amd._build
+// --diag` -> _hip_diag, loaded when CME_DIAG=1): their runtime tests cost the production launches 0.3-0.55 us per
+// step (profiles/r6/flags_stamps/).  The XCD-local pipeline has its own diagnostics instantiation (xstep.hip DIAG).
+#ifndef CME_DIAG_STAMPS
+#define CME_DIAG_STAMPS 0
+#endif
+
 namespace cme {
 
 // Gradient all-reduce fused into the weight-gradient launch (data parallel over xGMI, one process per

@@ -50,7 +50,7 @@ __global__ __launch_bounds__(64 * kF1KS) void fwd1_split_kernel(SplitStepArgs a,
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   TileGeom g{a.H, a.n, a.P, (bid / tiles_n) * 16 * kF1MB, (bid % tiles_n) * 16 * kF1NB};
   EpiSig epi{a.b1, a.a1, a.ld, a.xscale, {}};
-  fwd_tile<NPW, kF1NB, VEC, 4, AF>(a, g, epi, red, a.stamps);
+  fwd_tile<NPW, kF1NB, VEC, 4, AF>(a, g, epi, red, CME_DIAG_STAMPS ? a.stamps : nullptr);
 }
 
 
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
   __shared__ float xsx[FU == 2 ? 2 * kXpTile : 1];
   float* xs = FU == 2 ? xsx : red + kWKS * 4 * 64;
   float* xo = xs + kXpTile;
-  unsigned long long* wst = a.wstamps ? a.wstamps + (size_t)blockIdx.x * 8 : nullptr;  // diagnostics only
+  unsigned long long* wst = (CME_DIAG_STAMPS && a.wstamps) ? a.wstamps + (size_t)blockIdx.x * 8 : nullptr;  // diagnostics
   auto wstamp = [&](int i) {
     if (wst && threadIdx.x == 0) wst[i] = __builtin_amdgcn_s_memrealtime();
   };
@@ -322,14 +322,14 @@ __global__ __launch_bounds__(kWT) void wgrad_split_kernel(SplitStepArgs a, int t
     constexpr int U = 4;
     if constexpr (AF && DSWZ)
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, 3, uint8_t, float, true>(
-          a.dZ1, (a.ld + 63) / 64, static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi, red, 0, a.stamps);
+          a.dZ1, (a.ld + 63) / 64, static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi, red, 0, CME_DIAG_STAMPS ? a.stamps : nullptr);
     else if constexpr (AF)
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, 3, uint8_t>(a.dZ1, a.ld, static_cast<const uint8_t*>(a.XT),
-                                                                       a.ldxt, g, epi, red, 0, a.stamps);
+                                                                       a.ldxt, g, epi, red, 0, CME_DIAG_STAMPS ? a.stamps : nullptr);
     else
       wsk_tile<bf16, kWMB, kWNB, kWKS, true, true, VEC, U, NPZ, uint8_t>(static_cast<const bf16*>(a.dZ1p), a.ld,
                                                                 static_cast<const uint8_t*>(a.XT), a.ldxt, g, epi,
-                                                                red, a.H * a.ld * (int)sizeof(bf16), a.stamps);
+                                                                red, a.H * a.ld * (int)sizeof(bf16), CME_DIAG_STAMPS ? a.stamps : nullptr);
     wstamp(1);
     if (push && (xdbg & 16)) return;  // (diagnostics: no exchange work at all after the tile)
     if (push) {  // the owner-tile exchange: thread e holds element (e / 32, e % 32) of the tile
@@ -439,9 +439,9 @@ __device__ __forceinline__ void wgrad_roles(const SplitStepArgs& a, int bid, int
       }
       if (ok) epi(0, c, h, v);
     } else if (a.n % 4 == 0) {
-      wsk_tile<float, 1, 1, kWKS, true, true, 1, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red, 0, a.stamps);
+      wsk_tile<float, 1, 1, kWKS, true, true, 1, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red, 0, CME_DIAG_STAMPS ? a.stamps : nullptr);
     } else {
-      wsk_tile<float, 1, 1, kWKS, true, true, 0, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red, 0, a.stamps);
+      wsk_tile<float, 1, 1, kWKS, true, true, 0, 8>(a.D, a.ld, a.a1, a.ld, g, epi, red, 0, CME_DIAG_STAMPS ? a.stamps : nullptr);
     }
     if (!live || (push && (xdbg & 32))) return;  // (xp_dbg 32: diagnostics, the roles stop after the GEMM)
     if (push) {  // the owner-tile exchange: element e < 256 is W2[e / 16][tb * 16 + e % 16]
