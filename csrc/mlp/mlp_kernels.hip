@@ -336,8 +336,8 @@ __device__ __forceinline__ void head32(const HeadArgs& a, int ct, int t, Head32L
 #pragma unroll
     for (int j = 0; j < 4; ++j) xe[tt][j] = ld_a1((kq + 4 * tt) * 16 + 4 * g + j);
   const int lab = (int)__builtin_amdgcn_raw_buffer_load_b32(make_rsrc(a.labels), cval ? col * 4 : kOOB, 0, 0);
-  auto hstamp = [&](int i) {  // diagnostics (HeadArgs::stamps): drained, wave 0 lane 0
-    if (a.stamps) {
+  auto hstamp = [&](int i) {  // diagnostics (HeadArgs::stamps): drained, wave 0 lane 0 (the diagnostics library only)
+    if (CME_DIAG_STAMPS && a.stamps) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       const unsigned long long tt = __builtin_amdgcn_s_memrealtime();
       if (t == 0) a.stamps[(size_t)ct * 8 + i] = tt;
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
   const int H = a.H, C = a.C, ld = a.lda;
   const int row0 = (rb * 8 + w) * 16 * RT;
   auto hstamp = [&](int i) {  // diagnostics (HeadArgs::stamps, bench/stamps_hw.py): wave 0 lane 0 of the block
-    if (a.stamps && t == 0) a.stamps[(size_t)blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+    if (CME_DIAG_STAMPS && a.stamps && t == 0) a.stamps[(size_t)blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
   };
   hstamp(0);
   // ---- one burst: the z2 partial sums of (class t>>5, column t&31), W2^T operands, a1 of the tiles
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(512) void head_wide_kernel(HeadArgs a, int nrb) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  if (a.stamps) {
+  if (CME_DIAG_STAMPS && a.stamps) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     hstamp(3);
   }

@@ -622,7 +622,7 @@ __device__ __forceinline__ void ag_wave_sync() {
 // stamp i of this workgroup's 8: 0 entry, 1 K loop done, 2 z2 granules stored, 3 hand-off 1 done, 4 D stored
 // (reducers), 5 D arrived, 6 end (stores drained)
 __device__ __forceinline__ void ag_stamp(const SplitStepArgs& a, int i, bool drain = false) {
-  if (!a.stamps) return;
+  if (!CME_DIAG_STAMPS || !a.stamps) return;  // (the diagnostics library only)
   if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
 }
@@ -864,7 +864,7 @@ __device__ __forceinline__ void wide_head_ag(const SplitStepArgs& a, const RegaA
       }
     }
   }
-  if (a.stamps) {
+  if (CME_DIAG_STAMPS && a.stamps) {
     __syncthreads();
     ag_stamp(a, 6, true);
   }
