@@ -1,7 +1,7 @@
 # Round-6 wide configs: the bench form (20 warm-up steps, as the VERDICT's targets) and after 600 warm-up steps,
 # then the PMC passes of 784-4096-10 fp32 and bf16 (scripts/gpu_pmc_wide.sh) and their tables.
 set -o pipefail
-O=gpurun_out/r6/wide
+O=gpurun_out/r6/wide${TAG:-}
 mkdir -p $O
 B() { timeout -k 10 300 python bench.py --gpus 1 --steps 200 "$@"; }
 B --hidden 4096 --warmup 20 > $O/w4096_f32.json 2> $O/w4096_f32.err &&
