@@ -22,15 +22,19 @@
 //     also writes the master b2 at the plan's last step);
 //   * the other slots idle.  (Extra workgroups pulling the pixels each XCD reads next into its L2 -- this step's XT,
 //     the next step's X -- measured slower, +1.5 us per step, and so did the workers' own LDS-DMA pull during the z2
-//     wait: profiles/r6/xstep_ab_r6b.jsonl, xstep_ab_r6c_prefetch_rejected.jsonl.)
+//     wait and an LDS-DMA of the dW1 tile's pixels ahead of its GEMM (the DMAs share the in-order vmcnt with the
+//     critical loads): profiles/r6/xstep_ab_r6b.jsonl, xstep_ab_r6c_prefetch_rejected.jsonl, xpf_rejected/.)
 //
-// The two barriers per step are XCD-local (XsBar): each participant drains its stores (s_waitcnt vmcnt(0) + workgroup
-// barrier) and signals on its XCD's flag line (or counter); every read of data another workgroup of the launch wrote
-// goes through sc1 (L1-bypassing, L2-served) loads, so a CU never reuses a stale L1 line, and the producer's plain
-// stores stay in the XCD's L2 (bench/micro/xcd_barrier.hip: the same-XCD read-back checked word by word, and priced,
-// profiles/r6/xcd_barrier_micro*.jsonl).  Arithmetic
-// and summation orders are those of the two-launch step, so the parameters are bitwise equal to it
-// (tests/test_gpu_xstep.py).
+// Synchronisation is XCD-local (XsBar), in four forms (XStepPlan::bar; the default, 3, has no full barrier left):
+// each participant drains its stores (s_waitcnt vmcnt(0) + workgroup barrier) and signals on its XCD's flag line (one
+// 128-byte line, a plain-store tag per slot) or counter; in form 3 each dW1 wave waits only for the column tiles its
+// K range reads (EpiW1Gate) and each forward wave of the next step only for the dW1 tiles its K range reads (fha_body
+// PsGate; its wave 7, which has no K range, waits for all of them and the role and stages b1 / W2 / b2).  Every read
+// of data another workgroup of the launch wrote goes through sc1 (L1-bypassing, L2-served) loads, so a CU never reuses
+// a stale L1 line, and the producer's plain stores stay in the XCD's L2 (bench/micro/xcd_barrier.hip: the same-XCD
+// read-back checked word by word, and priced, profiles/r6/xcd_barrier_micro*.jsonl).  Arithmetic and summation
+// orders are those of the two-launch step, so the parameters are bitwise equal to it (tests/test_gpu_xstep.py).
+// Walking step at n = 800: 9.4-9.5 us against the two-launch loop's 14.0 (profiles/r6/flags/, docs/ROUND6_STATUS.md).
 //
 // Failure semantics: a z2 hand-off wait that outlasts SplitStepArgs::ag_wait_us sets *err and makes its workgroup
 // arrive "bad" at the first barrier; every XCD's workgroup of that column tile waits for the same missing granule,
