@@ -345,6 +345,10 @@ def _run_dp_timed(ctx, global_batch: int, mode: str, tune: dict) -> dict:
     native_exec = all(tr.native_plan(p) is not None for p in timed_plans)
     runners = [tr.plan_runner(p, LR, REG) for p in timed_plans]  # resolved before the clock starts
     dt = timed(ctx, runners)
+    # which step form the native loop ran: the XCD-local pipeline (one launch per plan, csrc/mlp/xstep.hip) or the
+    # two-launch step (and why not the pipeline)
+    step = tr.engine._step if a.backend == "hip" else None
+    pipeline = None if step is None else {"used": bool(step.xstep_used), "why_not": step.xstep_reason or None}
     res = _dp_checks(ctx, tr)
     ar = measure_allreduce(tr, ctx.comm, ctx.sync) if res["ok"] else {}
     e = tr.engine
@@ -357,6 +361,7 @@ def _run_dp_timed(ctx, global_batch: int, mode: str, tune: dict) -> dict:
                parallelism=f"dp{ctx.R}",
                config={"hip_graphs": tr.use_graphs and not native_exec,
                        "executor": "native" if native_exec else ("graph" if tr.use_graphs else "eager"),
+                       **({"xstep_pipeline": pipeline} if pipeline is not None and native_exec else {}),
                        "allreduce": tr.allreduce_impl, **ar,
                        "allreduce_pred_us": round(allreduce_cost_us(ctx.R, wire, shots, fp_bytes=fp_bytes), 2)
                        if ctx.R > 1 else None,
