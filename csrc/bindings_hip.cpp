@@ -475,35 +475,53 @@ struct MlpStep {
   // The plan's step as the two-launch form would run it (run(): the all-gather forward + head with the fragment-ordered
   // operands, fp32 dZ1 in fragment order, the head's dW2 partials, SGD fused into the weight-gradient launch), or false
   // when any of those choices would differ -- the XCD-local pipeline then does not apply and run_steps launches per step.
-  const char* xstep_args(int64_t off, int n, double scale, double reg, double lr, uintptr_t stream,
+  // grid16: every step of the plan starts a 16-sample tile.  Otherwise (or below 257 columns, where dZ1 has no
+  // fragment order) the pipeline's row-major form: the pixels read row-major and fp32 dZ1 row-major -- as run() takes
+  // such a step with a_fp32 bit 1 (n = 100 takes dZ1 planes by default there: the pipeline has no plane form).
+  const char* xstep_args(int64_t off, int n, double scale, double reg, double lr, uintptr_t stream, bool grid16,
                          cme::SplitStepArgs& a, cme::HeadArgs& h) {
-    if (!split || !XT || !W1p || !dZ1p || !w1s || !xs || !dz1s || !dw2p || !bias_col) return "not the split3 H <= 128 "
-                                                                                               "layout";
+    if (!split || !XT || !W1p || !dZ1p || !w1s || !dw2p || !bias_col) return "not the split3 H <= 128 layout";
     if (!fh_allgather || !ag_counters || !ag_slabs || !ag_err) return "the all-gather forward + head is off";
-    if (!w1_swz || !x_swz || !dz_swz) return "a fragment-ordered operand is off";
-    if (off % 16 != 0) return "a step off the 16-sample grid";
+    if (!w1_swz) return "the fragment-ordered W1 is off";
     // (head_dw2 auto: the pipeline always takes the head's dW2 partials -- its role workgroup sums them; below 768
     // columns the two-launch form forms dW2 in its own role instead, so the bits there match head_dw2 = 1)
     if (C > 16 || head_dw2 == 0) return "the head leaves no dW2 partials";
     a = split_args(off, n, scale, reg, lr, 1, 0);
-    if (!cme::mlp_fwd_swz_ok(a) || cme::mlp_split_w1_planes_read(a) || !cme::mlp_split_wgrad_fp32_dz(a))
-      return "the forward / weight gradient would not read fp32 operands";
+    if (!cme::mlp_fwd_swz_ok(a) || cme::mlp_split_w1_planes_read(a)) return "the forward would not read fp32 W1";
     a.w1_swz = 1;
     a.W1s = P_<float>(w1s);
-    a.x_swz = 1;
-    a.Xs = reinterpret_cast<const char*>(xs) + off / 16 * ((int64_t)((P + 63) / 64) * 1024);
     h = cme::HeadArgs{};
     h.a1 = a.a1; h.lda = ld; h.W2 = a.W2; h.b2 = a.b2; h.labels = a.labels; h.H = H; h.C = C;
     h.n = n; h.scale = scale; h.D = a.D; h.ldd = ld; h.dZ1 = a.dZ1; h.ldz = ld; h.dZ1_bf16 = nullptr;
     h.dZ1_planes = nullptr; h.npz = npz; h.loss_partial = nullptr; h.shift = shift; h.mode = cme::HEAD_TRAIN;
     h.z2part = P_<float>(z2p);
     h.stamps = hstamps ? reinterpret_cast<unsigned long long*>(hstamps) : nullptr;  // (diagnostics)
+    bool frag = grid16 && x_swz && dz_swz && xs && dz1s && cme::mlp_split_wgrad_fp32_dz(a);
+    if (frag) {
+      cme::SplitStepArgs t = a;
+      t.x_swz = 1;
+      t.dZ1 = P_<float>(dz1s);
+      frag = cme::mlp_wgrad_dz_swz_ok(t);
+    }
+    if (frag) {
+      a.x_swz = 1;
+      a.Xs = reinterpret_cast<const char*>(xs) + off / 16 * ((int64_t)((P + 63) / 64) * 1024);
+    } else {
+      a.a_fp32 |= 2;  // (fp32 dZ1, row-major)
+      if (xs_stamps || hstamps || ag_test_skip >= 0) return "the row-major form has no diagnostics build";
+      if (xstep_bar != 3 || xstep_pf != 0) return "the row-major form exists in barrier form 3 only";
+      if (!cme::mlp_xstep_rm(a)) return "the row-major form needs n % 4 == 0 and 4-byte aligned pixel columns";
+    }
     if (!cme::mlp_fwd1_head_ok(a, h) || !cme::mlp_fwd1_head_ag_fits(a)) return "the all-gather head does not fit";
-    a.dZ1 = P_<float>(dz1s);
-    if (!cme::mlp_wgrad_dz_swz_ok(a)) return "dZ1 cannot be read in fragment order";
-    a.dz_swz = 1;
+    if (frag) {
+      a.dZ1 = P_<float>(dz1s);
+      a.dz_swz = 1;
+      h.dz_swz = 1;
+    } else {
+      a.dz_swz = 0;
+      h.dz_swz = 0;
+    }
     h.dZ1 = a.dZ1;
-    h.dz_swz = 1;
     h.dw2part = P_<float>(dw2p);
     a.dw2part = h.dw2part;
     a.dw2_cols = 16;
@@ -522,8 +540,9 @@ struct MlpStep {
                  double reg, double lr, uintptr_t stream) {
     xstep_reason = "off";
     if (xstep == 0) return false;
-    xstep_reason = "the plan's steps are off the 16-sample grid";
-    if (count <= 0 || count > (1 << 30) || gstart0 % 16 || B % 16 || shard_off % 16) return false;
+    xstep_reason = "the plan's steps start off 4-byte aligned pixel columns";
+    if (count <= 0 || count > (1 << 30) || gstart0 % 4 || B % 4 || shard_off % 4) return false;
+    const bool grid16 = gstart0 % 16 == 0 && B % 16 == 0 && shard_off % 16 == 0;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     HIP_CHECK(hipStreamIsCapturing(S(stream), &cap));
     xstep_reason = "the stream is capturing a graph";
@@ -531,7 +550,7 @@ struct MlpStep {
     int64_t g0 = gstart0 + B > N_end ? 0 : gstart0;
     cme::SplitStepArgs a;
     cme::HeadArgs h;
-    if (const char* why = xstep_args(g0 + shard_off, n, scale, reg, lr, stream, a, h)) {
+    if (const char* why = xstep_args(g0 + shard_off, n, scale, reg, lr, stream, grid16, a, h)) {
       xstep_reason = why;
       return false;
     }
@@ -561,7 +580,7 @@ struct MlpStep {
     xs_ep += (unsigned)count;
     xs_launch += 1;
     dw2_left = 1;
-    dz_left_swz = 1;
+    dz_left_swz = a.dz_swz;
     dw2_cols_last = 16;
     return true;
   }

@@ -234,8 +234,9 @@ void mlp_split_wgrad(const SplitStepArgs& a, hipStream_t s);
 // The XCD-local step pipeline (xstep.hip): every step of a native step-loop plan (MlpStep::run_steps) in ONE
 // persistent launch -- row tile rt's forward + head, dW1 tiles and W2 rows on XCD rt, two XCD-local barriers per step,
 // the z2 all-gather the only cross-XCD hand-off.  `a` / `h` are the plan's step as the two-launch form would run it
-// (fragment-ordered W1, pixels and dZ1, the head's dW2 partials, fused SGD; their pixel / label pointers are
-// re-based per step from the plan's bases).
+// (fragment-ordered W1, pixels and dZ1 -- or, a.dz_swz == 0, row-major pixels and fp32 dZ1 for steps off the
+// 16-sample grid such as n = 100 -- the head's dW2 partials, fused SGD; their pixel / label pointers are re-based per
+// step from the plan's bases).
 struct XStepPlan {
   int64_t gstart0 = 0, B = 0, shard_off = 0, N_end = 0;  // MlpStep::run_steps's walk over the dataset
   int count = 0;
@@ -262,6 +263,7 @@ struct XStepPlan {
   int stamp_steps = 0;
 };
 bool mlp_xstep_ok(const SplitStepArgs& a, const HeadArgs& h);
+int mlp_xstep_rm(const SplitStepArgs& a);  // the row-major form's dW1 vector form (0: the form does not apply)
 int mlp_xstep_workers(const SplitStepArgs& a);
 void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hipStream_t s);
 constexpr int64_t kXstepGranules = 2 * 32 * 8 * 16 * 32;

@@ -121,29 +121,44 @@ __device__ __forceinline__ __hip_bfloat16 buf_load1<__hip_bfloat16>(__amdgpu_buf
 // contiguous (KCONTIG: X[r*ld + k]) or r contiguous (X[k*ld + r]).
 // VEC: 16-byte vector loads; the caller guarantees 16-byte alignment of every
 // full vector and that kend is a multiple of V (a vector is fully in or out).
-template <typename T, int V, bool KCONTIG, int VEC>
+// CP: the loads' cache policy (kSc1: L1-bypassing, for an operand another workgroup of the launch rewrote)
+template <typename T, int V, bool KCONTIG, int VEC, int CP = 0>
 __device__ __forceinline__ void load_frag(__amdgpu_buffer_rsrc_t rs, int ld, int r, int rmax, int k, int kend,
                                           T (&out)[V], int base_off = 0) {
   // VEC == 1: 16-byte loads, every vector fully in or out (kend % V == 0)
   // VEC == 2: two 8-byte halves with separate range checks (kend % (V/2) == 0)
   // VEC == 0: element loads
+  // VEC == 4: 16-byte loads with the tail past kend zeroed in registers (fp32)
   const bool rok = r < rmax;
   if constexpr (KCONTIG && VEC == 1) {
     static_assert((V * sizeof(T)) % 16 == 0, "vector fragment must be a multiple of 16 B");
     const int off = (rok && k < kend) ? (r * ld + k) * (int)sizeof(T) + base_off : kOOB;
 #pragma unroll
     for (int q = 0; q < (int)(V * sizeof(T) / 16); ++q) {
-      const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 16 * q, 0);
+      const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 16 * q, CP);
       __builtin_memcpy(reinterpret_cast<char*>(out) + 16 * q, &w, 16);
     }
+  } else if constexpr (KCONTIG && VEC == 4) {
+    // VEC == 4 (fp32): 16-byte loads for kend % 4 == 0 -- a vector that starts in range is loaded whole (the row's
+    // pitch covers it) and its elements past kend are zeroed in registers: the same MFMA operands as element loads
+    // (out-of-range elements read 0), 2 loads instead of 8 per fragment
+    static_assert(std::is_same_v<T, float> && V == 8, "tail-masked vectors: 8 fp32 per fragment");
+    const int off = (rok && k < kend) ? (r * ld + k) * (int)sizeof(T) + base_off : kOOB;
+    const auto w0 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, CP);
+    const auto w1 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 16, CP);
+    __builtin_memcpy(reinterpret_cast<char*>(out), &w0, 16);
+    __builtin_memcpy(reinterpret_cast<char*>(out) + 16, &w1, 16);
+#pragma unroll
+    for (int j = 0; j < V; ++j)
+      if (k + j >= kend) out[j] = 0.f;
   } else if constexpr (KCONTIG && VEC == 2) {
     constexpr int HV = V / 2;  // elements per 8-byte half
     static_assert(HV * sizeof(T) == 8, "half-vector path expects 8-byte halves");
     const int base = (r * ld + k) * (int)sizeof(T) + base_off;
     const int o0 = (rok && k + HV <= kend) ? base : kOOB;
     const int o1 = (rok && k + V <= kend) ? base + 8 : kOOB;
-    const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(rs, o0, 0, 0);
-    const auto w1 = __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, 0);
+    const auto w0 = __builtin_amdgcn_raw_buffer_load_b64(rs, o0, 0, CP);
+    const auto w1 = __builtin_amdgcn_raw_buffer_load_b64(rs, o1, 0, CP);
     __builtin_memcpy(reinterpret_cast<char*>(out), &w0, 8);
     __builtin_memcpy(reinterpret_cast<char*>(out) + 8, &w1, 8);
   } else {
@@ -151,7 +166,13 @@ __device__ __forceinline__ void load_frag(__amdgpu_buffer_rsrc_t rs, int ld, int
     for (int j = 0; j < V; ++j) {
       const int kj = k + j;
       const int idx = KCONTIG ? r * ld + kj : kj * ld + r;
-      out[j] = buf_load1<T>(rs, (rok && kj < kend) ? idx * (int)sizeof(T) + base_off : kOOB);
+      const int o = (rok && kj < kend) ? idx * (int)sizeof(T) + base_off : kOOB;
+      if constexpr (CP != 0) {
+        static_assert(std::is_same_v<T, float>, "a cache policy on element loads: fp32 only");
+        out[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, o, 0, CP));
+      } else {
+        out[j] = buf_load1<T>(rs, o);
+      }
     }
   }
 }
@@ -316,9 +337,9 @@ __host__ __device__ __forceinline__ int64_t xs_off(int64_t s, int k, int npair) 
   return (((s >> 4) * npair + p) * 64 + lane) * 16 + (w & 15);
 }
 //
-// CPA (fp32 fragment-ordered A only): the A loads' cache policy -- kSc1 for an operand another workgroup of the same
-// launch rewrote since this CU last read it (the XCD-local step pipeline, xstep.hip: W1s and dZ1 are read with
-// L1-bypassing, L2-served loads; a plain load could return this CU's stale L1 line)
+// CPA (fp32 A only): the A loads' cache policy -- kSc1 for an operand another workgroup of the same launch rewrote
+// since this CU last read it (the XCD-local step pipeline, xstep.hip: W1s and dZ1 -- fragment-ordered or row-major --
+// are read with L1-bypassing, L2-served loads; a plain load could return this CU's stale L1 line)
 template <typename T, int MB, int NB, int KS, bool AK, bool BK, int VEC, int U, int NPA = 1, typename TB = T,
           typename TA = T, bool ASWZ = false, bool BSWZ = false, int CPA = 0, class Epi>
 __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, const TB* __restrict__ B, int ldb,
@@ -388,7 +409,7 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
   constexpr bool AF32 = std::is_same_v<TA, float> && !std::is_same_v<T, float>;
   static_assert(!AF32 || (std::is_same_v<T, __hip_bfloat16> && NPA == 3 && AK), "fp32 A: split3 bf16, K-contiguous");
   constexpr bool BU8 = std::is_same_v<TB, uint8_t>;
-  static_assert(CPA == 0 || (AF32 && ASWZ), "an A cache policy only on the fragment-ordered fp32 A loads");
+  static_assert(CPA == 0 || AF32, "an A cache policy only on the fp32 A loads");
   // VEC == 3 (u8 B only): chunks go in PAIRS.  Lane group grp of chunk pair (u, u + 1) covers the 16 k
   // kp + 16 grp .. kp + 16 grp + 15 (kp = the pair's first k): chunk u takes the first 8, chunk u + 1 the
   // last 8 (the MFMA sums over its chunk, so any bijection of k onto (lane group, element) that A and B
@@ -396,8 +417,10 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
   // (the u8 rows are 16 B per lane group); A keeps its 16-byte vectors.  Needs kend % 16 == 0 and 16-byte
   // aligned B rows.
   static_assert(VEC != 3 || (BU8 && U % 2 == 0 && V == 8), "paired chunks: u8 B, even U");
+  // VEC == 4 (fp32 A, u8 B): A as 16-byte vectors with the tail zeroed in registers (load_frag), B as VEC 1 / 2
+  static_assert(VEC != 4 || (AF32 && BU8), "tail-masked vectors: fp32 A, u8 B");
   constexpr int VECA = VEC == 3 ? 1 : VEC;  // the A operand's load form
-  constexpr int VA = VECA == 1 ? 1 : 0;     // fp32 A: 2 x 16-byte loads, or element loads
+  constexpr int VA = VECA == 1 ? 1 : VECA == 4 ? 4 : 0;  // fp32 A: 2 x 16-byte loads (tail-masked), or element loads
   for (int kc = kbeg; kc < kend; kc += KC * U) {
     T af[U][NPA][MB][V];
     float ar[AF32 ? U : 1][MB][V];
@@ -417,7 +440,8 @@ __device__ __forceinline__ void wsk_tile(const TA* __restrict__ A, int lda, cons
         __builtin_memcpy(reinterpret_cast<char*>(ar[u][0]) + 16, &w1, 16);
       } else if constexpr (AF32) {
 #pragma unroll
-        for (int i = 0; i < MB; ++i) load_frag<float, V, true, VA>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, ar[u][i]);
+        for (int i = 0; i < MB; ++i)
+          load_frag<float, V, true, VA, CPA>(rsA, lda, g.m0 + 16 * i + c, g.M, k, kend, ar[u][i]);
       } else {
 #pragma unroll
         for (int p = 0; p < NPA; ++p)

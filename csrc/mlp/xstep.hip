@@ -215,10 +215,19 @@ struct XsWalk {
 // HeadArgs::stamps) and the hand-off test hook (SplitStepArgs::ag_test_skip); the production one has none of their
 // branches (dropping the stamps' took the walking step 9.86 -> 9.55 us, profiles/r6/xstep_ab_r6k_diag_templated.jsonl) (a runtime diagnostics branch in a production
 // kernel cost a launch 0.8 us in round 5, profiles/r5/regression_bisect.md).
-template <int BAR, int FG, bool DIAG = false, int HK = 0>
+// RM: the operand form.  0: the fragment-ordered pixels and dZ1 (steps on the 16-sample grid, n % 16 == 0, n >= 257);
+// 1 / 2 / 3: the row-major form for every other step -- the forward reads the pixels row-major (fha_body SWZ = 1),
+// the head writes fp32 dZ1 row-major and the dW1 tile reads it with sc1 loads, 2 x 16-byte vectors (RM 1, n % 8 == 0)
+// or 16-byte pixel pairs (RM 3: a plan on the 16-sample grid, n % 16 == 0) -- the two-launch step's own forms for such
+// a step (mlp_split_wgrad vec 1 / 3) -- or, n % 4 == 0, 2 x 16-byte vectors with the tail past n zeroed in registers
+// (RM 4: the same MFMA operands as the two-launch step's element loads, vec 2; 9.25 -> see docs/ROUND6_STATUS.md), so
+// the bits are its bits.
+template <int BAR, int FG, bool DIAG = false, int HK = 0, int RM = 0>
 __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h, XStepPlan p, int tm, int tn,
                                                     int t1n) {
   static_assert(FG == 0 || BAR == 1, "the fine-grained barriers need the flag line");
+  static_assert(RM == 0 || (BAR == 1 && FG == 2), "the row-major form: barrier form 3");
+  constexpr int kSwz = RM == 0 ? 7 : 1;  // fha_body: fragment-ordered W1 (+ pixels and dZ1 in form 0)
   __shared__ __attribute__((aligned(16))) float red[8 * 1 * 2 * 4 * 64];  // both GEMM tiles' K reductions
   __shared__ int s_slot, s_stop;
   __shared__ unsigned s_x;
@@ -297,7 +306,7 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
       SplitStepArgs f = a;
       if constexpr (!DIAG) f.stamps = nullptr;  // (fha_body's per-workgroup stamps)
       f.X = p.X0 + off * a.P;
-      f.Xs = p.Xs0 + off / 16 * p.xs_tile;
+      if constexpr (RM == 0) f.Xs = p.Xs0 + off / 16 * p.xs_tile;
       f.XT = p.XT0 + off;
       HeadArgs hh = h;
       if constexpr (!DIAG) hh.stamps = nullptr;  // (the forward K loop's per-wave stamps)
@@ -315,7 +324,7 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
         gate.s_stop = &s_stop;
         gate.err = p.err;
         gate.limit_us = limit_us;
-        bad = !fha_body<3, 3, true, 7, true, true, DIAG, HK>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red,
+        bad = !fha_body<3, 3, true, kSwz, true, true, DIAG, HK>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red,
                                                              x, slot, p.ep0 + (unsigned)s, &gate);
       } else {
         bad = !fha_body<3, 3, true, 7, true, false, DIAG>(f, hh, nullptr, slabs, p.err, tm, tn, slot * 8 + x, red, x,
@@ -337,8 +346,12 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
         if constexpr (FG > 0) {
           EpiW1Gate epi{e1, &bar, 2 * s, tn, &s_stop};
           epi.W1s = a.W1s;
-          wsk_tile<bf16, 1, 2, 8, true, true, 3, 4, 3, uint8_t, float, true, false, kSc1>(
-              a.dZ1, (ld + 63) / 64, static_cast<const uint8_t*>(p.XT0) + off, a.ldxt, g, epi, red, 0, nullptr);
+          if constexpr (RM == 0)
+            wsk_tile<bf16, 1, 2, 8, true, true, 3, 4, 3, uint8_t, float, true, false, kSc1>(
+                a.dZ1, (ld + 63) / 64, static_cast<const uint8_t*>(p.XT0) + off, a.ldxt, g, epi, red, 0, nullptr);
+          else
+            wsk_tile<bf16, 1, 2, 8, true, true, RM, 4, 3, uint8_t, float, false, false, kSc1>(
+                a.dZ1, ld, static_cast<const uint8_t*>(p.XT0) + off, a.ldxt, g, epi, red, 0, nullptr);
         } else {
           EpiW1 epi = e1;
           epi.W1s = a.W1s;
@@ -431,17 +444,30 @@ __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h,
 
 }  // namespace
 
+// The row-major form's dW1 vector form (xstep_kernel RM): 1 (n % 8 == 0), 2 (n % 4 == 0), 0 none -- fp32 dZ1 and
+// 4-byte pixel rows, as the two-launch weight gradient takes them (mlp_split_wgrad: base_ok, vec)
+int mlp_xstep_rm(const SplitStepArgs& a) {
+  const bool ok = a.npz == 3 && (a.a_fp32 & 2) && a.dZ1 && ((uintptr_t)a.dZ1 & 15) == 0 && a.ld % 8 == 0 &&
+                  ((uintptr_t)a.XT & 3) == 0 && a.ldxt % 4 == 0;
+  const bool pairs = ((uintptr_t)a.XT & 15) == 0 && a.ldxt % 16 == 0 && a.n % 16 == 0;
+  return !ok ? 0 : a.n % 8 == 0 ? (pairs ? 3 : 1) : a.n % 4 == 0 ? 4 : 0;
+}
+
 bool mlp_xstep_ok(const SplitStepArgs& a, const HeadArgs& h) {
   const int tm = xs_cdiv(a.H, 16), tn = xs_cdiv(a.n, kXsCols), t1n = xs_cdiv(a.P + a.bias_col, 32);
   const int nw = std::max(tn, t1n);
-  return a.H <= 128 && tm <= 8 && a.C <= 16 && a.bias_col && a.sgd == 1 && a.xf_world == 0 && a.npw == 3 &&
-         a.npz == 3 && a.w1_swz && a.W1s && a.x_swz && a.Xs && a.dz_swz == 1 && a.dZ1 && h.dz_swz == 1 &&
-         h.dZ1 == a.dZ1 && !h.dZ1_planes && a.dw2part && h.dw2part == a.dw2part && a.dw2_cols == 16 && !h.a1 && !a.a1 &&
-         !h.loss_partial && a.n > 0 && a.n % 16 == 0 && nw + 1 <= kXsWgsPerXcd && nw + 1 <= 31 &&
-         device_cu_count() == 8 * kXsWgsPerXcd && mlp_wgrad_dz_swz_ok(a) &&
-         // (the forward GEMM's wave 7 has no K range: the gated forward stages b1 / W2 / b2 there, fha_body PsGate)
-         xs_cdiv(xs_cdiv(a.P, 32), 8) * 7 * 32 >= a.P &&
-         (int64_t)a.P * a.ldxt < (int64_t)kOOB && (int64_t)xs_cdiv(a.H, 16) * 16 * a.ld < (int64_t)kOOB / 4;
+  const bool common =
+      a.H <= 128 && tm <= 8 && a.C <= 16 && a.bias_col && a.sgd == 1 && a.xf_world == 0 && a.npw == 3 &&
+      a.npz == 3 && a.w1_swz && a.W1s && a.dZ1 && h.dZ1 == a.dZ1 && !h.dZ1_planes && a.dw2part &&
+      h.dw2part == a.dw2part && a.dw2_cols == 16 && !h.a1 && !a.a1 && !h.loss_partial && a.n > 0 &&
+      nw + 1 <= kXsWgsPerXcd && nw + 1 <= 31 && device_cu_count() == 8 * kXsWgsPerXcd &&
+      // (the forward GEMM's wave 7 has no K range: the gated forward stages b1 / W2 / b2 there, fha_body PsGate)
+      xs_cdiv(xs_cdiv(a.P, 32), 8) * 7 * 32 >= a.P && (int64_t)a.P * a.ldxt < (int64_t)kOOB &&
+      (int64_t)xs_cdiv(a.H, 16) * 16 * a.ld < (int64_t)kOOB / 4;
+  if (!common) return false;
+  if (a.dz_swz == 1)  // the fragment-ordered form
+    return a.x_swz && a.Xs && h.dz_swz == 1 && a.n % 16 == 0 && mlp_wgrad_dz_swz_ok(a);
+  return a.dz_swz == 0 && h.dz_swz == 0 && !a.x_swz && mlp_xstep_rm(a) > 0;  // the row-major form
 }
 
 int mlp_xstep_workers(const SplitStepArgs& a) { return std::max(xs_cdiv(a.n, kXsCols), xs_cdiv(a.P + a.bias_col, 32)); }
@@ -455,13 +481,22 @@ void mlp_xstep(const SplitStepArgs& a, const HeadArgs& h, const XStepPlan& p, hi
               "xstep: the workers + the role (+ prefetch workgroups, flag-line barrier only) must fit one XCD's CUs");
   CME_REQUIRE(p.gran && p.ctl && p.Dx && p.b2x && p.err && p.X0 && p.XT0 && p.Xs0 && p.lab0 && p.xs_tile > 0,
               "xstep: scratch buffers missing");
-  CME_REQUIRE(p.gstart0 % 16 == 0 && p.B % 16 == 0 && p.shard_off % 16 == 0 && p.B >= a.n && p.N_end >= p.B,
-              "xstep: every step must start a 16-sample tile of the fragment-ordered pixels");
+  const bool grid16 = p.gstart0 % 16 == 0 && p.B % 16 == 0 && p.shard_off % 16 == 0;
+  int rm = a.dz_swz ? 0 : mlp_xstep_rm(a);
+  if (rm == 3 && !grid16) rm = 1;  // (16-byte pixel pairs need every step's columns 16-byte aligned)
+  const int grid = rm ? 4 : 16;
+  CME_REQUIRE(p.gstart0 % grid == 0 && p.B % grid == 0 && p.shard_off % grid == 0 && p.B >= a.n && p.N_end >= p.B,
+              "xstep: every step must start a 16-sample tile of the fragment-ordered pixels (row-major form: 4-byte "
+              "aligned pixel columns)");
   CME_REQUIRE(a.ld >= a.n && a.ld % 16 == 0, "xstep: activation pitch");
   const bool diag = p.stamps || a.stamps || h.stamps || a.ag_test_skip >= 0;
   CME_REQUIRE(!diag || p.bar == 3 || p.bar == 1,
               "xstep: the stamps and the hand-off test hook exist in the diagnostics builds of barrier forms 1 and 3");
-  if (diag && p.bar == 3) xstep_kernel<1, 2, true><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  CME_REQUIRE(!rm || (p.bar == 3 && p.npf == 0 && !diag), "xstep: the row-major form exists in barrier form 3 only");
+  if (rm == 1) xstep_kernel<1, 2, false, 7, 1><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  else if (rm == 4) xstep_kernel<1, 2, false, 7, 4><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  else if (rm == 3) xstep_kernel<1, 2, false, 7, 3><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
+  else if (diag && p.bar == 3) xstep_kernel<1, 2, true><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   else if (diag) xstep_kernel<1, 0, true><<<8 * kXsWgsPerXcd, 512, 0, s>>>(a, h, p, tm, tn, t1n);
   // (the production form keeps fha_body's three no-op runtime tests, HK = 7: measured 9.55-9.61 us against 9.81-9.86
   // without them and 9.62-9.94 with any one or two -- the compiler schedules the body differently; alternated four

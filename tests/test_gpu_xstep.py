@@ -19,14 +19,14 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-def _pair(H, n, N, seed):
-    """Two engines with the same weights and data: [0] the two-launch step (xstep = 0), [1] the pipeline
+def _pair(H, n, N, seed, forms=(0, -1)):
+    """Engines with the same weights and data: [0] the two-launch step (xstep = 0), [1] the pipeline
     (auto); the head's dW2 partials on below 768 columns too (the pipeline always takes them, and [1]'s own
     two-launch steps must then match [0]'s)."""
     x, y = synthetic_mnist(N, seed=seed)
     nn = NeuralNetwork([784, H, 10])
     out = []
-    for xs in (0, -1):
+    for xs in forms:
         e = MlpEngine(nn.H, "f32", max_cols=n, device="cuda", path="split3")
         e.set_params(*nn.params)
         e.load_dataset(x, y)
@@ -67,21 +67,64 @@ def test_xstep_is_bitwise_the_two_launch_step(H, n):
         assert not e.kernel_error()
 
 
+@pytest.mark.parametrize("H,n,g0", [(100, 100, 0), (128, 100, 0), (100, 104, 0), (64, 200, 4), (100, 256, 0),
+                                    (100, 800, 8)])
+def test_xstep_row_major_form_is_bitwise_the_two_launch_step(H, n, g0):
+    """Steps off the 16-sample grid (n = 100: three batches in four; a plan starting at sample 8) or below 257
+    columns run the pipeline's row-major form (row-major pixels, fp32 dZ1 row-major, read with sc1 loads; dW1 as 2 x
+    16-byte vectors for n % 8 == 0, the same with the tail past n zeroed in registers for n % 4 == 0, 16-byte pixel
+    pairs on the grid at n % 16 == 0) -- bitwise the two-launch step that takes fp32 dZ1
+    (a_fp32 = 3; at n = 100 the default two-launch step takes dZ1 planes instead).  A one-step plan is first checked
+    against the torch backend's fp32 step (raw 0-255 pixels at lr 0.05 amplify rounding differences over steps, so
+    only the bitwise comparison runs longer)."""
+    N = 5 * n + 48
+    engines = _pair(H, n, N, seed=H + n + g0)
+    for e in engines:
+        e._hip_step().a_fp32 = 3
+    ref = MlpEngine([784, H, 10], "f32", max_cols=n, device="cuda", backend="torch")
+    ref.set_params(*(t.cpu().numpy() for t in (engines[0].W1, engines[0].b1, engines[0].W2, engines[0].b2)))
+    ref.load_dataset(*synthetic_mnist(N, seed=H + n + g0))
+
+    def both(fn, stage=""):
+        for e in engines:
+            fn(e)
+        torch.cuda.synchronize()
+        diff = {k: float((getattr(engines[0], k) - getattr(engines[1], k)).abs().max()) for k in ("W1", "b1", "W2", "b2")}
+        assert torch.equal(engines[0].params, engines[1].params), (stage, diff)
+
+    both(lambda e: _plan(e, g0, 1, n, N), "one-step plan")
+    ref.run(g0, n, 1.0 / n, REG, LR, sgd=True)
+    torch.cuda.synchronize()
+    assert engines[1]._hip_step().xstep_used == 1, engines[1]._hip_step().xstep_reason
+    err = (engines[1].params - ref.params).abs().max() / ref.params.abs().max()
+    assert err < 2e-5, float(err)
+    # (n = 800 from sample 8: no wrap to sample 0, where the two-launch step would take the fragment-ordered forms)
+    both(lambda e: _plan(e, g0, 2 * (N // n) if g0 % 16 == 0 else N // n - 1, n, N), "two epochs")
+    assert engines[1]._hip_step().xstep_used == 1, engines[1]._hip_step().xstep_reason
+    assert engines[1]._hip_step().dz_left_swz == 0
+    both(lambda e: _plan(e, 2 * n + g0, 2, n, N))
+    both(lambda e: e.run(16, n, 1.0 / n, REG, LR, sgd=True))  # a two-launch step between plans
+    both(lambda e: _plan(e, n + g0, 3, n, N))
+    assert torch.equal(engines[0].dz1()[:, :n], engines[1].dz1()[:, :n])
+    for e in engines:
+        assert not e.kernel_error()
+
+
 def test_xstep_falls_back_where_it_does_not_apply():
-    """Plans the pipeline does not take run the two-launch loop (bitwise the same as xstep = 0): steps off the
-    16-sample grid, the head's dW2 partials off; xstep = 1 (required) then raises."""
+    """Plans the pipeline does not take run the two-launch loop (bitwise the same as xstep = 0): steps off 4-byte
+    aligned pixel columns, the head's dW2 partials off; xstep = 1 (required) then raises."""
     n, N = 800, 3 * 800 + 48
     engines = _pair(100, n, N, seed=7)
     for e in engines:
-        _plan(e, 8, 2, n, N)  # (first sample 8: off the fragment-ordered pixels' 16-sample grid)
+        _plan(e, 2, 2, n, N)  # (first sample 2: the dW1 tiles' pixel loads need 4-byte aligned columns)
     torch.cuda.synchronize()
     assert engines[1]._hip_step().xstep_used == 0
-    assert "16-sample grid" in engines[1]._hip_step().xstep_reason
+    assert "4-byte" in engines[1]._hip_step().xstep_reason
     assert torch.equal(engines[0].params, engines[1].params)
     st = engines[1]._hip_step()
     st.xstep = 1
     with pytest.raises(ValueError, match="xstep"):
-        _plan(engines[1], 8, 1, n, N)
+        _plan(engines[1], 2, 1, n, N)
     small = _pair(100, 400, 2000, seed=8)
     for e in small:
         e._hip_step().head_dw2 = 0
