@@ -34,7 +34,8 @@
 // a stale L1 line, and the producer's plain stores stay in the XCD's L2 (bench/micro/xcd_barrier.hip: the same-XCD
 // read-back checked word by word, and priced, profiles/r6/xcd_barrier_micro*.jsonl).  Arithmetic and summation
 // orders are those of the two-launch step, so the parameters are bitwise equal to it (tests/test_gpu_xstep.py).
-// Walking step at n = 800: 9.4-9.5 us against the two-launch loop's 14.0 (profiles/r6/flags/, docs/ROUND6_STATUS.md).
+// Walking step at n = 800: 9.4-9.5 us against the two-launch loop's 14.0 (profiles/r6/flags/, docs/ROUND6_STATUS.md);
+// n = 100 (the row-major form, RM below): 8.90 us against 12.33 (profiles/r6/rm_form/).
 //
 // Failure semantics: a z2 hand-off wait that outlasts SplitStepArgs::ag_wait_us sets *err and makes its workgroup
 // arrive "bad" at the first barrier; every XCD's workgroup of that column tile waits for the same missing granule,
@@ -220,8 +221,8 @@ struct XsWalk {
 // the head writes fp32 dZ1 row-major and the dW1 tile reads it with sc1 loads, 2 x 16-byte vectors (RM 1, n % 8 == 0)
 // or 16-byte pixel pairs (RM 3: a plan on the 16-sample grid, n % 16 == 0) -- the two-launch step's own forms for such
 // a step (mlp_split_wgrad vec 1 / 3) -- or, n % 4 == 0, 2 x 16-byte vectors with the tail past n zeroed in registers
-// (RM 4: the same MFMA operands as the two-launch step's element loads, vec 2; 9.25 -> see docs/ROUND6_STATUS.md), so
-// the bits are its bits.
+// (RM 4: the same MFMA operands as the two-launch step's element loads, vec 2; n = 100 walking step 9.25 -> 8.90 us,
+// profiles/r6/rm_form/), so the bits are its bits.
 template <int BAR, int FG, bool DIAG = false, int HK = 0, int RM = 0>
 __global__ __launch_bounds__(512) void xstep_kernel(SplitStepArgs a, HeadArgs h, XStepPlan p, int tm, int tn,
                                                     int t1n) {
