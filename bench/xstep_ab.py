@@ -28,6 +28,8 @@ def main(argv=None):
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--bar", type=int, nargs="*", default=[3], help="MlpStep.xstep_bar values (XStepPlan::bar)")
     ap.add_argument("--pf", type=int, nargs="*", default=[0], help="MlpStep.xstep_pf values (XStepPlan::npf)")
+    ap.add_argument("--rm", action="store_true",
+                    help="also the pipeline's row-major form on plans the fragment-ordered form takes (MlpStep.dz_swz = 0)")
     ap.add_argument("--stamps", type=int, default=0)
     ap.add_argument("--fha-stamps", type=int, default=0, help="forward + head body stamps of the last of K steps")
     ap.add_argument("--gemm-stamps", action="store_true",
@@ -65,9 +67,13 @@ def main(argv=None):
 
         forms = [("two_launch", 0, 1, 0)] + [(f"xstep_bar{b}_pf{q}", -1, b, q) for b in a.bar for q in a.pf
                                              if b == 1 or q == 0]
+        if a.rm:
+            forms.append(("xstep_rm", -1, 3, 0))
+        dz0 = st.dz_swz
         for rnd in range(a.rounds):
             for name, xs, b, q in forms:
                 st.xstep, st.xstep_bar, st.xstep_pf = xs, b, q
+                st.dz_swz = 0 if name == "xstep_rm" else dz0
                 walk(20)
                 torch.cuda.synchronize()
                 best = float("inf")
